@@ -1,0 +1,643 @@
+// vo_api.cpp -- host side of libvo_mi355x.so: the C ABI of include/vo_mi355x.h.
+//
+// One vo_ctx = one GPU + one HIP stream + every device buffer of the path allocated
+// once (HBM layout: vo_internal.h).  Per frame the host only enqueues kernels; all
+// per-frame decisions of the reference's trajectory loop (skip on < 8 matches /
+// inliers, descriptor carry-forward, RANSAC model leak, GT scale) are taken on the
+// device from VoState, so frames can be enqueued back to back with no host sync.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <climits>
+#include <map>
+#include <mutex>
+#include <new>
+#include <utility>
+#include <vector>
+
+#include "vo_internal.h"
+#include "../../include/vo_mi355x.h"
+
+
+struct vo_ctx {
+    vo_config cfg;
+    VoDev d;
+    hipStream_t s = nullptr;
+    int max_hyp = VO_MAX_HYP;
+    int gt_cap = 0;
+    VoFrameOut* out_dev = nullptr;
+    int out_cap = 0;
+    VoFrameOut* out_host = nullptr;   // pinned
+    uint8_t* stage_host = nullptr;    // pinned frame staging
+    uint16_t* tab_dev = nullptr;
+    bool timing = false;
+    std::vector<float> ktime_ms;
+    std::vector<int> kcount;
+};
+
+namespace {
+
+int hip_ok(hipError_t e)
+{
+    if (e != hipSuccess) {
+        fprintf(stderr, "[vo_mi355x] HIP error %d: %s\n", (int)e, hipGetErrorString(e));
+        return VO_ERR_HIP;
+    }
+    return VO_OK;
+}
+#define HIPCHK(x)                          \
+    do {                                   \
+        int _rc = hip_ok(x);               \
+        if (_rc != VO_OK) return _rc;      \
+    } while (0)
+
+// ransac.cpp:131 -- double -> int as compiled on x86 (cvttsd2si), see oracle to_int_x86
+int to_int_x86(double q)
+{
+    if (!(q > -2147483649.0 && q < 2147483648.0)) return INT_MIN;
+    return (int)q;
+}
+
+// maxIterations after a strictly better count (ransac.cpp:179-190), evaluated with the
+// host libm exactly as the reference evaluates it; 0xFFFF = "denom == 0: no update".
+// Table row M holds entries best = 0..M at offset M(M+1)/2.
+std::mutex g_tab_mu;
+std::map<std::pair<int, double>, std::vector<uint16_t>> g_tab_cache;
+
+const std::vector<uint16_t>& maxit_table(int N, double prob)
+{
+    std::lock_guard<std::mutex> lk(g_tab_mu);
+    auto key = std::make_pair(N, prob);
+    auto it = g_tab_cache.find(key);
+    if (it != g_tab_cache.end()) return it->second;
+    std::vector<uint16_t> tab((size_t)(N + 1) * (N + 2) / 2, 0xFFFFu);
+    const double lp = std::log(1.0 - prob);
+    for (int M = 8; M <= N; ++M) {
+        uint16_t* row = tab.data() + (size_t)M * (M + 1) / 2;
+        for (int best = 1; best <= M; ++best) {
+            double outlierRatio = 1.0 - (double)best / (double)M;
+            double denom = std::log(1.0 - std::pow(1.0 - outlierRatio, 8.0));
+            if (denom == 0.0) { row[best] = 0xFFFFu; continue; }
+            int v = to_int_x86(lp / denom);
+            v = std::min(std::max(v, 100), 2000);
+            row[best] = (uint16_t)v;
+        }
+    }
+    return g_tab_cache.emplace(key, std::move(tab)).first->second;
+}
+
+template <typename T>
+int dalloc(T** p, size_t n)
+{
+    return hip_ok(hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T)));
+}
+
+int read_state(vo_ctx* c, VoState* h)
+{
+    HIPCHK(hipMemcpyAsync(h, c->d.st, sizeof(VoState), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    return VO_OK;
+}
+int write_state(vo_ctx* c, const VoState* h)
+{
+    HIPCHK(hipMemcpyAsync(c->d.st, h, sizeof(VoState), hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    return VO_OK;
+}
+
+// host frame (any stride) -> frame_in, via the pinned staging buffer
+int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride)
+{
+    const int W = c->cfg.width, H = c->cfg.height;
+    if (stride == 0) stride = (size_t)W;
+    HIPCHK(hipStreamSynchronize(c->s));   // staging buffer may still be in flight
+    if (stride == (size_t)W) {
+        std::memcpy(c->stage_host, gray, (size_t)W * H);
+    } else {
+        for (int y = 0; y < H; ++y) std::memcpy(c->stage_host + (size_t)y * W, gray + (size_t)y * stride, W);
+    }
+    HIPCHK(hipMemcpyAsync(c->d.frame_in, c->stage_host, (size_t)W * H, hipMemcpyHostToDevice, c->s));
+    return VO_OK;
+}
+
+void enqueue_extract(vo_ctx* c, const uint8_t* dframe, int write_response)
+{
+    vo::launch_stencil(c->d, dframe, write_response, c->s);
+    vo::launch_select(c->d, c->s);
+    vo::launch_describe(c->d, c->s);
+}
+
+void enqueue_ransac(vo_ctx* c)
+{
+    vo::launch_ransac_hyp(c->d, 0, VO_HYP_CHUNK0, c->s);
+    vo::launch_ransac_replay(c->d, VO_HYP_CHUNK0, c->s);
+    vo::launch_ransac_hyp(c->d, VO_HYP_CHUNK0, c->max_hyp, c->s);
+    vo::launch_ransac_replay(c->d, c->max_hyp, c->s);
+    vo::launch_refit(c->d, c->s);
+}
+
+// the full trajectory-loop iteration for one frame (VisualOdometry.cpp:68-189)
+void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, std::vector<hipEvent_t>* ev)
+{
+    auto mark = [&](int) {
+        if (ev) {
+            hipEvent_t e;
+            (void)hipEventCreate(&e);
+            (void)hipEventRecord(e, c->s);
+            ev->push_back(e);
+        }
+    };
+    VoDev d = c->d;
+    d.out = out;
+    mark(0);
+    vo::launch_frame_begin(d, dframe ? VO_MODE_FRAME : VO_MODE_MISSING, c->s);
+    mark(1);
+    if (dframe) {
+        vo::launch_stencil(d, dframe, 0, c->s); mark(2);
+        vo::launch_select(d, c->s); mark(3);
+        vo::launch_describe(d, c->s); mark(4);
+        vo::launch_match(d, c->s); mark(5);
+        vo::launch_compact(d, c->s); mark(6);
+        vo::launch_ransac_hyp(d, 0, VO_HYP_CHUNK0, c->s); mark(7);
+        vo::launch_ransac_replay(d, VO_HYP_CHUNK0, c->s); mark(8);
+        vo::launch_ransac_hyp(d, VO_HYP_CHUNK0, c->max_hyp, c->s); mark(9);
+        vo::launch_ransac_replay(d, c->max_hyp, c->s); mark(10);
+        vo::launch_refit(d, c->s); mark(11);
+        vo::launch_pose_prep(d, c->s); mark(12);
+        vo::launch_triangulate(d, c->s); mark(13);
+    } else {
+        for (int k = 2; k <= 13; ++k) mark(k);
+    }
+    vo::launch_finalize(d, c->s);
+    mark(14);
+}
+
+int ensure_out(vo_ctx* c, int n)
+{
+    if (n <= c->out_cap) return VO_OK;
+    if (c->out_dev) (void)hipFree(c->out_dev);
+    if (c->out_host) (void)hipHostFree(c->out_host);
+    c->out_dev = nullptr; c->out_host = nullptr; c->out_cap = 0;
+    HIPCHK(hipMalloc((void**)&c->out_dev, sizeof(VoFrameOut) * (size_t)n));
+    HIPCHK(hipHostMalloc((void**)&c->out_host, sizeof(VoFrameOut) * (size_t)n, hipHostMallocDefault));
+    c->out_cap = n;
+    return VO_OK;
+}
+
+void init_state(vo_ctx* c, VoState* h)
+{
+    std::memset(h, 0, sizeof(*h));
+    h->frame = 0;
+    h->status = VO_STATUS_OK;
+    h->cur = 0; h->prev = 0;
+    h->bestk = -1;
+    h->scale_override = std::nan("");
+    for (int i = 0; i < 16; ++i) h->Tcurr[i] = (i % 5 == 0) ? 1.0 : 0.0;
+    (void)c;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vo_abi_version(void) { return VO_ABI_VERSION; }
+
+const char* vo_strerror(int code)
+{
+    switch (code) {
+    case VO_OK: return "ok";
+    case VO_ERR_ARG: return "invalid argument";
+    case VO_ERR_HIP: return "HIP runtime error";
+    case VO_ERR_NO_DEVICE: return "no HIP device";
+    case VO_ERR_CAPACITY: return "capacity exceeded";
+    case VO_ERR_STATE: return "invalid state";
+    case VO_ERR_DEGENERATE_E: return "Degenerate essential matrix";
+    default: return "unknown error";
+    }
+}
+
+void vo_config_default(vo_config* c, int width, int height)
+{
+    std::memset(c, 0, sizeof(*c));
+    c->width = width; c->height = height;
+    c->max_kpts = 2000; c->nms_k = 3; c->resp_thr = 20000.0f;
+    c->border_row = 35; c->border_col = 37;
+    c->ratio = 0.75f; c->match_bits = 32;
+    c->ransac_p = 0.99; c->sampson_thr = 1.0; c->ransac_chunk_threads = 8;
+    c->seed = 0xACE0ULL;
+    const double K[9] = {7.188560000000e+02, 0, 6.071928000000e+02, 0, 7.188560000000e+02, 1.852157000000e+02, 0, 0, 1.0};
+    std::memcpy(c->K, K, sizeof(K));
+    c->device = 0;
+}
+
+void vo_unpack_descriptor(const uint64_t words[8], uint8_t bytes[512])
+{
+    for (int t = 0; t < 512; ++t) bytes[t] = (uint8_t)((words[t >> 6] >> (t & 63)) & 1u);
+}
+
+int vo_create(const vo_config* cfg, vo_ctx** out)
+{
+    if (!cfg || !out) return VO_ERR_ARG;
+    *out = nullptr;
+    const vo_config& k = *cfg;
+    if (k.width < 8 || k.height < 8 || k.width > 65535 || k.height > 65535) return VO_ERR_ARG;
+    if (k.max_kpts < 1 || k.max_kpts > 4096) return VO_ERR_ARG;
+    if (k.nms_k != 3) return VO_ERR_ARG;                     // the VO path uses k = 3
+    if (!(k.resp_thr >= 0.0f)) return VO_ERR_ARG;
+    if (k.match_bits != 32 && k.match_bits != 512) return VO_ERR_ARG;
+    if (!(k.ransac_p > 0.0 && k.ransac_p < 1.0) || k.ransac_chunk_threads < 1) return VO_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return VO_ERR_NO_DEVICE;
+    if (k.device < 0 || k.device >= ndev) return VO_ERR_NO_DEVICE;
+    if (hip_ok(hipSetDevice(k.device)) != VO_OK) return VO_ERR_HIP;
+
+    vo_ctx* c = new (std::nothrow) vo_ctx();
+    if (!c) return VO_ERR_CAPACITY;
+    c->cfg = k;
+    VoDev& d = c->d;
+    std::memset(&d, 0, sizeof(d));
+    const int W = k.width, H = k.height, N = k.max_kpts;
+    d.W = W; d.H = H; d.N = N;
+    d.nms_k = k.nms_k; d.brow = k.border_row; d.bcol = k.border_col;
+    d.resp_thr = k.resp_thr;
+    std::memcpy(&d.thr_bits, &k.resp_thr, 4);
+    d.ratio = k.ratio; d.match_bits = k.match_bits;
+    d.ransac_p = k.ransac_p; d.sampson_thr = k.sampson_thr; d.T = k.ransac_chunk_threads;
+    d.seed = k.seed;
+    std::memcpy(d.K, k.K, sizeof(d.K));
+    {
+        double outlierRatio = 0.5;
+        d.maxit_initial = to_int_x86(std::log(1.0 - k.ransac_p) / std::log(1.0 - std::pow(1.0 - outlierRatio, 8.0)));
+    }
+    c->max_hyp = std::max(VO_MAX_HYP, std::min(d.maxit_initial, 1 << 20));
+    d.cand_cap = (uint32_t)(((H + 1) / 2) * ((W + 1) / 2));
+    int rc = VO_OK;
+    auto bail = [&](int r) { vo_destroy(c); return r; };
+    if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
+    rc |= dalloc(&d.frame_in, (size_t)W * H);
+    rc |= dalloc(&d.blurred, (size_t)W * H);
+    rc |= dalloc(&d.response, (size_t)W * H);
+    rc |= dalloc(&d.cand, d.cand_cap);
+    rc |= dalloc(&d.hist, VO_HIST_BINS);
+    for (int s = 0; s < 2; ++s) {
+        rc |= dalloc(&d.kps[s], N);
+        rc |= dalloc(&d.desc[s], (size_t)N * 8);
+        rc |= dalloc(&d.pre[s], N);
+    }
+    rc |= dalloc(&d.match_j, N);
+    rc |= dalloc(&d.match_pairs, N);
+    rc |= dalloc(&d.pts, (size_t)N * 4);
+    rc |= dalloc(&d.hypF, (size_t)c->max_hyp * 9);
+    rc |= dalloc(&d.counts, c->max_hyp);
+    rc |= dalloc(&d.inl, N);
+    rc |= dalloc(&d.model_p, (size_t)N * 4);
+    rc |= dalloc(&d.st, 1);
+    if (rc != VO_OK) return bail(VO_ERR_HIP);
+    const std::vector<uint16_t>& tab = maxit_table(N, k.ransac_p);
+    if (dalloc(&c->tab_dev, tab.size()) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(hipMemcpy(c->tab_dev, tab.data(), tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice)) != VO_OK)
+        return bail(VO_ERR_HIP);
+    d.maxit_tab = c->tab_dev;
+    if (hip_ok(hipHostMalloc((void**)&c->stage_host, (size_t)W * H, hipHostMallocDefault)) != VO_OK) return bail(VO_ERR_HIP);
+    // zero the descriptor / keypoint slots (deterministic contents before first use)
+    for (int s = 0; s < 2; ++s) {
+        (void)hipMemset(d.kps[s], 0, sizeof(int2) * N);
+        (void)hipMemset(d.desc[s], 0, sizeof(uint64_t) * 8 * N);
+        (void)hipMemset(d.pre[s], 0, sizeof(uint32_t) * N);
+    }
+    if (ensure_out(c, 16) != VO_OK) return bail(VO_ERR_HIP);
+    VoState h;
+    init_state(c, &h);
+    if (hip_ok(hipMemcpy(d.st, &h, sizeof(h), hipMemcpyHostToDevice)) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(hipDeviceSynchronize()) != VO_OK) return bail(VO_ERR_HIP);
+    *out = c;
+    return VO_OK;
+}
+
+void vo_destroy(vo_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->cfg.device);
+    if (c->s) (void)hipStreamSynchronize(c->s);
+    VoDev& d = c->d;
+    void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.hist, d.kps[0], d.kps[1], d.desc[0], d.desc[1],
+                    d.pre[0], d.pre[1], d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.model_p,
+                    d.st, (void*)d.gt, c->tab_dev, c->out_dev};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (c->out_host) (void)hipHostFree(c->out_host);
+    if (c->stage_host) (void)hipHostFree(c->stage_host);
+    if (c->s) (void)hipStreamDestroy(c->s);
+    delete c;
+}
+
+int vo_reset(vo_ctx* c)
+{
+    if (!c) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    VoState h;
+    init_state(c, &h);
+    return write_state(c, &h);
+}
+
+int vo_set_ground_truth(vo_ctx* c, const double* poses12, int n)
+{
+    if (!c || n < 0 || (n > 0 && !poses12)) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipStreamSynchronize(c->s));
+    if (n > c->gt_cap) {
+        if (c->d.gt) (void)hipFree((void*)c->d.gt);
+        double* g = nullptr;
+        HIPCHK(hipMalloc((void**)&g, sizeof(double) * 12 * (size_t)n));
+        c->d.gt = g;
+        c->gt_cap = n;
+    }
+    if (n) HIPCHK(hipMemcpy((void*)c->d.gt, poses12, sizeof(double) * 12 * (size_t)n, hipMemcpyHostToDevice));
+    c->d.gt_n = n;
+    return VO_OK;
+}
+
+int vo_extract(vo_ctx* c, const uint8_t* gray, size_t stride, vo_kp* kps, uint64_t* desc, int* n, uint8_t* blurred)
+{
+    if (!c || !gray || !n) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    int rc = upload_frame(c, gray, stride);
+    if (rc) return rc;
+    vo::launch_frame_begin(c->d, VO_MODE_EXTRACT, c->s);
+    enqueue_extract(c, c->d.frame_in, 0);
+    HIPCHK(hipGetLastError());
+    VoState h;
+    rc = read_state(c, &h);
+    if (rc) return rc;
+    if (h.status != VO_STATUS_OK) return VO_ERR_CAPACITY;
+    const int nk = h.n_kps[0];
+    *n = nk;
+    if (kps && nk) HIPCHK(hipMemcpy(kps, c->d.kps[0], sizeof(vo_kp) * nk, hipMemcpyDeviceToHost));
+    if (desc && nk) HIPCHK(hipMemcpy(desc, c->d.desc[0], sizeof(uint64_t) * 8 * nk, hipMemcpyDeviceToHost));
+    if (blurred)
+        HIPCHK(hipMemcpy(blurred, c->d.blurred, (size_t)c->cfg.width * c->cfg.height, hipMemcpyDeviceToHost));
+    // vo_extract leaves the trajectory state untouched except slot 0 contents
+    h.status = VO_STATUS_OK;
+    return VO_OK;
+}
+
+int vo_response(vo_ctx* c, const uint8_t* gray, size_t stride, float* R)
+{
+    if (!c || !gray || !R) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    int rc = upload_frame(c, gray, stride);
+    if (rc) return rc;
+    const size_t np = (size_t)c->cfg.width * c->cfg.height;
+    HIPCHK(hipMemsetAsync(c->d.response, 0, np * sizeof(float), c->s));
+    vo::launch_frame_begin(c->d, VO_MODE_EXTRACT, c->s);
+    vo::launch_stencil(c->d, c->d.frame_in, 1, c->s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(R, c->d.response, np * sizeof(float), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    return VO_OK;
+}
+
+int vo_match(vo_ctx* c, const uint64_t* d_prev, int n_prev, const uint64_t* d_cur, int n_cur, vo_match_t* out, int* m)
+{
+    if (!c || !m || n_prev < 0 || n_cur < 0 || n_prev > c->cfg.max_kpts || n_cur > c->cfg.max_kpts) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    *m = 0;
+    if (n_prev == 0 || n_cur == 0) return VO_OK;   // feature_matching_parallel.cpp:57
+    std::vector<uint32_t> p0(n_prev), p1(n_cur);
+    for (int i = 0; i < n_prev; ++i) p0[i] = (uint32_t)d_prev[8 * (size_t)i];
+    for (int i = 0; i < n_cur; ++i) p1[i] = (uint32_t)d_cur[8 * (size_t)i];
+    HIPCHK(hipStreamSynchronize(c->s));
+    HIPCHK(hipMemcpy(c->d.desc[0], d_prev, sizeof(uint64_t) * 8 * n_prev, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d.desc[1], d_cur, sizeof(uint64_t) * 8 * n_cur, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d.pre[0], p0.data(), sizeof(uint32_t) * n_prev, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d.pre[1], p1.data(), sizeof(uint32_t) * n_cur, hipMemcpyHostToDevice));
+    VoState h;
+    int rc = read_state(c, &h);
+    if (rc) return rc;
+    VoState saved = h;
+    h.prev = 0; h.cur = 1; h.n_kps[0] = n_prev; h.n_kps[1] = n_cur;
+    h.status = VO_STATUS_OK; h.mode = VO_MODE_STAGE;
+    rc = write_state(c, &h);
+    if (rc) return rc;
+    vo::launch_match(c->d, c->s);
+    vo::launch_compact(c->d, c->s);
+    HIPCHK(hipGetLastError());
+    rc = read_state(c, &h);
+    if (rc) return rc;
+    *m = h.M;
+    if (out && h.M) HIPCHK(hipMemcpy(out, c->d.match_pairs, sizeof(vo_match_t) * h.M, hipMemcpyDeviceToHost));
+    // restore the trajectory bookkeeping (stage calls do not advance the loop)
+    saved.n_kps[0] = h.n_kps[0]; saved.n_kps[1] = h.n_kps[1];
+    return write_state(c, &saved);
+}
+
+int vo_ransac_F(vo_ctx* c, const double* pts, int m, uint64_t seed, double F[9], int* fitted, int32_t* inlier_idx,
+                int* n_inl, int* best_k, int* n_evaluated, int32_t* counts)
+{
+    if (!c || !pts || m < 8 || m > c->cfg.max_kpts) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipStreamSynchronize(c->s));
+    HIPCHK(hipMemcpy(c->d.pts, pts, sizeof(double) * 4 * (size_t)m, hipMemcpyHostToDevice));
+    VoState h;
+    int rc = read_state(c, &h);
+    if (rc) return rc;
+    VoState saved = h;
+    h.status = VO_STATUS_OK; h.mode = VO_MODE_STAGE;
+    h.M = m; h.scored = (m / c->cfg.ransac_chunk_threads) * c->cfg.ransac_chunk_threads;
+    h.frame_seed = seed; h.bestk = -1; h.need_more = 0; h.fitted = 0; h.n_inl = 0;
+    rc = write_state(c, &h);
+    if (rc) return rc;
+    enqueue_ransac(c);
+    HIPCHK(hipGetLastError());
+    rc = read_state(c, &h);
+    if (rc) return rc;
+    if (F) std::memcpy(F, h.model_F, sizeof(h.model_F));
+    if (fitted) *fitted = h.fitted;
+    if (n_inl) *n_inl = h.n_inl;
+    if (best_k) *best_k = h.bestk;
+    if (n_evaluated) *n_evaluated = h.n_eval;
+    if (inlier_idx && h.bestk >= 0 && h.n_inl > 0)
+        HIPCHK(hipMemcpy(inlier_idx, c->d.inl, sizeof(int32_t) * h.n_inl, hipMemcpyDeviceToHost));
+    if (counts && h.n_eval > 0)
+        HIPCHK(hipMemcpy(counts, c->d.counts, sizeof(int32_t) * std::min(h.n_eval, VO_MAX_HYP), hipMemcpyDeviceToHost));
+    // the model (F + inliers) persists like FundamentalMatrix model (VisualOdometry.cpp:49)
+    saved.model_n = h.model_n;
+    std::memcpy(saved.model_F, h.model_F, sizeof(h.model_F));
+    return write_state(c, &saved);
+}
+
+int vo_pose(vo_ctx* c, const double F[9], const float* p1, const float* p2, int n, double scale, double R[9],
+            double t[3], int32_t* counts4)
+{
+    if (!c || !F || !p1 || !p2 || n < 8 || n > c->cfg.max_kpts) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    std::vector<float> mp((size_t)n * 4);
+    for (int i = 0; i < n; ++i) {
+        mp[4 * i] = p1[2 * i]; mp[4 * i + 1] = p1[2 * i + 1];
+        mp[4 * i + 2] = p2[2 * i]; mp[4 * i + 3] = p2[2 * i + 1];
+    }
+    HIPCHK(hipStreamSynchronize(c->s));
+    HIPCHK(hipMemcpy(c->d.model_p, mp.data(), sizeof(float) * mp.size(), hipMemcpyHostToDevice));
+    VoState h;
+    int rc = read_state(c, &h);
+    if (rc) return rc;
+    VoState saved = h;
+    h.status = VO_STATUS_OK; h.mode = VO_MODE_STAGE;
+    h.model_n = n;
+    std::memcpy(h.model_F, F, sizeof(h.model_F));
+    h.scale_override = scale;
+    rc = write_state(c, &h);
+    if (rc) return rc;
+    vo::launch_pose_prep(c->d, c->s);
+    vo::launch_triangulate(c->d, c->s);
+    vo::launch_finalize(c->d, c->s);
+    HIPCHK(hipGetLastError());
+    rc = read_state(c, &h);
+    if (rc) return rc;
+    int ret = VO_OK;
+    if (h.status == VO_STATUS_DEGENERATE) ret = VO_ERR_DEGENERATE_E;
+    else if (h.status != VO_STATUS_OK) ret = VO_ERR_STATE;
+    if (ret == VO_OK) {
+        if (R) std::memcpy(R, h.pose_R, sizeof(h.pose_R));
+        if (t) std::memcpy(t, h.pose_t, sizeof(h.pose_t));
+    }
+    if (counts4) std::memcpy(counts4, h.counts4, sizeof(h.counts4));
+    rc = write_state(c, &saved);
+    return ret != VO_OK ? ret : rc;
+}
+
+int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_out[12], int* status, int32_t* info)
+{
+    if (!c) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    if (gray) {
+        int rc = upload_frame(c, gray, stride);
+        if (rc) return rc;
+    }
+    enqueue_frame(c, gray ? c->d.frame_in : nullptr, c->out_dev, nullptr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(c->out_host, c->out_dev, sizeof(VoFrameOut), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    const VoFrameOut& o = c->out_host[0];
+    if (pose_out) std::memcpy(pose_out, o.pose, sizeof(o.pose));
+    if (status) *status = o.status;
+    if (info) {
+        info[0] = o.n_kps; info[1] = o.n_matches; info[2] = o.n_inl; info[3] = o.best_k;
+        info[4] = o.n_eval; info[5] = o.fitted; info[6] = 0; info[7] = 0;
+    }
+    return o.status == VO_STATUS_DEGENERATE ? VO_ERR_DEGENERATE_E : VO_OK;
+}
+
+int vo_process_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_bytes, int nframes, double* poses_out,
+                             int* status_out, int32_t* info_out)
+{
+    if (!c || !d_frames || nframes < 0) return VO_ERR_ARG;
+    if (frame_bytes < (size_t)c->cfg.width * c->cfg.height) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    int rc = ensure_out(c, std::max(nframes, 1));
+    if (rc) return rc;
+    std::vector<hipEvent_t> ev;
+    std::vector<hipEvent_t>* evp = c->timing ? &ev : nullptr;
+    if (evp) ev.reserve((size_t)nframes * 15);
+    for (int f = 0; f < nframes; ++f) enqueue_frame(c, d_frames + (size_t)f * frame_bytes, c->out_dev + f, evp);
+    HIPCHK(hipGetLastError());
+    if (nframes)
+        HIPCHK(hipMemcpyAsync(c->out_host, c->out_dev, sizeof(VoFrameOut) * nframes, hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    if (evp) {
+        const int nk = vo::kernel_count();
+        c->ktime_ms.assign(nk, 0.f);
+        c->kcount.assign(nk, 0);
+        for (int f = 0; f < nframes; ++f) {
+            for (int k = 0; k < nk; ++k) {
+                float ms = 0.f;
+                (void)hipEventElapsedTime(&ms, ev[(size_t)f * 15 + k], ev[(size_t)f * 15 + k + 1]);
+                c->ktime_ms[k] += ms;
+                c->kcount[k] += 1;
+            }
+        }
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+    for (int f = 0; f < nframes; ++f) {
+        const VoFrameOut& o = c->out_host[f];
+        if (poses_out) std::memcpy(poses_out + 12 * (size_t)f, o.pose, sizeof(o.pose));
+        if (status_out) status_out[f] = o.status;
+        if (info_out) {
+            int32_t* p = info_out + 8 * (size_t)f;
+            p[0] = o.n_kps; p[1] = o.n_matches; p[2] = o.n_inl; p[3] = o.best_k;
+            p[4] = o.n_eval; p[5] = o.fitted; p[6] = o.frame; p[7] = 0;
+        }
+    }
+    return VO_OK;
+}
+
+int vo_enable_kernel_timing(vo_ctx* c, int on)
+{
+    if (!c) return VO_ERR_ARG;
+    c->timing = on != 0;
+    return VO_OK;
+}
+
+int vo_last_kernel_times(vo_ctx* c, const char** names, float* ms, int cap)
+{
+    if (!c) return VO_ERR_ARG;
+    int nk = std::min<int>((int)c->ktime_ms.size(), cap);
+    for (int k = 0; k < nk; ++k) {
+        if (names) names[k] = vo::kernel_name(k);
+        if (ms) ms[k] = c->kcount[k] ? c->ktime_ms[k] / (float)c->kcount[k] : 0.f;
+    }
+    return nk;
+}
+
+int vo_device_alloc(vo_ctx* c, size_t bytes, void** dptr)
+{
+    if (!c || !dptr) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipMalloc(dptr, std::max<size_t>(bytes, 1)));
+    return VO_OK;
+}
+
+int vo_device_free(vo_ctx* c, void* dptr)
+{
+    if (!c) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipStreamSynchronize(c->s));
+    if (dptr) HIPCHK(hipFree(dptr));
+    return VO_OK;
+}
+
+int vo_device_upload(vo_ctx* c, void* dptr, const void* src, size_t bytes)
+{
+    if (!c || !dptr || !src) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipMemcpy(dptr, src, bytes, hipMemcpyHostToDevice));
+    return VO_OK;
+}
+
+// test hook: device arithmetic self-test (sqrtf, f32 '/', f64 sqrt and '/', det-math)
+int vo_selftest_arith(const float* fa, const float* fb, float* fo, const double* da, const double* db, double* dout,
+                      int n, int device)
+{
+    if (n <= 0) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(device));
+    float *a, *b, *o;
+    double *x, *y, *z;
+    HIPCHK(hipMalloc((void**)&a, n * 4)); HIPCHK(hipMalloc((void**)&b, n * 4)); HIPCHK(hipMalloc((void**)&o, n * 16));
+    HIPCHK(hipMalloc((void**)&x, n * 8)); HIPCHK(hipMalloc((void**)&y, n * 8)); HIPCHK(hipMalloc((void**)&z, n * 32));
+    HIPCHK(hipMemcpy(a, fa, n * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b, fb, n * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(x, da, n * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(y, db, n * 8, hipMemcpyHostToDevice));
+    vo::launch_selftest_arith(a, b, o, x, y, z, n, nullptr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(fo, o, n * 16, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(dout, z, n * 32, hipMemcpyDeviceToHost));
+    (void)hipFree(a); (void)hipFree(b); (void)hipFree(o); (void)hipFree(x); (void)hipFree(y); (void)hipFree(z);
+    return VO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,123 @@
+// vo_internal.h -- device-resident state and buffer layout of one vo_ctx, shared by
+// the HIP kernels (vo_kernels.hip) and the host driver (vo_api.cpp).
+//
+// HBM layout (allocated once per ctx in vo_create; the reference allocates every
+// cl::Buffer per frame, corner_detection_parallel_GPU.cpp:45-49,85 and
+// FREAK_feature_descriptor_parallel_GPU.cpp:53-78):
+//   frame_in    u8  W*H         staging for host-supplied frames
+//   blurred     u8  W*H         7x7 Gaussian output (read back by describe)
+//   response    f32 W*H         optional dense R map (debug / parity only)
+//   cand        u64 cand_cap    NMS survivors, key = Rbits<<32 | row<<16 | col
+//   hist        u32 4096        coarse histogram of candidate R (top-N boundary)
+//   kps[2]      int2 N          raster-ordered keypoints, slot ping-pong
+//   desc[2]     u64 8N          packed 512-test descriptors (slot ping-pong)
+//   pre[2]      u32 N           tests 0..31 (the matcher's 32-bit prefix)
+//   match_j     i32 N           best cur index per prev query, -1 if rejected
+//   pts         f64 4N          matched (x1,y1,x2,y2), ascending prev index
+//   hypF        f64 9*2000      per-hypothesis F (kept for the refit)
+//   counts      i32 2000        per-hypothesis inlier counts
+//   inl         i32 N           bestInlierSet indices
+//   model_p     f32 4N          model inliers (x1,y1,x2,y2) as cv::Point2f pairs
+//   maxit_tab   u16 tri(N)      ransac.cpp:179-190 iteration bound per (M, best)
+//   gt          f64 12*gt_cap   ground-truth rows for the GT scale
+//   out         VoFrameOut per frame of a batch
+#pragma once
+#include <stdint.h>
+
+#define VO_HIST_BINS 4096
+#define VO_MAX_HYP 2000
+#define VO_HYP_CHUNK0 256
+#define VO_RED_THREADS 256
+
+// frame modes for k_frame_begin
+#define VO_MODE_FRAME 0        // full trajectory-loop iteration
+#define VO_MODE_MISSING 1      // image missing: only push T_curr
+#define VO_MODE_EXTRACT 2      // vo_extract: extract into slot 0, no state change
+#define VO_MODE_STAGE 3        // stage APIs (match / ransac / pose): status OK, no trajectory
+
+struct VoFrameOut {
+    int32_t status, n_kps, n_matches, n_inl, best_k, n_eval, fitted, frame;
+    double pose[12];
+};
+
+struct VoState {
+    int32_t frame;        // index of the frame being processed
+    int32_t status;       // VO_STATUS_* of the current frame
+    int32_t mode;
+    int32_t cur, prev;    // descriptor / keypoint slots
+    int32_t n_kps[2];
+    uint32_t cand_count;
+    int32_t M;            // matches
+    int32_t scored;       // T * floor(M / T)   (ransac.cpp:152-157)
+    int32_t maxit, best, bestk, k_done, need_more, n_eval;
+    int32_t n_inl, fitted;
+    int32_t model_n;
+    int32_t degenerate;
+    int32_t counts4[4];
+    int32_t last_valid;
+    int32_t out_index;    // slot in the batch output array
+    int32_t pad0;
+    uint64_t frame_seed;
+    double model_F[9];
+    double R1[9], R2[9], t[3];
+    double pose_R[9], pose_t[3];   // last getPose result (stage API)
+    double scale_override;         // NaN: GT-derived scale
+    double Tcurr[16];
+};
+
+// Everything a kernel needs, passed by value.
+struct VoDev {
+    int W, H, N;
+    int nms_k, brow, bcol;
+    float resp_thr;
+    uint32_t thr_bits;
+    float ratio;
+    int match_bits;
+    double ransac_p, sampson_thr;
+    int T;
+    int maxit_initial;
+    uint64_t seed;
+    double K[9];
+    uint32_t cand_cap;
+    int gt_n;
+    uint8_t* frame_in;
+    uint8_t* blurred;
+    float* response;
+    uint64_t* cand;
+    uint32_t* hist;
+    int2* kps[2];
+    uint64_t* desc[2];
+    uint32_t* pre[2];
+    int32_t* match_j;
+    int2* match_pairs;
+    double* pts;
+    double* hypF;
+    int32_t* counts;
+    int32_t* inl;
+    float* model_p;
+    const uint16_t* maxit_tab;
+    const double* gt;
+    VoState* st;
+    VoFrameOut* out;
+};
+
+// launch wrappers (vo_kernels.hip)
+#include <hip/hip_runtime.h>
+namespace vo {
+void launch_frame_begin(const VoDev& d, int mode, hipStream_t s);
+void launch_stencil(const VoDev& d, const uint8_t* frame, int write_response, hipStream_t s);
+void launch_select(const VoDev& d, hipStream_t s);
+void launch_describe(const VoDev& d, hipStream_t s);
+void launch_match(const VoDev& d, hipStream_t s);
+void launch_compact(const VoDev& d, hipStream_t s);
+void launch_ransac_hyp(const VoDev& d, int k0, int k1, hipStream_t s);
+void launch_ransac_replay(const VoDev& d, int k1, hipStream_t s);
+void launch_refit(const VoDev& d, hipStream_t s);
+void launch_pose_prep(const VoDev& d, hipStream_t s);
+void launch_triangulate(const VoDev& d, hipStream_t s);
+void launch_finalize(const VoDev& d, hipStream_t s);
+void launch_selftest_arith(const float* fa, const float* fb, float* fo, const double* da,
+                           const double* db, double* dout, int n, hipStream_t s);
+int kernel_count();
+const char* kernel_name(int i);
+}  // namespace vo

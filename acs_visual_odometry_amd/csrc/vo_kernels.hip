@@ -1,0 +1,1396 @@
+// vo_kernels.hip -- gfx950 (CDNA4) kernels of the extract -> match -> pose hot path.
+//
+// Arithmetic contract: compiled with -ffp-contract=off; f32/f64 '/' and sqrt are the
+// correctly rounded HIP defaults; every expression is written in the operation order
+// of oracle/vo_oracle.c (which cites the reference file:line it restates), so keypoints,
+// descriptor bits, matches, per-hypothesis inlier counts, F, R and t are bit-identical
+// to the CPU oracle on the same inputs.  No MFMA: the path is stencil / bit-count /
+// small-f64 bound.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "vo_internal.h"
+#include "../../include/vo_freak_tables.h"
+#include "../../include/vo_mi355x.h"
+
+namespace vo {
+
+// ---------------------------------------------------------------------------
+// constant tables
+// ---------------------------------------------------------------------------
+__constant__ int8_t c_pt_x[VO_FREAK_NPOINTS];
+__constant__ int8_t c_pt_y[VO_FREAK_NPOINTS];
+__constant__ uint8_t c_pair_p[VO_FREAK_NPAIRS];
+__constant__ uint8_t c_pair_q[VO_FREAK_NPAIRS];
+__constant__ int16_t c_patch[VO_FREAK_NTESTS];
+
+static bool g_tables_ready = false;
+static void ensure_tables()
+{
+    if (g_tables_ready) return;
+    int8_t px[VO_FREAK_NPOINTS], py[VO_FREAK_NPOINTS];
+    uint8_t pp[VO_FREAK_NPAIRS], pq[VO_FREAK_NPAIRS];
+    for (int i = 0; i < VO_FREAK_NPOINTS; ++i) { px[i] = (int8_t)vo_freak_points[i][0]; py[i] = (int8_t)vo_freak_points[i][1]; }
+    int e = 0;
+    for (int p = 0; p < VO_FREAK_NPOINTS; ++p)
+        for (int q = p + 1; q < VO_FREAK_NPOINTS; ++q) { pp[e] = (uint8_t)p; pq[e] = (uint8_t)q; ++e; }
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pt_x), px, sizeof(px));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pt_y), py, sizeof(py));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pair_p), pp, sizeof(pp));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pair_q), pq, sizeof(pq));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_patch), vo_freak_patch, sizeof(vo_freak_patch));
+    g_tables_ready = true;
+}
+
+// ---------------------------------------------------------------------------
+// deterministic math (mirror of oracle/vo_oracle.c, same constants, same order)
+// ---------------------------------------------------------------------------
+__device__ __constant__ double c_atan_hi[9] = {
+    0.0, 0.12435499454676144, 0.24497866312686414, 0.35877067027057225,
+    0.4636476090008061, 0.5585993153435624, 0.6435011087932844,
+    0.7188299996216245, 0.7853981633974483};
+__device__ __constant__ double c_atan_lo[9] = {
+    0.0, -3.1253241424539383e-18, 1.0698755618734451e-17, -2.4623815582638635e-17,
+    2.2698777452961687e-17, -5.4556305485916264e-18, 1.5834785051444286e-17,
+    -2.1478388444456983e-17, 3.061616997868383e-17};
+
+__device__ __forceinline__ bool sgnbit(double x) { return (__double_as_longlong(x) >> 63) != 0; }
+
+__device__ double det_atan01(double r)
+{
+    int i = (int)(r * 8.0 + 0.5);
+    double c = (double)i * 0.125;
+    double z = (r - c) / (1.0 + r * c);
+    double z2 = z * z;
+    double p = 1.0 / 17.0;
+    p = p * z2 - 1.0 / 15.0;
+    p = p * z2 + 1.0 / 13.0;
+    p = p * z2 - 1.0 / 11.0;
+    p = p * z2 + 1.0 / 9.0;
+    p = p * z2 - 1.0 / 7.0;
+    p = p * z2 + 1.0 / 5.0;
+    p = p * z2 - 1.0 / 3.0;
+    double az = z + z * (z2 * p);
+    return c_atan_hi[i] + (az + c_atan_lo[i]);
+}
+
+__device__ double det_atan2(double y, double x)
+{
+    const double PI_HI = 3.141592653589793, PI_LO = 1.2246467991473532e-16;
+    const double PIO2_HI = 1.5707963267948966, PIO2_LO = 6.123233995736766e-17;
+    double ax = fabs(x), ay = fabs(y), t;
+    if (ay == 0.0 && ax == 0.0) {
+        t = sgnbit(x) ? PI_HI : 0.0;
+    } else if (ay > ax) {
+        double b = det_atan01(ax / ay);
+        t = sgnbit(x) ? (PIO2_HI + b) + PIO2_LO : (PIO2_HI - b) + PIO2_LO;
+    } else {
+        double b = det_atan01(ay / ax);
+        t = sgnbit(x) ? (PI_HI - b) + PI_LO : b;
+    }
+    if (sgnbit(y)) t = -t;
+    return t;
+}
+
+__device__ void det_sincos(double x, double* s_out, double* c_out)
+{
+    const double PIO2_1 = 1.570796325802803, PIO2_2 = 9.920935791635221e-10,
+                 PIO2_3 = 5.170182981794105e-19, TWO_OVER_PI = 0.6366197723675814;
+    double kf = floor(x * TWO_OVER_PI + 0.5);
+    int k = (int)kf;
+    double r = ((x - kf * PIO2_1) - kf * PIO2_2) - kf * PIO2_3;
+    double r2 = r * r;
+    double ps = -1.0 / 355687428096000.0;
+    ps = ps * r2 + 1.0 / 1307674368000.0;
+    ps = ps * r2 - 1.0 / 6227020800.0;
+    ps = ps * r2 + 1.0 / 39916800.0;
+    ps = ps * r2 - 1.0 / 362880.0;
+    ps = ps * r2 + 1.0 / 5040.0;
+    ps = ps * r2 - 1.0 / 120.0;
+    ps = ps * r2 + 1.0 / 6.0;
+    double sr = r - r * (r2 * ps);
+    double pc = 1.0 / 6402373705728000.0;
+    pc = pc * r2 - 1.0 / 20922789888000.0;
+    pc = pc * r2 + 1.0 / 87178291200.0;
+    pc = pc * r2 - 1.0 / 479001600.0;
+    pc = pc * r2 + 1.0 / 3628800.0;
+    pc = pc * r2 - 1.0 / 40320.0;
+    pc = pc * r2 + 1.0 / 720.0;
+    pc = pc * r2 - 1.0 / 24.0;
+    pc = pc * r2 + 0.5;
+    double cr = 1.0 - r2 * pc;
+    switch (k & 3) {
+    case 0: *s_out = sr;  *c_out = cr;  break;
+    case 1: *s_out = cr;  *c_out = -sr; break;
+    case 2: *s_out = -sr; *c_out = -cr; break;
+    default: *s_out = -cr; *c_out = sr; break;
+    }
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+// voo_sample8: Floyd's algorithm + insertion sort (oracle/vo_oracle.c).
+__device__ void sample8(uint64_t seed, int k, int m, int out[8])
+{
+    uint64_t st = mix64(seed ^ (0x9E3779B97F4A7C15ULL * (uint64_t)(k + 1)));
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        int j = m - 8 + c;
+        st += 0x9E3779B97F4A7C15ULL;
+        uint64_t r = mix64(st);
+        int t = (int)__umul64hi(r, (uint64_t)(j + 1));
+        bool present = false;
+#pragma unroll
+        for (int i = 0; i < c; ++i) present |= (out[i] == t);
+        out[c] = present ? j : t;
+    }
+    // insertion sort with static indices (sorting network of adjacent swaps, same result)
+#pragma unroll
+    for (int i = 1; i < 8; ++i) {
+#pragma unroll
+        for (int j = i; j > 0; --j) {
+            int a = out[j - 1], b = out[j];
+            bool sw = a > b;
+            out[j - 1] = sw ? b : a;
+            out[j] = sw ? a : b;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// small dense linear algebra (mirror of oracle/vo_oracle.c)
+// ---------------------------------------------------------------------------
+template <int n>
+__device__ void jacobi_eig(double* A, double* V)
+{
+    for (int i = 0; i < n * n; ++i) V[i] = 0.0;
+    for (int i = 0; i < n; ++i) V[i * n + i] = 1.0;
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        double off = 0.0, dia = 0.0;
+#pragma unroll
+        for (int p = 0; p < n; ++p) {
+            dia = dia + A[p * n + p] * A[p * n + p];
+#pragma unroll
+            for (int q = p + 1; q < n; ++q) off = off + A[p * n + q] * A[p * n + q];
+        }
+        if (off == 0.0 || off <= 1e-30 * dia) break;
+#pragma unroll
+        for (int p = 0; p < n - 1; ++p) {
+#pragma unroll
+            for (int q = p + 1; q < n; ++q) {
+                double apq = A[p * n + q];
+                if (apq == 0.0) continue;
+                double app = A[p * n + p], aqq = A[q * n + q];
+                double theta = (aqq - app) / (2.0 * apq);
+                double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+                if (theta < 0.0) t = -t;
+                double c = 1.0 / sqrt(t * t + 1.0);
+                double s = t * c;
+                A[p * n + p] = app - t * apq;
+                A[q * n + q] = aqq + t * apq;
+                A[p * n + q] = 0.0;
+                A[q * n + p] = 0.0;
+#pragma unroll
+                for (int k = 0; k < n; ++k) {
+                    if (k == p || k == q) continue;
+                    double akp = A[k * n + p], akq = A[k * n + q];
+                    double nkp = c * akp - s * akq;
+                    double nkq = s * akp + c * akq;
+                    A[k * n + p] = nkp; A[p * n + k] = nkp;
+                    A[k * n + q] = nkq; A[q * n + k] = nkq;
+                }
+#pragma unroll
+                for (int k = 0; k < n; ++k) {
+                    double vkp = V[k * n + p], vkq = V[k * n + q];
+                    V[k * n + p] = c * vkp - s * vkq;
+                    V[k * n + q] = s * vkp + c * vkq;
+                }
+            }
+        }
+    }
+}
+
+template <int n>
+__device__ __forceinline__ int argmin_diag(const double* A)
+{
+    int b = 0;
+#pragma unroll
+    for (int i = 1; i < n; ++i)
+        if (A[i * n + i] < A[b * n + b]) b = i;
+    return b;
+}
+
+__device__ __forceinline__ void mm3(const double* A, const double* B, double* C)
+{
+    double T[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            T[i * 3 + j] = (A[i * 3 + 0] * B[0 * 3 + j] + A[i * 3 + 1] * B[1 * 3 + j]) + A[i * 3 + 2] * B[2 * 3 + j];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) C[i] = T[i];
+}
+__device__ __forceinline__ void mtm3(const double* A, const double* B, double* C)
+{
+    double T[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            T[i * 3 + j] = (A[0 * 3 + i] * B[0 * 3 + j] + A[1 * 3 + i] * B[1 * 3 + j]) + A[2 * 3 + i] * B[2 * 3 + j];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) C[i] = T[i];
+}
+__device__ __forceinline__ double det3(const double* M)
+{
+    return (M[0] * (M[4] * M[8] - M[5] * M[7]) - M[1] * (M[3] * M[8] - M[5] * M[6])) +
+           M[2] * (M[3] * M[7] - M[4] * M[6]);
+}
+
+__device__ void rank2(double* F)
+{
+    double FtF[9], V[9];
+    mtm3(F, F, FtF);
+    jacobi_eig<3>(FtF, V);
+    int k = argmin_diag<3>(FtF);
+    double v0 = 0, v1 = 0, v2 = 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+        if (c == k) { v0 = V[0 * 3 + c]; v1 = V[1 * 3 + c]; v2 = V[2 * 3 + c]; }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        double fv = (F[i * 3 + 0] * v0 + F[i * 3 + 1] * v1) + F[i * 3 + 2] * v2;
+        F[i * 3 + 0] = F[i * 3 + 0] - fv * v0;
+        F[i * 3 + 1] = F[i * 3 + 1] - fv * v1;
+        F[i * 3 + 2] = F[i * 3 + 2] - fv * v2;
+    }
+}
+
+__device__ __forceinline__ void denormalize(const double* F0, double s1, double mx1, double my1,
+                                            double s2, double mx2, double my2, double* F)
+{
+    double T1[9] = {s1, 0.0, -(s1 * mx1), 0.0, s1, -(s1 * my1), 0.0, 0.0, 1.0};
+    double T2[9] = {s2, 0.0, -(s2 * mx2), 0.0, s2, -(s2 * my2), 0.0, 0.0, 1.0};
+    double G[9];
+    mtm3(T2, F0, G);
+    mm3(G, T1, F);
+}
+
+__device__ __forceinline__ void design_row(double p1x, double p1y, double p2x, double p2y, double* a)
+{
+    a[0] = p1x * p2x; a[1] = p1x * p2y; a[2] = p1x;
+    a[3] = p1y * p2x; a[4] = p1y * p2y; a[5] = p1y;
+    a[6] = p2x; a[7] = p2y; a[8] = 1.0;
+}
+
+// computeSampsonError, ransac.cpp:12-23 (mirror of voo_sampson)
+__device__ __forceinline__ double sampson(const double* F, double x, double y, double xp, double yp)
+{
+    double Fx0 = (F[0] * x + F[1] * y) + F[2] * 1.0;
+    double Fx1 = (F[3] * x + F[4] * y) + F[5] * 1.0;
+    double Ft0 = (F[0] * xp + F[3] * yp) + F[6] * 1.0;
+    double Ft1 = (F[1] * xp + F[4] * yp) + F[7] * 1.0;
+    double Ft2 = (F[2] * xp + F[5] * yp) + F[8] * 1.0;
+    double v = (Ft0 * x + Ft1 * y) + Ft2 * 1.0;
+    double num = v * v;
+    double den = ((Fx0 * Fx0 + Fx1 * Fx1) + Ft0 * Ft0) + Ft1 * Ft1;
+    if (den < 1e-12) return 1.7976931348623157e308;
+    return num / den;
+}
+
+__device__ __forceinline__ unsigned long long ballot64(bool p) { return __ballot(p); }
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// ---------------------------------------------------------------------------
+// frame begin: reset per-frame counters (1 block)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_frame_begin(VoDev d, int mode)
+{
+    VoState* st = d.st;
+    for (int i = threadIdx.x; i < VO_HIST_BINS; i += blockDim.x) d.hist[i] = 0;
+    if (threadIdx.x == 0) {
+        st->mode = mode;
+        st->cand_count = 0;
+        st->M = 0;
+        st->n_inl = 0;
+        st->fitted = 0;
+        st->degenerate = 0;
+        st->bestk = -1;
+        st->n_eval = 0;
+        st->need_more = 0;
+        for (int c = 0; c < 4; ++c) st->counts4[c] = 0;
+        if (mode == VO_MODE_FRAME) {
+            st->status = st->frame == 0 ? VO_STATUS_FIRST : VO_STATUS_OK;
+            st->cur = st->frame == 0 ? 0 : 1 - st->prev;
+            st->frame_seed = mix64(d.seed + 0x632BE59BD9B4E019ULL * (uint64_t)(st->frame + 1));
+        } else if (mode == VO_MODE_MISSING) {
+            st->status = VO_STATUS_MISSING;
+        } else if (mode == VO_MODE_EXTRACT) {
+            st->status = VO_STATUS_OK;
+            st->cur = 0;
+        } else {
+            st->status = VO_STATUS_OK;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// stencil: blur7x7 -> gradients -> 5x5 response -> strict 3x3 NMS candidates
+// One 256-thread workgroup per 64x16 output tile; every intermediate lives in LDS.
+// kernels/feature_extraction_kernel_functions.c:43-120, corner_detection_parallel_GPU.cpp:146-180
+// ---------------------------------------------------------------------------
+#define ST_TW 64
+#define ST_TH 16
+#define ST_SW (ST_TW + 14)   // source tile (blur radius 3 + gradient 1 + window 2 + nms 1)
+#define ST_SH (ST_TH + 14)
+#define ST_BW (ST_TW + 8)    // blurred tile
+#define ST_BH (ST_TH + 8)
+#define ST_GW (ST_TW + 6)    // gradient tile
+#define ST_GH (ST_TH + 6)
+#define ST_RW (ST_TW + 2)    // response tile
+#define ST_RH (ST_TH + 2)
+
+__device__ __forceinline__ int refl101(int i, int n)
+{
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
+    return i;
+}
+
+__global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restrict__ img, int write_response)
+{
+    if (d.st->status != VO_STATUS_OK && d.st->status != VO_STATUS_FIRST) return;
+    __shared__ uint8_t s_src[ST_SH][ST_SW];
+    __shared__ uint32_t s_hb[ST_SH][ST_BW];
+    __shared__ float s_bl[ST_BH][ST_BW];
+    __shared__ float s_jx[ST_GH][ST_GW], s_jy[ST_GH][ST_GW], s_jxy[ST_GH][ST_GW];
+    __shared__ float s_r[ST_RH][ST_RW];
+    __shared__ uint64_t s_keys[ST_TW * ST_TH / 4];
+    __shared__ int s_nk, s_base;
+
+    const int W = d.W, H = d.H;
+    const int x0 = blockIdx.x * ST_TW, y0 = blockIdx.y * ST_TH;
+    const int tid = threadIdx.x;
+    if (tid == 0) s_nk = 0;
+
+    // 1. source tile with BORDER_REFLECT_101 addressing
+    for (int e = tid; e < ST_SH * ST_SW; e += 256) {
+        int r = e / ST_SW, c = e - r * ST_SW;
+        int y = refl101(y0 - 7 + r, H), x = refl101(x0 - 7 + c, W);
+        s_src[r][c] = img[(size_t)y * W + x];
+    }
+    __syncthreads();
+    // 2. horizontal 7-tap (exact u32)
+    for (int e = tid; e < ST_SH * ST_BW; e += 256) {
+        int r = e / ST_BW, c = e - r * ST_BW;
+        const uint8_t* s = &s_src[r][c];
+        uint32_t h = 8u * s[0] + 28u * s[1] + 56u * s[2] + 72u * s[3] + 56u * s[4] + 28u * s[5] + 8u * s[6];
+        s_hb[r][c] = h;
+    }
+    __syncthreads();
+    // 3. vertical 7-tap, round, u8 (cv::GaussianBlur 8U fixed point); blurred -> HBM
+    for (int e = tid; e < ST_BH * ST_BW; e += 256) {
+        int r = e / ST_BW, c = e - r * ST_BW;
+        uint32_t v = 8u * s_hb[r][c] + 28u * s_hb[r + 1][c] + 56u * s_hb[r + 2][c] + 72u * s_hb[r + 3][c] +
+                     56u * s_hb[r + 4][c] + 28u * s_hb[r + 5][c] + 8u * s_hb[r + 6][c];
+        uint32_t b = (v + 32768u) >> 16;
+        s_bl[r][c] = (float)b;
+        int y = y0 - 4 + r, x = x0 - 4 + c;
+        if (r >= 4 && r < 4 + ST_TH && c >= 4 && c < 4 + ST_TW && y < H && x < W)
+            d.blurred[(size_t)y * W + x] = (uint8_t)b;
+    }
+    __syncthreads();
+    // 4. gradients (kernel .c:59-76), 0 outside 1<=i<=H-2, 1<=j<=W-2
+    for (int e = tid; e < ST_GH * ST_GW; e += 256) {
+        int r = e / ST_GW, c = e - r * ST_GW;
+        int y = y0 - 3 + r, x = x0 - 3 + c;
+        float jx = 0.f, jy = 0.f, jxy = 0.f;
+        if (y >= 1 && y <= H - 2 && x >= 1 && x <= W - 2) {
+            float sx[3], sy[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                float a = s_bl[r][c + k], m = s_bl[r + 1][c + k], cc = s_bl[r + 2][c + k];
+                sx[k] = a - cc;
+                sy[k] = (a + 2.0f * m) + cc;
+            }
+            jx = (sx[0] + 2.0f * sx[1]) + sx[2];
+            jy = sy[0] - sy[2];
+            jxy = sx[0] - sx[2];
+        }
+        s_jx[r][c] = jx; s_jy[r][c] = jy; s_jxy[r][c] = jxy;
+    }
+    __syncthreads();
+    // 5. response (kernel .c:97-114), m-outer n-inner f32 accumulation; 0 outside 2<=i<=H-3
+    const float thr = d.resp_thr;
+    for (int e = tid; e < ST_RH * ST_RW; e += 256) {
+        int r = e / ST_RW, c = e - r * ST_RW;
+        int y = y0 - 1 + r, x = x0 - 1 + c;
+        float out = 0.0f;
+        if (y >= 2 && y <= H - 3 && x >= 2 && x <= W - 3) {
+            float jx2 = 0.0f, jy2 = 0.0f, s = 0.0f;
+#pragma unroll
+            for (int m = 0; m < 5; ++m)
+#pragma unroll
+                for (int n = 0; n < 5; ++n) {
+                    float jx = s_jx[r + m][c + n], jy = s_jy[r + m][c + n], jxy = s_jxy[r + m][c + n];
+                    s = s + jxy;
+                    jx2 = jx2 + jx * jx;
+                    jy2 = jy2 + jy * jy;
+                }
+            float det = (jx2 * jy2) - (s * s);
+            float tr = jx2 + jy2;
+            float rv = (tr / 2.0f) - (0.5f * sqrtf(tr * tr - 4.0f * det));
+            out = rv > thr ? rv : 0.0f;
+        }
+        s_r[r][c] = out;
+        if (write_response && r >= 1 && r <= ST_TH && c >= 1 && c <= ST_TW && y < H && x < W)
+            d.response[(size_t)y * W + x] = out;
+    }
+    __syncthreads();
+    // 6. strict 3x3 NMS inside the retinal margin (corner_detection_parallel_GPU.cpp:152-180)
+    const int hk = d.nms_k / 2;
+    for (int e = tid; e < ST_TH * ST_TW; e += 256) {
+        int r = e / ST_TW, c = e - r * ST_TW;
+        int i = y0 + r, j = x0 + c;
+        if (i >= H || j >= W) continue;
+        if (i < hk || i >= H - hk || j < hk || j >= W - hk) continue;
+        if (!((j >= d.bcol) && (j <= W - d.bcol) && (i >= d.brow) && (i <= H - d.brow))) continue;
+        float cv = s_r[r + 1][c + 1];
+        bool mx = true;
+#pragma unroll
+        for (int a = -1; a <= 1; ++a)
+#pragma unroll
+            for (int b = -1; b <= 1; ++b)
+                if ((a | b) != 0 && s_r[r + 1 + a][c + 1 + b] >= cv) mx = false;
+        if (mx) {
+            uint32_t bits = __float_as_uint(cv);
+            uint64_t key = ((uint64_t)bits << 32) | ((uint64_t)i << 16) | (uint64_t)j;
+            int slot = atomicAdd(&s_nk, 1);
+            s_keys[slot] = key;
+            uint32_t bin = (bits - d.thr_bits) >> 15;
+            if (bin > VO_HIST_BINS - 1) bin = VO_HIST_BINS - 1;
+            atomicAdd(&d.hist[bin], 1u);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) s_base = s_nk ? (int)atomicAdd(&d.st->cand_count, (uint32_t)s_nk) : 0;
+    __syncthreads();
+    for (int e = tid; e < s_nk; e += 256) {
+        uint32_t pos = (uint32_t)s_base + e;
+        if (pos < d.cand_cap) d.cand[pos] = s_keys[e];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// select: exact top-N of the candidate keys + raster sort (1 workgroup of 1024)
+// Equivalent to popping N times from std::priority_queue<tuple<float,int,int>>
+// (corner_detection_parallel_GPU.cpp:147,182-186) then std::sort by (row, col)
+// (feature_extraction_parallel_GPU.cpp:259-265).
+// ---------------------------------------------------------------------------
+#define SEL_MAX 4096
+#define BND_CAP 4096
+
+template <typename T, bool ASC>
+__device__ void bitonic_lds(T* a, int n_pow2)
+{
+    for (int k = 2; k <= n_pow2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n_pow2; i += blockDim.x) {
+                int ixj = i ^ j;
+                if (ixj > i) {
+                    T x = a[i], y = a[ixj];
+                    bool up = ((i & k) == 0) == ASC;
+                    if ((x > y) == up) { a[i] = y; a[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_select(VoDev d)
+{
+    VoState* st = d.st;
+    if (st->status != VO_STATUS_OK && st->status != VO_STATUS_FIRST) return;
+    __shared__ uint32_t s_sel[SEL_MAX];
+    __shared__ uint64_t s_bnd[BND_CAP];
+    __shared__ uint32_t s_tot[1024];
+    __shared__ int s_nsel, s_nbnd, s_b, s_above;
+    const int tid = threadIdx.x;
+    const int N = d.N;
+    uint32_t C = st->cand_count;
+    if (C > d.cand_cap) C = d.cand_cap;
+    int nout;
+    if (tid == 0) { s_nsel = 0; s_nbnd = 0; s_b = -1; s_above = 0; }
+    __syncthreads();
+    if ((int)C <= N) {
+        for (uint32_t e = tid; e < C; e += 1024) {
+            uint64_t key = d.cand[e];
+            s_sel[e] = (uint32_t)key;               // row<<16 | col
+        }
+        nout = (int)C;
+    } else {
+        // boundary bin from the stencil's histogram
+        uint32_t h0 = d.hist[4 * tid], h1 = d.hist[4 * tid + 1], h2 = d.hist[4 * tid + 2], h3 = d.hist[4 * tid + 3];
+        s_tot[tid] = h0 + h1 + h2 + h3;
+        __syncthreads();
+        // suffix sums (Hillis-Steele over 1024 entries, from the top bins down)
+        for (int off = 1; off < 1024; off <<= 1) {
+            uint32_t v = (tid + off < 1024) ? s_tot[tid + off] : 0u;
+            __syncthreads();
+            s_tot[tid] += v;
+            __syncthreads();
+        }
+        uint32_t above = (tid + 1 < 1024) ? s_tot[tid + 1] : 0u;   // bins > 4*tid+3
+        uint32_t hb[4] = {h0, h1, h2, h3};
+        uint32_t run = above;
+        for (int q = 3; q >= 0; --q) {
+            if (run < (uint32_t)N && run + hb[q] >= (uint32_t)N) { s_b = 4 * tid + q; s_above = (int)run; }
+            run += hb[q];
+        }
+        __syncthreads();
+        const int b = s_b;
+        for (uint32_t e = tid; e < C; e += 1024) {
+            uint64_t key = d.cand[e];
+            uint32_t bits = (uint32_t)(key >> 32);
+            uint32_t bin = (bits - d.thr_bits) >> 15;
+            if (bin > VO_HIST_BINS - 1) bin = VO_HIST_BINS - 1;
+            if ((int)bin > b) {
+                int p = atomicAdd(&s_nsel, 1);
+                s_sel[p] = (uint32_t)key;
+            } else if ((int)bin == b) {
+                int p = atomicAdd(&s_nbnd, 1);
+                if (p < BND_CAP) s_bnd[p] = key;
+            }
+        }
+        __syncthreads();
+        int nb = s_nbnd;
+        if (nb > BND_CAP) {
+            // boundary bin too large for LDS: flag (never observed)
+            if (tid == 0) st->status = VO_STATUS_OVERFLOW;
+            return;
+        }
+        int p2 = 1;
+        while (p2 < nb) p2 <<= 1;
+        for (int e = nb + tid; e < p2; e += 1024) s_bnd[e] = 0ull;
+        __syncthreads();
+        bitonic_lds<uint64_t, false>(s_bnd, p2);
+        const int need = N - s_above;
+        for (int e = tid; e < need; e += 1024) s_sel[s_above + e] = (uint32_t)s_bnd[e];
+        nout = N;
+    }
+    __syncthreads();
+    int p2 = 1;
+    while (p2 < nout) p2 <<= 1;
+    for (int e = nout + tid; e < p2; e += 1024) s_sel[e] = 0xFFFFFFFFu;
+    __syncthreads();
+    bitonic_lds<uint32_t, true>(s_sel, p2);
+    const int cur = st->cur;
+    int2* kp = d.kps[cur];
+    for (int e = tid; e < nout; e += 1024) {
+        uint32_t v = s_sel[e];
+        kp[e] = make_int2((int)(v & 0xFFFF), (int)(v >> 16));
+    }
+    if (tid == 0) st->n_kps[cur] = nout;
+}
+
+// ---------------------------------------------------------------------------
+// describe: orientation (903-term sequential f32 sums) + rotation + 512 tests
+// 8 keypoints per 256-thread workgroup.  FREAK_feature_descriptor_parallel_GPU.cpp:10-210,
+// kernels .c:124-225, orientation order FREAK_feature_descriptor_parallel.cpp:16-44.
+// ---------------------------------------------------------------------------
+#define DS_KPB 8
+#define DS_TSTRIDE 905
+
+__global__ void __launch_bounds__(256) k_describe(VoDev d)
+{
+    VoState* st = d.st;
+    if (st->status != VO_STATUS_OK && st->status != VO_STATUS_FIRST) return;
+    const int cur = st->cur;
+    const int n = st->n_kps[cur];
+    const int base = blockIdx.x * DS_KPB;
+    if (base >= n) return;
+    const int nk = min(DS_KPB, n - base);
+    __shared__ float s_I0[DS_KPB][VO_FREAK_NPOINTS];
+    __shared__ float s_term[DS_KPB * 2][DS_TSTRIDE];
+    __shared__ float s_O[DS_KPB][2];
+    __shared__ float s_cs[DS_KPB][2];
+    __shared__ uint8_t s_I1[DS_KPB][48];
+    const int tid = threadIdx.x;
+    const int W = d.W, H = d.H;
+    const uint8_t* img = d.blurred;
+    const int2* kps = d.kps[cur] + base;
+
+    for (int e = tid; e < nk * VO_FREAK_NPOINTS; e += 256) {
+        int k = e / VO_FREAK_NPOINTS, p = e - k * VO_FREAK_NPOINTS;
+        int2 kp = kps[k];
+        s_I0[k][p] = (float)img[(size_t)(kp.y + c_pt_y[p]) * W + (kp.x + c_pt_x[p])];
+    }
+    __syncthreads();
+    for (int e = tid; e < nk * VO_FREAK_NPAIRS; e += 256) {
+        int k = e / VO_FREAK_NPAIRS, t = e - k * VO_FREAK_NPAIRS;
+        int p = c_pair_p[t], q = c_pair_q[t];
+        float ic = s_I0[k][p] - s_I0[k][q];
+        float dx = (float)(c_pt_x[p] - c_pt_x[q]), dy = (float)(c_pt_y[p] - c_pt_y[q]);
+        float nrm = sqrtf(dx * dx + dy * dy);
+        s_term[2 * k][t] = (ic * dx) / nrm;
+        s_term[2 * k + 1][t] = (ic * dy) / nrm;
+    }
+    __syncthreads();
+    if (tid < 2 * nk) {
+        const float* row = s_term[tid];
+        float acc = 0.0f;
+        for (int t = 0; t < VO_FREAK_NPAIRS; ++t) acc = acc + row[t];
+        s_O[tid >> 1][tid & 1] = acc;
+    }
+    __syncthreads();
+    if (tid < nk) {
+        float Ox = s_O[tid][0], Oy = s_O[tid][1];
+        float angle = 0.0f;
+        if (!(isnan(Ox) || isnan(Oy))) angle = (float)det_atan2((double)Oy, (double)Ox);
+        double sd, cd;
+        det_sincos((double)angle, &sd, &cd);
+        s_cs[tid][0] = (float)cd;
+        s_cs[tid][1] = (float)sd;
+    }
+    __syncthreads();
+    for (int e = tid; e < nk * VO_FREAK_NPOINTS; e += 256) {
+        int k = e / VO_FREAK_NPOINTS, p = e - k * VO_FREAK_NPOINTS;
+        int2 kp = kps[k];
+        float c = s_cs[k][0], s = s_cs[k][1];
+        float ms = -1.0f * s;
+        int px = c_pt_x[p], py = c_pt_y[p];
+        int x = (int)(((float)kp.x + (float)px * c) + (float)py * s);
+        int y = (int)(((float)kp.y + (float)(-1 * px) * ms) + (float)py * c);
+        x = min(max(x, 0), W - 1);   // in range for every keypoint inside the margin
+        y = min(max(y, 0), H - 1);
+        s_I1[k][p] = img[(size_t)y * W + x];
+    }
+    __syncthreads();
+    const int wave = tid >> 6, lane = tid & 63;
+    for (int it = wave; it < nk * 8; it += 4) {
+        int k = it >> 3, w = it & 7;
+        int t = w * 64 + lane;
+        int e = c_patch[t];
+        bool bit = s_I1[k][c_pair_p[e]] > s_I1[k][c_pair_q[e]];
+        unsigned long long word = ballot64(bit);
+        if (lane == 0) {
+            d.desc[cur][(size_t)(base + k) * 8 + w] = word;
+            if (w == 0) d.pre[cur][base + k] = (uint32_t)word;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// match: brute-force Hamming top-2 + Lowe ratio, one query per wave
+// feature_matching_parallel.cpp:39-113; key = dist<<16 | j so min key = (min dist, first j)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_match(VoDev d)
+{
+    VoState* st = d.st;
+    if (st->status != VO_STATUS_OK) return;
+    const int prev = st->prev, cur = st->cur;
+    const int n1 = st->n_kps[prev], n2 = st->n_kps[cur];
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (q >= n1) return;
+    uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
+    if (d.match_bits == 32) {
+        const uint32_t qv = d.pre[prev][q];
+        const uint32_t* cand = d.pre[cur];
+        for (int j = lane; j < n2; j += 64) {
+            uint32_t key = ((uint32_t)__popc(qv ^ cand[j]) << 16) | (uint32_t)j;
+            if (key < m1) { m2 = m1; m1 = key; } else if (key < m2) m2 = key;
+        }
+    } else {
+        const uint64_t* qd = d.desc[prev] + (size_t)q * 8;
+        uint64_t qw[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) qw[w] = qd[w];
+        const uint64_t* cd = d.desc[cur];
+        for (int j = lane; j < n2; j += 64) {
+            int dist = 0;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) dist += __popcll(qw[w] ^ cd[(size_t)j * 8 + w]);
+            uint32_t key = ((uint32_t)dist << 16) | (uint32_t)j;
+            if (key < m1) { m2 = m1; m1 = key; } else if (key < m2) m2 = key;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        uint32_t o1 = __shfl_xor(m1, off), o2 = __shfl_xor(m2, off);
+        uint32_t n1v = min(m1, o1);
+        uint32_t n2v = min(max(m1, o1), min(m2, o2));
+        m1 = n1v; m2 = n2v;
+    }
+    if (lane == 0) {
+        int res = -1;
+        if (m1 != 0xFFFFFFFFu && m2 != 0xFFFFFFFFu) {
+            int d1 = (int)(m1 >> 16), d2 = (int)(m2 >> 16);
+            if ((float)d1 < d.ratio * (float)d2) res = (int)(m1 & 0xFFFF);
+        }
+        d.match_j[q] = res;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// compact: ordered stream compaction of accepted queries -> matches + f64 points
+// (VisualOdometry.cpp:100-123); 1 workgroup of 1024
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_compact(VoDev d)
+{
+    VoState* st = d.st;
+    if (st->status != VO_STATUS_OK) return;
+    __shared__ int s_wsum[16];
+    __shared__ int s_base;
+    const int prev = st->prev, cur = st->cur;
+    const int n1 = st->n_kps[prev];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int2* kp1 = d.kps[prev];
+    const int2* kp2 = d.kps[cur];
+    if (tid == 0) s_base = 0;
+    __syncthreads();
+    for (int b0 = 0; b0 < n1; b0 += 1024) {
+        int i = b0 + tid;
+        int j = i < n1 ? d.match_j[i] : -1;
+        bool f = j >= 0;
+        unsigned long long bal = ballot64(f);
+        int pre = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) s_wsum[wave] = __popcll(bal);
+        __syncthreads();
+        int woff = 0;
+        for (int w = 0; w < wave; ++w) woff += s_wsum[w];
+        int pos = s_base + woff + pre;
+        if (f) {
+            d.match_pairs[pos] = make_int2(i, j);
+            int2 a = kp1[i], b = kp2[j];
+            double* p = d.pts + 4 * (size_t)pos;
+            p[0] = (double)a.x; p[1] = (double)a.y; p[2] = (double)b.x; p[3] = (double)b.y;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int tot = 0;
+            for (int w = 0; w < 16; ++w) tot += s_wsum[w];
+            s_base += tot;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        int M = s_base;
+        st->M = M;
+        st->scored = (M / d.T) * d.T;
+        if (M < 8) st->status = VO_STATUS_FEW_MATCHES;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// RANSAC hypotheses: one hypothesis per wavefront (Ransac::run, ransac.cpp:138-176)
+// lanes 0..7 hold the 8 design-matrix rows for the Gauss-Jordan null vector; all
+// 64 lanes then score the Sampson error over the scored matches, counted by ballot.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double shfl_d(double v, int src) { return __shfl(v, src); }
+__device__ __forceinline__ double shfl_xor_d(double v, int m) { return __shfl_xor(v, m); }
+
+__device__ void fit_F8_wave(const double* __restrict__ pts, const int s8[8], int lane, double F[9])
+{
+    double P[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double* p = pts + 4 * (size_t)s8[i];
+        P[i][0] = p[0]; P[i][1] = p[1]; P[i][2] = p[2]; P[i][3] = p[3];
+    }
+    double mx1 = 0, my1 = 0, mx2 = 0, my2 = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { mx1 = mx1 + P[i][0]; my1 = my1 + P[i][1]; mx2 = mx2 + P[i][2]; my2 = my2 + P[i][3]; }
+    mx1 = mx1 / 8.0; my1 = my1 / 8.0; mx2 = mx2 / 8.0; my2 = my2 / 8.0;
+    double sc1 = 0, sc2 = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        double a = P[i][0] - mx1, b = P[i][1] - my1, c = P[i][2] - mx2, e = P[i][3] - my2;
+        sc1 = sc1 + (a * a + b * b);
+        sc2 = sc2 + (c * c + e * e);
+    }
+    sc1 = sqrt(2.0) / sqrt(sc1 / 8.0);
+    sc2 = sqrt(2.0) / sqrt(sc2 / 8.0);
+    double o1x = -(sc1 * mx1), o1y = -(sc1 * my1), o2x = -(sc2 * mx2), o2y = -(sc2 * my2);
+    // my row
+    double x1 = 0, y1 = 0, x2 = 0, y2 = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if (i == lane) { x1 = P[i][0]; y1 = P[i][1]; x2 = P[i][2]; y2 = P[i][3]; }
+    double a[9];
+    design_row(sc1 * x1 + o1x, sc1 * y1 + o1y, sc2 * x2 + o2x, sc2 * y2 + o2y, a);
+    const bool row_lane = lane < 8;
+    uint32_t used_c = 0, used_r = 0;
+    int prs[8], pcs[8];
+    int steps = 0;
+#pragma unroll
+    for (int step = 0; step < 8; ++step) {
+        double bv = 0.0; int bc = -1;
+        if (row_lane && !((used_r >> lane) & 1u)) {
+#pragma unroll
+            for (int c = 0; c < 9; ++c)
+                if (!((used_c >> c) & 1u)) { double v = fabs(a[c]); if (v > bv) { bv = v; bc = c; } }
+        }
+        int br = bc >= 0 ? lane : 64;
+        if (bc < 0) bv = 0.0;
+#pragma unroll
+        for (int off = 1; off <= 4; off <<= 1) {
+            double ov = shfl_xor_d(bv, off);
+            int orr = __shfl_xor(br, off), oc = __shfl_xor(bc, off);
+            if (ov > bv || (ov == bv && orr < br)) { bv = ov; br = orr; bc = oc; }
+        }
+        bv = shfl_d(bv, 0); br = __shfl(br, 0); bc = __shfl(bc, 0);
+        if (!(bv > 0.0)) break;
+        used_r |= 1u << br; used_c |= 1u << bc;
+        prs[step] = br; pcs[step] = bc; steps = step + 1;
+        double prow[9];
+#pragma unroll
+        for (int c = 0; c < 9; ++c) prow[c] = shfl_d(a[c], br);
+        double piv = 0.0, mine = 0.0;
+#pragma unroll
+        for (int c = 0; c < 9; ++c) if (c == bc) { piv = prow[c]; mine = a[c]; }
+        if (row_lane && lane != br) {
+            double fct = mine / piv;
+#pragma unroll
+            for (int c = 0; c < 9; ++c) a[c] = a[c] - fct * prow[c];
+        }
+    }
+    int fc = 0;
+#pragma unroll
+    for (int c = 8; c >= 0; --c) if (!((used_c >> c) & 1u)) fc = c;
+    double f[9];
+#pragma unroll
+    for (int c = 0; c < 9; ++c) f[c] = (c == fc) ? 1.0 : 0.0;
+    // my pivot column (if my row was a pivot row)
+    int mypc = -1;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) if (s < steps && prs[s] == lane) mypc = pcs[s];
+    double afc = 0.0, apc = 1.0;
+#pragma unroll
+    for (int c = 0; c < 9; ++c) { if (c == fc) afc = a[c]; if (c == mypc) apc = a[c]; }
+    double myval = -(afc / apc);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        if (s < steps) {
+            double v = shfl_d(myval, prs[s]);
+#pragma unroll
+            for (int c = 0; c < 9; ++c) if (c == pcs[s]) f[c] = v;
+        }
+    }
+    double nn = 0.0;
+#pragma unroll
+    for (int c = 0; c < 9; ++c) nn = nn + f[c] * f[c];
+    nn = sqrt(nn);
+#pragma unroll
+    for (int c = 0; c < 9; ++c) f[c] = f[c] / nn;
+    denormalize(f, sc1, mx1, my1, sc2, mx2, my2, F);
+    rank2(F);
+}
+
+__global__ void __launch_bounds__(256) k_ransac_hyp(VoDev d, int k0, int k1)
+{
+    VoState* st = d.st;
+    if (st->status != VO_STATUS_OK) return;
+    if (k0 > 0 && !st->need_more) return;
+    const int k = k0 + blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (k >= k1) return;
+    const int lane = threadIdx.x & 63;
+    const int M = st->M, scored = st->scored;
+    int s8[8];
+    sample8(st->frame_seed, k, M, s8);
+    double F[9];
+    fit_F8_wave(d.pts, s8, lane, F);
+    if (lane < 9) {
+        double v = 0.0;
+#pragma unroll
+        for (int c = 0; c < 9; ++c) if (c == lane) v = F[c];
+        d.hypF[(size_t)k * 9 + lane] = v;
+    }
+    const double thr = d.sampson_thr;
+    int cnt = 0;
+    for (int b = 0; b < scored; b += 64) {
+        int i = b + lane;
+        bool in = false;
+        if (i < scored) {
+            const double2* p = reinterpret_cast<const double2*>(d.pts + 4 * (size_t)i);
+            double2 a = p[0], c = p[1];
+            in = sampson(F, a.x, a.y, c.x, c.y) < thr;
+        }
+        cnt += __popcll(ballot64(in));
+    }
+    if (lane == 0) d.counts[k] = cnt;
+}
+
+// sequential replay of the adaptive stopping rule over the per-hypothesis counts
+// (ransac.cpp:139-190): picks the same best hypothesis as the sequential loop.
+__global__ void k_ransac_replay(VoDev d, int k1)
+{
+    VoState* st = d.st;
+    if (threadIdx.x != 0 || st->status != VO_STATUS_OK) return;
+    int k, maxit, best, bestk;
+    if (k1 <= VO_HYP_CHUNK0 || !st->need_more) {
+        if (k1 > VO_HYP_CHUNK0) return;   // chunk 1 not needed: state is final
+        k = 0; maxit = d.maxit_initial; best = 0; bestk = -1;
+    } else {
+        k = st->k_done; maxit = st->maxit; best = st->best; bestk = st->bestk;
+    }
+    const int M = st->M;
+    const uint16_t* tab = d.maxit_tab + (size_t)M * (M + 1) / 2;
+    for (; k < maxit && k < k1; ++k) {
+        int c = d.counts[k];
+        if (c > best) {
+            best = c; bestk = k;
+            uint16_t u = tab[best];
+            if (u != 0xFFFFu) maxit = (int)u;
+        }
+    }
+    st->k_done = k; st->maxit = maxit; st->best = best; st->bestk = bestk;
+    st->need_more = (k < maxit) ? 1 : 0;
+    st->n_eval = k;
+}
+
+// ---------------------------------------------------------------------------
+// refit on the best hypothesis' inliers (model.fit(bestInlierSet), ransac.cpp:193)
+// one workgroup of 256; reductions in the fixed order mirrored by the oracle
+// ---------------------------------------------------------------------------
+__device__ double block_sum256(double v, double* s_w)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + shfl_xor_d(v, off);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) s_w[wave] = v;
+    __syncthreads();
+    return ((s_w[0] + s_w[1]) + s_w[2]) + s_w[3];
+}
+
+__global__ void __launch_bounds__(256) k_refit(VoDev d)
+{
+    VoState* st = d.st;
+    if (st->status != VO_STATUS_OK) return;
+    __shared__ double s_w[4];
+    __shared__ int s_wc[4];
+    __shared__ int s_base;
+    __shared__ double s_F[9];
+    __shared__ double s_A[81], s_V[81];
+    __shared__ double s_prm[6];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int bestk = st->bestk;
+    const int scored = st->scored;
+    if (bestk < 0) {
+        if (tid == 0) { st->n_inl = 0; st->fitted = 0; }
+        return;
+    }
+    if (tid < 9) s_F[tid] = d.hypF[(size_t)bestk * 9 + tid];
+    if (tid == 0) s_base = 0;
+    __syncthreads();
+    double F[9];
+#pragma unroll
+    for (int c = 0; c < 9; ++c) F[c] = s_F[c];
+    const double thr = d.sampson_thr;
+    for (int b0 = 0; b0 < scored; b0 += 256) {
+        int i = b0 + tid;
+        bool in = false;
+        if (i < scored) {
+            const double* p = d.pts + 4 * (size_t)i;
+            in = sampson(F, p[0], p[1], p[2], p[3]) < thr;
+        }
+        unsigned long long bal = ballot64(in);
+        if (lane == 0) s_wc[wave] = __popcll(bal);
+        __syncthreads();
+        int off = s_base;
+        for (int w = 0; w < wave; ++w) off += s_wc[w];
+        if (in) d.inl[off + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+        __syncthreads();
+        if (tid == 0) s_base += ((s_wc[0] + s_wc[1]) + s_wc[2]) + s_wc[3];
+        __syncthreads();
+    }
+    const int n = s_base;
+    if (tid == 0) st->n_inl = n;
+    if (n < 8) {                  // fit() returns early: previous model stays (quirk 9)
+        if (tid == 0) st->fitted = 0;
+        return;
+    }
+    const int32_t* idx = d.inl;
+    double mean[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        double s = 0.0;
+        for (int i = tid; i < n; i += 256) s = s + d.pts[4 * (size_t)idx[i] + c];
+        mean[c] = block_sum256(s, s_w) / (double)n;
+    }
+    double scl[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        double s = 0.0;
+        for (int i = tid; i < n; i += 256) {
+            const double* p = d.pts + 4 * (size_t)idx[i];
+            double a = p[2 * g] - mean[2 * g], b = p[2 * g + 1] - mean[2 * g + 1];
+            s = s + (a * a + b * b);
+        }
+        scl[g] = block_sum256(s, s_w);
+    }
+    const double sc1 = sqrt(2.0) / sqrt(scl[0] / (double)n);
+    const double sc2 = sqrt(2.0) / sqrt(scl[1] / (double)n);
+    const double o1x = -(sc1 * mean[0]), o1y = -(sc1 * mean[1]), o2x = -(sc2 * mean[2]), o2y = -(sc2 * mean[3]);
+    double acc[45];
+#pragma unroll
+    for (int e = 0; e < 45; ++e) acc[e] = 0.0;
+    for (int i = tid; i < n; i += 256) {
+        const double* p = d.pts + 4 * (size_t)idx[i];
+        double a[9];
+        design_row(sc1 * p[0] + o1x, sc1 * p[1] + o1y, sc2 * p[2] + o2x, sc2 * p[3] + o2y, a);
+        int e = 0;
+#pragma unroll
+        for (int u = 0; u < 9; ++u)
+#pragma unroll
+            for (int v = u; v < 9; ++v) { acc[e] = acc[e] + a[u] * a[v]; ++e; }
+    }
+    {
+        int e = 0;
+#pragma unroll
+        for (int u = 0; u < 9; ++u)
+#pragma unroll
+            for (int v = u; v < 9; ++v) {
+                double x = block_sum256(acc[e], s_w);
+                ++e;
+                if (tid == 0) { s_A[u * 9 + v] = x; s_A[v * 9 + u] = x; }
+            }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        jacobi_eig<9>(s_A, s_V);
+        int k = argmin_diag<9>(s_A);
+        double f[9];
+        for (int i = 0; i < 9; ++i) f[i] = s_V[i * 9 + k];
+        double Fn[9];
+        denormalize(f, sc1, mean[0], mean[1], sc2, mean[2], mean[3], Fn);
+        rank2(Fn);
+        for (int i = 0; i < 9; ++i) st->model_F[i] = Fn[i];
+        st->fitted = 1;
+        st->model_n = n;
+    }
+    for (int i = tid; i < n; i += 256) {
+        const double* p = d.pts + 4 * (size_t)idx[i];
+        float* o = d.model_p + 4 * (size_t)i;
+        o[0] = (float)p[0]; o[1] = (float)p[1]; o[2] = (float)p[2]; o[3] = (float)p[3];
+    }
+    (void)s_prm;
+}
+
+// ---------------------------------------------------------------------------
+// pose: E = K^T F K, SVD, candidates (PoseUpdate.hpp:61-96); 1 thread
+// ---------------------------------------------------------------------------
+__device__ void svd3(const double* A, double* U, double* S, double* Vt)
+{
+    double AtA[9], V[9];
+    mtm3(A, A, AtA);
+    jacobi_eig<3>(AtA, V);
+    int o0 = 0, o1 = 1, o2 = 2;
+    // stable insertion sort of {0,1,2} by eigenvalue descending (oracle svd3)
+    double e0 = AtA[0], e1 = AtA[4], e2 = AtA[8];
+    double ev[3] = {e0, e1, e2};
+    int o[3] = {o0, o1, o2};
+    for (int i = 1; i < 3; ++i) {
+        int v = o[i], j = i - 1;
+        while (j >= 0 && ev[o[j]] < ev[v]) { o[j + 1] = o[j]; --j; }
+        o[j + 1] = v;
+    }
+    double u[3][3];
+    for (int c = 0; c < 2; ++c) {
+        double v0 = V[0 * 3 + o[c]], v1 = V[1 * 3 + o[c]], v2 = V[2 * 3 + o[c]];
+        double a0 = (A[0] * v0 + A[1] * v1) + A[2] * v2;
+        double a1 = (A[3] * v0 + A[4] * v1) + A[5] * v2;
+        double a2 = (A[6] * v0 + A[7] * v1) + A[8] * v2;
+        double s = sqrt((a0 * a0 + a1 * a1) + a2 * a2);
+        S[c] = s;
+        if (s > 0.0) { u[c][0] = a0 / s; u[c][1] = a1 / s; u[c][2] = a2 / s; }
+        else { u[c][0] = c == 0 ? 1.0 : 0.0; u[c][1] = c == 1 ? 1.0 : 0.0; u[c][2] = 0.0; }
+    }
+    {
+        double v0 = V[0 * 3 + o[2]], v1 = V[1 * 3 + o[2]], v2 = V[2 * 3 + o[2]];
+        double a0 = (A[0] * v0 + A[1] * v1) + A[2] * v2;
+        double a1 = (A[3] * v0 + A[4] * v1) + A[5] * v2;
+        double a2 = (A[6] * v0 + A[7] * v1) + A[8] * v2;
+        S[2] = sqrt((a0 * a0 + a1 * a1) + a2 * a2);
+    }
+    u[2][0] = u[0][1] * u[1][2] - u[0][2] * u[1][1];
+    u[2][1] = u[0][2] * u[1][0] - u[0][0] * u[1][2];
+    u[2][2] = u[0][0] * u[1][1] - u[0][1] * u[1][0];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            U[r * 3 + c] = u[c][r];
+            Vt[c * 3 + r] = V[r * 3 + o[c]];
+        }
+}
+
+__global__ void k_pose_prep(VoDev d)
+{
+    VoState* st = d.st;
+    if (threadIdx.x != 0 || st->status != VO_STATUS_OK) return;
+    if (st->model_n < 8) { st->status = VO_STATUS_FEW_INLIERS; return; }
+    double E[9], G[9];
+    mtm3(d.K, st->model_F, G);
+    mm3(G, d.K, E);
+    double nn = 0.0;
+    for (int i = 0; i < 9; ++i) nn = nn + E[i] * E[i];
+    nn = sqrt(nn);
+    double inv = 1.0 / nn;
+    int nz = 0;
+    for (int i = 0; i < 9; ++i) { E[i] = E[i] * inv; nz += (E[i] != 0.0); }
+    if (nz < 5) { st->status = VO_STATUS_DEGENERATE; st->degenerate = 1; return; }
+    double U[9], S[3], Vt[9];
+    svd3(E, U, S, Vt);
+    if (det3(U) < 0) for (int i = 0; i < 9; ++i) U[i] = -U[i];
+    if (det3(Vt) < 0) for (int i = 0; i < 9; ++i) Vt[i] = -Vt[i];
+    const double W[9] = {0, -1, 0, 1, 0, 0, 0, 0, 1};
+    const double Wt[9] = {0, 1, 0, -1, 0, 0, 0, 0, 1};
+    double R1[9], R2[9], T[9];
+    mm3(U, W, T); mm3(T, Vt, R1);
+    mm3(U, Wt, T); mm3(T, Vt, R2);
+    if (det3(R1) < 0) for (int i = 0; i < 9; ++i) R1[i] = -R1[i];
+    if (det3(R2) < 0) for (int i = 0; i < 9; ++i) R2[i] = -R2[i];
+    for (int i = 0; i < 9; ++i) { st->R1[i] = R1[i]; st->R2[i] = R2[i]; }
+    st->t[0] = U[2]; st->t[1] = U[5]; st->t[2] = U[8];
+    for (int c = 0; c < 4; ++c) st->counts4[c] = 0;
+}
+
+// cheirality test of the 4 (R, t) candidates: one model inlier per thread
+// (cv::undistortPoints + cv::triangulatePoints + depth test, PoseUpdate.hpp:101-147)
+__global__ void __launch_bounds__(256) k_triangulate(VoDev d)
+{
+    VoState* st = d.st;
+    if (st->status != VO_STATUS_OK) return;
+    __shared__ int s_cnt[4];
+    const int n = st->model_n;
+    if (blockIdx.x * 256 >= n) return;
+    if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+        const double fx = d.K[0], fy = d.K[4], cx = d.K[2], cy = d.K[5];
+        const double ifx = 1.0 / fx, ify = 1.0 / fy;
+        const float* p = d.model_p + 4 * (size_t)i;
+        float x1 = (float)(((double)p[0] - cx) * ifx), y1 = (float)(((double)p[1] - cy) * ify);
+        float x2 = (float)(((double)p[2] - cx) * ifx), y2 = (float)(((double)p[3] - cy) * ify);
+        double X1 = x1, Y1 = y1, X2 = x2, Y2 = y2;
+        for (int cnd = 0; cnd < 4; ++cnd) {
+            const double* R = cnd < 2 ? st->R1 : st->R2;
+            double sg = (cnd & 1) ? -1.0 : 1.0;
+            double tc0 = st->t[0] * sg, tc1 = st->t[1] * sg, tc2 = st->t[2] * sg;
+            double P2[12] = {R[0], R[1], R[2], tc0, R[3], R[4], R[5], tc1, R[6], R[7], R[8], tc2};
+            const double P1[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+            double A[16];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                A[0 * 4 + k] = X1 * P1[8 + k] - P1[0 + k];
+                A[1 * 4 + k] = Y1 * P1[8 + k] - P1[4 + k];
+                A[2 * 4 + k] = X2 * P2[8 + k] - P2[0 + k];
+                A[3 * 4 + k] = Y2 * P2[8 + k] - P2[4 + k];
+            }
+            double AtA[16], V[16];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    AtA[a * 4 + b] = ((A[0 * 4 + a] * A[0 * 4 + b] + A[1 * 4 + a] * A[1 * 4 + b]) + A[2 * 4 + a] * A[2 * 4 + b]) +
+                                     A[3 * 4 + a] * A[3 * 4 + b];
+            jacobi_eig<4>(AtA, V);
+            int km = argmin_diag<4>(AtA);
+            double X[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (c == km) { X[0] = V[0 * 4 + c]; X[1] = V[1 * 4 + c]; X[2] = V[2 * 4 + c]; X[3] = V[3 * 4 + c]; }
+            double h0 = (double)(float)X[0], h1 = (double)(float)X[1], h2 = (double)(float)X[2], h3 = (double)(float)X[3];
+            double w = h3;
+            if (fabs(w) < 1e-6) continue;
+            double iw = 1.0 / w;
+            double Xh0 = h0 * iw, Xh1 = h1 * iw, Xh2 = h2 * iw;
+            double z1 = Xh2;
+            double z2 = ((R[6] * Xh0 + R[7] * Xh1) + R[8] * Xh2) + tc2;
+            if (z1 > 0 && z2 > 0) atomicAdd(&s_cnt[cnd], 1);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 4 && s_cnt[threadIdx.x]) atomicAdd(&st->counts4[threadIdx.x], s_cnt[threadIdx.x]);
+}
+
+// 4x4 helpers for the GT scale (mirror of oracle inv4 / mm4)
+__device__ void mm4(const double* A, const double* B, double* C)
+{
+    double T[16];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            T[i * 4 + j] = ((A[i * 4 + 0] * B[0 * 4 + j] + A[i * 4 + 1] * B[1 * 4 + j]) + A[i * 4 + 2] * B[2 * 4 + j]) +
+                           A[i * 4 + 3] * B[3 * 4 + j];
+    for (int i = 0; i < 16; ++i) C[i] = T[i];
+}
+__device__ void inv4(const double* M, double* Inv)
+{
+    double a[4][8];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 8; ++j) a[i][j] = j < 4 ? M[i * 4 + j] : (j - 4 == i ? 1.0 : 0.0);
+    for (int c = 0; c < 4; ++c) {
+        int p = c;
+        for (int r = c + 1; r < 4; ++r) if (fabs(a[r][c]) > fabs(a[p][c])) p = r;
+        if (p != c) for (int j = 0; j < 8; ++j) { double t = a[c][j]; a[c][j] = a[p][j]; a[p][j] = t; }
+        double pv = a[c][c];
+        for (int j = 0; j < 8; ++j) a[c][j] = a[c][j] / pv;
+        for (int r = 0; r < 4; ++r) {
+            if (r == c) continue;
+            double f = a[r][c];
+            for (int j = 0; j < 8; ++j) a[r][j] = a[r][j] - f * a[c][j];
+        }
+    }
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) Inv[i * 4 + j] = a[i][j + 4];
+}
+
+// finalize: pick the candidate, scale t, compose T_curr, emit the pose row
+// (PoseUpdate.hpp:142-178, VisualOdometry.cpp:106-186); 1 thread
+__global__ void k_finalize(VoDev d)
+{
+    VoState* st = d.st;
+    if (threadIdx.x != 0) return;
+    const int status = st->status;
+    const int mode = st->mode;
+    if (mode == VO_MODE_EXTRACT) return;
+    double* Tc = st->Tcurr;
+    double Rf[9], tf[3];
+    bool have_pose = false;
+    if (status == VO_STATUS_OK) {
+        int maxPos = -1, bestc = 0;
+        for (int c = 0; c < 4; ++c) if (st->counts4[c] > maxPos) { maxPos = st->counts4[c]; bestc = c; }
+        const double* R = bestc < 2 ? st->R1 : st->R2;
+        double sg = (bestc & 1) ? -1.0 : 1.0;
+        for (int i = 0; i < 9; ++i) Rf[i] = R[i];
+        if (det3(Rf) < 0) for (int i = 0; i < 9; ++i) Rf[i] = -Rf[i];
+        tf[0] = st->t[0] * sg; tf[1] = st->t[1] * sg; tf[2] = st->t[2] * sg;
+        double scale = st->scale_override;
+        if (mode == VO_MODE_FRAME) {
+            scale = 1.0;
+            const int fi = st->frame, last = st->last_valid;
+            if (d.gt_n > 0 && fi < d.gt_n && last < d.gt_n) {
+                double Gi[16], Gl[16], Ii[16], Tr[16];
+                for (int r = 0; r < 16; ++r) {
+                    Gi[r] = r < 12 ? d.gt[12 * (size_t)fi + r] : (r == 15 ? 1.0 : 0.0);
+                    Gl[r] = r < 12 ? d.gt[12 * (size_t)last + r] : (r == 15 ? 1.0 : 0.0);
+                }
+                inv4(Gi, Ii);
+                mm4(Ii, Gl, Tr);
+                scale = sqrt((Tr[3] * Tr[3] + Tr[7] * Tr[7]) + Tr[11] * Tr[11]);
+            }
+        }
+        double tn = sqrt((tf[0] * tf[0] + tf[1] * tf[1]) + tf[2] * tf[2]);
+        if (tn > 1e-6) {
+            double f = scale / tn;
+            tf[0] = tf[0] * f; tf[1] = tf[1] * f; tf[2] = tf[2] * f;
+        }
+        for (int i = 0; i < 9; ++i) st->pose_R[i] = Rf[i];
+        for (int i = 0; i < 3; ++i) st->pose_t[i] = tf[i];
+        have_pose = true;
+    }
+    if (mode == VO_MODE_STAGE) return;
+    VoFrameOut* o = d.out;
+    int flip = 1;
+    if (status == VO_STATUS_FIRST || status == VO_STATUS_MISSING) flip = 0;
+    if (status == VO_STATUS_OK || status == VO_STATUS_DEGENERATE) {
+        // VisualOdometry.cpp:161-166 happen before getPose
+        st->last_valid = st->frame;
+        st->prev = st->cur;
+    }
+    if (status == VO_STATUS_FIRST) { st->prev = st->cur; st->last_valid = 0; }
+    if (have_pose) {
+        double Trel[16] = {Rf[0], Rf[1], Rf[2], tf[0], Rf[3], Rf[4], Rf[5], tf[1], Rf[6], Rf[7], Rf[8], tf[2], 0, 0, 0, 1};
+        mm4(Tc, Trel, Tc);
+    }
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 4; ++c) o->pose[r * 4 + c] = (flip && r == 2) ? -Tc[r * 4 + c] : Tc[r * 4 + c];
+    o->status = status;
+    o->n_kps = status == VO_STATUS_MISSING ? 0 : st->n_kps[st->cur];
+    o->n_matches = st->M;
+    o->n_inl = st->n_inl;
+    o->best_k = st->bestk;
+    o->n_eval = st->n_eval;
+    o->fitted = st->fitted;
+    o->frame = st->frame;
+    st->frame = st->frame + 1;
+}
+
+// arithmetic self-test: the ops whose rounding the parity contract depends on
+__global__ void k_selftest_arith(const float* fa, const float* fb, float* fo, const double* da, const double* db,
+                                 double* dout, int n)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fo[4 * i + 0] = sqrtf(fa[i]);
+    fo[4 * i + 1] = fa[i] / fb[i];
+    double s, c;
+    det_sincos(da[i], &s, &c);
+    fo[4 * i + 2] = (float)det_atan2(da[i], db[i]);
+    fo[4 * i + 3] = (float)s;
+    dout[4 * i + 0] = sqrt(fabs(da[i]));
+    dout[4 * i + 1] = da[i] / db[i];
+    dout[4 * i + 2] = det_atan2(da[i], db[i]);
+    dout[4 * i + 3] = c;
+}
+
+// ---------------------------------------------------------------------------
+// launch wrappers
+// ---------------------------------------------------------------------------
+static const char* g_names[] = {"frame_begin", "stencil", "select", "describe", "match", "compact",
+                                "ransac_hyp0", "replay0", "ransac_hyp1", "replay1", "refit", "pose_prep",
+                                "triangulate", "finalize"};
+int kernel_count() { return (int)(sizeof(g_names) / sizeof(g_names[0])); }
+const char* kernel_name(int i) { return g_names[i]; }
+
+void launch_frame_begin(const VoDev& d, int mode, hipStream_t s)
+{
+    ensure_tables();
+    hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(1024), 0, s, d, mode);
+}
+void launch_stencil(const VoDev& d, const uint8_t* frame, int write_response, hipStream_t s)
+{
+    dim3 g((d.W + ST_TW - 1) / ST_TW, (d.H + ST_TH - 1) / ST_TH);
+    hipLaunchKernelGGL(k_stencil, g, dim3(256), 0, s, d, frame, write_response);
+}
+void launch_select(const VoDev& d, hipStream_t s) { hipLaunchKernelGGL(k_select, dim3(1), dim3(1024), 0, s, d); }
+void launch_describe(const VoDev& d, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_describe, dim3((d.N + DS_KPB - 1) / DS_KPB), dim3(256), 0, s, d);
+}
+void launch_match(const VoDev& d, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_match, dim3((d.N + 3) / 4), dim3(256), 0, s, d);
+}
+void launch_compact(const VoDev& d, hipStream_t s) { hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, d); }
+void launch_ransac_hyp(const VoDev& d, int k0, int k1, hipStream_t s)
+{
+    int nb = (k1 - k0 + 3) / 4;
+    if (nb > 0) hipLaunchKernelGGL(k_ransac_hyp, dim3(nb), dim3(256), 0, s, d, k0, k1);
+}
+void launch_ransac_replay(const VoDev& d, int k1, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_ransac_replay, dim3(1), dim3(64), 0, s, d, k1);
+}
+void launch_refit(const VoDev& d, hipStream_t s) { hipLaunchKernelGGL(k_refit, dim3(1), dim3(256), 0, s, d); }
+void launch_pose_prep(const VoDev& d, hipStream_t s) { hipLaunchKernelGGL(k_pose_prep, dim3(1), dim3(64), 0, s, d); }
+void launch_triangulate(const VoDev& d, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_triangulate, dim3((d.N + 255) / 256), dim3(256), 0, s, d);
+}
+void launch_finalize(const VoDev& d, hipStream_t s) { hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, d); }
+void launch_selftest_arith(const float* fa, const float* fb, float* fo, const double* da, const double* db,
+                           double* dout, int n, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_selftest_arith, dim3((n + 255) / 256), dim3(256), 0, s, fa, fb, fo, da, db, dout, n);
+}
+
+}  // namespace vo

@@ -1,0 +1,231 @@
+"""Host-side mirror of the reference's per-frame interface, over the C ABI.
+
+``Context`` wraps one ``vo_ctx`` (one GPU, one HIP stream, persistent HBM buffers).
+``VisualOdometry`` mirrors the reference class (VisualOdometry.h:15-31): same method
+names, same argument meaning, same error behaviour (``RuntimeError`` where the
+reference throws ``std::runtime_error``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, load
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class Context:
+    """One vo_ctx: HIP device buffers + stream for a width x height stream."""
+
+    def __init__(self, width: int, height: int, **cfg):
+        self.lib = load()
+        self.cfg = _lib.default_config(width, height, **cfg)
+        h = C.c_void_p()
+        check(self.lib.vo_create(C.byref(self.cfg), C.byref(h)), "vo_create")
+        self.h = h
+        self.W, self.H, self.N = width, height, self.cfg.max_kpts
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.vo_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- stage calls --------------------------------------------------------
+    def extract(self, gray: np.ndarray, want_blurred: bool = False):
+        g = np.ascontiguousarray(gray, dtype=np.uint8)
+        assert g.shape == (self.H, self.W), g.shape
+        kps = np.empty((self.N, 2), np.int32)
+        desc = np.empty((self.N, 8), np.uint64)
+        bl = np.empty_like(g) if want_blurred else None
+        n = C.c_int()
+        check(self.lib.vo_extract(self.h, _p(g), self.W, _p(kps), _p(desc), C.byref(n), _p(bl)), "vo_extract")
+        out = (kps[:n.value].copy(), desc[:n.value].copy())
+        return out + (bl,) if want_blurred else out
+
+    def response(self, gray: np.ndarray) -> np.ndarray:
+        g = np.ascontiguousarray(gray, dtype=np.uint8)
+        R = np.empty((self.H, self.W), np.float32)
+        check(self.lib.vo_response(self.h, _p(g), self.W, _p(R)), "vo_response")
+        return R
+
+    def match(self, d_prev: np.ndarray, d_cur: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(d_prev, dtype=np.uint64).reshape(-1, 8)
+        b = np.ascontiguousarray(d_cur, dtype=np.uint64).reshape(-1, 8)
+        out = np.empty((max(a.shape[0], 1), 2), np.int32)
+        m = C.c_int()
+        check(self.lib.vo_match(self.h, _p(a), a.shape[0], _p(b), b.shape[0], _p(out), C.byref(m)), "vo_match")
+        return out[:m.value].copy()
+
+    def ransac(self, pts: np.ndarray, seed: int):
+        pts = np.ascontiguousarray(pts, dtype=np.float64).reshape(-1, 4)
+        m = pts.shape[0]
+        F = np.zeros(9)
+        inl = np.zeros(max(m, 1), np.int32)
+        counts = np.zeros(2000, np.int32)
+        fitted, n_inl, best_k, n_eval = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        check(self.lib.vo_ransac_F(self.h, _p(pts), m, seed, _p(F), C.byref(fitted), _p(inl), C.byref(n_inl),
+                                   C.byref(best_k), C.byref(n_eval), _p(counts)), "vo_ransac_F")
+        ne = n_eval.value
+        return dict(F=F.reshape(3, 3), fitted=fitted.value, n_inl=n_inl.value, best_k=best_k.value,
+                    n_evaluated=ne, counts=counts[:min(ne, 2000)].copy(),
+                    inliers=inl[:n_inl.value].copy() if best_k.value >= 0 else np.zeros(0, np.int32))
+
+    def pose(self, F, p1, p2, scale: float = 1.0):
+        F = np.ascontiguousarray(F, dtype=np.float64).reshape(9)
+        p1 = np.ascontiguousarray(p1, dtype=np.float32).reshape(-1, 2)
+        p2 = np.ascontiguousarray(p2, dtype=np.float32).reshape(-1, 2)
+        R = np.zeros(9)
+        t = np.zeros(3)
+        cnt = np.zeros(4, np.int32)
+        rc = self.lib.vo_pose(self.h, _p(F), _p(p1), _p(p2), p1.shape[0], scale, _p(R), _p(t), _p(cnt))
+        check(rc, "vo_pose")
+        return R.reshape(3, 3), t, cnt
+
+    # -- trajectory ---------------------------------------------------------
+    def set_ground_truth(self, gt: Optional[np.ndarray]):
+        if gt is None:
+            check(self.lib.vo_set_ground_truth(self.h, None, 0))
+            return
+        g = np.ascontiguousarray(gt, dtype=np.float64).reshape(-1, 12)
+        check(self.lib.vo_set_ground_truth(self.h, _p(g), g.shape[0]), "vo_set_ground_truth")
+
+    def reset(self):
+        check(self.lib.vo_reset(self.h), "vo_reset")
+
+    def process_frame(self, gray: Optional[np.ndarray]):
+        pose = np.zeros(12)
+        st = C.c_int()
+        info = np.zeros(8, np.int32)
+        g = None if gray is None else np.ascontiguousarray(gray, dtype=np.uint8)
+        rc = self.lib.vo_process_frame(self.h, _p(g), 0 if g is None else self.W, _p(pose), C.byref(st), _p(info))
+        if rc < 0 and rc != _lib.VO_ERR_DEGENERATE_E:
+            check(rc, "vo_process_frame")
+        return pose.reshape(3, 4), st.value, info
+
+    def device_frames(self, frames: np.ndarray) -> "DeviceFrames":
+        return DeviceFrames(self, frames)
+
+    def process_frames_device(self, dframes: "DeviceFrames", timing: bool = False):
+        n = dframes.n
+        poses = np.zeros((n, 12))
+        st = np.zeros(n, np.int32)
+        info = np.zeros((n, 8), np.int32)
+        check(self.lib.vo_enable_kernel_timing(self.h, 1 if timing else 0))
+        check(self.lib.vo_process_frames_device(self.h, dframes.ptr, dframes.frame_bytes, n, _p(poses), _p(st),
+                                                _p(info)), "vo_process_frames_device")
+        return poses.reshape(n, 3, 4), st, info
+
+    def kernel_times(self):
+        names = (C.c_char_p * 32)()
+        ms = (C.c_float * 32)()
+        k = self.lib.vo_last_kernel_times(self.h, names, ms, 32)
+        return {names[i].decode(): ms[i] for i in range(k)}
+
+
+class DeviceFrames:
+    """A batch of frames resident in HBM (uploaded once)."""
+
+    def __init__(self, ctx: Context, frames: np.ndarray):
+        f = np.ascontiguousarray(frames, dtype=np.uint8)
+        assert f.ndim == 3 and f.shape[1:] == (ctx.H, ctx.W)
+        self.ctx, self.n = ctx, f.shape[0]
+        self.frame_bytes = ctx.W * ctx.H
+        p = C.c_void_p()
+        check(ctx.lib.vo_device_alloc(ctx.h, f.nbytes, C.byref(p)), "vo_device_alloc")
+        self.ptr = p
+        check(ctx.lib.vo_device_upload(ctx.h, p, _p(f), f.nbytes), "vo_device_upload")
+
+    def free(self):
+        if self.ptr:
+            self.ctx.lib.vo_device_free(self.ctx.h, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def unpack_descriptor(words: np.ndarray) -> np.ndarray:
+    """8 x u64 words -> 512 bytes in {0,1} (the reference's byte-per-test descriptor)."""
+    w = np.ascontiguousarray(words, dtype=np.uint64).reshape(-1, 8)
+    bits = np.unpackbits(w.view(np.uint8).reshape(-1, 64), axis=1, bitorder="little")
+    return bits.astype(np.uint8)
+
+
+def pack_descriptor(bytes512: np.ndarray) -> np.ndarray:
+    b = np.ascontiguousarray(bytes512, dtype=np.uint8).reshape(-1, 512)
+    return np.packbits(b, axis=1, bitorder="little").view(np.uint64).reshape(-1, 8)
+
+
+class VisualOdometry:
+    """Mirror of the reference class VisualOdometry (VisualOdometry.h:15-31).
+
+    ``kernel_filename`` is accepted for signature compatibility (the reference loads an
+    OpenCL binary, main_pipeline.cpp:32); the HIP code objects are embedded in
+    libvo_mi355x.so.  ``num_threads`` keeps its one semantic effect on the results:
+    the RANSAC chunk count (ransac.cpp:152-157).
+    """
+
+    def __init__(self, kernel_filename: str = "", num_threads: int = 8, width: int = 1241, height: int = 376,
+                 **cfg):
+        self.kernel_filename = kernel_filename
+        self.number_of_threads = int(num_threads)
+        cfg.setdefault("ransac_chunk_threads", self.number_of_threads)
+        self.ctx = Context(width, height, **cfg)
+
+    def compute_descriptor_with_key_points(self, image: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """-> (descriptors n x 512 u8 in {0,1}, keypoints n x 2 (x=col, y=row)), raster order."""
+        kps, desc = self.ctx.extract(image)
+        return unpack_descriptor(desc), kps
+
+    def match_descriptors(self, desc1, desc2) -> List[Tuple[int, int]]:
+        d1 = np.asarray(desc1)
+        d2 = np.asarray(desc2)
+        if d1.size == 0 or d2.size == 0:
+            return []
+        w1 = pack_descriptor(d1) if d1.shape[-1] == 512 else d1
+        w2 = pack_descriptor(d2) if d2.shape[-1] == 512 else d2
+        return [tuple(map(int, r)) for r in self.ctx.match(w1, w2)]
+
+    def run(self, image_dir: str, num_images: int, pose_file: str, output_csv: str) -> None:
+        """VisualOdometry::run (VisualOdometry.cpp:38-193): KITTI sequence -> pose CSV."""
+        from .io import read_gray, read_kitti_poses, write_pose_csv
+        try:
+            gt = read_kitti_poses(pose_file)
+        except OSError:
+            import sys
+            print("Failed to open pose file.", file=sys.stderr)
+            return
+        self.ctx.reset()
+        self.ctx.set_ground_truth(gt)
+        poses = []
+        for i in range(int(num_images)):
+            img = read_gray(os.path.join(image_dir, f"{i:06d}.png"))
+            pose, status, _ = self.ctx.process_frame(img)
+            if status == 5:
+                raise RuntimeError("Degenerate essential matrix")
+            poses.append(pose)
+        write_pose_csv(output_csv, poses)
+        print(f"Wrote estimated poses to: {output_csv}")

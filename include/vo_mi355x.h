@@ -1,0 +1,150 @@
+/*
+ * vo_mi355x.h -- C ABI of the MI355X-native extract -> match -> pose hot path.
+ *
+ * Drop-in boundary for the reference's per-frame path (Bohdanok/ACS_Visual_Odometry,
+ * the `VisualOdometry` binary).  The reference exposes only C++ classes (no C ABI);
+ * each entry point below replaces the reference call named in its comment.  The C++
+ * facade `include/VisualOdometry.hpp` and the Python facade
+ * `acs_visual_odometry_amd.VisualOdometry` re-expose these under the reference's
+ * method names.
+ *
+ * Conventions
+ *  - return 0 on success, < 0 on error (vo_strerror); no exception crosses the ABI.
+ *  - all pointers are caller-owned HOST memory unless the name ends in _device.
+ *  - a vo_ctx is bound to one GPU and one HIP stream; it is not thread-safe
+ *    (one ctx per host thread / GPU, like one VisualOdometry object per run).
+ *  - keypoints are (x = column, y = row), raster (row, col) ascending order.
+ *  - descriptors are 512 test bits as 8 x uint64, bit t in word t/64, LSB first;
+ *    vo_unpack_descriptor gives the reference's byte-per-test layout.
+ */
+#ifndef VO_MI355X_H
+#define VO_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VO_ABI_VERSION 1
+
+/* error codes */
+#define VO_OK                 0
+#define VO_ERR_ARG           (-1)
+#define VO_ERR_HIP           (-2)
+#define VO_ERR_NO_DEVICE     (-3)   /* VisualOdometry.cpp:17-19 throws "No OpenCL devices" */
+#define VO_ERR_CAPACITY      (-4)
+#define VO_ERR_STATE         (-5)
+#define VO_ERR_DEGENERATE_E  (-10)  /* PoseUpdate.hpp:71-73 throws "Degenerate essential matrix" */
+
+/* per-frame status (VisualOdometry.cpp:68-189) */
+#define VO_STATUS_OK            0   /* pose updated                                  */
+#define VO_STATUS_FIRST         1   /* frame 0: identity pushed (:58)                */
+#define VO_STATUS_MISSING       2   /* image failed to load (:77-82), T_curr pushed  */
+#define VO_STATUS_FEW_MATCHES   3   /* < 8 matches (:108-115), flipZ*T_curr pushed   */
+#define VO_STATUS_FEW_INLIERS   4   /* < 8 model inliers (:147-153)                  */
+#define VO_STATUS_DEGENERATE    5   /* getPose threw (countNonZero(E) < 5)           */
+#define VO_STATUS_OVERFLOW      6   /* top-N boundary bin exceeded the LDS select buffer */
+
+typedef struct vo_ctx vo_ctx;
+
+typedef struct { int32_t x, y; } vo_kp;
+typedef struct { int32_t prev, cur; } vo_match_t;
+
+typedef struct {
+    int width, height;
+    int max_kpts;             /* N = 2000      feature_extraction_parallel_GPU.cpp:235 */
+    int nms_k;                /* 3             feature_extraction_parallel_GPU.cpp:235 */
+    float resp_thr;           /* 20000         corner_detection_parallel_GPU.h:25      */
+    int border_row;           /* 35            corner_detection_parallel_GPU.cpp:157   */
+    int border_col;           /* 37            corner_detection_parallel_GPU.cpp:157   */
+    float ratio;              /* 0.75          VisualOdometry.cpp:35                   */
+    int match_bits;           /* 32 (reference quirk 1) or 512 (matching_serial.cpp)   */
+    double ransac_p;          /* 0.99          VisualOdometry.cpp:130                  */
+    double sampson_thr;       /* 1.0           VisualOdometry.cpp:130                  */
+    int ransac_chunk_threads; /* T             ransac.cpp:152-157 (CLI num_threads)    */
+    uint64_t seed;            /* RANSAC sampler seed (replaces std::random_device)     */
+    double K[9];              /* PoseUpdate.hpp:36-39                                  */
+    int device;               /* HIP device ordinal                                    */
+} vo_config;
+
+/* Fill the reference defaults for a width x height stream. */
+void vo_config_default(vo_config* cfg, int width, int height);
+
+/* VisualOdometry::VisualOdometry(kernel_filename, num_threads)  VisualOdometry.h:23.
+ * Allocates every device buffer once (the reference re-allocates per frame). */
+int  vo_create(const vo_config* cfg, vo_ctx** out);
+void vo_destroy(vo_ctx* ctx);
+const char* vo_strerror(int code);
+int  vo_abi_version(void);
+
+/* VisualOdometry::compute_descriptor_with_key_points  VisualOdometry.h:25-26
+ * (-> feature_extraction_manager_with_points, feature_extraction_parallel_GPU.cpp:194).
+ * kps: max_kpts entries; desc: max_kpts * 8 words; blurred (optional): W*H bytes. */
+int  vo_extract(vo_ctx* ctx, const uint8_t* gray, size_t stride, vo_kp* kps, uint64_t* desc,
+                int* n, uint8_t* blurred);
+
+/* Dense response map R (W*H f32, 0 outside [2,H-3]x[2,W-3] and below threshold):
+ * gradient_convolution + shitomasi_response, kernels/feature_extraction_kernel_functions.c:43-120. */
+int  vo_response(vo_ctx* ctx, const uint8_t* gray, size_t stride, float* R);
+
+/* VisualOdometry::match_descriptors  VisualOdometry.h:27-29
+ * (-> matchCustomBinaryDescriptorsThreadPool, feature_matching_parallel.cpp:49-113). */
+int  vo_match(vo_ctx* ctx, const uint64_t* d_prev, int n_prev, const uint64_t* d_cur, int n_cur,
+              vo_match_t* out, int* m);
+
+/* Ransac::run(model, data, p, thr, T, pool)  ransac.hpp:42-47, + FundamentalMatrix::getMatrix/
+ * getInliers (ransac.hpp:31,33).  pts: m x (x1,y1,x2,y2).  seed: sampler seed for this call.
+ * F: refit model (valid iff *fitted).  inlier_idx (m entries, optional): bestInlierSet as
+ * indices into pts.  counts (optional, 2000 entries): inliers of hypothesis k for
+ * k < *n_evaluated. */
+int  vo_ransac_F(vo_ctx* ctx, const double* pts, int m, uint64_t seed, double F[9],
+                 int* fitted, int32_t* inlier_idx, int* n_inl, int* best_k, int* n_evaluated,
+                 int32_t* counts);
+
+/* PoseUpdate::getPose(F, points1, points2, scale)  PoseUpdate.hpp:61-62.
+ * p1/p2: n x 2 f32.  counts4 (optional): positive-depth count per candidate
+ * {R1,t},{R1,-t},{R2,t},{R2,-t}.  Returns VO_ERR_DEGENERATE_E where the reference throws. */
+int  vo_pose(vo_ctx* ctx, const double F[9], const float* p1, const float* p2, int n,
+             double scale, double R[9], double t[3], int32_t* counts4);
+
+/* Ground truth for the trajectory loop's scale (VisualOdometry.cpp:161-162): n rows of
+ * 12 doubles (KITTI 3x4 row-major).  Without it the scale is 1. */
+int  vo_set_ground_truth(vo_ctx* ctx, const double* poses12, int n);
+
+/* One iteration of VisualOdometry::run's loop (VisualOdometry.cpp:68-189): frame in,
+ * pose out.  gray == NULL marks a missing image.  pose_out: 12 doubles, the row the
+ * reference appends to estimated_poses.  info (optional, 8 ints): n_kpts, n_matches,
+ * n_inliers, best_k, n_evaluated, fitted, 0, 0. */
+int  vo_process_frame(vo_ctx* ctx, const uint8_t* gray, size_t stride, double pose_out[12],
+                      int* status, int32_t* info);
+
+/* Batched, device-resident variant: nframes frames already in HBM at
+ * d_frames + f * frame_bytes (dense W x H u8).  Enqueues every frame on the ctx stream
+ * with no host synchronisation between frames, then waits once.  poses_out: nframes*12,
+ * status_out: nframes (both host, optional). */
+int  vo_process_frames_device(vo_ctx* ctx, const uint8_t* d_frames, size_t frame_bytes, int nframes,
+                              double* poses_out, int* status_out, int32_t* info_out);
+
+/* Device memory helpers for callers without their own allocator (bench, tests). */
+int  vo_device_alloc(vo_ctx* ctx, size_t bytes, void** dptr);
+int  vo_device_free(vo_ctx* ctx, void* dptr);
+int  vo_device_upload(vo_ctx* ctx, void* dptr, const void* src, size_t bytes);
+
+/* Reset the trajectory state (frame counter, T_curr, model, prev descriptors). */
+int  vo_reset(vo_ctx* ctx);
+
+/* Per-kernel timing of the last vo_process_frames_device call (HIP events on the ctx
+ * stream).  names/ms: up to cap entries; returns the number written. */
+int  vo_last_kernel_times(vo_ctx* ctx, const char** names, float* ms, int cap);
+int  vo_enable_kernel_timing(vo_ctx* ctx, int on);
+
+/* desc512 (8 words) -> 512 bytes in {0,1}: the reference's byte-per-test layout
+ * (FREAK_feature_descriptor_parallel_GPU.cpp:334-336). */
+void vo_unpack_descriptor(const uint64_t words[8], uint8_t bytes[512]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,243 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle, bit for bit.
+
+Every test here calls libvo_mi355x.so; the oracle (oracle/) is only the checker.
+Bit-exact: keypoints, descriptor bits, match pairs, per-hypothesis inlier counts,
+best hypothesis, inlier set, F, R, t, trajectory rows.  Tolerances are stated where a
+reference-semantics comparison (not the oracle) is made.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from acs_visual_odometry_amd import Context, load
+from acs_visual_odometry_amd.io import read_gray
+from acs_visual_odometry_amd.synth import SceneSequence, noise_frames
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+@pytest.fixture(scope="module")
+def scene():
+    seq = SceneSequence(nframes=6, step=0.05)
+    return seq, seq.frames()
+
+
+@pytest.fixture(scope="module")
+def factory():
+    return [read_gray(os.path.join(GOLD, f"factory{i}.png")) for i in (1, 2)]
+
+
+@pytest.fixture(scope="module")
+def ctx_kitti(scene):
+    seq, _ = scene
+    c = Context(seq.W, seq.H, K=seq.K)
+    yield c
+    c.close()
+
+
+def test_device_arithmetic_matches_host():
+    """sqrtf, f32 '/', f64 sqrt and '/', and the det-math atan2/sincos: device == host."""
+    L = load()
+    rng = np.random.default_rng(7)
+    n = 1 << 16
+    fa = (rng.random(n, dtype=np.float32) * 1e6).astype(np.float32)
+    fb = (rng.random(n, dtype=np.float32) * 1e3 + 1e-3).astype(np.float32)
+    da = rng.standard_normal(n) * 1e3
+    db = rng.standard_normal(n) * 1e3
+    da[:16] = [0.0, -0.0, 1.0, -1.0, 3.14159, -3.14159, 1e-300, 5.0, 7.0, -7.0, 0.0, -0.0, 2.0, -2.0, 1.5, -1.5]
+    db[:16] = [0.0, -0.0, 0.0, -0.0, 1.0, -1.0, 1.0, -5.0, 7.0, 7.0, 3.0, -3.0, -2.0, 2.0, 1e-9, -1e-9]
+    fo = np.zeros((n, 4), np.float32)
+    do = np.zeros((n, 4), np.float64)
+    assert L.vo_selftest_arith(_p(fa), _p(fb), _p(fo), _p(da), _p(db), _p(do), n, 0) == 0
+    assert np.array_equal(fo[:, 0], np.sqrt(fa)), "device sqrtf is not correctly rounded"
+    assert np.array_equal(fo[:, 1], fa / fb), "device f32 division is not correctly rounded"
+    assert np.array_equal(do[:, 0], np.sqrt(np.abs(da)))
+    with np.errstate(all="ignore"):
+        assert np.array_equal(do[:, 1], da / db, equal_nan=True)
+    lib = O.lib()
+    ref_at = np.array([lib.voo_det_atan2(a, b) for a, b in zip(da[:4096], db[:4096])])
+    ref_c = np.array([lib.voo_det_cos(a) for a in da[:4096]])
+    ref_s = np.array([lib.voo_det_sin(a) for a in da[:4096]])
+    assert np.array_equal(do[:4096, 2], ref_at)
+    assert np.array_equal(do[:4096, 3], ref_c)
+    assert np.array_equal(fo[:4096, 2], ref_at.astype(np.float32))
+    assert np.array_equal(fo[:4096, 3], ref_s.astype(np.float32))
+
+
+def test_response_map_bit_exact(ctx_kitti, scene, factory):
+    seq, frames = scene
+    R = ctx_kitti.response(frames[0])
+    Rr = O.response(O.blur7(frames[0]))
+    assert np.array_equal(R.view(np.uint32), Rr.view(np.uint32))
+    c2 = Context(752, 480)
+    for img in factory:
+        R = c2.response(img)
+        Rr = O.response(O.blur7(img))
+        assert np.array_equal(R.view(np.uint32), Rr.view(np.uint32))
+    c2.close()
+
+
+@pytest.mark.parametrize("which", ["scene0", "scene3", "noise", "factory1", "factory2"])
+def test_extract_bit_exact(which, ctx_kitti, scene, factory):
+    seq, frames = scene
+    if which.startswith("scene"):
+        img, ctx = frames[int(which[-1])], ctx_kitti
+        cfg = O.config(seq.W, seq.H, K=seq.K.reshape(9))
+    elif which == "noise":
+        img, ctx = noise_frames(nframes=1)[0], ctx_kitti
+        cfg = O.config(seq.W, seq.H, K=seq.K.reshape(9))
+    else:
+        img = factory[int(which[-1]) - 1]
+        ctx = Context(752, 480)
+        cfg = O.config(752, 480)
+    k, d, bl = ctx.extract(img, want_blurred=True)
+    kr, dr, blr = O.extract(img, cfg)
+    assert np.array_equal(bl, blr), "blur differs"
+    assert k.shape == kr.shape, (k.shape, kr.shape)
+    assert np.array_equal(k, kr), "keypoints differ"
+    assert np.array_equal(d, dr), "descriptor bits differ"
+
+
+@pytest.mark.parametrize("bits", [32, 512])
+def test_match_bit_exact(bits, scene):
+    seq, frames = scene
+    cfg = O.config(seq.W, seq.H, K=seq.K.reshape(9))
+    _, d0, _ = O.extract(frames[0], cfg)
+    _, d1, _ = O.extract(frames[1], cfg)
+    ctx = Context(seq.W, seq.H, match_bits=bits)
+    m = ctx.match(d0, d1)
+    mr = O.match(d0, d1, match_bits=bits)
+    assert np.array_equal(m, mr)
+    ctx.close()
+
+
+def test_match_edge_cases(ctx_kitti):
+    rng = np.random.default_rng(3)
+    d = rng.integers(0, 2**63, size=(64, 8), dtype=np.uint64)
+    # ties: duplicate candidates, identical best/second
+    d2 = np.concatenate([d[:10], d[:10], d[10:20]])
+    for a, b in [(d, d2), (d[:1], d2), (d, d2[:1]), (d[:5], d[:2]), (d2, d2)]:
+        assert np.array_equal(ctx_kitti.match(a, b), O.match(a, b))
+    assert ctx_kitti.match(d[:0], d).shape[0] == 0
+    assert ctx_kitti.match(d, d[:0]).shape[0] == 0
+
+
+def _matched_points(frames, cfg, a=0, b=1):
+    k0, d0, _ = O.extract(frames[a], cfg)
+    k1, d1, _ = O.extract(frames[b], cfg)
+    m = O.match(d0, d1)
+    return np.concatenate([k0[m[:, 0]], k1[m[:, 1]]], axis=1).astype(np.float64)
+
+
+@pytest.mark.parametrize("T,seed", [(8, 1), (1, 2), (3, 3), (64, 4)])
+def test_ransac_bit_exact(T, seed, scene):
+    seq, frames = scene
+    cfg = O.config(seq.W, seq.H, K=seq.K.reshape(9))
+    pts = _matched_points(frames, cfg)
+    ctx = Context(seq.W, seq.H, ransac_chunk_threads=T)
+    g = ctx.ransac(pts, seed)
+    r = O.ransac(pts, T=T, seed=seed)
+    assert g["n_evaluated"] == r["n_evaluated"]
+    assert g["best_k"] == r["best_k"]
+    assert np.array_equal(g["counts"], r["counts"])
+    assert g["n_inl"] == r["n_inl"]
+    assert np.array_equal(g["inliers"], r["inliers"])
+    assert g["fitted"] == r["fitted"]
+    if r["fitted"]:
+        assert np.array_equal(g["F"], r["F"])
+    ctx.close()
+
+
+def test_ransac_low_inlier_ratio_many_hypotheses(scene):
+    """Random correspondences: best ratio < 0.0825 -> INT_MIN -> 100 iterations (quirk 8),
+    and a moderate ratio -> up to 2000 hypotheses (second chunk)."""
+    rng = np.random.default_rng(11)
+    pts = np.concatenate([rng.integers(40, 1200, (600, 1)), rng.integers(40, 340, (600, 1)),
+                          rng.integers(40, 1200, (600, 1)), rng.integers(40, 340, (600, 1))], axis=1).astype(float)
+    ctx = Context(1241, 376)
+    for seed in (5, 6):
+        g = ctx.ransac(pts, seed)
+        r = O.ransac(pts, seed=seed)
+        assert (g["n_evaluated"], g["best_k"], g["n_inl"]) == (r["n_evaluated"], r["best_k"], r["n_inl"])
+        assert np.array_equal(g["counts"], r["counts"])
+    ctx.close()
+
+
+def test_pose_bit_exact(scene):
+    seq, frames = scene
+    cfg = O.config(seq.W, seq.H, K=seq.K.reshape(9))
+    pts = _matched_points(frames, cfg)
+    r = O.ransac(pts, seed=9)
+    inl = pts[r["inliers"]]
+    ctx = Context(seq.W, seq.H, K=seq.K)
+    R, t, cnt = ctx.pose(r["F"], inl[:, :2], inl[:, 2:], 1.0)
+    rc, Rr, tr, cntr = O.pose(r["F"], seq.K, inl[:, :2], inl[:, 2:], 1.0)
+    assert rc == 0
+    assert np.array_equal(cnt, cntr)
+    assert np.array_equal(R, Rr)
+    assert np.array_equal(t, tr)
+    ctx.close()
+
+
+def test_pose_degenerate_raises(ctx_kitti):
+    F = np.zeros((3, 3))
+    F[0, 0] = 1.0
+    p = np.full((10, 2), 100.0, np.float32)
+    with pytest.raises(RuntimeError, match="Degenerate essential matrix"):
+        ctx_kitti.pose(F, p, p, 1.0)
+
+
+def test_trajectory_bit_exact(scene):
+    seq, frames = scene
+    cfg = O.config(seq.W, seq.H, K=seq.K.reshape(9))
+    ctx = Context(seq.W, seq.H, K=seq.K)
+    ctx.set_ground_truth(seq.gt())
+    vo = O.VO(cfg, gt=seq.gt())
+    for f in range(seq.n):
+        img = None if f == 4 else frames[f]      # frame 4 "missing"
+        pg, sg, ig = ctx.process_frame(img)
+        pr, sr, ir = vo.process(img)
+        assert sg == sr, (f, sg, sr)
+        assert np.array_equal(ig[:6], ir[:6]), (f, ig, ir)
+        assert np.array_equal(pg, pr), (f, pg, pr)
+    ctx.close()
+
+
+def test_batched_device_frames_equal_per_frame(scene):
+    seq, frames = scene
+    ctx = Context(seq.W, seq.H, K=seq.K)
+    ctx.set_ground_truth(seq.gt())
+    per = [ctx.process_frame(frames[f]) for f in range(seq.n)]
+    ctx.reset()
+    df = ctx.device_frames(frames)
+    poses, st, info = ctx.process_frames_device(df)
+    for f in range(seq.n):
+        assert st[f] == per[f][1]
+        assert np.array_equal(poses[f], per[f][0])
+        assert np.array_equal(info[f, :6], per[f][2][:6])
+    df.free()
+    ctx.close()
+
+
+def test_skip_few_matches_keeps_previous_descriptors():
+    """A blank frame gives < 8 matches: flipZ*T_curr is pushed and desc1 is not advanced
+    (VisualOdometry.cpp:108-115,164-166)."""
+    seq = SceneSequence(nframes=4, step=0.05)
+    frames = seq.frames()
+    frames[2] = 128
+    cfg = O.config(seq.W, seq.H, K=seq.K.reshape(9))
+    ctx = Context(seq.W, seq.H, K=seq.K)
+    vo = O.VO(cfg)
+    for f in range(4):
+        pg, sg, ig = ctx.process_frame(frames[f])
+        pr, sr, ir = vo.process(frames[f])
+        assert sg == sr and np.array_equal(pg, pr) and np.array_equal(ig[:6], ir[:6]), (f, sg, sr, ig, ir)
+    ctx.close()
