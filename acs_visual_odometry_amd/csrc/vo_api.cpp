@@ -33,7 +33,8 @@ struct vo_ctx {
     VoFrameOut* out_host = nullptr;   // pinned
     uint8_t* stage_host = nullptr;    // pinned frame staging
     uint16_t* tab_dev = nullptr;
-    bool timing = false;
+    int timing = 0;                   // 0 off, 1 all kernels, 100+k only kernel k
+    std::vector<hipEvent_t> ev_pool;
     std::vector<float> ktime_ms;
     std::vector<int> kcount;
 };
@@ -139,16 +140,26 @@ void enqueue_ransac(vo_ctx* c)
     vo::launch_refit(c->d, c->s);
 }
 
-// the full trajectory-loop iteration for one frame (VisualOdometry.cpp:68-189)
-void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, std::vector<hipEvent_t>* ev)
+// the full trajectory-loop iteration for one frame (VisualOdometry.cpp:68-189).
+// Timing: ev_all records an event after every kernel (15 per frame); ev_one (kernel
+// index k >= 0) records only the two events bracketing kernel k.
+struct EvRec {
+    std::vector<hipEvent_t>* pool;
+    size_t used;
+    int only;   // -1: all kernels
+};
+
+void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev)
 {
-    auto mark = [&](int) {
-        if (ev) {
+    auto mark = [&](int k) {
+        if (!ev) return;
+        if (ev->only >= 0 && k != ev->only && k != ev->only + 1) return;
+        if (ev->used >= ev->pool->size()) {
             hipEvent_t e;
             (void)hipEventCreate(&e);
-            (void)hipEventRecord(e, c->s);
-            ev->push_back(e);
+            ev->pool->push_back(e);
         }
+        (void)hipEventRecord((*ev->pool)[ev->used++], c->s);
     };
     VoDev d = c->d;
     d.out = out;
@@ -330,6 +341,7 @@ void vo_destroy(vo_ctx* c)
         if (p) (void)hipFree(p);
     if (c->out_host) (void)hipHostFree(c->out_host);
     if (c->stage_host) (void)hipHostFree(c->stage_host);
+    for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
 }
@@ -539,9 +551,8 @@ int vo_process_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
     HIPCHK(hipSetDevice(c->cfg.device));
     int rc = ensure_out(c, std::max(nframes, 1));
     if (rc) return rc;
-    std::vector<hipEvent_t> ev;
-    std::vector<hipEvent_t>* evp = c->timing ? &ev : nullptr;
-    if (evp) ev.reserve((size_t)nframes * 15);
+    EvRec rec{&c->ev_pool, 0, c->timing >= 100 ? c->timing - 100 : -1};
+    EvRec* evp = c->timing ? &rec : nullptr;
     for (int f = 0; f < nframes; ++f) enqueue_frame(c, d_frames + (size_t)f * frame_bytes, c->out_dev + f, evp);
     HIPCHK(hipGetLastError());
     if (nframes)
@@ -551,15 +562,16 @@ int vo_process_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
         const int nk = vo::kernel_count();
         c->ktime_ms.assign(nk, 0.f);
         c->kcount.assign(nk, 0);
+        const int per = rec.only >= 0 ? 2 : nk + 1;
         for (int f = 0; f < nframes; ++f) {
-            for (int k = 0; k < nk; ++k) {
+            for (int k = 0; k + 1 < per; ++k) {
                 float ms = 0.f;
-                (void)hipEventElapsedTime(&ms, ev[(size_t)f * 15 + k], ev[(size_t)f * 15 + k + 1]);
-                c->ktime_ms[k] += ms;
-                c->kcount[k] += 1;
+                (void)hipEventElapsedTime(&ms, c->ev_pool[(size_t)f * per + k], c->ev_pool[(size_t)f * per + k + 1]);
+                int kk = rec.only >= 0 ? rec.only : k;
+                c->ktime_ms[kk] += ms;
+                c->kcount[kk] += 1;
             }
         }
-        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
     }
     for (int f = 0; f < nframes; ++f) {
         const VoFrameOut& o = c->out_host[f];
@@ -577,7 +589,8 @@ int vo_process_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
 int vo_enable_kernel_timing(vo_ctx* c, int on)
 {
     if (!c) return VO_ERR_ARG;
-    c->timing = on != 0;
+    if (on != 0 && on != 1 && !(on >= 100 && on < 100 + vo::kernel_count())) return VO_ERR_ARG;
+    c->timing = on;
     return VO_OK;
 }
 
@@ -587,7 +600,7 @@ int vo_last_kernel_times(vo_ctx* c, const char** names, float* ms, int cap)
     int nk = std::min<int>((int)c->ktime_ms.size(), cap);
     for (int k = 0; k < nk; ++k) {
         if (names) names[k] = vo::kernel_name(k);
-        if (ms) ms[k] = c->kcount[k] ? c->ktime_ms[k] / (float)c->kcount[k] : 0.f;
+        if (ms) ms[k] = c->kcount[k] ? c->ktime_ms[k] / (float)c->kcount[k] : -1.f;
     }
     return nk;
 }

@@ -125,12 +125,13 @@ class Context:
     def device_frames(self, frames: np.ndarray) -> "DeviceFrames":
         return DeviceFrames(self, frames)
 
-    def process_frames_device(self, dframes: "DeviceFrames", timing: bool = False):
+    def process_frames_device(self, dframes: "DeviceFrames", timing: int = 0):
+        """timing: 0 off, 1 every kernel, 100+k only kernel k (see kernel_times())."""
         n = dframes.n
         poses = np.zeros((n, 12))
         st = np.zeros(n, np.int32)
         info = np.zeros((n, 8), np.int32)
-        check(self.lib.vo_enable_kernel_timing(self.h, 1 if timing else 0))
+        check(self.lib.vo_enable_kernel_timing(self.h, int(timing)))
         check(self.lib.vo_process_frames_device(self.h, dframes.ptr, dframes.frame_bytes, n, _p(poses), _p(st),
                                                 _p(info)), "vo_process_frames_device")
         return poses.reshape(n, 3, 4), st, info
@@ -139,7 +140,7 @@ class Context:
         names = (C.c_char_p * 32)()
         ms = (C.c_float * 32)()
         k = self.lib.vo_last_kernel_times(self.h, names, ms, 32)
-        return {names[i].decode(): ms[i] for i in range(k)}
+        return {names[i].decode(): ms[i] for i in range(k) if ms[i] >= 0}
 
 
 class DeviceFrames:

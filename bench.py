@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""VO frames/sec (extract + match + pose) at 1241x376, 2000 keypoints/frame.
+
+One step = one pass of the full per-frame hot path (blur -> response -> NMS/top-N ->
+orientation/descriptor -> Hamming match -> 8-point RANSAC -> refit -> getPose ->
+trajectory update) over a synthetic KITTI-shape sequence of --frames frames that is
+already resident in HBM (uploaded before the timed region).  Frames are enqueued back
+to back on the ctx's HIP stream; the step ends with one stream synchronisation.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+replicas -- rank r processes its own sequence (seq = r) on GPU LOCAL_RANK with no
+data-path collective; the barrier and the max-over-ranks step time go over RCCL
+("nccl" backend).  value = frames processed by all ranks / max rank time (weak scaling).
+
+Also reported, on the same JSON line:
+  roofline      -- the dominant kernel's algorithmic bytes per launch / its average
+                   launch time (HIP events on the ctx stream, inside the timed region)
+                   against the MI355X HBM peak (8 TB/s)
+  cpu_baseline  -- the CPU oracle (a plain-C restatement of the reference path, one host
+                   core) timed on a bounded sample of the same sequence (rank 0, N=1)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+METRIC = "VO frames/sec (extract+match+pose), 1241×376 mono, 2000 kpts/frame"
+HBM_PEAK_GBS = 8000.0
+KERNELS = ["frame_begin", "stencil", "select", "describe", "match", "compact", "ransac_hyp0", "replay0",
+           "ransac_hyp1", "replay1", "refit", "pose_prep", "triangulate", "finalize"]
+
+
+def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray, N: int) -> float:
+    """Algorithmic HBM bytes per launch of `kernel`, averaged over the frames in `info`
+    (n_kps, n_matches, n_inliers, ...).  DESIGN.md section 4 derives each figure."""
+    n = info[:, 0].astype(np.float64)
+    M = info[:, 1].astype(np.float64)
+    if kernel == "stencil":
+        return float(2 * W * H + 12 * 4 * n.mean())            # frame in, blurred out, ~candidates
+    if kernel == "describe":
+        return float((86 + 8 + 68) * n.mean())                  # 86 sample px + kp in, 64+4 B out
+    if kernel == "match":
+        return float(4 * n.mean() + 4 * n.mean() + 4 * n.mean())  # prefixes prev + cur, result
+    if kernel.startswith("ransac_hyp"):
+        return float(32 * M.mean() + 36 * 4)                    # matches read once (+F out), L2 re-reads excluded
+    if kernel == "select":
+        return float(8 * 4 * n.mean() + 8 * n.mean())
+    return float(W * H + 80 * n.mean() + 24 * M.mean() + 96)   # whole-path figure
+
+
+def cpu_baseline(frames: np.ndarray, seq, budget_s: float) -> dict:
+    import oracle as O
+    cfg = O.config(seq.W, seq.H, K=seq.K.reshape(9))
+    vo = O.VO(cfg, gt=seq.gt())
+    t0 = time.perf_counter()
+    done = 0
+    for f in range(frames.shape[0]):
+        vo.process(frames[f])
+        done += 1
+        if time.perf_counter() - t0 > budget_s and done >= 2:
+            break
+    dt = time.perf_counter() - t0
+    vo.close()
+    return {"value": done / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"first {done} frames of the same sequence (seq 0, {seq.W}x{seq.H}, N=2000), "
+                      f"oracle/vo_oracle.c single thread, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=200, help="frames per step (one sequence pass)")
+    ap.add_argument("--width", type=int, default=1241)
+    ap.add_argument("--height", type=int, default=376)
+    ap.add_argument("--max-kpts", type=int, default=2000)
+    ap.add_argument("--motion", type=float, default=0.05, help="metres per frame of the synthetic camera")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--breakdown", action="store_true", help="print the per-kernel table to stderr")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from acs_visual_odometry_amd import Context
+    from acs_visual_odometry_amd.synth import SceneSequence
+
+    seq = SceneSequence(args.width, args.height, nframes=args.frames, seq=rank, step=args.motion)
+    frames = seq.frames()
+    ctx = Context(seq.W, seq.H, K=seq.K, max_kpts=args.max_kpts, device=local)
+    ctx.set_ground_truth(seq.gt())
+    dframes = ctx.device_frames(frames)
+
+    def step(timing=0):
+        ctx.reset()
+        return ctx.process_frames_device(dframes, timing=timing)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    # per-kernel breakdown (untimed pass): every kernel bracketed by events
+    _, st, info = step(timing=1)
+    kt = ctx.kernel_times()
+    per_frame = {k: kt.get(k, 0.0) for k in KERNELS}
+    dominant = max(per_frame, key=lambda k: per_frame[k])
+    kidx = KERNELS.index(dominant)
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        poses, st, info = step(timing=100 + kidx)       # two events around the dominant kernel
+    t1 = time.perf_counter()
+    barrier()
+    dt = t1 - t0
+    dom_ms = ctx.kernel_times().get(dominant, float("nan"))
+
+    if dist is not None:
+        import torch
+        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    total_frames = args.steps * args.frames * world
+    value = total_frames / dt
+
+    if rank == 0:
+        abytes = algorithmic_bytes(dominant, seq.W, seq.H, info, args.max_kpts)
+        achieved = abytes / (dom_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None, "avg_launch_ms": dom_ms,
+                "algorithmic_bytes_per_launch": abytes}
+        path_bytes = algorithmic_bytes("path", seq.W, seq.H, info, args.max_kpts)
+        cpu = None
+        if not args.no_cpu and world == 1:
+            cpu = cpu_baseline(frames, seq, args.cpu_seconds)
+        ok = int((st == 0).sum())
+        line = {
+            "metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8/f32/u32/f64", "data": "synthetic",
+            "config": {"workload": "kitti_1241x376_2000kpts_full_path" if (seq.W, seq.H) == (1241, 376)
+                       else f"{seq.W}x{seq.H}_{args.max_kpts}kpts_full_path",
+                       "frames_per_step": args.frames, "width": seq.W, "height": seq.H,
+                       "max_kpts": args.max_kpts, "sequence": f"scene seq=rank, {args.motion} m/frame",
+                       "parallelism": f"replicas: 1 sequence per GPU x {world}",
+                       "mean_kpts": float(info[:, 0].mean()), "mean_matches": float(info[:, 1].mean()),
+                       "mean_inliers": float(info[:, 2].mean()), "mean_hypotheses": float(info[:, 4].mean()),
+                       "frames_ok": ok},
+            "roofline": roof,
+            "path_roofline": {"algorithmic_bytes_per_frame": path_bytes,
+                              "achieved_GBs": path_bytes * value / world / 1e9,
+                              "frac": path_bytes * value / world / 1e9 / HBM_PEAK_GBS},
+            "kernels_ms_per_frame": {k: round(v, 5) for k, v in per_frame.items()},
+            "cpu_baseline": cpu,
+        }
+        if args.breakdown:
+            for k in KERNELS:
+                print(f"{k:14s} {per_frame[k] * 1e3:9.1f} us", file=sys.stderr)
+        print(json.dumps(line))
+    dframes.free()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -135,8 +135,9 @@ int  vo_device_upload(vo_ctx* ctx, void* dptr, const void* src, size_t bytes);
 /* Reset the trajectory state (frame counter, T_curr, model, prev descriptors). */
 int  vo_reset(vo_ctx* ctx);
 
-/* Per-kernel timing of the last vo_process_frames_device call (HIP events on the ctx
- * stream).  names/ms: up to cap entries; returns the number written. */
+/* Per-kernel timing of vo_process_frames_device (HIP events on the ctx stream).
+ * on: 0 off, 1 every kernel, 100+k only kernel k (two events per frame).  times: average
+ * ms per launch over the last call (-1 if not timed).  Returns the number written. */
 int  vo_last_kernel_times(vo_ctx* ctx, const char** names, float* ms, int cap);
 int  vo_enable_kernel_timing(vo_ctx* ctx, int on);
 
