@@ -131,13 +131,13 @@ void enqueue_extract(vo_ctx* c, const uint8_t* dframe, int write_response)
     vo::launch_describe(c->d, c->s);
 }
 
-void enqueue_ransac(vo_ctx* c)
+// stage calls borrow the ctx; they restore the trajectory state (and the zeroed
+// histogram / arrival counters the next frame expects) afterwards
+int restore_state(vo_ctx* c, const VoState* saved)
 {
-    vo::launch_ransac_hyp(c->d, 0, VO_HYP_CHUNK0, c->s);
-    vo::launch_ransac_replay(c->d, VO_HYP_CHUNK0, c->s);
-    vo::launch_ransac_hyp(c->d, VO_HYP_CHUNK0, c->max_hyp, c->s);
-    vo::launch_ransac_replay(c->d, c->max_hyp, c->s);
-    vo::launch_refit(c->d, c->s);
+    HIPCHK(hipMemsetAsync(c->d.hist, 0, sizeof(uint32_t) * VO_HIST_BINS, c->s));
+    HIPCHK(hipMemsetAsync(c->d.ctr, 0, sizeof(unsigned) * 4, c->s));
+    return write_state(c, saved);
 }
 
 // the full trajectory-loop iteration for one frame (VisualOdometry.cpp:68-189).
@@ -152,7 +152,7 @@ struct EvRec {
 void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev)
 {
     auto mark = [&](int k) {
-        if (!ev) return;
+        if (!ev) return;   // marks 0..7 bracket the 7 kernels of a frame
         if (ev->only >= 0 && k != ev->only && k != ev->only + 1) return;
         if (ev->used >= ev->pool->size()) {
             hipEvent_t e;
@@ -164,26 +164,18 @@ void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev)
     VoDev d = c->d;
     d.out = out;
     mark(0);
-    vo::launch_frame_begin(d, dframe ? VO_MODE_FRAME : VO_MODE_MISSING, c->s);
-    mark(1);
     if (dframe) {
-        vo::launch_stencil(d, dframe, 0, c->s); mark(2);
-        vo::launch_select(d, c->s); mark(3);
-        vo::launch_describe(d, c->s); mark(4);
-        vo::launch_match(d, c->s); mark(5);
-        vo::launch_compact(d, c->s); mark(6);
-        vo::launch_ransac_hyp(d, 0, VO_HYP_CHUNK0, c->s); mark(7);
-        vo::launch_ransac_replay(d, VO_HYP_CHUNK0, c->s); mark(8);
-        vo::launch_ransac_hyp(d, VO_HYP_CHUNK0, c->max_hyp, c->s); mark(9);
-        vo::launch_ransac_replay(d, c->max_hyp, c->s); mark(10);
-        vo::launch_refit(d, c->s); mark(11);
-        vo::launch_pose_prep(d, c->s); mark(12);
-        vo::launch_triangulate(d, c->s); mark(13);
+        vo::launch_stencil(d, dframe, 0, c->s); mark(1);
+        vo::launch_select(d, c->s); mark(2);
+        vo::launch_describe(d, c->s); mark(3);
+        vo::launch_match(d, c->s); mark(4);
+        vo::launch_ransac(d, c->max_hyp, c->s); mark(5);
+        vo::launch_refit(d, 1, c->s); mark(6);
+        vo::launch_triangulate(d, c->s); mark(7);
     } else {
-        for (int k = 2; k <= 13; ++k) mark(k);
+        vo::launch_missing(d, c->s);
+        for (int k = 1; k <= 7; ++k) mark(k);
     }
-    vo::launch_finalize(d, c->s);
-    mark(14);
 }
 
 int ensure_out(vo_ctx* c, int n)
@@ -306,6 +298,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc(&d.inl, N);
     rc |= dalloc(&d.model_p, (size_t)N * 4);
     rc |= dalloc(&d.st, 1);
+    rc |= dalloc(&d.ctr, 4);
     if (rc != VO_OK) return bail(VO_ERR_HIP);
     const std::vector<uint16_t>& tab = maxit_table(N, k.ransac_p);
     if (dalloc(&c->tab_dev, tab.size()) != VO_OK) return bail(VO_ERR_HIP);
@@ -320,9 +313,8 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
         (void)hipMemset(d.pre[s], 0, sizeof(uint32_t) * N);
     }
     if (ensure_out(c, 16) != VO_OK) return bail(VO_ERR_HIP);
-    VoState h;
-    init_state(c, &h);
-    if (hip_ok(hipMemcpy(d.st, &h, sizeof(h), hipMemcpyHostToDevice)) != VO_OK) return bail(VO_ERR_HIP);
+    (void)hipMemset(d.ctr, 0, sizeof(unsigned) * 4);
+    if (vo_reset(c) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipDeviceSynchronize()) != VO_OK) return bail(VO_ERR_HIP);
     *out = c;
     return VO_OK;
@@ -336,7 +328,7 @@ void vo_destroy(vo_ctx* c)
     VoDev& d = c->d;
     void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.hist, d.kps[0], d.kps[1], d.desc[0], d.desc[1],
                     d.pre[0], d.pre[1], d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.model_p,
-                    d.st, (void*)d.gt, c->tab_dev, c->out_dev};
+                    d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->out_host) (void)hipHostFree(c->out_host);
@@ -352,7 +344,13 @@ int vo_reset(vo_ctx* c)
     HIPCHK(hipSetDevice(c->cfg.device));
     VoState h;
     init_state(c, &h);
-    return write_state(c, &h);
+    int rc = write_state(c, &h);
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(c->d.ctr, 0, sizeof(unsigned) * 4, c->s));
+    vo::launch_frame_begin(c->d, VO_MODE_FRAME, c->s);     // frame 0 set up on the device
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->s));
+    return VO_OK;
 }
 
 int vo_set_ground_truth(vo_ctx* c, const double* poses12, int n)
@@ -376,13 +374,17 @@ int vo_extract(vo_ctx* c, const uint8_t* gray, size_t stride, vo_kp* kps, uint64
 {
     if (!c || !gray || !n) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    int rc = upload_frame(c, gray, stride);
+    VoState saved, h;
+    int rc = read_state(c, &saved);
+    if (rc) return rc;
+    rc = upload_frame(c, gray, stride);
     if (rc) return rc;
     vo::launch_frame_begin(c->d, VO_MODE_EXTRACT, c->s);
     enqueue_extract(c, c->d.frame_in, 0);
     HIPCHK(hipGetLastError());
-    VoState h;
     rc = read_state(c, &h);
+    if (rc) return rc;
+    rc = restore_state(c, &saved);
     if (rc) return rc;
     if (h.status != VO_STATUS_OK) return VO_ERR_CAPACITY;
     const int nk = h.n_kps[0];
@@ -392,7 +394,6 @@ int vo_extract(vo_ctx* c, const uint8_t* gray, size_t stride, vo_kp* kps, uint64
     if (blurred)
         HIPCHK(hipMemcpy(blurred, c->d.blurred, (size_t)c->cfg.width * c->cfg.height, hipMemcpyDeviceToHost));
     // vo_extract leaves the trajectory state untouched except slot 0 contents
-    h.status = VO_STATUS_OK;
     return VO_OK;
 }
 
@@ -400,7 +401,10 @@ int vo_response(vo_ctx* c, const uint8_t* gray, size_t stride, float* R)
 {
     if (!c || !gray || !R) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    int rc = upload_frame(c, gray, stride);
+    VoState saved;
+    int rc = read_state(c, &saved);
+    if (rc) return rc;
+    rc = upload_frame(c, gray, stride);
     if (rc) return rc;
     const size_t np = (size_t)c->cfg.width * c->cfg.height;
     HIPCHK(hipMemsetAsync(c->d.response, 0, np * sizeof(float), c->s));
@@ -409,7 +413,7 @@ int vo_response(vo_ctx* c, const uint8_t* gray, size_t stride, float* R)
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(R, c->d.response, np * sizeof(float), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
-    return VO_OK;
+    return restore_state(c, &saved);
 }
 
 int vo_match(vo_ctx* c, const uint64_t* d_prev, int n_prev, const uint64_t* d_cur, int n_cur, vo_match_t* out, int* m)
@@ -435,7 +439,6 @@ int vo_match(vo_ctx* c, const uint64_t* d_prev, int n_prev, const uint64_t* d_cu
     rc = write_state(c, &h);
     if (rc) return rc;
     vo::launch_match(c->d, c->s);
-    vo::launch_compact(c->d, c->s);
     HIPCHK(hipGetLastError());
     rc = read_state(c, &h);
     if (rc) return rc;
@@ -443,7 +446,7 @@ int vo_match(vo_ctx* c, const uint64_t* d_prev, int n_prev, const uint64_t* d_cu
     if (out && h.M) HIPCHK(hipMemcpy(out, c->d.match_pairs, sizeof(vo_match_t) * h.M, hipMemcpyDeviceToHost));
     // restore the trajectory bookkeeping (stage calls do not advance the loop)
     saved.n_kps[0] = h.n_kps[0]; saved.n_kps[1] = h.n_kps[1];
-    return write_state(c, &saved);
+    return restore_state(c, &saved);
 }
 
 int vo_ransac_F(vo_ctx* c, const double* pts, int m, uint64_t seed, double F[9], int* fitted, int32_t* inlier_idx,
@@ -462,7 +465,8 @@ int vo_ransac_F(vo_ctx* c, const double* pts, int m, uint64_t seed, double F[9],
     h.frame_seed = seed; h.bestk = -1; h.need_more = 0; h.fitted = 0; h.n_inl = 0;
     rc = write_state(c, &h);
     if (rc) return rc;
-    enqueue_ransac(c);
+    vo::launch_ransac(c->d, c->max_hyp, c->s);
+    vo::launch_refit(c->d, 0, c->s);
     HIPCHK(hipGetLastError());
     rc = read_state(c, &h);
     if (rc) return rc;
@@ -478,7 +482,7 @@ int vo_ransac_F(vo_ctx* c, const double* pts, int m, uint64_t seed, double F[9],
     // the model (F + inliers) persists like FundamentalMatrix model (VisualOdometry.cpp:49)
     saved.model_n = h.model_n;
     std::memcpy(saved.model_F, h.model_F, sizeof(h.model_F));
-    return write_state(c, &saved);
+    return restore_state(c, &saved);
 }
 
 int vo_pose(vo_ctx* c, const double F[9], const float* p1, const float* p2, int n, double scale, double R[9],
@@ -505,7 +509,6 @@ int vo_pose(vo_ctx* c, const double F[9], const float* p1, const float* p2, int 
     if (rc) return rc;
     vo::launch_pose_prep(c->d, c->s);
     vo::launch_triangulate(c->d, c->s);
-    vo::launch_finalize(c->d, c->s);
     HIPCHK(hipGetLastError());
     rc = read_state(c, &h);
     if (rc) return rc;
@@ -517,7 +520,7 @@ int vo_pose(vo_ctx* c, const double F[9], const float* p1, const float* p2, int 
         if (t) std::memcpy(t, h.pose_t, sizeof(h.pose_t));
     }
     if (counts4) std::memcpy(counts4, h.counts4, sizeof(h.counts4));
-    rc = write_state(c, &saved);
+    rc = restore_state(c, &saved);
     return ret != VO_OK ? ret : rc;
 }
 

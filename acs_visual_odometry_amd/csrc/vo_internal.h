@@ -99,6 +99,7 @@ struct VoDev {
     const double* gt;
     VoState* st;
     VoFrameOut* out;
+    unsigned* ctr;        // in-launch arrival counters: [0] match, [1] ransac, [2] triangulate
 };
 
 // launch wrappers (vo_kernels.hip)
@@ -108,14 +109,12 @@ void launch_frame_begin(const VoDev& d, int mode, hipStream_t s);
 void launch_stencil(const VoDev& d, const uint8_t* frame, int write_response, hipStream_t s);
 void launch_select(const VoDev& d, hipStream_t s);
 void launch_describe(const VoDev& d, hipStream_t s);
-void launch_match(const VoDev& d, hipStream_t s);
-void launch_compact(const VoDev& d, hipStream_t s);
-void launch_ransac_hyp(const VoDev& d, int k0, int k1, hipStream_t s);
-void launch_ransac_replay(const VoDev& d, int k1, hipStream_t s);
-void launch_refit(const VoDev& d, hipStream_t s);
+void launch_match(const VoDev& d, hipStream_t s);          // + ordered compaction (last workgroup)
+void launch_ransac(const VoDev& d, int nhyp, hipStream_t s); // all hypotheses + replay (last workgroup)
+void launch_refit(const VoDev& d, int with_pose, hipStream_t s);
 void launch_pose_prep(const VoDev& d, hipStream_t s);
-void launch_triangulate(const VoDev& d, hipStream_t s);
-void launch_finalize(const VoDev& d, hipStream_t s);
+void launch_triangulate(const VoDev& d, hipStream_t s);    // + finalize / next-frame setup
+void launch_missing(const VoDev& d, hipStream_t s);
 void launch_selftest_arith(const float* fa, const float* fb, float* fo, const double* da,
                            const double* db, double* dout, int n, hipStream_t s);
 int kernel_count();

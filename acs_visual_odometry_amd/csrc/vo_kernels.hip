@@ -688,111 +688,160 @@ __global__ void __launch_bounds__(256) k_describe(VoDev d)
 }
 
 // ---------------------------------------------------------------------------
-// match: brute-force Hamming top-2 + Lowe ratio, one query per wave
-// feature_matching_parallel.cpp:39-113; key = dist<<16 | j so min key = (min dist, first j)
+// in-launch hand-off: the last workgroup to arrive consumes what the others produced.
+// Valid form of MI355X_MICROARCH.md "Workgroup dispatch ... visibility" (table row 1):
+// payload stored sc1 (agent-scope relaxed atomic stores), every storing wave drains
+// vmcnt(0), one lane per workgroup adds to ONE unsharded counter, the workgroup whose
+// add returns total-1 loads the payload with sc1 loads only.  The counter is reset by
+// that last workgroup for the next launch (kernel boundary orders it).
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) int gi32;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+__device__ __forceinline__ void st_sc1(int* p, int v)
+{
+    __hip_atomic_store((gi32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_sc1(const int* p)
+{
+    return __hip_atomic_load((gi32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool arrive_last(unsigned* ctr, unsigned total, unsigned* s_flag)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned prev = __hip_atomic_fetch_add((gu32*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_flag = (prev == total - 1) ? 1u : 0u;
+    }
+    __syncthreads();
+    return *s_flag != 0u;
+}
+
+// next frame's bookkeeping (VisualOdometry.cpp:68-100 loop head): status, slot, sampler
+// seed, counters, histogram.  Run by the workgroup that finalizes the current frame.
+__device__ void setup_next_frame(const VoDev& d, VoState* st)
+{
+    for (int i = threadIdx.x; i < VO_HIST_BINS; i += blockDim.x) d.hist[i] = 0u;
+    if (threadIdx.x == 0) {
+        const int f = st->frame;        // already incremented
+        st->mode = VO_MODE_FRAME;
+        st->status = f == 0 ? VO_STATUS_FIRST : VO_STATUS_OK;
+        st->cur = f == 0 ? 0 : 1 - st->prev;
+        st->frame_seed = mix64(d.seed + 0x632BE59BD9B4E019ULL * (uint64_t)(f + 1));
+        st->cand_count = 0; st->M = 0; st->n_inl = 0; st->fitted = 0; st->degenerate = 0;
+        st->bestk = -1; st->n_eval = 0; st->need_more = 0;
+        for (int c = 0; c < 4; ++c) st->counts4[c] = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// match: brute-force Hamming top-2 + Lowe ratio, one query per wave; the last workgroup
+// compacts the accepted queries in ascending order into matches + f64 points.
+// feature_matching_parallel.cpp:39-113; VisualOdometry.cpp:100-123.
+// key = dist<<16 | j, so the min key is (min dist, first j) and the 2nd key gives `second`
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_match(VoDev d)
 {
     VoState* st = d.st;
     if (st->status != VO_STATUS_OK) return;
+    __shared__ unsigned s_last;
+    __shared__ int s_wsum[4];
     const int prev = st->prev, cur = st->cur;
     const int n1 = st->n_kps[prev], n2 = st->n_kps[cur];
     const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (q >= n1) return;
-    uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
-    if (d.match_bits == 32) {
-        const uint32_t qv = d.pre[prev][q];
-        const uint32_t* cand = d.pre[cur];
-        for (int j = lane; j < n2; j += 64) {
-            uint32_t key = ((uint32_t)__popc(qv ^ cand[j]) << 16) | (uint32_t)j;
-            if (key < m1) { m2 = m1; m1 = key; } else if (key < m2) m2 = key;
+    if (q < n1) {
+        uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
+        if (d.match_bits == 32) {
+            const uint32_t qv = d.pre[prev][q];
+            const uint32_t* cand = d.pre[cur];
+            for (int j = lane; j < n2; j += 64) {
+                uint32_t key = ((uint32_t)__popc(qv ^ cand[j]) << 16) | (uint32_t)j;
+                if (key < m1) { m2 = m1; m1 = key; } else if (key < m2) m2 = key;
+            }
+        } else {
+            const uint64_t* qd = d.desc[prev] + (size_t)q * 8;
+            uint64_t qw[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) qw[w] = qd[w];
+            const uint64_t* cd = d.desc[cur];
+            for (int j = lane; j < n2; j += 64) {
+                int dist = 0;
+#pragma unroll
+                for (int w = 0; w < 8; ++w) dist += __popcll(qw[w] ^ cd[(size_t)j * 8 + w]);
+                uint32_t key = ((uint32_t)dist << 16) | (uint32_t)j;
+                if (key < m1) { m2 = m1; m1 = key; } else if (key < m2) m2 = key;
+            }
         }
-    } else {
-        const uint64_t* qd = d.desc[prev] + (size_t)q * 8;
-        uint64_t qw[8];
 #pragma unroll
-        for (int w = 0; w < 8; ++w) qw[w] = qd[w];
-        const uint64_t* cd = d.desc[cur];
-        for (int j = lane; j < n2; j += 64) {
-            int dist = 0;
-#pragma unroll
-            for (int w = 0; w < 8; ++w) dist += __popcll(qw[w] ^ cd[(size_t)j * 8 + w]);
-            uint32_t key = ((uint32_t)dist << 16) | (uint32_t)j;
-            if (key < m1) { m2 = m1; m1 = key; } else if (key < m2) m2 = key;
+        for (int off = 32; off >= 1; off >>= 1) {
+            uint32_t o1 = __shfl_xor(m1, off), o2 = __shfl_xor(m2, off);
+            uint32_t n1v = min(m1, o1);
+            uint32_t n2v = min(max(m1, o1), min(m2, o2));
+            m1 = n1v; m2 = n2v;
+        }
+        if (lane == 0) {
+            int res = -1;
+            if (m1 != 0xFFFFFFFFu && m2 != 0xFFFFFFFFu) {
+                int d1 = (int)(m1 >> 16), d2 = (int)(m2 >> 16);
+                if ((float)d1 < d.ratio * (float)d2) res = (int)(m1 & 0xFFFF);
+            }
+            st_sc1(d.match_j + q, res);
         }
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        uint32_t o1 = __shfl_xor(m1, off), o2 = __shfl_xor(m2, off);
-        uint32_t n1v = min(m1, o1);
-        uint32_t n2v = min(max(m1, o1), min(m2, o2));
-        m1 = n1v; m2 = n2v;
-    }
-    if (lane == 0) {
-        int res = -1;
-        if (m1 != 0xFFFFFFFFu && m2 != 0xFFFFFFFFu) {
-            int d1 = (int)(m1 >> 16), d2 = (int)(m2 >> 16);
-            if ((float)d1 < d.ratio * (float)d2) res = (int)(m1 & 0xFFFF);
-        }
-        d.match_j[q] = res;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// compact: ordered stream compaction of accepted queries -> matches + f64 points
-// (VisualOdometry.cpp:100-123); 1 workgroup of 1024
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(1024) k_compact(VoDev d)
-{
-    VoState* st = d.st;
-    if (st->status != VO_STATUS_OK) return;
-    __shared__ int s_wsum[16];
-    __shared__ int s_base;
-    const int prev = st->prev, cur = st->cur;
-    const int n1 = st->n_kps[prev];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (!arrive_last(d.ctr + 0, gridDim.x, &s_last)) return;
+    // ---- last workgroup: ordered compaction, thread t owns queries [t*per, (t+1)*per) ----
+    const int tid = threadIdx.x, wave = tid >> 6;
     const int2* kp1 = d.kps[prev];
     const int2* kp2 = d.kps[cur];
-    if (tid == 0) s_base = 0;
+    const int per = (n1 + 255) / 256;            // <= 16 (N <= 4096)
+    const int q0 = tid * per;
+    int js[16];
+    int cnt = 0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        int i = q0 + u;
+        js[u] = (u < per && i < n1) ? ld_sc1(d.match_j + i) : -1;
+        cnt += js[u] >= 0;
+    }
+    // block exclusive scan of cnt (wave inclusive scan + wave totals)
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        int v = __shfl_up(incl, off);
+        if (lane >= off) incl += v;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
     __syncthreads();
-    for (int b0 = 0; b0 < n1; b0 += 1024) {
-        int i = b0 + tid;
-        int j = i < n1 ? d.match_j[i] : -1;
-        bool f = j >= 0;
-        unsigned long long bal = ballot64(f);
-        int pre = __popcll(bal & ((1ull << lane) - 1ull));
-        if (lane == 0) s_wsum[wave] = __popcll(bal);
-        __syncthreads();
-        int woff = 0;
-        for (int w = 0; w < wave; ++w) woff += s_wsum[w];
-        int pos = s_base + woff + pre;
-        if (f) {
+    int pos = incl - cnt;
+    for (int w = 0; w < wave; ++w) pos += s_wsum[w];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        if (js[u] >= 0) {
+            int i = q0 + u, j = js[u];
             d.match_pairs[pos] = make_int2(i, j);
             int2 a = kp1[i], b = kp2[j];
-            double* p = d.pts + 4 * (size_t)pos;
-            p[0] = (double)a.x; p[1] = (double)a.y; p[2] = (double)b.x; p[3] = (double)b.y;
+            double2* p = reinterpret_cast<double2*>(d.pts + 4 * (size_t)pos);
+            p[0] = make_double2((double)a.x, (double)a.y);
+            p[1] = make_double2((double)b.x, (double)b.y);
+            ++pos;
         }
-        __syncthreads();
-        if (tid == 0) {
-            int tot = 0;
-            for (int w = 0; w < 16; ++w) tot += s_wsum[w];
-            s_base += tot;
-        }
-        __syncthreads();
     }
     if (tid == 0) {
-        int M = s_base;
+        int M = ((s_wsum[0] + s_wsum[1]) + s_wsum[2]) + s_wsum[3];
         st->M = M;
         st->scored = (M / d.T) * d.T;
         if (M < 8) st->status = VO_STATUS_FEW_MATCHES;
+        d.ctr[0] = 0u;
     }
 }
 
 // ---------------------------------------------------------------------------
-// RANSAC hypotheses: one hypothesis per wavefront (Ransac::run, ransac.cpp:138-176)
-// lanes 0..7 hold the 8 design-matrix rows for the Gauss-Jordan null vector; all
-// 64 lanes then score the Sampson error over the scored matches, counted by ballot.
+// RANSAC: every hypothesis k < max_hyp in one launch, one per wavefront (ransac.cpp:138-176);
+// the last workgroup replays the adaptive stopping rule (ransac.cpp:139-190) over the
+// per-hypothesis counts, which selects exactly the sequential loop's best hypothesis.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double shfl_d(double v, int src) { return __shfl(v, src); }
 __device__ __forceinline__ double shfl_xor_d(double v, int m) { return __shfl_xor(v, m); }
@@ -894,200 +943,6 @@ __device__ void fit_F8_wave(const double* __restrict__ pts, const int s8[8], int
     rank2(F);
 }
 
-__global__ void __launch_bounds__(256) k_ransac_hyp(VoDev d, int k0, int k1)
-{
-    VoState* st = d.st;
-    if (st->status != VO_STATUS_OK) return;
-    if (k0 > 0 && !st->need_more) return;
-    const int k = k0 + blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (k >= k1) return;
-    const int lane = threadIdx.x & 63;
-    const int M = st->M, scored = st->scored;
-    int s8[8];
-    sample8(st->frame_seed, k, M, s8);
-    double F[9];
-    fit_F8_wave(d.pts, s8, lane, F);
-    if (lane < 9) {
-        double v = 0.0;
-#pragma unroll
-        for (int c = 0; c < 9; ++c) if (c == lane) v = F[c];
-        d.hypF[(size_t)k * 9 + lane] = v;
-    }
-    const double thr = d.sampson_thr;
-    int cnt = 0;
-    for (int b = 0; b < scored; b += 64) {
-        int i = b + lane;
-        bool in = false;
-        if (i < scored) {
-            const double2* p = reinterpret_cast<const double2*>(d.pts + 4 * (size_t)i);
-            double2 a = p[0], c = p[1];
-            in = sampson(F, a.x, a.y, c.x, c.y) < thr;
-        }
-        cnt += __popcll(ballot64(in));
-    }
-    if (lane == 0) d.counts[k] = cnt;
-}
-
-// sequential replay of the adaptive stopping rule over the per-hypothesis counts
-// (ransac.cpp:139-190): picks the same best hypothesis as the sequential loop.
-__global__ void k_ransac_replay(VoDev d, int k1)
-{
-    VoState* st = d.st;
-    if (threadIdx.x != 0 || st->status != VO_STATUS_OK) return;
-    int k, maxit, best, bestk;
-    if (k1 <= VO_HYP_CHUNK0 || !st->need_more) {
-        if (k1 > VO_HYP_CHUNK0) return;   // chunk 1 not needed: state is final
-        k = 0; maxit = d.maxit_initial; best = 0; bestk = -1;
-    } else {
-        k = st->k_done; maxit = st->maxit; best = st->best; bestk = st->bestk;
-    }
-    const int M = st->M;
-    const uint16_t* tab = d.maxit_tab + (size_t)M * (M + 1) / 2;
-    for (; k < maxit && k < k1; ++k) {
-        int c = d.counts[k];
-        if (c > best) {
-            best = c; bestk = k;
-            uint16_t u = tab[best];
-            if (u != 0xFFFFu) maxit = (int)u;
-        }
-    }
-    st->k_done = k; st->maxit = maxit; st->best = best; st->bestk = bestk;
-    st->need_more = (k < maxit) ? 1 : 0;
-    st->n_eval = k;
-}
-
-// ---------------------------------------------------------------------------
-// refit on the best hypothesis' inliers (model.fit(bestInlierSet), ransac.cpp:193)
-// one workgroup of 256; reductions in the fixed order mirrored by the oracle
-// ---------------------------------------------------------------------------
-__device__ double block_sum256(double v, double* s_w)
-{
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = v + shfl_xor_d(v, off);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    __syncthreads();
-    if (lane == 0) s_w[wave] = v;
-    __syncthreads();
-    return ((s_w[0] + s_w[1]) + s_w[2]) + s_w[3];
-}
-
-__global__ void __launch_bounds__(256) k_refit(VoDev d)
-{
-    VoState* st = d.st;
-    if (st->status != VO_STATUS_OK) return;
-    __shared__ double s_w[4];
-    __shared__ int s_wc[4];
-    __shared__ int s_base;
-    __shared__ double s_F[9];
-    __shared__ double s_A[81], s_V[81];
-    __shared__ double s_prm[6];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int bestk = st->bestk;
-    const int scored = st->scored;
-    if (bestk < 0) {
-        if (tid == 0) { st->n_inl = 0; st->fitted = 0; }
-        return;
-    }
-    if (tid < 9) s_F[tid] = d.hypF[(size_t)bestk * 9 + tid];
-    if (tid == 0) s_base = 0;
-    __syncthreads();
-    double F[9];
-#pragma unroll
-    for (int c = 0; c < 9; ++c) F[c] = s_F[c];
-    const double thr = d.sampson_thr;
-    for (int b0 = 0; b0 < scored; b0 += 256) {
-        int i = b0 + tid;
-        bool in = false;
-        if (i < scored) {
-            const double* p = d.pts + 4 * (size_t)i;
-            in = sampson(F, p[0], p[1], p[2], p[3]) < thr;
-        }
-        unsigned long long bal = ballot64(in);
-        if (lane == 0) s_wc[wave] = __popcll(bal);
-        __syncthreads();
-        int off = s_base;
-        for (int w = 0; w < wave; ++w) off += s_wc[w];
-        if (in) d.inl[off + __popcll(bal & ((1ull << lane) - 1ull))] = i;
-        __syncthreads();
-        if (tid == 0) s_base += ((s_wc[0] + s_wc[1]) + s_wc[2]) + s_wc[3];
-        __syncthreads();
-    }
-    const int n = s_base;
-    if (tid == 0) st->n_inl = n;
-    if (n < 8) {                  // fit() returns early: previous model stays (quirk 9)
-        if (tid == 0) st->fitted = 0;
-        return;
-    }
-    const int32_t* idx = d.inl;
-    double mean[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        double s = 0.0;
-        for (int i = tid; i < n; i += 256) s = s + d.pts[4 * (size_t)idx[i] + c];
-        mean[c] = block_sum256(s, s_w) / (double)n;
-    }
-    double scl[2];
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-        double s = 0.0;
-        for (int i = tid; i < n; i += 256) {
-            const double* p = d.pts + 4 * (size_t)idx[i];
-            double a = p[2 * g] - mean[2 * g], b = p[2 * g + 1] - mean[2 * g + 1];
-            s = s + (a * a + b * b);
-        }
-        scl[g] = block_sum256(s, s_w);
-    }
-    const double sc1 = sqrt(2.0) / sqrt(scl[0] / (double)n);
-    const double sc2 = sqrt(2.0) / sqrt(scl[1] / (double)n);
-    const double o1x = -(sc1 * mean[0]), o1y = -(sc1 * mean[1]), o2x = -(sc2 * mean[2]), o2y = -(sc2 * mean[3]);
-    double acc[45];
-#pragma unroll
-    for (int e = 0; e < 45; ++e) acc[e] = 0.0;
-    for (int i = tid; i < n; i += 256) {
-        const double* p = d.pts + 4 * (size_t)idx[i];
-        double a[9];
-        design_row(sc1 * p[0] + o1x, sc1 * p[1] + o1y, sc2 * p[2] + o2x, sc2 * p[3] + o2y, a);
-        int e = 0;
-#pragma unroll
-        for (int u = 0; u < 9; ++u)
-#pragma unroll
-            for (int v = u; v < 9; ++v) { acc[e] = acc[e] + a[u] * a[v]; ++e; }
-    }
-    {
-        int e = 0;
-#pragma unroll
-        for (int u = 0; u < 9; ++u)
-#pragma unroll
-            for (int v = u; v < 9; ++v) {
-                double x = block_sum256(acc[e], s_w);
-                ++e;
-                if (tid == 0) { s_A[u * 9 + v] = x; s_A[v * 9 + u] = x; }
-            }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        jacobi_eig<9>(s_A, s_V);
-        int k = argmin_diag<9>(s_A);
-        double f[9];
-        for (int i = 0; i < 9; ++i) f[i] = s_V[i * 9 + k];
-        double Fn[9];
-        denormalize(f, sc1, mean[0], mean[1], sc2, mean[2], mean[3], Fn);
-        rank2(Fn);
-        for (int i = 0; i < 9; ++i) st->model_F[i] = Fn[i];
-        st->fitted = 1;
-        st->model_n = n;
-    }
-    for (int i = tid; i < n; i += 256) {
-        const double* p = d.pts + 4 * (size_t)idx[i];
-        float* o = d.model_p + 4 * (size_t)i;
-        o[0] = (float)p[0]; o[1] = (float)p[1]; o[2] = (float)p[2]; o[3] = (float)p[3];
-    }
-    (void)s_prm;
-}
-
-// ---------------------------------------------------------------------------
-// pose: E = K^T F K, SVD, candidates (PoseUpdate.hpp:61-96); 1 thread
-// ---------------------------------------------------------------------------
 __device__ void svd3(const double* A, double* U, double* S, double* Vt)
 {
     double AtA[9], V[9];
@@ -1131,96 +986,6 @@ __device__ void svd3(const double* A, double* U, double* S, double* Vt)
         }
 }
 
-__global__ void k_pose_prep(VoDev d)
-{
-    VoState* st = d.st;
-    if (threadIdx.x != 0 || st->status != VO_STATUS_OK) return;
-    if (st->model_n < 8) { st->status = VO_STATUS_FEW_INLIERS; return; }
-    double E[9], G[9];
-    mtm3(d.K, st->model_F, G);
-    mm3(G, d.K, E);
-    double nn = 0.0;
-    for (int i = 0; i < 9; ++i) nn = nn + E[i] * E[i];
-    nn = sqrt(nn);
-    double inv = 1.0 / nn;
-    int nz = 0;
-    for (int i = 0; i < 9; ++i) { E[i] = E[i] * inv; nz += (E[i] != 0.0); }
-    if (nz < 5) { st->status = VO_STATUS_DEGENERATE; st->degenerate = 1; return; }
-    double U[9], S[3], Vt[9];
-    svd3(E, U, S, Vt);
-    if (det3(U) < 0) for (int i = 0; i < 9; ++i) U[i] = -U[i];
-    if (det3(Vt) < 0) for (int i = 0; i < 9; ++i) Vt[i] = -Vt[i];
-    const double W[9] = {0, -1, 0, 1, 0, 0, 0, 0, 1};
-    const double Wt[9] = {0, 1, 0, -1, 0, 0, 0, 0, 1};
-    double R1[9], R2[9], T[9];
-    mm3(U, W, T); mm3(T, Vt, R1);
-    mm3(U, Wt, T); mm3(T, Vt, R2);
-    if (det3(R1) < 0) for (int i = 0; i < 9; ++i) R1[i] = -R1[i];
-    if (det3(R2) < 0) for (int i = 0; i < 9; ++i) R2[i] = -R2[i];
-    for (int i = 0; i < 9; ++i) { st->R1[i] = R1[i]; st->R2[i] = R2[i]; }
-    st->t[0] = U[2]; st->t[1] = U[5]; st->t[2] = U[8];
-    for (int c = 0; c < 4; ++c) st->counts4[c] = 0;
-}
-
-// cheirality test of the 4 (R, t) candidates: one model inlier per thread
-// (cv::undistortPoints + cv::triangulatePoints + depth test, PoseUpdate.hpp:101-147)
-__global__ void __launch_bounds__(256) k_triangulate(VoDev d)
-{
-    VoState* st = d.st;
-    if (st->status != VO_STATUS_OK) return;
-    __shared__ int s_cnt[4];
-    const int n = st->model_n;
-    if (blockIdx.x * 256 >= n) return;
-    if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < n) {
-        const double fx = d.K[0], fy = d.K[4], cx = d.K[2], cy = d.K[5];
-        const double ifx = 1.0 / fx, ify = 1.0 / fy;
-        const float* p = d.model_p + 4 * (size_t)i;
-        float x1 = (float)(((double)p[0] - cx) * ifx), y1 = (float)(((double)p[1] - cy) * ify);
-        float x2 = (float)(((double)p[2] - cx) * ifx), y2 = (float)(((double)p[3] - cy) * ify);
-        double X1 = x1, Y1 = y1, X2 = x2, Y2 = y2;
-        for (int cnd = 0; cnd < 4; ++cnd) {
-            const double* R = cnd < 2 ? st->R1 : st->R2;
-            double sg = (cnd & 1) ? -1.0 : 1.0;
-            double tc0 = st->t[0] * sg, tc1 = st->t[1] * sg, tc2 = st->t[2] * sg;
-            double P2[12] = {R[0], R[1], R[2], tc0, R[3], R[4], R[5], tc1, R[6], R[7], R[8], tc2};
-            const double P1[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
-            double A[16];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                A[0 * 4 + k] = X1 * P1[8 + k] - P1[0 + k];
-                A[1 * 4 + k] = Y1 * P1[8 + k] - P1[4 + k];
-                A[2 * 4 + k] = X2 * P2[8 + k] - P2[0 + k];
-                A[3 * 4 + k] = Y2 * P2[8 + k] - P2[4 + k];
-            }
-            double AtA[16], V[16];
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    AtA[a * 4 + b] = ((A[0 * 4 + a] * A[0 * 4 + b] + A[1 * 4 + a] * A[1 * 4 + b]) + A[2 * 4 + a] * A[2 * 4 + b]) +
-                                     A[3 * 4 + a] * A[3 * 4 + b];
-            jacobi_eig<4>(AtA, V);
-            int km = argmin_diag<4>(AtA);
-            double X[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (c == km) { X[0] = V[0 * 4 + c]; X[1] = V[1 * 4 + c]; X[2] = V[2 * 4 + c]; X[3] = V[3 * 4 + c]; }
-            double h0 = (double)(float)X[0], h1 = (double)(float)X[1], h2 = (double)(float)X[2], h3 = (double)(float)X[3];
-            double w = h3;
-            if (fabs(w) < 1e-6) continue;
-            double iw = 1.0 / w;
-            double Xh0 = h0 * iw, Xh1 = h1 * iw, Xh2 = h2 * iw;
-            double z1 = Xh2;
-            double z2 = ((R[6] * Xh0 + R[7] * Xh1) + R[8] * Xh2) + tc2;
-            if (z1 > 0 && z2 > 0) atomicAdd(&s_cnt[cnd], 1);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 4 && s_cnt[threadIdx.x]) atomicAdd(&st->counts4[threadIdx.x], s_cnt[threadIdx.x]);
-}
 
 // 4x4 helpers for the GT scale (mirror of oracle inv4 / mm4)
 __device__ void mm4(const double* A, const double* B, double* C)
@@ -1253,75 +1018,491 @@ __device__ void inv4(const double* M, double* Inv)
         for (int j = 0; j < 4; ++j) Inv[i * 4 + j] = a[i][j + 4];
 }
 
-// finalize: pick the candidate, scale t, compose T_curr, emit the pose row
-// (PoseUpdate.hpp:142-178, VisualOdometry.cpp:106-186); 1 thread
-__global__ void k_finalize(VoDev d)
+__global__ void __launch_bounds__(64) k_ransac_hyp(VoDev d, int k0, int k1, int nhyp)
 {
     VoState* st = d.st;
-    if (threadIdx.x != 0) return;
-    const int status = st->status;
-    const int mode = st->mode;
-    if (mode == VO_MODE_EXTRACT) return;
-    double* Tc = st->Tcurr;
-    double Rf[9], tf[3];
-    bool have_pose = false;
-    if (status == VO_STATUS_OK) {
-        int maxPos = -1, bestc = 0;
-        for (int c = 0; c < 4; ++c) if (st->counts4[c] > maxPos) { maxPos = st->counts4[c]; bestc = c; }
-        const double* R = bestc < 2 ? st->R1 : st->R2;
-        double sg = (bestc & 1) ? -1.0 : 1.0;
-        for (int i = 0; i < 9; ++i) Rf[i] = R[i];
-        if (det3(Rf) < 0) for (int i = 0; i < 9; ++i) Rf[i] = -Rf[i];
-        tf[0] = st->t[0] * sg; tf[1] = st->t[1] * sg; tf[2] = st->t[2] * sg;
-        double scale = st->scale_override;
-        if (mode == VO_MODE_FRAME) {
-            scale = 1.0;
-            const int fi = st->frame, last = st->last_valid;
-            if (d.gt_n > 0 && fi < d.gt_n && last < d.gt_n) {
-                double Gi[16], Gl[16], Ii[16], Tr[16];
-                for (int r = 0; r < 16; ++r) {
-                    Gi[r] = r < 12 ? d.gt[12 * (size_t)fi + r] : (r == 15 ? 1.0 : 0.0);
-                    Gl[r] = r < 12 ? d.gt[12 * (size_t)last + r] : (r == 15 ? 1.0 : 0.0);
+    if (st->status != VO_STATUS_OK) return;
+    if (k0 > 0 && !st->need_more) return;          // the replay of [0, k0) already stopped
+    __shared__ unsigned s_last;
+    const int k = k0 + blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int M = st->M, scored = st->scored;
+    {
+        int s8[8];
+        sample8(st->frame_seed, k, M, s8);
+        double F[9];
+        fit_F8_wave(d.pts, s8, lane, F);
+        if (lane < 9) {
+            double v = 0.0;
+#pragma unroll
+            for (int c = 0; c < 9; ++c) if (c == lane) v = F[c];
+            d.hypF[(size_t)k * 9 + lane] = v;
+        }
+        const double thr = d.sampson_thr;
+        int cnt = 0;
+        for (int b = 0; b < scored; b += 64) {
+            int i = b + lane;
+            bool in = false;
+            if (i < scored) {
+                const double2* p = reinterpret_cast<const double2*>(d.pts + 4 * (size_t)i);
+                double2 a = p[0], c = p[1];
+                in = sampson(F, a.x, a.y, c.x, c.y) < thr;
+            }
+            cnt += __popcll(ballot64(in));
+        }
+        if (lane == 0) st_sc1(d.counts + k, cnt);
+    }
+    unsigned* ctr = d.ctr + (k0 == 0 ? 1 : 3);
+    if (!arrive_last(ctr, gridDim.x, &s_last)) return;
+    // ---- last workgroup (one wave): replay of ransac.cpp:139-190 over [kk, k1), 64 per step ----
+    const uint16_t* tab = d.maxit_tab + (size_t)M * (M + 1) / 2;
+    int kk, maxit, best, bestk;
+    if (k0 == 0) { kk = 0; maxit = d.maxit_initial; best = 0; bestk = -1; }
+    else { kk = st->k_done; maxit = st->maxit; best = st->best; bestk = st->bestk; }
+    if (maxit > nhyp) maxit = nhyp;
+    const int lim = k1;
+    while (kk < maxit && kk < lim) {
+        int idx = kk + lane;
+        int c = (idx < maxit && idx < lim) ? ld_sc1(d.counts + idx) : -1;
+        unsigned long long bal = ballot64(c > best);
+        if (bal == 0ull) {
+            kk = min(min(kk + 64, maxit), lim);
+            continue;
+        }
+        int j = __ffsll((long long)bal) - 1;
+        best = __shfl(c, j);
+        bestk = kk + j;
+        uint16_t u = tab[best];
+        if (u != 0xFFFFu) maxit = min((int)u, nhyp);
+        kk = bestk + 1;
+    }
+    if (lane == 0) {
+        st->k_done = kk; st->maxit = maxit; st->best = best; st->bestk = bestk;
+        st->need_more = kk < maxit ? 1 : 0;
+        st->n_eval = kk;
+        *ctr = 0u;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// refit on the best hypothesis' inliers (model.fit(bestInlierSet), ransac.cpp:193) and the
+// getPose prologue (PoseUpdate.hpp:61-96).  One wavefront; sums in the oracle's order.
+// ---------------------------------------------------------------------------
+
+// E = K^T F K, SVD, the 4 (R, t) candidates; sets FEW_INLIERS / DEGENERATE (1 thread)
+__device__ void pose_prep(const VoDev& d, VoState* st)
+{
+    if (st->model_n < 8) { st->status = VO_STATUS_FEW_INLIERS; return; }
+    double E[9], G[9];
+    mtm3(d.K, st->model_F, G);
+    mm3(G, d.K, E);
+    double nn = 0.0;
+    for (int i = 0; i < 9; ++i) nn = nn + E[i] * E[i];
+    nn = sqrt(nn);
+    double inv = 1.0 / nn;
+    int nz = 0;
+    for (int i = 0; i < 9; ++i) { E[i] = E[i] * inv; nz += (E[i] != 0.0); }
+    if (nz < 5) { st->status = VO_STATUS_DEGENERATE; st->degenerate = 1; return; }
+    double U[9], S[3], Vt[9];
+    svd3(E, U, S, Vt);
+    if (det3(U) < 0) for (int i = 0; i < 9; ++i) U[i] = -U[i];
+    if (det3(Vt) < 0) for (int i = 0; i < 9; ++i) Vt[i] = -Vt[i];
+    const double W[9] = {0, -1, 0, 1, 0, 0, 0, 0, 1};
+    const double Wt[9] = {0, 1, 0, -1, 0, 0, 0, 0, 1};
+    double R1[9], R2[9], T[9];
+    mm3(U, W, T); mm3(T, Vt, R1);
+    mm3(U, Wt, T); mm3(T, Vt, R2);
+    if (det3(R1) < 0) for (int i = 0; i < 9; ++i) R1[i] = -R1[i];
+    if (det3(R2) < 0) for (int i = 0; i < 9; ++i) R2[i] = -R2[i];
+    for (int i = 0; i < 9; ++i) { st->R1[i] = R1[i]; st->R2[i] = R2[i]; }
+    st->t[0] = U[2]; st->t[1] = U[5]; st->t[2] = U[8];
+    for (int c = 0; c < 4; ++c) st->counts4[c] = 0;
+}
+
+#define RF_T 128
+// one sum over the refit threads in the oracle's order (red_finish): per-thread partials
+// -> LDS -> thread e sums the RF_T partials of quantity e sequentially
+template <int NS>
+__device__ __forceinline__ void refit_sums(const double (&part)[NS], double (*s_part)[RF_T + 1], double* s_out)
+{
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < NS; ++e) s_part[e][tid] = part[e];
+    __syncthreads();
+    if (tid < NS) {
+        double s = 0.0;
+        for (int t = 0; t < RF_T; ++t) s = s + s_part[tid][t];
+        s_out[tid] = s;
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
+{
+    VoState* st = d.st;
+    if (st->status != VO_STATUS_OK) return;
+    __shared__ double s_part[45][RF_T + 1];
+    __shared__ double s_sum[45];
+    __shared__ double s_A[81], s_V[81], s_B[81], s_Vn[81];
+    __shared__ double s_c[9], s_s[9], s_offr[9], s_diar[9];
+    __shared__ double s_ov[4][2];
+    __shared__ int s_part_i[9], s_role[9], s_ovi[4][3];
+    __shared__ int s_n;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int bestk = st->bestk;
+    const int scored = st->scored;
+    if (tid < 64) {                       // wave 0: ordered inlier compaction
+        int n = 0;
+        if (bestk >= 0) {
+            double F[9];
+#pragma unroll
+            for (int c = 0; c < 9; ++c) F[c] = d.hypF[(size_t)bestk * 9 + c];
+            const double thr = d.sampson_thr;
+            for (int b0 = 0; b0 < scored; b0 += 64) {
+                int i = b0 + lane;
+                bool in = false;
+                if (i < scored) {
+                    const double* p = d.pts + 4 * (size_t)i;
+                    in = sampson(F, p[0], p[1], p[2], p[3]) < thr;
                 }
-                inv4(Gi, Ii);
-                mm4(Ii, Gl, Tr);
-                scale = sqrt((Tr[3] * Tr[3] + Tr[7] * Tr[7]) + Tr[11] * Tr[11]);
+                unsigned long long bal = ballot64(in);
+                if (in) d.inl[n + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+                n += __popcll(bal);
             }
         }
-        double tn = sqrt((tf[0] * tf[0] + tf[1] * tf[1]) + tf[2] * tf[2]);
-        if (tn > 1e-6) {
-            double f = scale / tn;
-            tf[0] = tf[0] * f; tf[1] = tf[1] * f; tf[2] = tf[2] * f;
+        if (lane == 0) { s_n = n; st->n_inl = n; }
+    }
+    __threadfence_block();
+    __syncthreads();
+    const int n = s_n;
+    if (bestk >= 0 && n >= 8) {
+        const int32_t* idx = d.inl;
+        double pm[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int i = tid; i < n; i += RF_T) {
+            const double* p = d.pts + 4 * (size_t)idx[i];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) pm[c] = pm[c] + p[c];
         }
-        for (int i = 0; i < 9; ++i) st->pose_R[i] = Rf[i];
-        for (int i = 0; i < 3; ++i) st->pose_t[i] = tf[i];
-        have_pose = true;
+        refit_sums<4>(pm, s_part, s_sum);
+        double mean[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) mean[c] = s_sum[c] / (double)n;
+        double ps[2] = {0.0, 0.0};
+        for (int i = tid; i < n; i += RF_T) {
+            const double* p = d.pts + 4 * (size_t)idx[i];
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                double a = p[2 * g] - mean[2 * g], b = p[2 * g + 1] - mean[2 * g + 1];
+                ps[g] = ps[g] + (a * a + b * b);
+            }
+        }
+        refit_sums<2>(ps, s_part, s_sum);
+        const double sc1 = sqrt(2.0) / sqrt(s_sum[0] / (double)n);
+        const double sc2 = sqrt(2.0) / sqrt(s_sum[1] / (double)n);
+        const double o1x = -(sc1 * mean[0]), o1y = -(sc1 * mean[1]), o2x = -(sc2 * mean[2]), o2y = -(sc2 * mean[3]);
+        double acc[45];
+#pragma unroll
+        for (int e = 0; e < 45; ++e) acc[e] = 0.0;
+        for (int i = tid; i < n; i += RF_T) {
+            const double* p = d.pts + 4 * (size_t)idx[i];
+            double a[9];
+            design_row(sc1 * p[0] + o1x, sc1 * p[1] + o1y, sc2 * p[2] + o2x, sc2 * p[3] + o2y, a);
+            int e = 0;
+#pragma unroll
+            for (int u = 0; u < 9; ++u)
+#pragma unroll
+                for (int v = u; v < 9; ++v) { acc[e] = acc[e] + a[u] * a[v]; ++e; }
+        }
+        refit_sums<45>(acc, s_part, s_sum);
+        if (tid < 45) {
+            int u = 0, e = tid;
+            while (e >= 9 - u) { e -= 9 - u; ++u; }
+            int v = u + e;
+            s_A[u * 9 + v] = s_sum[tid];
+            s_A[v * 9 + u] = s_sum[tid];
+        }
+        if (tid < 81) s_V[tid] = (tid % 10 == 0) ? 1.0 : 0.0;
+        __syncthreads();
+        // parallel-order Jacobi (oracle jacobi_par9): thread e < 81 owns entry e
+        for (int sweep = 0; sweep < 50; ++sweep) {
+            if (tid < 9) {
+                double o = 0.0;
+                for (int q = tid + 1; q < 9; ++q) o = o + s_A[tid * 9 + q] * s_A[tid * 9 + q];
+                s_offr[tid] = o;
+                s_diar[tid] = s_A[tid * 9 + tid] * s_A[tid * 9 + tid];
+            }
+            __syncthreads();
+            double off = 0.0, dia = 0.0;
+            for (int r = 0; r < 9; ++r) { off = off + s_offr[r]; dia = dia + s_diar[r]; }
+            if (off == 0.0 || off <= 1e-30 * dia) break;
+            for (int rnd = 0; rnd < 9; ++rnd) {
+                if (tid < 9) {
+                    const int i = tid;
+                    int part = i, role = 0;
+                    double c = 1.0, sn = 0.0;
+                    if (i != rnd) {
+                        int dd = (i - rnd + 9) % 9;
+                        int k = dd <= 4 ? dd : 9 - dd;
+                        int a = (rnd + k) % 9, b = (rnd - k + 9) % 9;
+                        int pp = a < b ? a : b, qq = a < b ? b : a;
+                        double apq = s_A[pp * 9 + qq];
+                        if (apq != 0.0) {
+                            double app = s_A[pp * 9 + pp], aqq = s_A[qq * 9 + qq];
+                            double theta = (aqq - app) / (2.0 * apq);
+                            double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+                            if (theta < 0.0) t = -t;
+                            c = 1.0 / sqrt(t * t + 1.0);
+                            sn = t * c;
+                            part = (i == pp) ? qq : pp;
+                            role = (i == pp) ? 1 : 2;
+                            if (role == 1) {
+                                s_ov[k - 1][0] = app - t * apq;
+                                s_ov[k - 1][1] = aqq + t * apq;
+                                s_ovi[k - 1][0] = pp; s_ovi[k - 1][1] = qq; s_ovi[k - 1][2] = 1;
+                            }
+                        } else if (i == pp) {
+                            s_ovi[k - 1][2] = 0;
+                        }
+                    }
+                    s_part_i[i] = part; s_role[i] = role; s_c[i] = c; s_s[i] = sn;
+                }
+                __syncthreads();
+                if (tid < 81) {
+                    const int e = tid, i = e / 9, j = e - i * 9;
+                    int pj = s_part_i[j], rj = s_role[j];
+                    double a = s_A[i * 9 + j], b = s_A[i * 9 + pj];
+                    double va = s_V[i * 9 + j], vb = s_V[i * 9 + pj];
+                    double cj = s_c[j], sj = s_s[j];
+                    double bv, vv;
+                    if (rj == 1) { bv = cj * a - sj * b; vv = cj * va - sj * vb; }
+                    else if (rj == 2) { bv = sj * b + cj * a; vv = sj * vb + cj * va; }
+                    else { bv = a; vv = va; }
+                    s_B[e] = bv;
+                    s_Vn[e] = vv;
+                }
+                __syncthreads();
+                if (tid < 81) {
+                    const int e = tid, i = e / 9, j = e - i * 9;
+                    s_V[e] = s_Vn[e];
+                    if (j >= i) {
+                        int pi = s_part_i[i], ri = s_role[i];
+                        double a = s_B[i * 9 + j], b = s_B[pi * 9 + j];
+                        double ci = s_c[i], si = s_s[i];
+                        double v;
+                        if (ri == 1) v = ci * a - si * b;
+                        else if (ri == 2) v = si * b + ci * a;
+                        else v = a;
+                        s_A[i * 9 + j] = v;
+                        s_A[j * 9 + i] = v;
+                    }
+                }
+                __syncthreads();
+                if (tid < 4 && s_ovi[tid][2]) {
+                    int pp = s_ovi[tid][0], qq = s_ovi[tid][1];
+                    s_A[pp * 9 + pp] = s_ov[tid][0];
+                    s_A[qq * 9 + qq] = s_ov[tid][1];
+                    s_A[pp * 9 + qq] = 0.0;
+                    s_A[qq * 9 + pp] = 0.0;
+                }
+                __syncthreads();
+            }
+        }
+        for (int i = tid; i < n; i += RF_T) {
+            const double* p = d.pts + 4 * (size_t)idx[i];
+            float4 o = make_float4((float)p[0], (float)p[1], (float)p[2], (float)p[3]);
+            reinterpret_cast<float4*>(d.model_p)[i] = o;
+        }
+        if (tid == 0) {
+            int k = argmin_diag<9>(s_A);
+            double f[9];
+            for (int i = 0; i < 9; ++i) f[i] = s_V[i * 9 + k];
+            double Fn[9];
+            denormalize(f, sc1, mean[0], mean[1], sc2, mean[2], mean[3], Fn);
+            rank2(Fn);
+            for (int i = 0; i < 9; ++i) st->model_F[i] = Fn[i];
+            st->fitted = 1;
+            st->model_n = n;
+        }
+    } else if (tid == 0) {
+        st->fitted = 0;            // fit() returns early: the previous model stays (quirk 9)
     }
-    if (mode == VO_MODE_STAGE) return;
-    VoFrameOut* o = d.out;
-    int flip = 1;
-    if (status == VO_STATUS_FIRST || status == VO_STATUS_MISSING) flip = 0;
-    if (status == VO_STATUS_OK || status == VO_STATUS_DEGENERATE) {
-        // VisualOdometry.cpp:161-166 happen before getPose
-        st->last_valid = st->frame;
-        st->prev = st->cur;
+    if (with_pose && tid == 0) pose_prep(d, st);
+}
+
+__global__ void k_pose_prep(VoDev d)
+{
+    VoState* st = d.st;
+    if (threadIdx.x != 0 || st->status != VO_STATUS_OK) return;
+    pose_prep(d, st);
+}
+
+// finalize (PoseUpdate.hpp:142-178, VisualOdometry.cpp:106-186): pick the candidate, scale
+// t, compose T_curr, emit the pose row, then set up the next frame.  Thread 0 works; the
+// whole workgroup zeroes the next frame's histogram.
+__device__ void finalize_frame(const VoDev& d, VoState* st)
+{
+    __shared__ int s_mode;
+    if (threadIdx.x == 0) {
+        const int status = st->status;
+        const int mode = st->mode;
+        s_mode = mode;
+        double* Tc = st->Tcurr;
+        double Rf[9], tf[3];
+        bool have_pose = false;
+        if (status == VO_STATUS_OK) {
+            int maxPos = -1, bestc = 0;
+            for (int c = 0; c < 4; ++c) {
+                int v = __hip_atomic_load((gi32*)&st->counts4[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v > maxPos) { maxPos = v; bestc = c; }
+            }
+            const double* R = bestc < 2 ? st->R1 : st->R2;
+            double sg = (bestc & 1) ? -1.0 : 1.0;
+            for (int i = 0; i < 9; ++i) Rf[i] = R[i];
+            if (det3(Rf) < 0) for (int i = 0; i < 9; ++i) Rf[i] = -Rf[i];
+            tf[0] = st->t[0] * sg; tf[1] = st->t[1] * sg; tf[2] = st->t[2] * sg;
+            double scale = st->scale_override;
+            if (mode == VO_MODE_FRAME) {
+                scale = 1.0;
+                const int fi = st->frame, last = st->last_valid;
+                if (d.gt_n > 0 && fi < d.gt_n && last < d.gt_n) {
+                    double Gi[16], Gl[16], Ii[16], Tr[16];
+                    for (int r = 0; r < 16; ++r) {
+                        Gi[r] = r < 12 ? d.gt[12 * (size_t)fi + r] : (r == 15 ? 1.0 : 0.0);
+                        Gl[r] = r < 12 ? d.gt[12 * (size_t)last + r] : (r == 15 ? 1.0 : 0.0);
+                    }
+                    inv4(Gi, Ii);
+                    mm4(Ii, Gl, Tr);
+                    scale = sqrt((Tr[3] * Tr[3] + Tr[7] * Tr[7]) + Tr[11] * Tr[11]);
+                }
+            }
+            double tn = sqrt((tf[0] * tf[0] + tf[1] * tf[1]) + tf[2] * tf[2]);
+            if (tn > 1e-6) {
+                double f = scale / tn;
+                tf[0] = tf[0] * f; tf[1] = tf[1] * f; tf[2] = tf[2] * f;
+            }
+            for (int i = 0; i < 9; ++i) st->pose_R[i] = Rf[i];
+            for (int i = 0; i < 3; ++i) st->pose_t[i] = tf[i];
+            have_pose = true;
+        }
+        if (mode == VO_MODE_FRAME || mode == VO_MODE_MISSING) {
+            VoFrameOut* o = d.out;
+            int flip = 1;
+            if (status == VO_STATUS_FIRST || status == VO_STATUS_MISSING) flip = 0;
+            if (status == VO_STATUS_OK || status == VO_STATUS_DEGENERATE) {
+                st->last_valid = st->frame;      // VisualOdometry.cpp:161-166 precede getPose
+                st->prev = st->cur;
+            }
+            if (status == VO_STATUS_FIRST) { st->prev = st->cur; st->last_valid = 0; }
+            if (have_pose) {
+                double Trel[16] = {Rf[0], Rf[1], Rf[2], tf[0], Rf[3], Rf[4], Rf[5], tf[1],
+                                   Rf[6], Rf[7], Rf[8], tf[2], 0, 0, 0, 1};
+                mm4(Tc, Trel, Tc);
+            }
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 4; ++c) o->pose[r * 4 + c] = (flip && r == 2) ? -Tc[r * 4 + c] : Tc[r * 4 + c];
+            o->status = status;
+            o->n_kps = status == VO_STATUS_MISSING ? 0 : st->n_kps[st->cur];
+            o->n_matches = st->M;
+            o->n_inl = st->n_inl;
+            o->best_k = st->bestk;
+            o->n_eval = st->n_eval;
+            o->fitted = st->fitted;
+            o->frame = st->frame;
+            st->frame = st->frame + 1;
+        }
     }
-    if (status == VO_STATUS_FIRST) { st->prev = st->cur; st->last_valid = 0; }
-    if (have_pose) {
-        double Trel[16] = {Rf[0], Rf[1], Rf[2], tf[0], Rf[3], Rf[4], Rf[5], tf[1], Rf[6], Rf[7], Rf[8], tf[2], 0, 0, 0, 1};
-        mm4(Tc, Trel, Tc);
+    __syncthreads();
+    if (s_mode == VO_MODE_FRAME || s_mode == VO_MODE_MISSING) setup_next_frame(d, st);
+}
+
+// cheirality test of the 4 (R, t) candidates, one thread per (model inlier, candidate)
+// (cv::undistortPoints + cv::triangulatePoints + depth test, PoseUpdate.hpp:101-147);
+// the last workgroup finalizes the frame.  On a skipped frame workgroup 0 finalizes.
+#define TRI_BLOCK 128
+__global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d)
+{
+    VoState* st = d.st;
+    __shared__ int s_cnt[4];
+    __shared__ unsigned s_last;
+    const int status = st->status;
+    if (status != VO_STATUS_OK) {
+        if (blockIdx.x == 0) finalize_frame(d, st);
+        return;
     }
-    for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 4; ++c) o->pose[r * 4 + c] = (flip && r == 2) ? -Tc[r * 4 + c] : Tc[r * 4 + c];
-    o->status = status;
-    o->n_kps = status == VO_STATUS_MISSING ? 0 : st->n_kps[st->cur];
-    o->n_matches = st->M;
-    o->n_inl = st->n_inl;
-    o->best_k = st->bestk;
-    o->n_eval = st->n_eval;
-    o->fitted = st->fitted;
-    o->frame = st->frame;
-    st->frame = st->frame + 1;
+    const int n = st->model_n;
+    const unsigned active = (unsigned)((4 * n + TRI_BLOCK - 1) / TRI_BLOCK);
+    if (blockIdx.x >= active) return;
+    if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int g = blockIdx.x * TRI_BLOCK + threadIdx.x;   // (point, candidate) = (g >> 2, g & 3)
+    const int i = g >> 2, cnd = g & 3;
+    bool pos = false;
+    if (i < n) {
+        const double fx = d.K[0], fy = d.K[4], cx = d.K[2], cy = d.K[5];
+        const double ifx = 1.0 / fx, ify = 1.0 / fy;
+        const float4 p = reinterpret_cast<const float4*>(d.model_p)[i];
+        float x1 = (float)(((double)p.x - cx) * ifx), y1 = (float)(((double)p.y - cy) * ify);
+        float x2 = (float)(((double)p.z - cx) * ifx), y2 = (float)(((double)p.w - cy) * ify);
+        double X1 = x1, Y1 = y1, X2 = x2, Y2 = y2;
+        const double* R = cnd < 2 ? st->R1 : st->R2;
+        double sg = (cnd & 1) ? -1.0 : 1.0;
+        double tc0 = st->t[0] * sg, tc1 = st->t[1] * sg, tc2 = st->t[2] * sg;
+        double P2[12] = {R[0], R[1], R[2], tc0, R[3], R[4], R[5], tc1, R[6], R[7], R[8], tc2};
+        const double P1[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+        double A[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            A[0 * 4 + k] = X1 * P1[8 + k] - P1[0 + k];
+            A[1 * 4 + k] = Y1 * P1[8 + k] - P1[4 + k];
+            A[2 * 4 + k] = X2 * P2[8 + k] - P2[0 + k];
+            A[3 * 4 + k] = Y2 * P2[8 + k] - P2[4 + k];
+        }
+        double AtA[16], V[16];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                AtA[a * 4 + b] = ((A[0 * 4 + a] * A[0 * 4 + b] + A[1 * 4 + a] * A[1 * 4 + b]) + A[2 * 4 + a] * A[2 * 4 + b]) +
+                                 A[3 * 4 + a] * A[3 * 4 + b];
+        jacobi_eig<4>(AtA, V);
+        int km = argmin_diag<4>(AtA);
+        double X[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (c == km) { X[0] = V[0 * 4 + c]; X[1] = V[1 * 4 + c]; X[2] = V[2 * 4 + c]; X[3] = V[3 * 4 + c]; }
+        double h0 = (double)(float)X[0], h1 = (double)(float)X[1], h2 = (double)(float)X[2], h3 = (double)(float)X[3];
+        double w = h3;
+        if (!(fabs(w) < 1e-6)) {
+            double iw = 1.0 / w;
+            double Xh0 = h0 * iw, Xh1 = h1 * iw, Xh2 = h2 * iw;
+            double z1 = Xh2;
+            double z2 = ((R[6] * Xh0 + R[7] * Xh1) + R[8] * Xh2) + tc2;
+            pos = (z1 > 0 && z2 > 0);
+        }
+    }
+    unsigned long long bal = ballot64(pos);
+    const int lane = threadIdx.x & 63;
+    if (lane < 4) {
+        const unsigned long long mask = 0x1111111111111111ull << lane;
+        int c = __popcll(bal & mask);
+        if (c) atomicAdd(&s_cnt[lane], c);
+    }
+    __syncthreads();
+    if (threadIdx.x < 4 && s_cnt[threadIdx.x])
+        __hip_atomic_fetch_add((gi32*)&st->counts4[threadIdx.x], s_cnt[threadIdx.x], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    if (!arrive_last(d.ctr + 2, active, &s_last)) return;
+    if (threadIdx.x == 0) d.ctr[2] = 0u;
+    finalize_frame(d, st);
+}
+
+// a missing image (VisualOdometry.cpp:77-82): push T_curr, advance the frame counter
+__global__ void __launch_bounds__(128) k_missing(VoDev d)
+{
+    VoState* st = d.st;
+    if (threadIdx.x == 0) { st->status = VO_STATUS_MISSING; st->mode = VO_MODE_MISSING; }
+    __syncthreads();
+    finalize_frame(d, st);
 }
 
 // arithmetic self-test: the ops whose rounding the parity contract depends on
@@ -1345,9 +1526,7 @@ __global__ void k_selftest_arith(const float* fa, const float* fb, float* fo, co
 // ---------------------------------------------------------------------------
 // launch wrappers
 // ---------------------------------------------------------------------------
-static const char* g_names[] = {"frame_begin", "stencil", "select", "describe", "match", "compact",
-                                "ransac_hyp0", "replay0", "ransac_hyp1", "replay1", "refit", "pose_prep",
-                                "triangulate", "finalize"};
+static const char* g_names[] = {"stencil", "select", "describe", "match", "ransac", "refit", "triangulate"};
 int kernel_count() { return (int)(sizeof(g_names) / sizeof(g_names[0])); }
 const char* kernel_name(int i) { return g_names[i]; }
 
@@ -1358,6 +1537,7 @@ void launch_frame_begin(const VoDev& d, int mode, hipStream_t s)
 }
 void launch_stencil(const VoDev& d, const uint8_t* frame, int write_response, hipStream_t s)
 {
+    ensure_tables();
     dim3 g((d.W + ST_TW - 1) / ST_TW, (d.H + ST_TH - 1) / ST_TH);
     hipLaunchKernelGGL(k_stencil, g, dim3(256), 0, s, d, frame, write_response);
 }
@@ -1370,23 +1550,22 @@ void launch_match(const VoDev& d, hipStream_t s)
 {
     hipLaunchKernelGGL(k_match, dim3((d.N + 3) / 4), dim3(256), 0, s, d);
 }
-void launch_compact(const VoDev& d, hipStream_t s) { hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, d); }
-void launch_ransac_hyp(const VoDev& d, int k0, int k1, hipStream_t s)
+void launch_ransac(const VoDev& d, int nhyp, hipStream_t s)
 {
-    int nb = (k1 - k0 + 3) / 4;
-    if (nb > 0) hipLaunchKernelGGL(k_ransac_hyp, dim3(nb), dim3(256), 0, s, d, k0, k1);
+    const int k0 = nhyp < VO_HYP_CHUNK0 ? nhyp : VO_HYP_CHUNK0;
+    hipLaunchKernelGGL(k_ransac_hyp, dim3(k0), dim3(64), 0, s, d, 0, k0, nhyp);
+    if (nhyp > k0) hipLaunchKernelGGL(k_ransac_hyp, dim3(nhyp - k0), dim3(64), 0, s, d, k0, nhyp, nhyp);
 }
-void launch_ransac_replay(const VoDev& d, int k1, hipStream_t s)
+void launch_refit(const VoDev& d, int with_pose, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_ransac_replay, dim3(1), dim3(64), 0, s, d, k1);
+    hipLaunchKernelGGL(k_refit, dim3(1), dim3(RF_T), 0, s, d, with_pose);
 }
-void launch_refit(const VoDev& d, hipStream_t s) { hipLaunchKernelGGL(k_refit, dim3(1), dim3(256), 0, s, d); }
 void launch_pose_prep(const VoDev& d, hipStream_t s) { hipLaunchKernelGGL(k_pose_prep, dim3(1), dim3(64), 0, s, d); }
 void launch_triangulate(const VoDev& d, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_triangulate, dim3((d.N + 255) / 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_triangulate, dim3((4 * d.N + TRI_BLOCK - 1) / TRI_BLOCK), dim3(TRI_BLOCK), 0, s, d);
 }
-void launch_finalize(const VoDev& d, hipStream_t s) { hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, d); }
+void launch_missing(const VoDev& d, hipStream_t s) { hipLaunchKernelGGL(k_missing, dim3(1), dim3(128), 0, s, d); }
 void launch_selftest_arith(const float* fa, const float* fb, float* fo, const double* da, const double* db,
                            double* dout, int n, hipStream_t s)
 {

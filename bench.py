@@ -34,8 +34,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "VO frames/sec (extract+match+pose), 1241×376 mono, 2000 kpts/frame"
 HBM_PEAK_GBS = 8000.0
-KERNELS = ["frame_begin", "stencil", "select", "describe", "match", "compact", "ransac_hyp0", "replay0",
-           "ransac_hyp1", "replay1", "refit", "pose_prep", "triangulate", "finalize"]
+KERNELS = ["stencil", "select", "describe", "match", "ransac", "refit", "triangulate"]
 
 
 def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray, N: int) -> float:
@@ -49,7 +48,7 @@ def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray, N: int) -> 
         return float((86 + 8 + 68) * n.mean())                  # 86 sample px + kp in, 64+4 B out
     if kernel == "match":
         return float(4 * n.mean() + 4 * n.mean() + 4 * n.mean())  # prefixes prev + cur, result
-    if kernel.startswith("ransac_hyp"):
+    if kernel.startswith("ransac"):
         return float(32 * M.mean() + 36 * 4)                    # matches read once (+F out), L2 re-reads excluded
     if kernel == "select":
         return float(8 * 4 * n.mean() + 8 * n.mean())

@@ -221,6 +221,84 @@ static void jacobi_eig(double* A, int n, double* V)
     }
 }
 
+/* Parallel-order Jacobi for the 9x9 refit (A^T A): round-robin schedule over 10 slots
+ * (slot 9 = idle), round r pairs ((r+k)%9, (r-k)%9), k = 1..4, so a sweep of 9 rounds
+ * visits all 36 pairs; the 4 disjoint rotations of a round are applied together as
+ * B = A J (columns), A' = J^T B (rows, upper triangle mirrored), V' = V J, then the NR
+ * diagonal / zero overrides.  This is the exact operation order of the device refit
+ * (k_refit), so refit outputs agree bit for bit. */
+static void jacobi_par9(double* A, double* V)
+{
+    const int n = 9;
+    for (int i = 0; i < 81; ++i) V[i] = 0.0;
+    for (int i = 0; i < 9; ++i) V[i * 9 + i] = 1.0;
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        double offr[9], diar[9];
+        for (int r = 0; r < 9; ++r) {
+            double o = 0.0;
+            for (int q = r + 1; q < 9; ++q) o = o + A[r * 9 + q] * A[r * 9 + q];
+            offr[r] = o;
+            diar[r] = A[r * 9 + r] * A[r * 9 + r];
+        }
+        double off = 0.0, dia = 0.0;
+        for (int r = 0; r < 9; ++r) { off = off + offr[r]; dia = dia + diar[r]; }
+        if (off == 0.0 || off <= 1e-30 * dia) break;
+        for (int rnd = 0; rnd < 9; ++rnd) {
+            int partner[9], role[9];      /* role 0 idle, 1 p, 2 q */
+            double cc[9], ss[9];
+            double tt[4], app_[4], aqq_[4], apq_[4];
+            int pp[4], qq[4], act[4];
+            for (int i = 0; i < 9; ++i) { partner[i] = i; role[i] = 0; cc[i] = 1.0; ss[i] = 0.0; }
+            for (int k = 1; k <= 4; ++k) {
+                int a = (rnd + k) % 9, b = (rnd - k + 9) % 9;
+                int p = a < b ? a : b, q = a < b ? b : a;
+                pp[k - 1] = p; qq[k - 1] = q;
+                double apq = A[p * 9 + q];
+                act[k - 1] = apq != 0.0;
+                if (!act[k - 1]) continue;
+                double app = A[p * 9 + p], aqq = A[q * 9 + q];
+                double theta = (aqq - app) / (2.0 * apq);
+                double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+                if (theta < 0.0) t = -t;
+                double c = 1.0 / sqrt(t * t + 1.0);
+                double sn = t * c;
+                tt[k - 1] = t; app_[k - 1] = app; aqq_[k - 1] = aqq; apq_[k - 1] = apq;
+                partner[p] = q; partner[q] = p; role[p] = 1; role[q] = 2;
+                cc[p] = c; cc[q] = c; ss[p] = sn; ss[q] = sn;
+            }
+            double B[81], Vn[81];
+            for (int i = 0; i < 9; ++i)
+                for (int j = 0; j < 9; ++j) {
+                    int pj = partner[j];
+                    double a = A[i * 9 + j], b = A[i * 9 + pj];
+                    double va = V[i * 9 + j], vb = V[i * 9 + pj];
+                    if (role[j] == 1) { B[i * 9 + j] = cc[j] * a - ss[j] * b; Vn[i * 9 + j] = cc[j] * va - ss[j] * vb; }
+                    else if (role[j] == 2) { B[i * 9 + j] = ss[j] * b + cc[j] * a; Vn[i * 9 + j] = ss[j] * vb + cc[j] * va; }
+                    else { B[i * 9 + j] = a; Vn[i * 9 + j] = va; }
+                }
+            for (int i = 0; i < 9; ++i)
+                for (int j = i; j < 9; ++j) {
+                    int pi = partner[i];
+                    double a = B[i * 9 + j], b = B[pi * 9 + j];
+                    double v;
+                    if (role[i] == 1) v = cc[i] * a - ss[i] * b;
+                    else if (role[i] == 2) v = ss[i] * b + cc[i] * a;
+                    else v = a;
+                    A[i * 9 + j] = v; A[j * 9 + i] = v;
+                }
+            for (int k = 0; k < 4; ++k) {
+                if (!act[k]) continue;
+                int p = pp[k], q = qq[k];
+                A[p * 9 + p] = app_[k] - tt[k] * apq_[k];
+                A[q * 9 + q] = aqq_[k] + tt[k] * apq_[k];
+                A[p * 9 + q] = 0.0; A[q * 9 + p] = 0.0;
+            }
+            memcpy(V, Vn, sizeof(Vn));
+        }
+    }
+    (void)n;
+}
+
 static int argmin_diag(const double* A, int n)
 {
     int b = 0;
@@ -325,24 +403,16 @@ static void nullvec_8x9(double M[8][9], double f[9])
     for (int c = 0; c < 9; ++c) f[c] = f[c] / nn;
 }
 
-/* Fixed-order parallel sum used by the device refit (256 threads, strided
- * accumulation, wave64 xor-butterfly, then waves 0..3 summed in order).  The oracle
- * reproduces the exact order so refit/pose outputs are comparable bit for bit. */
-#define VOO_RED_THREADS 256
+/* Fixed-order parallel sum used by the device refit (128 threads): thread t accumulates
+ * elements t, t+128, ... in order; the total is the sequential sum of the 128 partials in
+ * thread order.  The oracle reproduces that order so refit outputs compare bit for bit. */
+#define VOO_RED_THREADS 128
 typedef struct { double v[VOO_RED_THREADS]; } red256;
 static double red_finish(red256* r)
 {
-    double w[4];
-    for (int wv = 0; wv < 4; ++wv) {
-        double* L = r->v + wv * 64;
-        for (int off = 32; off >= 1; off >>= 1) {
-            double nv[64];
-            for (int l = 0; l < 64; ++l) nv[l] = L[l] + L[l ^ off];
-            memcpy(L, nv, sizeof(nv));
-        }
-        w[wv] = L[0];
-    }
-    return ((w[0] + w[1]) + w[2]) + w[3];
+    double s = 0.0;
+    for (int t = 0; t < VOO_RED_THREADS; ++t) s = s + r->v[t];
+    return s;
 }
 
 /* ========================================================================== */
@@ -726,7 +796,7 @@ int voo_fit_F(const double* pts, const int32_t* idx, int n, double F[9])
             }
     }
     double V[81], f[9];
-    jacobi_eig(AtA, 9, V);
+    jacobi_par9(AtA, V);
     int k = argmin_diag(AtA, 9);
     for (int i = 0; i < 9; ++i) f[i] = V[i * 9 + k];
     denormalize(f, sc1, mean[0], mean[1], sc2, mean[2], mean[3], F);

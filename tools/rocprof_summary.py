@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 output dir (kernel-trace stats + separate FETCH_SIZE / WRITE_SIZE
+PMC passes) into the markdown table committed under profiles/.
+
+usage: rocprof_summary.py <dir> <title> [--fetch-x2]
+HBM bytes per launch = FETCH_SIZE*1024 (*2 with --fetch-x2: gfx950 reports half of wide
+coalesced streaming reads, MI355X_MICROARCH.md 'HBM') + WRITE_SIZE*1024.
+"""
+import csv
+import glob
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    m = re.match(r"(?:vo::)?(\w+)", name)
+    return m.group(1) if m else name[:40]
+
+
+def pmc(d, prefix, counter):
+    acc = defaultdict(list)
+    for f in glob.glob(os.path.join(d, f"{prefix}*counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter:
+                acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    d, title = sys.argv[1], sys.argv[2]
+    x2 = "--fetch-x2" in sys.argv
+    stats = list(csv.DictReader(open(glob.glob(os.path.join(d, "*kernel_stats.csv"))[0])))
+    fetch = pmc(d, "fetch", "FETCH_SIZE")
+    write = pmc(d, "write", "WRITE_SIZE")
+    print(f"# {title}\n")
+    print("rocprofv3 --kernel-trace --stats (durations) and separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes.\n")
+    print("| kernel | calls | avg us | share % | FETCH_SIZE KB/launch | WRITE_SIZE KB/launch | HBM bytes/launch |")
+    print("|---|---:|---:|---:|---:|---:|---:|")
+    for r in stats:
+        k = short(r["Name"])
+        f, w = fetch.get(k), write.get(k)
+        hb = "" if f is None or w is None else f"{(f * (2 if x2 else 1) + w) * 1024:,.0f}"
+        print(f"| {k} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} | "
+              f"{'' if f is None else f'{f:.1f}'} | {'' if w is None else f'{w:.1f}'} | {hb} |")
+
+
+if __name__ == "__main__":
+    main()
