@@ -23,6 +23,11 @@ __constant__ int8_t c_pt_y[VO_FREAK_NPOINTS];
 __constant__ uint8_t c_pair_p[VO_FREAK_NPAIRS];
 __constant__ uint8_t c_pair_q[VO_FREAK_NPAIRS];
 __constant__ int16_t c_patch[VO_FREAK_NTESTS];
+// per pair: dx, dy (f32) and 1/|d| (f64).  (ic*d)/|d| in f32 == (float)((double)(ic*d) * (1/|d|))
+// for every ic in [-255,255] and every pair (tests/test_describe_division.py, exhaustive)
+__constant__ float c_pdx[VO_FREAK_NPAIRS];
+__constant__ float c_pdy[VO_FREAK_NPAIRS];
+__constant__ double c_prn[VO_FREAK_NPAIRS];
 
 static bool g_tables_ready = false;
 static void ensure_tables()
@@ -39,6 +44,16 @@ static void ensure_tables()
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pair_p), pp, sizeof(pp));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pair_q), pq, sizeof(pq));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_patch), vo_freak_patch, sizeof(vo_freak_patch));
+    float pdx[VO_FREAK_NPAIRS], pdy[VO_FREAK_NPAIRS];
+    double prn[VO_FREAK_NPAIRS];
+    for (int t = 0; t < VO_FREAK_NPAIRS; ++t) {
+        float dx = (float)(px[pp[t]] - px[pq[t]]), dy = (float)(py[pp[t]] - py[pq[t]]);
+        float nrm = sqrtf(dx * dx + dy * dy);          // host sqrtf: correctly rounded
+        pdx[t] = dx; pdy[t] = dy; prn[t] = 1.0 / (double)nrm;
+    }
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pdx), pdx, sizeof(pdx));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pdy), pdy, sizeof(pdy));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_prn), prn, sizeof(prn));
     g_tables_ready = true;
 }
 
@@ -637,10 +652,9 @@ __global__ void __launch_bounds__(256) k_describe(VoDev d)
         int k = e / VO_FREAK_NPAIRS, t = e - k * VO_FREAK_NPAIRS;
         int p = c_pair_p[t], q = c_pair_q[t];
         float ic = s_I0[k][p] - s_I0[k][q];
-        float dx = (float)(c_pt_x[p] - c_pt_x[q]), dy = (float)(c_pt_y[p] - c_pt_y[q]);
-        float nrm = sqrtf(dx * dx + dy * dy);
-        s_term[2 * k][t] = (ic * dx) / nrm;
-        s_term[2 * k + 1][t] = (ic * dy) / nrm;
+        const double rn = c_prn[t];
+        s_term[2 * k][t] = (float)((double)(ic * c_pdx[t]) * rn);
+        s_term[2 * k + 1][t] = (float)((double)(ic * c_pdy[t]) * rn);
     }
     __syncthreads();
     if (tid < 2 * nk) {
@@ -1119,6 +1133,91 @@ __device__ void pose_prep(const VoDev& d, VoState* st)
     for (int c = 0; c < 4; ++c) st->counts4[c] = 0;
 }
 
+// least-squares null vector: Cholesky (pivot floor) + inverse iteration, warm start x0
+// (mirror of oracle ls_nullvec9; S read from LDS, L kept in registers)
+__device__ void ls_nullvec9(const double* S, const double* x0, double* f)
+{
+    double L[45], invd[9];           // packed lower triangle, row i at i(i+1)/2
+    double mx = 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+        if (S[i * 9 + i] > mx) mx = S[i * 9 + i];
+    double fl = 1e-15 * mx;
+    if (!(fl > 0.0)) fl = 1e-300;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        double sj = S[j * 9 + j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) sj = sj - L[j * (j + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+        if (!(sj > fl)) sj = fl;
+        double dj = sqrt(sj);
+        L[j * (j + 1) / 2 + j] = dj;
+        invd[j] = 1.0 / dj;
+#pragma unroll
+        for (int i = j + 1; i < 9; ++i) {
+            double v = S[i * 9 + j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) v = v - L[i * (i + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+            L[i * (i + 1) / 2 + j] = v * invd[j];
+        }
+    }
+    double x[9];
+    double n0 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) n0 = n0 + x0[i] * x0[i];
+    n0 = sqrt(n0);
+    if (n0 > 0.0 && n0 < 1e300) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) x[i] = x0[i] / n0;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) x[i] = 1.0 / 3.0;
+    }
+    for (int it = 0; it < 32; ++it) {
+        double y[9], z[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            double v = x[i];
+#pragma unroll
+            for (int k = 0; k < i; ++k) v = v - L[i * (i + 1) / 2 + k] * y[k];
+            y[i] = v * invd[i];
+        }
+#pragma unroll
+        for (int i = 8; i >= 0; --i) {
+            double v = y[i];
+#pragma unroll
+            for (int k = i + 1; k < 9; ++k) v = v - L[k * (k + 1) / 2 + i] * z[k];
+            z[i] = v * invd[i];
+        }
+        double nn = 0.0, dot = 0.0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) { nn = nn + z[i] * z[i]; dot = dot + z[i] * x[i]; }
+        nn = sqrt(nn);
+        double sg = dot < 0.0 ? -1.0 : 1.0;
+        double diff = 0.0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            double xn = (z[i] / nn) * sg;
+            double dd = fabs(xn - x[i]);
+            if (dd > diff) diff = dd;
+            x[i] = xn;
+        }
+        if (diff <= 4e-16) break;
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) f[i] = x[i];
+}
+
+__device__ __forceinline__ void warm_start(const double* Fb, double s1, double mx1, double my1, double s2,
+                                           double mx2, double my2, double* f0)
+{
+    double T1i[9] = {1.0 / s1, 0.0, mx1, 0.0, 1.0 / s1, my1, 0.0, 0.0, 1.0};
+    double T2i[9] = {1.0 / s2, 0.0, mx2, 0.0, 1.0 / s2, my2, 0.0, 0.0, 1.0};
+    double G[9];
+    mtm3(T2i, Fb, G);
+    mm3(G, T1i, f0);
+}
+
 #define RF_T 128
 // one sum over the refit threads in the oracle's order (red_finish): per-thread partials
 // -> LDS -> thread e sums the RF_T partials of quantity e sequentially
@@ -1143,10 +1242,7 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
     if (st->status != VO_STATUS_OK) return;
     __shared__ double s_part[45][RF_T + 1];
     __shared__ double s_sum[45];
-    __shared__ double s_A[81], s_V[81], s_B[81], s_Vn[81];
-    __shared__ double s_c[9], s_s[9], s_offr[9], s_diar[9];
-    __shared__ double s_ov[4][2];
-    __shared__ int s_part_i[9], s_role[9], s_ovi[4][3];
+    __shared__ double s_A[81];
     __shared__ int s_n;
     const int tid = threadIdx.x, lane = tid & 63;
     const int bestk = st->bestk;
@@ -1221,101 +1317,17 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
             s_A[u * 9 + v] = s_sum[tid];
             s_A[v * 9 + u] = s_sum[tid];
         }
-        if (tid < 81) s_V[tid] = (tid % 10 == 0) ? 1.0 : 0.0;
         __syncthreads();
-        // parallel-order Jacobi (oracle jacobi_par9): thread e < 81 owns entry e
-        for (int sweep = 0; sweep < 50; ++sweep) {
-            if (tid < 9) {
-                double o = 0.0;
-                for (int q = tid + 1; q < 9; ++q) o = o + s_A[tid * 9 + q] * s_A[tid * 9 + q];
-                s_offr[tid] = o;
-                s_diar[tid] = s_A[tid * 9 + tid] * s_A[tid * 9 + tid];
-            }
-            __syncthreads();
-            double off = 0.0, dia = 0.0;
-            for (int r = 0; r < 9; ++r) { off = off + s_offr[r]; dia = dia + s_diar[r]; }
-            if (off == 0.0 || off <= 1e-30 * dia) break;
-            for (int rnd = 0; rnd < 9; ++rnd) {
-                if (tid < 9) {
-                    const int i = tid;
-                    int part = i, role = 0;
-                    double c = 1.0, sn = 0.0;
-                    if (i != rnd) {
-                        int dd = (i - rnd + 9) % 9;
-                        int k = dd <= 4 ? dd : 9 - dd;
-                        int a = (rnd + k) % 9, b = (rnd - k + 9) % 9;
-                        int pp = a < b ? a : b, qq = a < b ? b : a;
-                        double apq = s_A[pp * 9 + qq];
-                        if (apq != 0.0) {
-                            double app = s_A[pp * 9 + pp], aqq = s_A[qq * 9 + qq];
-                            double theta = (aqq - app) / (2.0 * apq);
-                            double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
-                            if (theta < 0.0) t = -t;
-                            c = 1.0 / sqrt(t * t + 1.0);
-                            sn = t * c;
-                            part = (i == pp) ? qq : pp;
-                            role = (i == pp) ? 1 : 2;
-                            if (role == 1) {
-                                s_ov[k - 1][0] = app - t * apq;
-                                s_ov[k - 1][1] = aqq + t * apq;
-                                s_ovi[k - 1][0] = pp; s_ovi[k - 1][1] = qq; s_ovi[k - 1][2] = 1;
-                            }
-                        } else if (i == pp) {
-                            s_ovi[k - 1][2] = 0;
-                        }
-                    }
-                    s_part_i[i] = part; s_role[i] = role; s_c[i] = c; s_s[i] = sn;
-                }
-                __syncthreads();
-                if (tid < 81) {
-                    const int e = tid, i = e / 9, j = e - i * 9;
-                    int pj = s_part_i[j], rj = s_role[j];
-                    double a = s_A[i * 9 + j], b = s_A[i * 9 + pj];
-                    double va = s_V[i * 9 + j], vb = s_V[i * 9 + pj];
-                    double cj = s_c[j], sj = s_s[j];
-                    double bv, vv;
-                    if (rj == 1) { bv = cj * a - sj * b; vv = cj * va - sj * vb; }
-                    else if (rj == 2) { bv = sj * b + cj * a; vv = sj * vb + cj * va; }
-                    else { bv = a; vv = va; }
-                    s_B[e] = bv;
-                    s_Vn[e] = vv;
-                }
-                __syncthreads();
-                if (tid < 81) {
-                    const int e = tid, i = e / 9, j = e - i * 9;
-                    s_V[e] = s_Vn[e];
-                    if (j >= i) {
-                        int pi = s_part_i[i], ri = s_role[i];
-                        double a = s_B[i * 9 + j], b = s_B[pi * 9 + j];
-                        double ci = s_c[i], si = s_s[i];
-                        double v;
-                        if (ri == 1) v = ci * a - si * b;
-                        else if (ri == 2) v = si * b + ci * a;
-                        else v = a;
-                        s_A[i * 9 + j] = v;
-                        s_A[j * 9 + i] = v;
-                    }
-                }
-                __syncthreads();
-                if (tid < 4 && s_ovi[tid][2]) {
-                    int pp = s_ovi[tid][0], qq = s_ovi[tid][1];
-                    s_A[pp * 9 + pp] = s_ov[tid][0];
-                    s_A[qq * 9 + qq] = s_ov[tid][1];
-                    s_A[pp * 9 + qq] = 0.0;
-                    s_A[qq * 9 + pp] = 0.0;
-                }
-                __syncthreads();
-            }
-        }
         for (int i = tid; i < n; i += RF_T) {
             const double* p = d.pts + 4 * (size_t)idx[i];
             float4 o = make_float4((float)p[0], (float)p[1], (float)p[2], (float)p[3]);
             reinterpret_cast<float4*>(d.model_p)[i] = o;
         }
         if (tid == 0) {
-            int k = argmin_diag<9>(s_A);
-            double f[9];
-            for (int i = 0; i < 9; ++i) f[i] = s_V[i * 9 + k];
+            double Fb[9], f0[9], f[9];
+            for (int i = 0; i < 9; ++i) Fb[i] = d.hypF[(size_t)bestk * 9 + i];
+            warm_start(Fb, sc1, mean[0], mean[1], sc2, mean[2], mean[3], f0);
+            ls_nullvec9(s_A, f0, f);
             double Fn[9];
             denormalize(f, sc1, mean[0], mean[1], sc2, mean[2], mean[3], Fn);
             rank2(Fn);

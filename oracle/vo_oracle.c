@@ -221,82 +221,80 @@ static void jacobi_eig(double* A, int n, double* V)
     }
 }
 
-/* Parallel-order Jacobi for the 9x9 refit (A^T A): round-robin schedule over 10 slots
- * (slot 9 = idle), round r pairs ((r+k)%9, (r-k)%9), k = 1..4, so a sweep of 9 rounds
- * visits all 36 pairs; the 4 disjoint rotations of a round are applied together as
- * B = A J (columns), A' = J^T B (rows, upper triangle mirrored), V' = V J, then the NR
- * diagonal / zero overrides.  This is the exact operation order of the device refit
- * (k_refit), so refit outputs agree bit for bit. */
-static void jacobi_par9(double* A, double* V)
+static void mm3(const double* A, const double* B, double* C);
+static void mtm3(const double* A, const double* B, double* C);
+
+/* Least-squares null vector of the refit's design matrix: the smallest eigenvector of the
+ * 9x9 PSD S = A^T A (Eigen::JacobiSVD V.col(8), ransac.cpp:77-78).  Cholesky S = L L^T with a
+ * pivot floor of 1e-15 * max diag (an exactly singular S -- e.g. 8 inliers -- has its null
+ * vector as the fixed point), then inverse iteration from the warm start x0 until the unit
+ * iterate moves by <= 4e-16 (at most 32 steps).  Same operation order as k_refit. */
+static void ls_nullvec9(const double* S, const double* x0, double* f)
 {
-    const int n = 9;
-    for (int i = 0; i < 81; ++i) V[i] = 0.0;
-    for (int i = 0; i < 9; ++i) V[i * 9 + i] = 1.0;
-    for (int sweep = 0; sweep < 50; ++sweep) {
-        double offr[9], diar[9];
-        for (int r = 0; r < 9; ++r) {
-            double o = 0.0;
-            for (int q = r + 1; q < 9; ++q) o = o + A[r * 9 + q] * A[r * 9 + q];
-            offr[r] = o;
-            diar[r] = A[r * 9 + r] * A[r * 9 + r];
-        }
-        double off = 0.0, dia = 0.0;
-        for (int r = 0; r < 9; ++r) { off = off + offr[r]; dia = dia + diar[r]; }
-        if (off == 0.0 || off <= 1e-30 * dia) break;
-        for (int rnd = 0; rnd < 9; ++rnd) {
-            int partner[9], role[9];      /* role 0 idle, 1 p, 2 q */
-            double cc[9], ss[9];
-            double tt[4], app_[4], aqq_[4], apq_[4];
-            int pp[4], qq[4], act[4];
-            for (int i = 0; i < 9; ++i) { partner[i] = i; role[i] = 0; cc[i] = 1.0; ss[i] = 0.0; }
-            for (int k = 1; k <= 4; ++k) {
-                int a = (rnd + k) % 9, b = (rnd - k + 9) % 9;
-                int p = a < b ? a : b, q = a < b ? b : a;
-                pp[k - 1] = p; qq[k - 1] = q;
-                double apq = A[p * 9 + q];
-                act[k - 1] = apq != 0.0;
-                if (!act[k - 1]) continue;
-                double app = A[p * 9 + p], aqq = A[q * 9 + q];
-                double theta = (aqq - app) / (2.0 * apq);
-                double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
-                if (theta < 0.0) t = -t;
-                double c = 1.0 / sqrt(t * t + 1.0);
-                double sn = t * c;
-                tt[k - 1] = t; app_[k - 1] = app; aqq_[k - 1] = aqq; apq_[k - 1] = apq;
-                partner[p] = q; partner[q] = p; role[p] = 1; role[q] = 2;
-                cc[p] = c; cc[q] = c; ss[p] = sn; ss[q] = sn;
-            }
-            double B[81], Vn[81];
-            for (int i = 0; i < 9; ++i)
-                for (int j = 0; j < 9; ++j) {
-                    int pj = partner[j];
-                    double a = A[i * 9 + j], b = A[i * 9 + pj];
-                    double va = V[i * 9 + j], vb = V[i * 9 + pj];
-                    if (role[j] == 1) { B[i * 9 + j] = cc[j] * a - ss[j] * b; Vn[i * 9 + j] = cc[j] * va - ss[j] * vb; }
-                    else if (role[j] == 2) { B[i * 9 + j] = ss[j] * b + cc[j] * a; Vn[i * 9 + j] = ss[j] * vb + cc[j] * va; }
-                    else { B[i * 9 + j] = a; Vn[i * 9 + j] = va; }
-                }
-            for (int i = 0; i < 9; ++i)
-                for (int j = i; j < 9; ++j) {
-                    int pi = partner[i];
-                    double a = B[i * 9 + j], b = B[pi * 9 + j];
-                    double v;
-                    if (role[i] == 1) v = cc[i] * a - ss[i] * b;
-                    else if (role[i] == 2) v = ss[i] * b + cc[i] * a;
-                    else v = a;
-                    A[i * 9 + j] = v; A[j * 9 + i] = v;
-                }
-            for (int k = 0; k < 4; ++k) {
-                if (!act[k]) continue;
-                int p = pp[k], q = qq[k];
-                A[p * 9 + p] = app_[k] - tt[k] * apq_[k];
-                A[q * 9 + q] = aqq_[k] + tt[k] * apq_[k];
-                A[p * 9 + q] = 0.0; A[q * 9 + p] = 0.0;
-            }
-            memcpy(V, Vn, sizeof(Vn));
+    double L[81], invd[9];
+    double mx = 0.0;
+    for (int i = 0; i < 9; ++i)
+        if (S[i * 9 + i] > mx) mx = S[i * 9 + i];
+    double fl = 1e-15 * mx;
+    if (!(fl > 0.0)) fl = 1e-300;
+    for (int i = 0; i < 81; ++i) L[i] = 0.0;
+    for (int j = 0; j < 9; ++j) {
+        double sj = S[j * 9 + j];
+        for (int k = 0; k < j; ++k) sj = sj - L[j * 9 + k] * L[j * 9 + k];
+        if (!(sj > fl)) sj = fl;
+        double dj = sqrt(sj);
+        L[j * 9 + j] = dj;
+        invd[j] = 1.0 / dj;
+        for (int i = j + 1; i < 9; ++i) {
+            double v = S[i * 9 + j];
+            for (int k = 0; k < j; ++k) v = v - L[i * 9 + k] * L[j * 9 + k];
+            L[i * 9 + j] = v * invd[j];
         }
     }
-    (void)n;
+    double x[9];
+    double n0 = 0.0;
+    for (int i = 0; i < 9; ++i) n0 = n0 + x0[i] * x0[i];
+    n0 = sqrt(n0);
+    if (n0 > 0.0 && n0 < 1e300) { for (int i = 0; i < 9; ++i) x[i] = x0[i] / n0; }
+    else { for (int i = 0; i < 9; ++i) x[i] = 1.0 / 3.0; }
+    for (int it = 0; it < 32; ++it) {
+        double y[9], z[9];
+        for (int i = 0; i < 9; ++i) {
+            double v = x[i];
+            for (int k = 0; k < i; ++k) v = v - L[i * 9 + k] * y[k];
+            y[i] = v * invd[i];
+        }
+        for (int i = 8; i >= 0; --i) {
+            double v = y[i];
+            for (int k = i + 1; k < 9; ++k) v = v - L[k * 9 + i] * z[k];
+            z[i] = v * invd[i];
+        }
+        double nn = 0.0, dot = 0.0;
+        for (int i = 0; i < 9; ++i) { nn = nn + z[i] * z[i]; dot = dot + z[i] * x[i]; }
+        nn = sqrt(nn);
+        double sg = dot < 0.0 ? -1.0 : 1.0;
+        double diff = 0.0;
+        for (int i = 0; i < 9; ++i) {
+            double xn = (z[i] / nn) * sg;
+            double dd = fabs(xn - x[i]);
+            if (dd > diff) diff = dd;
+            x[i] = xn;
+        }
+        if (diff <= 4e-16) break;
+    }
+    for (int i = 0; i < 9; ++i) f[i] = x[i];
+}
+
+/* warm start for ls_nullvec9: the best hypothesis' F mapped into the refit's normalized
+ * frame, f0 = T2^-T F T1^-1 (inverse of the quirk-6 denormalization F = T2^T f T1). */
+static void warm_start(const double* Fb, double s1, double mx1, double my1, double s2, double mx2, double my2,
+                       double* f0)
+{
+    double T1i[9] = {1.0 / s1, 0.0, mx1, 0.0, 1.0 / s1, my1, 0.0, 0.0, 1.0};
+    double T2i[9] = {1.0 / s2, 0.0, mx2, 0.0, 1.0 / s2, my2, 0.0, 0.0, 1.0};
+    double G[9];
+    mtm3(T2i, Fb, G);
+    mm3(G, T1i, f0);
 }
 
 static int argmin_diag(const double* A, int n)
@@ -747,6 +745,11 @@ int voo_fit_F8(const double* pts, const int32_t idx[8], double F[9])
  * null vector as the smallest eigenvector of A^T A; sums in the fixed device order. */
 int voo_fit_F(const double* pts, const int32_t* idx, int n, double F[9])
 {
+    return voo_fit_F_warm(pts, idx, n, NULL, F);
+}
+
+int voo_fit_F_warm(const double* pts, const int32_t* idx, int n, const double* Fb, double F[9])
+{
     if (n < 8) return -1;
     red256 r[4];
     double mean[4];
@@ -795,10 +798,10 @@ int voo_fit_F(const double* pts, const int32_t* idx, int n, double F[9])
                 AtA[u * 9 + v] = x; AtA[v * 9 + u] = x;
             }
     }
-    double V[81], f[9];
-    jacobi_par9(AtA, V);
-    int k = argmin_diag(AtA, 9);
-    for (int i = 0; i < 9; ++i) f[i] = V[i * 9 + k];
+    double f0[9], f[9];
+    if (Fb) warm_start(Fb, sc1, mean[0], mean[1], sc2, mean[2], mean[3], f0);
+    else for (int i = 0; i < 9; ++i) f0[i] = 1.0;
+    ls_nullvec9(AtA, f0, f);
     denormalize(f, sc1, mean[0], mean[1], sc2, mean[2], mean[3], F);
     rank2(F);
     return 0;
@@ -844,7 +847,7 @@ int voo_ransac(const double* pts, int m, double prob, double thr, int T, uint64_
         if (voo_sampson(F, pts + 4 * (size_t)i) < thr) idx[n++] = i;
     res->n_inl = n;
     if (inl_idx) memcpy(inl_idx, idx, sizeof(int32_t) * n);
-    if (n >= 8) { voo_fit_F(pts, idx, n, res->F); res->fitted = 1; }
+    if (n >= 8) { voo_fit_F_warm(pts, idx, n, F, res->F); res->fitted = 1; }
     free(idx);
     return 0;
 }

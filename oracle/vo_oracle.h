@@ -86,6 +86,7 @@ typedef struct {
 } voo_ransac_result;
 
 int  voo_fit_F(const double* pts, const int32_t* idx, int n, double F[9]);
+int  voo_fit_F_warm(const double* pts, const int32_t* idx, int n, const double* Fb, double F[9]);
 int  voo_fit_F8(const double* pts, const int32_t idx[8], double F[9]);
 double voo_sampson(const double F[9], const double* p);
 int  voo_ransac(const double* pts /* m*4: x1,y1,x2,y2 */, int m, double prob, double thr,
