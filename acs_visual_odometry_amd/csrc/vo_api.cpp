@@ -276,14 +276,21 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
         d.maxit_initial = to_int_x86(std::log(1.0 - k.ransac_p) / std::log(1.0 - std::pow(1.0 - outlierRatio, 8.0)));
     }
     c->max_hyp = std::max(VO_MAX_HYP, std::min(d.maxit_initial, 1 << 20));
-    d.cand_cap = (uint32_t)(((H + 1) / 2) * ((W + 1) / 2));
+    const int ntiles = ((W + 63) / 64) * ((H + 15) / 16);
+    if (ntiles > 2048) { delete c; return VO_ERR_ARG; }      // SEL_MAX_TILES (select kernel LDS)
+    d.cand_cap = (uint32_t)ntiles * 256u;
     int rc = VO_OK;
     auto bail = [&](int r) { vo_destroy(c); return r; };
     if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
+    d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
+    if (d.sel_lds < 0) return bail(VO_ERR_HIP);
     rc |= dalloc(&d.frame_in, (size_t)W * H);
     rc |= dalloc(&d.blurred, (size_t)W * H);
     rc |= dalloc(&d.response, (size_t)W * H);
     rc |= dalloc(&d.cand, d.cand_cap);
+    rc |= dalloc(&d.tilerows, (size_t)ntiles * 16);
+    rc |= dalloc(&d.ckeys, d.cand_cap);
+    rc |= dalloc(&d.selbits, d.cand_cap / 64 + 1);
     rc |= dalloc(&d.hist, VO_HIST_BINS);
     for (int s = 0; s < 2; ++s) {
         rc |= dalloc(&d.kps[s], N);
@@ -299,6 +306,9 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc(&d.model_p, (size_t)N * 4);
     rc |= dalloc(&d.st, 1);
     rc |= dalloc(&d.ctr, 4);
+#ifdef VO_STAMPS
+    rc |= dalloc(&d.dbg, (size_t)c->max_hyp * 16);
+#endif
     if (rc != VO_OK) return bail(VO_ERR_HIP);
     const std::vector<uint16_t>& tab = maxit_table(N, k.ransac_p);
     if (dalloc(&c->tab_dev, tab.size()) != VO_OK) return bail(VO_ERR_HIP);
@@ -326,9 +336,9 @@ void vo_destroy(vo_ctx* c)
     (void)hipSetDevice(c->cfg.device);
     if (c->s) (void)hipStreamSynchronize(c->s);
     VoDev& d = c->d;
-    void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.hist, d.kps[0], d.kps[1], d.desc[0], d.desc[1],
+    void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.tilerows, d.ckeys, d.selbits, d.hist, d.kps[0], d.kps[1], d.desc[0], d.desc[1],
                     d.pre[0], d.pre[1], d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.model_p,
-                    d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr};
+                    d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr, d.dbg};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->out_host) (void)hipHostFree(c->out_host);
@@ -606,6 +616,16 @@ int vo_last_kernel_times(vo_ctx* c, const char** names, float* ms, int cap)
         if (ms) ms[k] = c->kcount[k] ? c->ktime_ms[k] / (float)c->kcount[k] : -1.f;
     }
     return nk;
+}
+
+// diagnostics: copy the stamp buffer (VO_STAMPS builds; returns 0 entries otherwise)
+int vo_debug_stamps(vo_ctx* c, unsigned long long* out, int n)
+{
+    if (!c || !c->d.dbg) return 0;
+    int m = std::min(n, c->max_hyp * 16);
+    HIPCHK(hipStreamSynchronize(c->s));
+    HIPCHK(hipMemcpy(out, c->d.dbg, sizeof(unsigned long long) * m, hipMemcpyDeviceToHost));
+    return m;
 }
 
 int vo_device_alloc(vo_ctx* c, size_t bytes, void** dptr)

@@ -7,7 +7,10 @@
 //   frame_in    u8  W*H         staging for host-supplied frames
 //   blurred     u8  W*H         7x7 Gaussian output (read back by describe)
 //   response    f32 W*H         optional dense R map (debug / parity only)
-//   cand        u64 cand_cap    NMS survivors, key = Rbits<<32 | row<<16 | col
+//   cand        u64 256/tile    NMS survivors per 64x16 tile, key = Rbits<<32 | row<<16 | col
+//   tilerows    u8  16/tile     survivors per tile row (select emits raster order from them)
+//   ckeys       u64 256/tile    compact survivors (only when they overflow select's LDS)
+//   selbits     u64 4/tile      selected-survivor bitmap (only when it overflows LDS)
 //   hist        u32 4096        coarse histogram of candidate R (top-N boundary)
 //   kps[2]      int2 N          raster-ordered keypoints, slot ping-pong
 //   desc[2]     u64 8N          packed 512-test descriptors (slot ping-pong)
@@ -83,7 +86,11 @@ struct VoDev {
     uint8_t* frame_in;
     uint8_t* blurred;
     float* response;
-    uint64_t* cand;
+    uint64_t* cand;       // per stencil tile: up to 256 keys in tile-local raster order
+    uint8_t* tilerows;    // per stencil tile: candidate count of each of its 16 rows
+    uint64_t* ckeys;      // select: compact candidate keys when they exceed the LDS capacity
+    uint64_t* selbits;    // select: selected-key bitmap when it exceeds the LDS capacity
+    int sel_lds;          // select: dynamic LDS bytes
     uint32_t* hist;
     int2* kps[2];
     uint64_t* desc[2];
@@ -100,6 +107,7 @@ struct VoDev {
     VoState* st;
     VoFrameOut* out;
     unsigned* ctr;        // in-launch arrival counters: [0] match, [1] ransac, [2] triangulate
+    unsigned long long* dbg;   // diagnostic s_memtime stamps (VO_STAMPS builds only)
 };
 
 // launch wrappers (vo_kernels.hip)
@@ -108,6 +116,7 @@ namespace vo {
 void launch_frame_begin(const VoDev& d, int mode, hipStream_t s);
 void launch_stencil(const VoDev& d, const uint8_t* frame, int write_response, hipStream_t s);
 void launch_select(const VoDev& d, hipStream_t s);
+int select_lds_bytes(int W, int H, int* key_cap);     // sets the kernel attribute; <0 on failure
 void launch_describe(const VoDev& d, hipStream_t s);
 void launch_match(const VoDev& d, hipStream_t s);          // + ordered compaction (last workgroup)
 void launch_ransac(const VoDev& d, int nhyp, hipStream_t s); // all hypotheses + replay (last workgroup)

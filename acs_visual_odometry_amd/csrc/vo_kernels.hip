@@ -320,6 +320,18 @@ __device__ __forceinline__ double sampson(const double* F, double x, double y, d
 }
 
 __device__ __forceinline__ unsigned long long ballot64(bool p) { return __ballot(p); }
+
+// diagnostic stamps (separate VO_STAMPS build; never in the product library)
+#ifdef VO_STAMPS
+#define VO_STAMP(d, slot, idx)                                                                 \
+    do {                                                                                       \
+        unsigned long long _t;                                                                 \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");            \
+        if ((threadIdx.x & 63) == 0 && (d).dbg) (d).dbg[(size_t)(slot) * 16 + (idx)] = _t;   \
+    } while (0)
+#else
+#define VO_STAMP(d, slot, idx) do { } while (0)
+#endif
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 // ---------------------------------------------------------------------------
@@ -386,13 +398,11 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
     __shared__ float s_bl[ST_BH][ST_BW];
     __shared__ float s_jx[ST_GH][ST_GW], s_jy[ST_GH][ST_GW], s_jxy[ST_GH][ST_GW];
     __shared__ float s_r[ST_RH][ST_RW];
-    __shared__ uint64_t s_keys[ST_TW * ST_TH / 4];
-    __shared__ int s_nk, s_base;
+    __shared__ unsigned long long s_bal[ST_TH];
 
     const int W = d.W, H = d.H;
     const int x0 = blockIdx.x * ST_TW, y0 = blockIdx.y * ST_TH;
     const int tid = threadIdx.x;
-    if (tid == 0) s_nk = 0;
 
     // 1. source tile with BORDER_REFLECT_101 addressing
     for (int e = tid; e < ST_SH * ST_SW; e += 256) {
@@ -468,37 +478,48 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
             d.response[(size_t)y * W + x] = out;
     }
     __syncthreads();
-    // 6. strict 3x3 NMS inside the retinal margin (corner_detection_parallel_GPU.cpp:152-180)
+    // 6. strict 3x3 NMS inside the retinal margin (corner_detection_parallel_GPU.cpp:152-180).
+    //    Survivors are compacted in tile-local raster order: wave w owns tile rows w, w+4, ...
+    //    (lane = column), so ballots give the order; per-row counts go to tilerows[] so the
+    //    select kernel can emit the global raster order without sorting.
     const int hk = d.nms_k / 2;
-    for (int e = tid; e < ST_TH * ST_TW; e += 256) {
-        int r = e / ST_TW, c = e - r * ST_TW;
-        int i = y0 + r, j = x0 + c;
-        if (i >= H || j >= W) continue;
-        if (i < hk || i >= H - hk || j < hk || j >= W - hk) continue;
-        if (!((j >= d.bcol) && (j <= W - d.bcol) && (i >= d.brow) && (i <= H - d.brow))) continue;
+    const int lane = tid & 63, wave = tid >> 6;
+    float cvk[ST_TH / 4];
+    bool mxk[ST_TH / 4];
+#pragma unroll
+    for (int kk = 0; kk < ST_TH / 4; ++kk) {
+        const int r = 4 * kk + wave, c = lane;
+        const int i = y0 + r, j = x0 + c;
+        bool ok = i < H && j < W && i >= hk && i < H - hk && j >= hk && j < W - hk &&
+                  (j >= d.bcol) && (j <= W - d.bcol) && (i >= d.brow) && (i <= H - d.brow);
         float cv = s_r[r + 1][c + 1];
-        bool mx = true;
+        bool mx = ok;
 #pragma unroll
-        for (int a = -1; a <= 1; ++a)
+        for (int a2 = -1; a2 <= 1; ++a2)
 #pragma unroll
-            for (int b = -1; b <= 1; ++b)
-                if ((a | b) != 0 && s_r[r + 1 + a][c + 1 + b] >= cv) mx = false;
-        if (mx) {
-            uint32_t bits = __float_as_uint(cv);
-            uint64_t key = ((uint64_t)bits << 32) | ((uint64_t)i << 16) | (uint64_t)j;
-            int slot = atomicAdd(&s_nk, 1);
-            s_keys[slot] = key;
-            uint32_t bin = (bits - d.thr_bits) >> 15;
-            if (bin > VO_HIST_BINS - 1) bin = VO_HIST_BINS - 1;
-            atomicAdd(&d.hist[bin], 1u);
-        }
+            for (int b2 = -1; b2 <= 1; ++b2)
+                if ((a2 | b2) != 0 && s_r[r + 1 + a2][c + 1 + b2] >= cv) mx = false;
+        unsigned long long bal = ballot64(mx);
+        if (lane == 0) s_bal[r] = bal;
+        cvk[kk] = cv;
+        mxk[kk] = mx;
     }
     __syncthreads();
-    if (tid == 0) s_base = s_nk ? (int)atomicAdd(&d.st->cand_count, (uint32_t)s_nk) : 0;
-    __syncthreads();
-    for (int e = tid; e < s_nk; e += 256) {
-        uint32_t pos = (uint32_t)s_base + e;
-        if (pos < d.cand_cap) d.cand[pos] = s_keys[e];
+    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    if (tid < ST_TH) d.tilerows[tile * ST_TH + tid] = (uint8_t)__popcll(s_bal[tid]);
+#pragma unroll
+    for (int kk = 0; kk < ST_TH / 4; ++kk) {
+        if (!mxk[kk]) continue;
+        const int r = 4 * kk + wave, c = lane;
+        int off = 0;
+        for (int rr = 0; rr < r; ++rr) off += __popcll(s_bal[rr]);
+        off += __popcll(s_bal[r] & ((1ull << lane) - 1ull));
+        const int i = y0 + r, j = x0 + c;
+        const uint32_t bits = __float_as_uint(cvk[kk]);
+        d.cand[(size_t)tile * (ST_TW * ST_TH / 4) + off] = ((uint64_t)bits << 32) | ((uint64_t)i << 16) | (uint64_t)j;
+        uint32_t bin = (bits - d.thr_bits) >> 15;
+        if (bin > VO_HIST_BINS - 1) bin = VO_HIST_BINS - 1;
+        atomicAdd(&d.hist[bin], 1u);
     }
 }
 
@@ -509,7 +530,9 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
 // (feature_extraction_parallel_GPU.cpp:259-265).
 // ---------------------------------------------------------------------------
 #define SEL_MAX 4096
-#define BND_CAP 4096
+#define BND_CAP 2048
+#define SEL_MAX_TILES 2048
+#define SEL_LDS_BITS 65536
 
 template <typename T, bool ASC>
 __device__ void bitonic_lds(T* a, int n_pow2)
@@ -529,90 +552,298 @@ __device__ void bitonic_lds(T* a, int n_pow2)
     }
 }
 
+// Dynamic LDS layout of k_select (bytes; host and device derive it from the tile count).
+struct SelLayout {
+    int rows, tpre, segw, bits, chunk, keys, key_cap, total;
+};
+__host__ __device__ inline SelLayout sel_layout(int ntiles, int lds_bytes)
+{
+    auto al = [](int v) { return (v + 15) & ~15; };
+    SelLayout L;
+    const int nseg = ntiles * ST_TH;
+    L.rows = 0;
+    L.tpre = L.rows + al(ntiles * 16);
+    L.segw = L.tpre + al((ntiles + 1) * 4);
+    const int segb = al(nseg > BND_CAP * 8 ? nseg : BND_CAP * 8);     // u8 counts, aliased by boundary keys
+    L.bits = L.segw + segb;
+    L.chunk = L.bits + SEL_LDS_BITS / 8;
+    L.keys = L.chunk + 1024 * 4;
+    L.key_cap = (lds_bytes - L.keys) / 8;
+    L.total = lds_bytes;
+    return L;
+}
+
+__device__ __forceinline__ uint32_t sel_bin(uint64_t key, uint32_t thr_bits)
+{
+    uint32_t bin = ((uint32_t)(key >> 32) - thr_bits) >> 15;
+    return bin > VO_HIST_BINS - 1 ? VO_HIST_BINS - 1 : bin;
+}
+
+// select: exact top-N of the NMS survivors by (R,row,col) descending, emitted in raster
+// order (feature_extraction_parallel_GPU.cpp:235-265).  One workgroup; every phase is
+// parallel over keys (independent loads) -- no per-thread serial walks:
+//   A  per-tile row counts -> LDS, tile totals -> block scan (compact key index g, tile order)
+//   B  stage the C keys compactly (LDS if they fit, else a global scratch array)
+//   C  boundary bin from the stencil histogram; its keys ranked -> exact threshold key Tb
+//   D  selected-key bitmap (ballots) + per-(row, tile) selected counts (u8, LDS atomics)
+//   E  chunked block scan over the (row, tile) segments in raster order
+//   F  each selected key computes its raster position directly and writes its keypoint
 __global__ void __launch_bounds__(1024) k_select(VoDev d)
 {
     VoState* st = d.st;
     if (st->status != VO_STATUS_OK && st->status != VO_STATUS_FIRST) return;
-    __shared__ uint32_t s_sel[SEL_MAX];
-    __shared__ uint64_t s_bnd[BND_CAP];
-    __shared__ uint32_t s_tot[1024];
-    __shared__ int s_nsel, s_nbnd, s_b, s_above;
-    const int tid = threadIdx.x;
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ uint32_t s_hs[16];
+    __shared__ int s_wsum[16];
+    __shared__ int s_nbnd, s_b, s_above;
+    __shared__ uint64_t s_tb;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int N = d.N;
-    uint32_t C = st->cand_count;
-    if (C > d.cand_cap) C = d.cand_cap;
-    int nout;
-    if (tid == 0) { s_nsel = 0; s_nbnd = 0; s_b = -1; s_above = 0; }
+    const int ntx = (d.W + ST_TW - 1) / ST_TW, nty = (d.H + ST_TH - 1) / ST_TH, ntiles = ntx * nty;
+    const int nseg = ntiles * ST_TH;                    // (row, tile-column) segments, raster order
+    const SelLayout L = sel_layout(ntiles, d.sel_lds);
+    uint4* s_rows = reinterpret_cast<uint4*>(smem + L.rows);
+    int* s_tpre = reinterpret_cast<int*>(smem + L.tpre);
+    uint32_t* s_segw = reinterpret_cast<uint32_t*>(smem + L.segw);
+    const uint8_t* s_segb = smem + L.segw;
+    uint64_t* s_bnd = reinterpret_cast<uint64_t*>(smem + L.segw);        // phase C only
+    uint64_t* s_bitsl = reinterpret_cast<uint64_t*>(smem + L.bits);
+    int* s_chunk = reinterpret_cast<int*>(smem + L.chunk);
+    uint64_t* s_keys = reinterpret_cast<uint64_t*>(smem + L.keys);
+    const size_t TCAP = ST_TW * ST_TH / 4;
+    if (tid == 0) { s_nbnd = 0; s_b = -1; s_above = 0; }
+    VO_STAMP(d, 1990, 0);
+    // A
+    const int tpt = (ntiles + 1023) / 1024;            // tiles per thread (<= 2)
+    int tt[2] = {0, 0};
+    int myC = 0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int t = tid * tpt + u;
+        if (u < tpt && t < ntiles) {
+            uint4 rc = reinterpret_cast<const uint4*>(d.tilerows)[t];
+            s_rows[t] = rc;
+            const uint32_t w4[4] = {rc.x, rc.y, rc.z, rc.w};
+            int tot = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                tot += (int)(w4[q] & 0xFF) + (int)((w4[q] >> 8) & 0xFF) + (int)((w4[q] >> 16) & 0xFF) + (int)(w4[q] >> 24);
+            tt[u] = tot;
+            myC += tot;
+        }
+    }
+    int incl = myC;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        int v = __shfl_up(incl, off);
+        if (lane >= off) incl += v;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
     __syncthreads();
-    if ((int)C <= N) {
-        for (uint32_t e = tid; e < C; e += 1024) {
-            uint64_t key = d.cand[e];
-            s_sel[e] = (uint32_t)key;               // row<<16 | col
+    int base = incl - myC;
+    int C = 0;
+    for (int w = 0; w < 16; ++w) { if (w < wave) base += s_wsum[w]; C += s_wsum[w]; }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int t = tid * tpt + u;
+        if (u < tpt && t < ntiles) { s_tpre[t] = base; base += tt[u]; }
+    }
+    if (tid == 0) s_tpre[ntiles] = C;
+    const bool bits_lds = C <= SEL_LDS_BITS;
+    uint64_t* bits = bits_lds ? s_bitsl : d.selbits;
+    for (int w = tid; w < (C + 63) / 64; w += 1024) bits[w] = 0ull;
+    __syncthreads();
+    // B
+    const bool staged = C <= L.key_cap;
+    uint64_t* keys = staged ? s_keys : d.ckeys;
+    {
+        auto slot_of = [&](int g) -> size_t {
+            int lo = 0, hi = ntiles - 1;
+            while (lo < hi) {
+                int mid = (lo + hi + 1) >> 1;
+                if (s_tpre[mid] <= g) lo = mid; else hi = mid - 1;
+            }
+            return (size_t)lo * TCAP + (size_t)(g - s_tpre[lo]);
+        };
+        for (int g0 = tid; g0 < C; g0 += 4 * 1024) {
+            uint64_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int g = g0 + u * 1024;
+                v[u] = g < C ? d.cand[slot_of(g)] : 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (g0 + u * 1024 < C) keys[g0 + u * 1024] = v[u];
         }
-        nout = (int)C;
-    } else {
-        // boundary bin from the stencil's histogram
-        uint32_t h0 = d.hist[4 * tid], h1 = d.hist[4 * tid + 1], h2 = d.hist[4 * tid + 2], h3 = d.hist[4 * tid + 3];
-        s_tot[tid] = h0 + h1 + h2 + h3;
+    }
+    __syncthreads();
+    VO_STAMP(d, 1990, 1);
+    // C
+    int b = -1;
+    uint64_t Tb = 0ull;
+    if (C > N) {
+        uint32_t h[4], hs = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { h[q] = d.hist[4 * tid + q]; hs += h[q]; }
+        uint32_t suf = hs;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            uint32_t v = __shfl_down(suf, off);
+            if (lane + off < 64) suf += v;
+        }
+        if (lane == 0) s_hs[wave] = suf;
         __syncthreads();
-        // suffix sums (Hillis-Steele over 1024 entries, from the top bins down)
-        for (int off = 1; off < 1024; off <<= 1) {
-            uint32_t v = (tid + off < 1024) ? s_tot[tid + off] : 0u;
-            __syncthreads();
-            s_tot[tid] += v;
-            __syncthreads();
-        }
-        uint32_t above = (tid + 1 < 1024) ? s_tot[tid + 1] : 0u;   // bins > 4*tid+3
-        uint32_t hb[4] = {h0, h1, h2, h3};
+        uint32_t above = suf - hs;
+        for (int w = wave + 1; w < 16; ++w) above += s_hs[w];
         uint32_t run = above;
         for (int q = 3; q >= 0; --q) {
-            if (run < (uint32_t)N && run + hb[q] >= (uint32_t)N) { s_b = 4 * tid + q; s_above = (int)run; }
-            run += hb[q];
+            if (run < (uint32_t)N && run + h[q] >= (uint32_t)N) { s_b = 4 * tid + q; s_above = (int)run; }
+            run += h[q];
         }
         __syncthreads();
-        const int b = s_b;
-        for (uint32_t e = tid; e < C; e += 1024) {
-            uint64_t key = d.cand[e];
-            uint32_t bits = (uint32_t)(key >> 32);
-            uint32_t bin = (bits - d.thr_bits) >> 15;
-            if (bin > VO_HIST_BINS - 1) bin = VO_HIST_BINS - 1;
-            if ((int)bin > b) {
-                int p = atomicAdd(&s_nsel, 1);
-                s_sel[p] = (uint32_t)key;
-            } else if ((int)bin == b) {
-                int p = atomicAdd(&s_nbnd, 1);
-                if (p < BND_CAP) s_bnd[p] = key;
+        b = s_b;
+        VO_STAMP(d, 1990, 2);
+        for (int g0 = tid; g0 < C; g0 += 4 * 1024) {
+            uint64_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = g0 + u * 1024 < C ? keys[g0 + u * 1024] : 0ull;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (g0 + u * 1024 < C && (int)sel_bin(v[u], d.thr_bits) == b) {
+                    int p = atomicAdd(&s_nbnd, 1);
+                    if (p < BND_CAP) s_bnd[p] = v[u];
+                }
             }
         }
         __syncthreads();
-        int nb = s_nbnd;
-        if (nb > BND_CAP) {
-            // boundary bin too large for LDS: flag (never observed)
+        VO_STAMP(d, 1990, 3);
+        const int nb = s_nbnd;
+        if (nb > BND_CAP) {            // boundary bin too large for LDS (never observed)
             if (tid == 0) st->status = VO_STATUS_OVERFLOW;
             return;
         }
-        int p2 = 1;
-        while (p2 < nb) p2 <<= 1;
-        for (int e = nb + tid; e < p2; e += 1024) s_bnd[e] = 0ull;
-        __syncthreads();
-        bitonic_lds<uint64_t, false>(s_bnd, p2);
+        // the need-th largest boundary key: the one with exactly need-1 larger keys
         const int need = N - s_above;
-        for (int e = tid; e < need; e += 1024) s_sel[s_above + e] = (uint32_t)s_bnd[e];
-        nout = N;
+        Tb = ~0ull;
+        if (need > 0) {
+            for (int e = tid; e < nb; e += 1024) {
+                const uint64_t ke = s_bnd[e];
+                int rank = 0;
+                for (int f = 0; f < nb; ++f) rank += s_bnd[f] > ke;
+                if (rank == need - 1) s_tb = ke;        // keys are unique (they carry row, col)
+            }
+            __syncthreads();
+            Tb = s_tb;
+        }
+        if (tid == 0 && d.dbg) d.dbg[1990 * 16 + 10] = (unsigned long long)nb;
+    }
+    __syncthreads();                                    // s_bnd aliases the segment counts
+    for (int w = tid; w < (nseg + 3) / 4; w += 1024) s_segw[w] = 0u;
+    __syncthreads();
+    VO_STAMP(d, 1990, 4);
+    auto selected = [&](uint64_t key) -> bool {
+        if (b < 0) return true;
+        const int bin = (int)sel_bin(key, d.thr_bits);
+        return bin > b || (bin == b && key >= Tb);
+    };
+    // D
+    const int nround = (C + 1023) / 1024;
+    for (int r0 = 0; r0 < nround; r0 += 4) {
+        uint64_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int g = (r0 + u) * 1024 + tid;
+            v[u] = g < C ? keys[g] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (r0 + u >= nround) break;
+            const int g = (r0 + u) * 1024 + tid;
+            const bool sel = g < C && selected(v[u]);
+            const uint64_t bal = __ballot(sel);
+            if (lane == 0 && ((r0 + u) * 1024 + wave * 64) < C) bits[((r0 + u) * 1024 + wave * 64) >> 6] = bal;
+            if (sel) {
+                const int row = (int)((v[u] >> 16) & 0xFFFF), col = (int)(v[u] & 0xFFFF);
+                const int seg = row * ntx + (col >> 6);
+                atomicAdd(&s_segw[seg >> 2], 1u << (8 * (seg & 3)));
+            }
+        }
     }
     __syncthreads();
-    int p2 = 1;
-    while (p2 < nout) p2 <<= 1;
-    for (int e = nout + tid; e < p2; e += 1024) s_sel[e] = 0xFFFFFFFFu;
-    __syncthreads();
-    bitonic_lds<uint32_t, true>(s_sel, p2);
-    const int cur = st->cur;
-    int2* kp = d.kps[cur];
-    for (int e = tid; e < nout; e += 1024) {
-        uint32_t v = s_sel[e];
-        kp[e] = make_int2((int)(v & 0xFFFF), (int)(v >> 16));
+    // E: thread tid owns segments [tid*cs, tid*cs+cs)
+    const int cs = (nseg + 1023) / 1024;
+    auto bytesum = [&](int s0, int s1) -> int {         // sum of u8 counts in [s0, s1)
+        int acc = 0;
+        for (int s = s0; s < s1;) {
+            if ((s & 3) == 0 && s + 4 <= s1) {
+                const uint32_t w = s_segw[s >> 2];
+                const uint32_t p = (w & 0x00FF00FFu) + ((w >> 8) & 0x00FF00FFu);
+                acc += (int)((p & 0xFFFF) + (p >> 16));
+                s += 4;
+            } else {
+                acc += s_segb[s];
+                ++s;
+            }
+        }
+        return acc;
+    };
+    {
+        const int s0 = min(tid * cs, nseg), s1 = min(s0 + cs, nseg);
+        const int mine = bytesum(s0, s1);
+        int inc2 = mine;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            int v = __shfl_up(inc2, off);
+            if (lane >= off) inc2 += v;
+        }
+        if (lane == 63) s_wsum[wave] = inc2;
+        __syncthreads();
+        int pre = inc2 - mine;
+        for (int w = 0; w < wave; ++w) pre += s_wsum[w];
+        s_chunk[tid] = pre;
     }
-    if (tid == 0) st->n_kps[cur] = nout;
+    __syncthreads();
+    VO_STAMP(d, 1990, 5);
+    // F
+    int2* out = d.kps[st->cur];
+    for (int r0 = 0; r0 < nround; r0 += 4) {
+        uint64_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int g = (r0 + u) * 1024 + tid;
+            v[u] = g < C ? keys[g] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int g = (r0 + u) * 1024 + tid;
+            if (g >= C || !((bits[g >> 6] >> (g & 63)) & 1ull)) continue;
+            const int row = (int)((v[u] >> 16) & 0xFFFF), col = (int)(v[u] & 0xFFFF);
+            const int x = col >> 6, r = row & (ST_TH - 1), t = (row / ST_TH) * ntx + x;
+            const int seg = row * ntx + x;
+            // first compact index of this (row, tile) segment
+            const uint4 rc = s_rows[t];
+            const uint32_t w4[4] = {rc.x, rc.y, rc.z, rc.w};
+            int start = 0;
+#pragma unroll
+            for (int q = 0; q < ST_TH; ++q)
+                if (q < r) start += (int)((w4[q >> 2] >> (8 * (q & 3))) & 0xFF);
+            const int gs = s_tpre[t] + start;
+            // selected keys before g inside the segment
+            int within = 0;
+            for (int wi = gs >> 6; wi <= (g >> 6); ++wi) {
+                uint64_t m = bits[wi];
+                if (wi == (gs >> 6)) m &= ~0ull << (gs & 63);
+                if (wi == (g >> 6)) m &= (g & 63) ? (~0ull >> (64 - (g & 63))) : 0ull;
+                within += __popcll(m);
+            }
+            const int ch = seg / cs;
+            const int pos = s_chunk[ch] + bytesum(ch * cs, seg) + within;
+            out[pos] = make_int2(col, row);
+        }
+    }
+    VO_STAMP(d, 1990, 6);
+    if (tid == 0) st->n_kps[st->cur] = C < N ? C : N;
 }
 
 // ---------------------------------------------------------------------------
@@ -860,13 +1091,54 @@ __global__ void __launch_bounds__(256) k_match(VoDev d)
 __device__ __forceinline__ double shfl_d(double v, int src) { return __shfl(v, src); }
 __device__ __forceinline__ double shfl_xor_d(double v, int m) { return __shfl_xor(v, m); }
 
-__device__ void fit_F8_wave(const double* __restrict__ pts, const int s8[8], int lane, double F[9])
+// wave-wide max of a double, in every lane: DPP within rows of 16 (quad_perm 1032, 2301,
+// row_half_mirror, row_mirror), then the 4 row maxima via readlane.  No LDS round trips.
+__device__ __forceinline__ double dpp_f64(double v, int ctrl_sel)
+{
+    long long x = __double_as_longlong(v);
+    int lo = (int)(x & 0xFFFFFFFFll), hi = (int)(x >> 32);
+    int lo2, hi2;
+    switch (ctrl_sel) {
+    case 0: lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0xB1, 0xF, 0xF, false); hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0xB1, 0xF, 0xF, false); break;
+    case 1: lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0x4E, 0xF, 0xF, false); hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0x4E, 0xF, 0xF, false); break;
+    case 2: lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0x141, 0xF, 0xF, false); hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0x141, 0xF, 0xF, false); break;
+    default: lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0x140, 0xF, 0xF, false); hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0x140, 0xF, 0xF, false); break;
+    }
+    return __longlong_as_double(((long long)hi2 << 32) | (unsigned)lo2);
+}
+
+__device__ __forceinline__ double rdlane(double v, int l);
+
+__device__ __forceinline__ double wave_max_f64(double v)
+{
+    v = fmax(v, dpp_f64(v, 0));
+    v = fmax(v, dpp_f64(v, 1));
+    v = fmax(v, dpp_f64(v, 2));
+    v = fmax(v, dpp_f64(v, 3));
+    return fmax(fmax(rdlane(v, 0), rdlane(v, 16)), fmax(rdlane(v, 32), rdlane(v, 48)));
+}
+
+__device__ __forceinline__ double rdlane(double v, int l)
+{
+    long long x = __double_as_longlong(v);
+    int lo = __builtin_amdgcn_readlane((int)(x & 0xFFFFFFFFll), l);
+    int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// computeFundamentalMatrix on a minimal sample (ransac.cpp:63-93), one wavefront.
+// Gauss-Jordan with complete pivoting exactly as oracle nullvec_8x9: lane l = 8r + c holds
+// A[r][c] (r, c < 8) and every lane of row r holds A[r][8]; pivot = max |a| over unused
+// rows/cols, ties to the first in row-major order (max value, then min flat index).
+__device__ void fit_F8_wave(const VoDev& d, const double* __restrict__ pts, const int s8[8], int lane, double F[9],
+                            int slot)
 {
     double P[8][4];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const double* p = pts + 4 * (size_t)s8[i];
-        P[i][0] = p[0]; P[i][1] = p[1]; P[i][2] = p[2]; P[i][3] = p[3];
+        const double2* p = reinterpret_cast<const double2*>(pts + 4 * (size_t)s8[i]);
+        double2 a = p[0], b = p[1];
+        P[i][0] = a.x; P[i][1] = a.y; P[i][2] = b.x; P[i][3] = b.y;
     }
     double mx1 = 0, my1 = 0, mx2 = 0, my2 = 0;
 #pragma unroll
@@ -882,79 +1154,121 @@ __device__ void fit_F8_wave(const double* __restrict__ pts, const int s8[8], int
     sc1 = sqrt(2.0) / sqrt(sc1 / 8.0);
     sc2 = sqrt(2.0) / sqrt(sc2 / 8.0);
     double o1x = -(sc1 * mx1), o1y = -(sc1 * my1), o2x = -(sc2 * mx2), o2y = -(sc2 * my2);
-    // my row
+    VO_STAMP(d, slot, 2);
+    const int r = lane >> 3, c = lane & 7;
     double x1 = 0, y1 = 0, x2 = 0, y2 = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-        if (i == lane) { x1 = P[i][0]; y1 = P[i][1]; x2 = P[i][2]; y2 = P[i][3]; }
-    double a[9];
-    design_row(sc1 * x1 + o1x, sc1 * y1 + o1y, sc2 * x2 + o2x, sc2 * y2 + o2y, a);
-    const bool row_lane = lane < 8;
+        if (i == r) { x1 = P[i][0]; y1 = P[i][1]; x2 = P[i][2]; y2 = P[i][3]; }
+    double row[9];
+    design_row(sc1 * x1 + o1x, sc1 * y1 + o1y, sc2 * x2 + o2x, sc2 * y2 + o2y, row);
+    double arc = 0.0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) if (j == c) arc = row[j];
+    double ar8 = row[8];
     uint32_t used_c = 0, used_r = 0;
     int prs[8], pcs[8];
     int steps = 0;
 #pragma unroll
     for (int step = 0; step < 8; ++step) {
-        double bv = 0.0; int bc = -1;
-        if (row_lane && !((used_r >> lane) & 1u)) {
-#pragma unroll
-            for (int c = 0; c < 9; ++c)
-                if (!((used_c >> c) & 1u)) { double v = fabs(a[c]); if (v > bv) { bv = v; bc = c; } }
-        }
-        int br = bc >= 0 ? lane : 64;
-        if (bc < 0) bv = 0.0;
-#pragma unroll
-        for (int off = 1; off <= 4; off <<= 1) {
-            double ov = shfl_xor_d(bv, off);
-            int orr = __shfl_xor(br, off), oc = __shfl_xor(bc, off);
-            if (ov > bv || (ov == bv && orr < br)) { bv = ov; br = orr; bc = oc; }
-        }
-        bv = shfl_d(bv, 0); br = __shfl(br, 0); bc = __shfl(bc, 0);
-        if (!(bv > 0.0)) break;
-        used_r |= 1u << br; used_c |= 1u << bc;
-        prs[step] = br; pcs[step] = bc; steps = step + 1;
-        double prow[9];
-#pragma unroll
-        for (int c = 0; c < 9; ++c) prow[c] = shfl_d(a[c], br);
-        double piv = 0.0, mine = 0.0;
-#pragma unroll
-        for (int c = 0; c < 9; ++c) if (c == bc) { piv = prow[c]; mine = a[c]; }
-        if (row_lane && lane != br) {
-            double fct = mine / piv;
-#pragma unroll
-            for (int c = 0; c < 9; ++c) a[c] = a[c] - fct * prow[c];
+        const bool row_free = !((used_r >> r) & 1u);
+        double v1 = (row_free && !((used_c >> c) & 1u)) ? fabs(arc) : 0.0;
+        double v2 = (row_free && c == 0 && !((used_c >> 8) & 1u)) ? fabs(ar8) : 0.0;
+        if (!(v1 > 0.0)) v1 = -1.0;
+        if (!(v2 > 0.0)) v2 = -1.0;
+        // pivot: max value (DPP), ties to the first flat index r*9+col (ballot, scalar)
+        const double gmax = wave_max_f64(fmax(v1, v2));
+        if (!(gmax > 0.0)) break;                     // rank deficient: remaining columns free
+        const unsigned long long b1 = ballot64(v1 == gmax);
+        const unsigned long long b2 = ballot64(v2 == gmax);
+        int bi = 1 << 30;
+        if (b1) { int L = __ffsll((long long)b1) - 1; bi = (L >> 3) * 9 + (L & 7); }
+        if (b2) { int L = __ffsll((long long)b2) - 1; int i2 = (L >> 3) * 9 + 8; bi = i2 < bi ? i2 : bi; }
+        bi = __builtin_amdgcn_readfirstlane(bi);
+        const int pr = bi / 9, pc = bi - pr * 9;
+        used_r |= 1u << pr; used_c |= 1u << pc;
+        prs[step] = pr; pcs[step] = pc; steps = step + 1;
+        const double piv = pc < 8 ? rdlane(arc, pr * 8 + pc) : rdlane(ar8, pr * 8);
+        const double arpc = pc < 8 ? shfl_d(arc, r * 8 + pc) : ar8;      // A[r][pc]
+        const double aprc = shfl_d(arc, pr * 8 + c);                     // A[pr][c]
+        const double apr8 = rdlane(ar8, pr * 8);                         // A[pr][8]
+        if (r != pr) {
+            const double fct = arpc / piv;
+            arc = arc - fct * aprc;
+            ar8 = ar8 - fct * apr8;
         }
     }
     int fc = 0;
 #pragma unroll
-    for (int c = 8; c >= 0; --c) if (!((used_c >> c) & 1u)) fc = c;
+    for (int j = 8; j >= 0; --j) if (!((used_c >> j) & 1u)) fc = j;
     double f[9];
 #pragma unroll
-    for (int c = 0; c < 9; ++c) f[c] = (c == fc) ? 1.0 : 0.0;
-    // my pivot column (if my row was a pivot row)
-    int mypc = -1;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) if (s < steps && prs[s] == lane) mypc = pcs[s];
-    double afc = 0.0, apc = 1.0;
-#pragma unroll
-    for (int c = 0; c < 9; ++c) { if (c == fc) afc = a[c]; if (c == mypc) apc = a[c]; }
-    double myval = -(afc / apc);
+    for (int j = 0; j < 9; ++j) f[j] = (j == fc) ? 1.0 : 0.0;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
         if (s < steps) {
-            double v = shfl_d(myval, prs[s]);
+            const int pr = prs[s], pc = pcs[s];
+            const double afc = fc < 8 ? rdlane(arc, pr * 8 + fc) : rdlane(ar8, pr * 8);
+            const double apc = pc < 8 ? rdlane(arc, pr * 8 + pc) : rdlane(ar8, pr * 8);
+            const double v = -(afc / apc);
 #pragma unroll
-            for (int c = 0; c < 9; ++c) if (c == pcs[s]) f[c] = v;
+            for (int j = 0; j < 9; ++j) if (j == pc) f[j] = v;
         }
     }
     double nn = 0.0;
 #pragma unroll
-    for (int c = 0; c < 9; ++c) nn = nn + f[c] * f[c];
+    for (int j = 0; j < 9; ++j) nn = nn + f[j] * f[j];
     nn = sqrt(nn);
 #pragma unroll
-    for (int c = 0; c < 9; ++c) f[c] = f[c] / nn;
+    for (int j = 0; j < 9; ++j) f[j] = f[j] / nn;
+    VO_STAMP(d, slot, 3);
     denormalize(f, sc1, mx1, my1, sc2, mx2, my2, F);
     rank2(F);
+    VO_STAMP(d, slot, 4);
+}
+
+// Sampson inlier test (computeSampsonError < thr, ransac.cpp:12-23,163-166).  For thr == 1
+// the division is skipped: with den >= 1e-12, RN(num/den) < 1  <=>  num < den (exact; NaN
+// and inf cases agree), tests/test_sampson_no_div.py.
+__device__ __forceinline__ bool sampson_inlier(const double* F, double x, double y, double xp, double yp,
+                                               double thr, bool thr_is_one)
+{
+    double Fx0 = (F[0] * x + F[1] * y) + F[2] * 1.0;
+    double Fx1 = (F[3] * x + F[4] * y) + F[5] * 1.0;
+    double Ft0 = (F[0] * xp + F[3] * yp) + F[6] * 1.0;
+    double Ft1 = (F[1] * xp + F[4] * yp) + F[7] * 1.0;
+    double Ft2 = (F[2] * xp + F[5] * yp) + F[8] * 1.0;
+    double v = (Ft0 * x + Ft1 * y) + Ft2 * 1.0;
+    double num = v * v;
+    double den = ((Fx0 * Fx0 + Fx1 * Fx1) + Ft0 * Ft0) + Ft1 * Ft1;
+    if (den < 1e-12) return 1.7976931348623157e308 < thr;
+    return thr_is_one ? (num < den) : (num / den < thr);
+}
+
+// inliers of F among the first `scored` matches, counted by ballot; loads 4 steps ahead
+__device__ __forceinline__ int count_inliers(const double* __restrict__ pts, int scored, const double* F,
+                                             double thr, int lane)
+{
+    const bool one = thr == 1.0;
+    int cnt = 0;
+    for (int b = 0; b < scored; b += 256) {
+        double2 a[4], c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            int i = b + 64 * u + lane;
+            if (i < scored) {
+                const double2* p = reinterpret_cast<const double2*>(pts + 4 * (size_t)i);
+                a[u] = p[0]; c[u] = p[1];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            int i = b + 64 * u + lane;
+            bool in = i < scored && sampson_inlier(F, a[u].x, a[u].y, c[u].x, c[u].y, thr, one);
+            cnt += __popcll(ballot64(in));
+        }
+    }
+    return cnt;
 }
 
 __device__ void svd3(const double* A, double* U, double* S, double* Vt)
@@ -1042,29 +1356,22 @@ __global__ void __launch_bounds__(64) k_ransac_hyp(VoDev d, int k0, int k1, int 
     const int lane = threadIdx.x & 63;
     const int M = st->M, scored = st->scored;
     {
+        VO_STAMP(d, k, 0);
         int s8[8];
         sample8(st->frame_seed, k, M, s8);
+        VO_STAMP(d, k, 1);
         double F[9];
-        fit_F8_wave(d.pts, s8, lane, F);
+        fit_F8_wave(d, d.pts, s8, lane, F, k);
+        VO_STAMP(d, k, 5);
         if (lane < 9) {
             double v = 0.0;
 #pragma unroll
             for (int c = 0; c < 9; ++c) if (c == lane) v = F[c];
             d.hypF[(size_t)k * 9 + lane] = v;
         }
-        const double thr = d.sampson_thr;
-        int cnt = 0;
-        for (int b = 0; b < scored; b += 64) {
-            int i = b + lane;
-            bool in = false;
-            if (i < scored) {
-                const double2* p = reinterpret_cast<const double2*>(d.pts + 4 * (size_t)i);
-                double2 a = p[0], c = p[1];
-                in = sampson(F, a.x, a.y, c.x, c.y) < thr;
-            }
-            cnt += __popcll(ballot64(in));
-        }
+        const int cnt = count_inliers(d.pts, scored, F, d.sampson_thr, lane);
         if (lane == 0) st_sc1(d.counts + k, cnt);
+        VO_STAMP(d, k, 6);
     }
     unsigned* ctr = d.ctr + (k0 == 0 ? 1 : 3);
     if (!arrive_last(ctr, gridDim.x, &s_last)) return;
@@ -1254,12 +1561,13 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
 #pragma unroll
             for (int c = 0; c < 9; ++c) F[c] = d.hypF[(size_t)bestk * 9 + c];
             const double thr = d.sampson_thr;
+            const bool one = thr == 1.0;
             for (int b0 = 0; b0 < scored; b0 += 64) {
                 int i = b0 + lane;
                 bool in = false;
                 if (i < scored) {
                     const double* p = d.pts + 4 * (size_t)i;
-                    in = sampson(F, p[0], p[1], p[2], p[3]) < thr;
+                    in = sampson_inlier(F, p[0], p[1], p[2], p[3], thr, one);
                 }
                 unsigned long long bal = ballot64(in);
                 if (in) d.inl[n + __popcll(bal & ((1ull << lane) - 1ull))] = i;
@@ -1553,7 +1861,21 @@ void launch_stencil(const VoDev& d, const uint8_t* frame, int write_response, hi
     dim3 g((d.W + ST_TW - 1) / ST_TW, (d.H + ST_TH - 1) / ST_TH);
     hipLaunchKernelGGL(k_stencil, g, dim3(256), 0, s, d, frame, write_response);
 }
-void launch_select(const VoDev& d, hipStream_t s) { hipLaunchKernelGGL(k_select, dim3(1), dim3(1024), 0, s, d); }
+void launch_select(const VoDev& d, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(1024), (size_t)d.sel_lds, s, d);
+}
+int select_lds_bytes(int W, int H, int* key_cap)
+{
+    const int ntiles = ((W + ST_TW - 1) / ST_TW) * ((H + ST_TH - 1) / ST_TH);
+    const int bytes = 160 * 1024 - 512;                // static __shared__ of k_select < 512 B
+    if (hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
+        return -1;
+    const SelLayout L = sel_layout(ntiles, bytes);
+    if (L.key_cap < 1024) return -1;
+    if (key_cap) *key_cap = L.key_cap;
+    return bytes;
+}
 void launch_describe(const VoDev& d, hipStream_t s)
 {
     hipLaunchKernelGGL(k_describe, dim3((d.N + DS_KPB - 1) / DS_KPB), dim3(256), 0, s, d);

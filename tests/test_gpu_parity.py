@@ -106,6 +106,37 @@ def test_extract_bit_exact(which, ctx_kitti, scene, factory):
     assert np.array_equal(d, dr), "descriptor bits differ"
 
 
+@pytest.mark.parametrize("W,H,N,kind", [
+    (1920, 1080, 4096, "scene"),    # ~37k survivors: select stages keys in global scratch
+    (1920, 1080, 4096, "noise"),    # ~53k survivors
+    (1000, 300, 2000, "noise"),     # ragged: W, H not multiples of the 64x16 stencil tile
+    (752, 480, 2000, "sparse"),     # fewer survivors than N: no top-N threshold
+    (640, 480, 64, "scene"),        # tiny N: the boundary bin holds most of the ranking
+])
+def test_extract_sizes_bit_exact(W, H, N, kind):
+    if kind == "scene":
+        img = SceneSequence(W, H, nframes=2, step=0.05).frames()[1]
+    elif kind == "noise":
+        img = noise_frames(W, H, 1)[0]
+    else:
+        img = np.full((H, W), 100, np.uint8)
+        rng = np.random.default_rng(5)
+        for _ in range(40):
+            y, x = rng.integers(40, H - 48), rng.integers(40, W - 48)
+            img[y:y + 6, x:x + 6] = rng.integers(160, 255)
+    ctx = Context(W, H, max_kpts=N)
+    cfg = O.config(W, H, max_kpts=N)
+    k, d = ctx.extract(img)
+    kr, dr, _ = O.extract(img, cfg)
+    ctx.close()
+    if kind == "sparse":
+        assert 0 < kr.shape[0] < N
+    else:
+        assert kr.shape[0] == N
+    assert np.array_equal(k, kr), "keypoints differ"
+    assert np.array_equal(d, dr), "descriptor bits differ"
+
+
 @pytest.mark.parametrize("bits", [32, 512])
 def test_match_bit_exact(bits, scene):
     seq, frames = scene
