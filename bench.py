@@ -33,6 +33,11 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 METRIC = "VO frames/sec (extract+match+pose), 1241×376 mono, 2000 kpts/frame"
+# committed rocprofv3 FETCH_SIZE / WRITE_SIZE summary of this workload (tools/profile.sh ->
+# tools/rocprof_summary.py --fetch-x2 --json): source of roofline.traffic
+PMC_PROFILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1_select_kernels.json")
+ROCPROF_NAME = {"stencil": "k_stencil", "select": "k_select", "describe": "k_describe", "match": "k_match",
+                "ransac": "k_ransac_hyp", "refit": "k_refit", "triangulate": "k_triangulate"}
 HBM_PEAK_GBS = 8000.0
 KERNELS = ["stencil", "select", "describe", "match", "ransac", "refit", "triangulate"]
 
@@ -53,6 +58,43 @@ def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray, N: int) -> 
     if kernel == "select":
         return float(8 * 4 * n.mean() + 8 * n.mean())
     return float(W * H + 80 * n.mean() + 24 * M.mean() + 96)   # whole-path figure
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per frame of `kernel` from the committed PMC profile (None if absent)."""
+    try:
+        prof = json.load(open(PMC_PROFILE))["kernels"]
+        row = prof[ROCPROF_NAME[kernel]]
+        frames = prof["k_stencil"]["calls"]
+        return row["hbm_bytes_per_launch"] * row["calls"] / frames, os.path.relpath(PMC_PROFILE, ROOT)
+    except (OSError, KeyError, TypeError, ZeroDivisionError, ValueError):
+        return None, None
+
+
+def dist_init(world: int, local: int, backend: str = "nccl"):
+    """One process per GPU; RCCL ("nccl") carries only the barrier and the max-time
+    reduction (replicas: no data-path collective).  gloo is used by the CPU tests."""
+    if world <= 1:
+        return None
+    import torch
+    import torch.distributed as dist
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    return dist
+
+
+def aggregate(dist, dt: float, frames_per_rank: int, world: int, backend: str = "nccl", local: int = 0):
+    """Whole-job throughput: all ranks' frames / the slowest rank's time."""
+    if dist is not None:
+        import torch
+        dev = f"cuda:{local}" if backend == "nccl" else "cpu"
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    return dt, frames_per_rank * world / dt
 
 
 def cpu_baseline(frames: np.ndarray, seq, budget_s: float) -> dict:
@@ -94,12 +136,7 @@ def main():
     if world != args.gpus:
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
 
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dist = dist_init(world, local)
 
     from acs_visual_odometry_amd import Context
     from acs_visual_odometry_amd.synth import SceneSequence
@@ -136,20 +173,15 @@ def main():
     dt = t1 - t0
     dom_ms = ctx.kernel_times().get(dominant, float("nan"))
 
-    if dist is not None:
-        import torch
-        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    total_frames = args.steps * args.frames * world
-    value = total_frames / dt
+    dt, value = aggregate(dist, dt, args.steps * args.frames, world, local=local)
 
     if rank == 0:
         abytes = algorithmic_bytes(dominant, seq.W, seq.H, info, args.max_kpts)
         achieved = abytes / (dom_ms * 1e-3) / 1e9
+        traffic, tsrc = pmc_traffic(dominant)
         roof = {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None, "avg_launch_ms": dom_ms,
-                "algorithmic_bytes_per_launch": abytes}
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
+                "avg_launch_ms": dom_ms, "algorithmic_bytes_per_launch": abytes}
         path_bytes = algorithmic_bytes("path", seq.W, seq.H, info, args.max_kpts)
         cpu = None
         if not args.no_cpu and world == 1:

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Kernel-duration profile plus separate FETCH_SIZE / WRITE_SIZE PMC passes of bench.py
+# (MI355X_MICROARCH.md "rocprofv3 PMC slots": the two counters cannot share a pass; no
+# trace domains are combined with --pmc).  Run on the GPU box:
+#   tools/profile.sh gpurun_out/prof_<tag> [extra bench.py args]
+# then summarise with tools/rocprof_summary.py <dir> "<title>" --fetch-x2 --json <file>.
+set -eo pipefail
+OUT=$(realpath -m "$1"); shift
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd "$ROOT"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o stats -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu "$@" > "$OUT/bench_stats.json"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT" -o fetch -- \
+    python3 bench.py --steps 1 --warmup 1 --no-cpu "$@" > "$OUT/bench_fetch.json"
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT" -o write -- \
+    python3 bench.py --steps 1 --warmup 1 --no-cpu "$@" > "$OUT/bench_write.json"
+echo "profile written to $OUT"

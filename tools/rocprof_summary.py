@@ -2,12 +2,13 @@
 """Summarise a rocprofv3 output dir (kernel-trace stats + separate FETCH_SIZE / WRITE_SIZE
 PMC passes) into the markdown table committed under profiles/.
 
-usage: rocprof_summary.py <dir> <title> [--fetch-x2]
+usage: rocprof_summary.py <dir> <title> [--fetch-x2] [--json out.json]
 HBM bytes per launch = FETCH_SIZE*1024 (*2 with --fetch-x2: gfx950 reports half of wide
 coalesced streaming reads, MI355X_MICROARCH.md 'HBM') + WRITE_SIZE*1024.
 """
 import csv
 import glob
+import json
 import os
 import re
 import sys
@@ -34,6 +35,7 @@ def main():
     stats = list(csv.DictReader(open(glob.glob(os.path.join(d, "*kernel_stats.csv"))[0])))
     fetch = pmc(d, "fetch", "FETCH_SIZE")
     write = pmc(d, "write", "WRITE_SIZE")
+    table = {}
     print(f"# {title}\n")
     print("rocprofv3 --kernel-trace --stats (durations) and separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes.\n")
     print("| kernel | calls | avg us | share % | FETCH_SIZE KB/launch | WRITE_SIZE KB/launch | HBM bytes/launch |")
@@ -42,8 +44,15 @@ def main():
         k = short(r["Name"])
         f, w = fetch.get(k), write.get(k)
         hb = "" if f is None or w is None else f"{(f * (2 if x2 else 1) + w) * 1024:,.0f}"
+        table[k] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
+                    "fetch_kb": f, "write_kb": w,
+                    "hbm_bytes_per_launch": None if f is None or w is None else (f * (2 if x2 else 1) + w) * 1024}
         print(f"| {k} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} | "
               f"{'' if f is None else f'{f:.1f}'} | {'' if w is None else f'{w:.1f}'} | {hb} |")
+
+    if "--json" in sys.argv:
+        out = sys.argv[sys.argv.index("--json") + 1]
+        json.dump({"title": title, "fetch_x2": x2, "kernels": table}, open(out, "w"), indent=1)
 
 
 if __name__ == "__main__":
