@@ -43,21 +43,27 @@ KERNELS = ["stencil", "select", "describe", "match", "ransac", "refit", "triangu
 
 
 def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray, N: int) -> float:
-    """Algorithmic HBM bytes per launch of `kernel`, averaged over the frames in `info`
-    (n_kps, n_matches, n_inliers, ...).  DESIGN.md section 4 derives each figure."""
-    n = info[:, 0].astype(np.float64)
-    M = info[:, 1].astype(np.float64)
+    """Algorithmic HBM bytes per frame of `kernel` (one launch, two for ransac), averaged
+    over the frames in `info` (n_kps, n_matches, n_inliers, ...).  DESIGN.md section 4
+    derives each figure; n = keypoints, M = matches, I = inliers."""
+    n = float(info[:, 0].mean())
+    M = float(info[:, 1].mean())
+    I = float(info[:, 2].mean())
     if kernel == "stencil":
-        return float(2 * W * H + 12 * 4 * n.mean())            # frame in, blurred out, ~candidates
-    if kernel == "describe":
-        return float((86 + 8 + 68) * n.mean())                  # 86 sample px + kp in, 64+4 B out
-    if kernel == "match":
-        return float(4 * n.mean() + 4 * n.mean() + 4 * n.mean())  # prefixes prev + cur, result
-    if kernel.startswith("ransac"):
-        return float(32 * M.mean() + 36 * 4)                    # matches read once (+F out), L2 re-reads excluded
+        return 2.0 * W * H + 4 * 8 * n                # frame in + blurred out + ~4n candidate keys
     if kernel == "select":
-        return float(8 * 4 * n.mean() + 8 * n.mean())
-    return float(W * H + 80 * n.mean() + 24 * M.mean() + 96)   # whole-path figure (SURVEY 8(d))
+        return 4 * 8 * n + 8 * n                      # ~4n candidate keys in, n keypoints out
+    if kernel == "describe":
+        return (86 + 8 + 64 + 4) * n                  # 86 sampled px + kp in; descriptor + prefix out
+    if kernel == "match":
+        return 3 * 4 * n + 8 * M                      # two 32-bit prefix sets + best index; pairs out
+    if kernel == "ransac":
+        return 32 * M + 36 * 4                        # match coords once (L2 re-reads excluded)
+    if kernel == "refit":
+        return 32 * M + 4 * I + 72 + 16 * I           # coords + inlier ids; F + f32 inlier points out
+    if kernel == "triangulate":
+        return 16 * I + 96 + 96                       # f32 inlier points in; pose record out
+    return float(W * H + 80 * n + 24 * M + 96)       # whole path (SURVEY 8(d))
 
 
 def pmc_traffic(kernel: str):

@@ -111,11 +111,15 @@ def test_ref_stock_build_differences(images):
         flips = int(((R > 0) != (Rr > 0)).sum())      # R within rounding of the 20000 threshold
         rel = np.abs(R[both].astype(np.float64) - Rr[both]) / Rr[both]
         kps, desc, _ = O.extract(img, O.config(W, H))
+        ks = O.nms_topn(R)                              # top-N on the stock response
+        common = len(set(map(tuple, ks)) & set(map(tuple, kps)))
         _, rot_or = O.describe(bl, kps, with_rot=True)
         _, _, _, dcl = stock.orient_describe(bl, kps, rot_in=rot_or)
         bits = float(np.mean(dcl != unpack_descriptor(desc)))
         print(f"stock {W}x{H}: response differs at {int((R != Rr).sum())} px (max rel {rel.max():.2e}, "
-              f"{flips} threshold flips of {int(both.sum())}); descriptor bits differ {bits:.2e}")
-        assert rel.max() < 1e-4
+              f"{flips} threshold flips of {int(both.sum())}); keypoints shared {common}/{len(kps)}; "
+              f"descriptor bits differ {bits:.2e}")
+        assert rel.max() < 1e-3          # tr^2 - 4det cancels: contraction moves small R most
         assert flips <= 1e-3 * both.sum()
+        assert common >= 0.99 * len(kps)
         assert bits < 1e-2
