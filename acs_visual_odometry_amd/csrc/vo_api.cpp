@@ -1,10 +1,16 @@
 // vo_api.cpp -- host side of libvo_mi355x.so: the C ABI of include/vo_mi355x.h.
 //
-// One vo_ctx = one GPU + one HIP stream + every device buffer of the path allocated
+// One vo_ctx = one GPU + two HIP streams + every device buffer of the path allocated
 // once (HBM layout: vo_internal.h).  Per frame the host only enqueues kernels; all
 // per-frame decisions of the reference's trajectory loop (skip on < 8 matches /
 // inliers, descriptor carry-forward, RANSAC model leak, GT scale) are taken on the
 // device from VoState, so frames can be enqueued back to back with no host sync.
+//
+// Frame pipeline: extract(f) (stencil, select, describe) runs on stream `se` and waits
+// only for frame f-2's pose chain; the pose chain of frame f (match, RANSAC, refit,
+// triangulate + finalize) runs on stream `s` after extract(f).  So extract(f+1)
+// overlaps pose(f).  Three keypoint/descriptor slots make that safe: select(f) picks a
+// slot that is neither frame f-1's nor its prev (VoExt, k_select).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -25,7 +31,10 @@
 struct vo_ctx {
     vo_config cfg;
     VoDev d;
-    hipStream_t s = nullptr;
+    hipStream_t s = nullptr;          // pose chain (and stage APIs)
+    hipStream_t se = nullptr;         // extract stream of the frame pipeline
+    hipEvent_t ev_ext[2] = {nullptr, nullptr}, ev_pose[2] = {nullptr, nullptr};
+    int fidx = 0;                     // frames enqueued since vo_reset
     int max_hyp = VO_MAX_HYP;
     int gt_cap = 0;
     VoFrameOut* out_dev = nullptr;
@@ -98,6 +107,7 @@ int dalloc(T** p, size_t n)
 
 int read_state(vo_ctx* c, VoState* h)
 {
+    HIPCHK(hipStreamSynchronize(c->se));
     HIPCHK(hipMemcpyAsync(h, c->d.st, sizeof(VoState), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
     return VO_OK;
@@ -109,26 +119,36 @@ int write_state(vo_ctx* c, const VoState* h)
     return VO_OK;
 }
 
-// host frame (any stride) -> frame_in, via the pinned staging buffer
-int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride)
+int read_ext(vo_ctx* c, VoExt* h)
+{
+    HIPCHK(hipStreamSynchronize(c->se));
+    HIPCHK(hipMemcpyAsync(h, c->d.ext, sizeof(VoExt), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    return VO_OK;
+}
+
+// host frame (any stride) -> frame_in on stream `st`, via the pinned staging buffer
+int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride, hipStream_t st)
 {
     const int W = c->cfg.width, H = c->cfg.height;
     if (stride == 0) stride = (size_t)W;
-    HIPCHK(hipStreamSynchronize(c->s));   // staging buffer may still be in flight
+    HIPCHK(hipStreamSynchronize(c->s));   // staging buffer / frame_in may still be in use
+    HIPCHK(hipStreamSynchronize(c->se));
     if (stride == (size_t)W) {
         std::memcpy(c->stage_host, gray, (size_t)W * H);
     } else {
         for (int y = 0; y < H; ++y) std::memcpy(c->stage_host + (size_t)y * W, gray + (size_t)y * stride, W);
     }
-    HIPCHK(hipMemcpyAsync(c->d.frame_in, c->stage_host, (size_t)W * H, hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipMemcpyAsync(c->d.frame_in, c->stage_host, (size_t)W * H, hipMemcpyHostToDevice, st));
     return VO_OK;
 }
 
+// stage extract (vo_extract): slot VO_STAGE_SLOT, on the pose stream
 void enqueue_extract(vo_ctx* c, const uint8_t* dframe, int write_response)
 {
     vo::launch_stencil(c->d, dframe, write_response, c->s);
-    vo::launch_select(c->d, c->s);
-    vo::launch_describe(c->d, c->s);
+    vo::launch_select(c->d, -1, c->s);
+    vo::launch_describe(c->d, -1, c->s);
 }
 
 // stage calls borrow the ctx; they restore the trajectory state (and the zeroed
@@ -141,41 +161,64 @@ int restore_state(vo_ctx* c, const VoState* saved)
 }
 
 // the full trajectory-loop iteration for one frame (VisualOdometry.cpp:68-189).
-// Timing: ev_all records an event after every kernel (15 per frame); ev_one (kernel
-// index k >= 0) records only the two events bracketing kernel k.
+// Timing: every timed kernel is bracketed by two events on the stream it runs on (all
+// kernels, or only kernel `only`); vo_last_kernel_times averages end - start.
 struct EvRec {
     std::vector<hipEvent_t>* pool;
     size_t used;
     int only;   // -1: all kernels
+    std::vector<std::pair<int, size_t>> spans;   // (kernel, index of its start event)
 };
+
+size_t ev_mark(EvRec* ev, hipStream_t st)
+{
+    if (ev->used >= ev->pool->size()) {
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        ev->pool->push_back(e);
+    }
+    (void)hipEventRecord((*ev->pool)[ev->used], st);
+    return ev->used++;
+}
+
+template <typename F>
+void timed(EvRec* ev, int k, hipStream_t st, F&& launch)
+{
+    const bool on = ev && (ev->only < 0 || ev->only == k);
+    size_t b = on ? ev_mark(ev, st) : 0;
+    launch();
+    if (on) {
+        ev_mark(ev, st);
+        ev->spans.emplace_back(k, b);
+    }
+}
 
 void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev)
 {
-    auto mark = [&](int k) {
-        if (!ev) return;   // marks 0..7 bracket the 7 kernels of a frame
-        if (ev->only >= 0 && k != ev->only && k != ev->only + 1) return;
-        if (ev->used >= ev->pool->size()) {
-            hipEvent_t e;
-            (void)hipEventCreate(&e);
-            ev->pool->push_back(e);
-        }
-        (void)hipEventRecord((*ev->pool)[ev->used++], c->s);
-    };
+    const int f = c->fidx++;
     VoDev d = c->d;
     d.out = out;
-    mark(0);
+    // extract stream: frame f-2's pose chain must be done (its slots may be reused, and
+    // finalize(f-2) wrote the prev slot select(f) avoids)
+    if (f >= 2) (void)hipStreamWaitEvent(c->se, c->ev_pose[f & 1], 0);
     if (dframe) {
-        vo::launch_stencil(d, dframe, 0, c->s); mark(1);
-        vo::launch_select(d, c->s); mark(2);
-        vo::launch_describe(d, c->s); mark(3);
-        vo::launch_match(d, c->s); mark(4);
-        vo::launch_ransac(d, c->max_hyp, c->s); mark(5);
-        vo::launch_refit(d, 1, c->s); mark(6);
-        vo::launch_triangulate(d, c->s); mark(7);
+        timed(ev, 0, c->se, [&] { vo::launch_stencil(d, dframe, 0, c->se); });
+        timed(ev, 1, c->se, [&] { vo::launch_select(d, f, c->se); });
+        timed(ev, 2, c->se, [&] { vo::launch_describe(d, f, c->se); });
+    } else {
+        vo::launch_ext_missing(d, f, c->se);
+    }
+    (void)hipEventRecord(c->ev_ext[f & 1], c->se);
+    (void)hipStreamWaitEvent(c->s, c->ev_ext[f & 1], 0);
+    if (dframe) {
+        timed(ev, 3, c->s, [&] { vo::launch_match(d, c->s); });
+        timed(ev, 4, c->s, [&] { vo::launch_ransac(d, c->max_hyp, c->s); });
+        timed(ev, 5, c->s, [&] { vo::launch_refit(d, 1, c->s); });
+        timed(ev, 6, c->s, [&] { vo::launch_triangulate(d, c->s); });
     } else {
         vo::launch_missing(d, c->s);
-        for (int k = 1; k <= 7; ++k) mark(k);
     }
+    (void)hipEventRecord(c->ev_pose[f & 1], c->s);
 }
 
 int ensure_out(vo_ctx* c, int n)
@@ -282,6 +325,11 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     int rc = VO_OK;
     auto bail = [&](int r) { vo_destroy(c); return r; };
     if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(hipStreamCreateWithFlags(&c->se, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
+    for (int i = 0; i < 2; ++i) {
+        if (hip_ok(hipEventCreateWithFlags(&c->ev_ext[i], hipEventDisableTiming)) != VO_OK) return bail(VO_ERR_HIP);
+        if (hip_ok(hipEventCreateWithFlags(&c->ev_pose[i], hipEventDisableTiming)) != VO_OK) return bail(VO_ERR_HIP);
+    }
     d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
     if (d.sel_lds < 0) return bail(VO_ERR_HIP);
     rc |= dalloc(&d.frame_in, (size_t)W * H);
@@ -292,7 +340,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc(&d.ckeys, d.cand_cap);
     rc |= dalloc(&d.selbits, d.cand_cap / 64 + 1);
     rc |= dalloc(&d.hist, VO_HIST_BINS);
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < VO_SLOTS; ++s) {
         rc |= dalloc(&d.kps[s], N);
         rc |= dalloc(&d.desc[s], (size_t)N * 8);
         rc |= dalloc(&d.pre[s], N);
@@ -305,6 +353,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc(&d.inl, N);
     rc |= dalloc(&d.model_p, (size_t)N * 4);
     rc |= dalloc(&d.st, 1);
+    rc |= dalloc(&d.ext, 1);
     rc |= dalloc(&d.ctr, 4);
 #ifdef VO_STAMPS
     rc |= dalloc(&d.dbg, (size_t)c->max_hyp * 16);
@@ -317,7 +366,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     d.maxit_tab = c->tab_dev;
     if (hip_ok(hipHostMalloc((void**)&c->stage_host, (size_t)W * H, hipHostMallocDefault)) != VO_OK) return bail(VO_ERR_HIP);
     // zero the descriptor / keypoint slots (deterministic contents before first use)
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < VO_SLOTS; ++s) {
         (void)hipMemset(d.kps[s], 0, sizeof(int2) * N);
         (void)hipMemset(d.desc[s], 0, sizeof(uint64_t) * 8 * N);
         (void)hipMemset(d.pre[s], 0, sizeof(uint32_t) * N);
@@ -334,16 +383,27 @@ void vo_destroy(vo_ctx* c)
 {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
+    if (c->se) (void)hipStreamSynchronize(c->se);
     if (c->s) (void)hipStreamSynchronize(c->s);
     VoDev& d = c->d;
-    void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.tilerows, d.ckeys, d.selbits, d.hist, d.kps[0], d.kps[1], d.desc[0], d.desc[1],
-                    d.pre[0], d.pre[1], d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.model_p,
+    for (int s = 0; s < VO_SLOTS; ++s) {
+        void* sp[] = {d.kps[s], d.desc[s], d.pre[s]};
+        for (void* p : sp)
+            if (p) (void)hipFree(p);
+    }
+    void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.tilerows, d.ckeys, d.selbits, d.hist, d.ext,
+                    d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.model_p,
                     d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr, d.dbg};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->out_host) (void)hipHostFree(c->out_host);
     if (c->stage_host) (void)hipHostFree(c->stage_host);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    for (int i = 0; i < 2; ++i) {
+        if (c->ev_ext[i]) (void)hipEventDestroy(c->ev_ext[i]);
+        if (c->ev_pose[i]) (void)hipEventDestroy(c->ev_pose[i]);
+    }
+    if (c->se) (void)hipStreamDestroy(c->se);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
 }
@@ -352,10 +412,17 @@ int vo_reset(vo_ctx* c)
 {
     if (!c) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipStreamSynchronize(c->se));
     VoState h;
     init_state(c, &h);
     int rc = write_state(c, &h);
     if (rc) return rc;
+    VoExt e;
+    std::memset(&e, 0, sizeof(e));
+    for (int i = 0; i < 4; ++i) { e.slot[i] = -1; e.prev_for[i] = -1; e.status[i] = VO_STATUS_OK; }
+    HIPCHK(hipMemcpyAsync(c->d.ext, &e, sizeof(e), hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipMemsetAsync(c->d.hist, 0, sizeof(uint32_t) * VO_HIST_BINS, c->s));
+    c->fidx = 0;
     HIPCHK(hipMemsetAsync(c->d.ctr, 0, sizeof(unsigned) * 4, c->s));
     vo::launch_frame_begin(c->d, VO_MODE_FRAME, c->s);     // frame 0 set up on the device
     HIPCHK(hipGetLastError());
@@ -384,26 +451,21 @@ int vo_extract(vo_ctx* c, const uint8_t* gray, size_t stride, vo_kp* kps, uint64
 {
     if (!c || !gray || !n) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    VoState saved, h;
-    int rc = read_state(c, &saved);
+    int rc = upload_frame(c, gray, stride, c->s);
     if (rc) return rc;
-    rc = upload_frame(c, gray, stride);
-    if (rc) return rc;
-    vo::launch_frame_begin(c->d, VO_MODE_EXTRACT, c->s);
-    enqueue_extract(c, c->d.frame_in, 0);
+    enqueue_extract(c, c->d.frame_in, 0);      // slot VO_STAGE_SLOT: the trajectory's slots are untouched
     HIPCHK(hipGetLastError());
-    rc = read_state(c, &h);
+    VoExt e;
+    rc = read_ext(c, &e);
     if (rc) return rc;
-    rc = restore_state(c, &saved);
-    if (rc) return rc;
-    if (h.status != VO_STATUS_OK) return VO_ERR_CAPACITY;
-    const int nk = h.n_kps[0];
+    if (e.stage_status != VO_STATUS_OK) return VO_ERR_CAPACITY;
+    const int nk = e.n_kps[VO_STAGE_SLOT];
     *n = nk;
-    if (kps && nk) HIPCHK(hipMemcpy(kps, c->d.kps[0], sizeof(vo_kp) * nk, hipMemcpyDeviceToHost));
-    if (desc && nk) HIPCHK(hipMemcpy(desc, c->d.desc[0], sizeof(uint64_t) * 8 * nk, hipMemcpyDeviceToHost));
+    if (kps && nk) HIPCHK(hipMemcpy(kps, c->d.kps[VO_STAGE_SLOT], sizeof(vo_kp) * nk, hipMemcpyDeviceToHost));
+    if (desc && nk)
+        HIPCHK(hipMemcpy(desc, c->d.desc[VO_STAGE_SLOT], sizeof(uint64_t) * 8 * nk, hipMemcpyDeviceToHost));
     if (blurred)
         HIPCHK(hipMemcpy(blurred, c->d.blurred, (size_t)c->cfg.width * c->cfg.height, hipMemcpyDeviceToHost));
-    // vo_extract leaves the trajectory state untouched except slot 0 contents
     return VO_OK;
 }
 
@@ -411,19 +473,17 @@ int vo_response(vo_ctx* c, const uint8_t* gray, size_t stride, float* R)
 {
     if (!c || !gray || !R) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    VoState saved;
-    int rc = read_state(c, &saved);
-    if (rc) return rc;
-    rc = upload_frame(c, gray, stride);
+    int rc = upload_frame(c, gray, stride, c->s);
     if (rc) return rc;
     const size_t np = (size_t)c->cfg.width * c->cfg.height;
     HIPCHK(hipMemsetAsync(c->d.response, 0, np * sizeof(float), c->s));
-    vo::launch_frame_begin(c->d, VO_MODE_EXTRACT, c->s);
     vo::launch_stencil(c->d, c->d.frame_in, 1, c->s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(R, c->d.response, np * sizeof(float), hipMemcpyDeviceToHost, c->s));
+    // the stencil histogram is consumed by select; nothing selects here, so clear it
+    HIPCHK(hipMemsetAsync(c->d.hist, 0, sizeof(uint32_t) * VO_HIST_BINS, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
-    return restore_state(c, &saved);
+    return VO_OK;
 }
 
 int vo_match(vo_ctx* c, const uint64_t* d_prev, int n_prev, const uint64_t* d_cur, int n_cur, vo_match_t* out, int* m)
@@ -435,16 +495,20 @@ int vo_match(vo_ctx* c, const uint64_t* d_prev, int n_prev, const uint64_t* d_cu
     std::vector<uint32_t> p0(n_prev), p1(n_cur);
     for (int i = 0; i < n_prev; ++i) p0[i] = (uint32_t)d_prev[8 * (size_t)i];
     for (int i = 0; i < n_cur; ++i) p1[i] = (uint32_t)d_cur[8 * (size_t)i];
+    HIPCHK(hipStreamSynchronize(c->se));
     HIPCHK(hipStreamSynchronize(c->s));
-    HIPCHK(hipMemcpy(c->d.desc[0], d_prev, sizeof(uint64_t) * 8 * n_prev, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d.desc[1], d_cur, sizeof(uint64_t) * 8 * n_cur, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d.pre[0], p0.data(), sizeof(uint32_t) * n_prev, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d.pre[1], p1.data(), sizeof(uint32_t) * n_cur, hipMemcpyHostToDevice));
+    const int a = VO_STAGE_SLOT, b = VO_STAGE_SLOT + 1;     // stage slots: the trajectory's stay intact
+    HIPCHK(hipMemcpy(c->d.desc[a], d_prev, sizeof(uint64_t) * 8 * n_prev, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d.desc[b], d_cur, sizeof(uint64_t) * 8 * n_cur, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d.pre[a], p0.data(), sizeof(uint32_t) * n_prev, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d.pre[b], p1.data(), sizeof(uint32_t) * n_cur, hipMemcpyHostToDevice));
+    const int nk2[2] = {n_prev, n_cur};
+    HIPCHK(hipMemcpy(c->d.ext->n_kps + a, nk2, sizeof(nk2), hipMemcpyHostToDevice));
     VoState h;
     int rc = read_state(c, &h);
     if (rc) return rc;
     VoState saved = h;
-    h.prev = 0; h.cur = 1; h.n_kps[0] = n_prev; h.n_kps[1] = n_cur;
+    h.prev = a; h.cur = b;
     h.status = VO_STATUS_OK; h.mode = VO_MODE_STAGE;
     rc = write_state(c, &h);
     if (rc) return rc;
@@ -455,7 +519,6 @@ int vo_match(vo_ctx* c, const uint64_t* d_prev, int n_prev, const uint64_t* d_cu
     *m = h.M;
     if (out && h.M) HIPCHK(hipMemcpy(out, c->d.match_pairs, sizeof(vo_match_t) * h.M, hipMemcpyDeviceToHost));
     // restore the trajectory bookkeeping (stage calls do not advance the loop)
-    saved.n_kps[0] = h.n_kps[0]; saved.n_kps[1] = h.n_kps[1];
     return restore_state(c, &saved);
 }
 
@@ -539,7 +602,7 @@ int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_
     if (!c) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
     if (gray) {
-        int rc = upload_frame(c, gray, stride);
+        int rc = upload_frame(c, gray, stride, c->se);
         if (rc) return rc;
     }
     enqueue_frame(c, gray ? c->d.frame_in : nullptr, c->out_dev, nullptr);
@@ -564,7 +627,7 @@ int vo_process_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
     HIPCHK(hipSetDevice(c->cfg.device));
     int rc = ensure_out(c, std::max(nframes, 1));
     if (rc) return rc;
-    EvRec rec{&c->ev_pool, 0, c->timing >= 100 ? c->timing - 100 : -1};
+    EvRec rec{&c->ev_pool, 0, c->timing >= 100 ? c->timing - 100 : -1, {}};
     EvRec* evp = c->timing ? &rec : nullptr;
     for (int f = 0; f < nframes; ++f) enqueue_frame(c, d_frames + (size_t)f * frame_bytes, c->out_dev + f, evp);
     HIPCHK(hipGetLastError());
@@ -575,15 +638,11 @@ int vo_process_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
         const int nk = vo::kernel_count();
         c->ktime_ms.assign(nk, 0.f);
         c->kcount.assign(nk, 0);
-        const int per = rec.only >= 0 ? 2 : nk + 1;
-        for (int f = 0; f < nframes; ++f) {
-            for (int k = 0; k + 1 < per; ++k) {
-                float ms = 0.f;
-                (void)hipEventElapsedTime(&ms, c->ev_pool[(size_t)f * per + k], c->ev_pool[(size_t)f * per + k + 1]);
-                int kk = rec.only >= 0 ? rec.only : k;
-                c->ktime_ms[kk] += ms;
-                c->kcount[kk] += 1;
-            }
+        for (const auto& sp : rec.spans) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, c->ev_pool[sp.second], c->ev_pool[sp.second + 1]);
+            c->ktime_ms[sp.first] += ms;
+            c->kcount[sp.first] += 1;
         }
     }
     for (int f = 0; f < nframes; ++f) {

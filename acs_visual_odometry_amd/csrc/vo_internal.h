@@ -28,6 +28,9 @@
 #include <stdint.h>
 
 #define VO_HIST_BINS 4096
+#define VO_PIPE_SLOTS 3        // keypoint/descriptor slots of the frame pipeline
+#define VO_STAGE_SLOT 3        // stage APIs (vo_extract / vo_match) use slots 3 and 4
+#define VO_SLOTS 5
 #define VO_MAX_HYP 2000
 #define VO_HYP_CHUNK0 256
 #define VO_RED_THREADS 256
@@ -43,12 +46,24 @@ struct VoFrameOut {
     double pose[12];
 };
 
+// Extract-side state.  The extract kernels of frame f+1 run on their own stream while frame
+// f's match -> pose chain runs; they never touch VoState, and the pose chain only reads
+// the ring entries of its own frame here, so the two streams never write the same field.
+struct VoExt {
+    int32_t slot[4];       // slot extracted for frame f (ring f & 3), chosen by k_select
+    int32_t status[4];     // VO_STATUS_OK, or VO_STATUS_OVERFLOW (select capacity) for frame f
+    int32_t prev_for[4];   // prev slot of frame f, written by finalize(f-1); -1: none
+    int32_t n_kps[VO_SLOTS];
+    int32_t stage_status;  // status of the last stage extract (vo_extract)
+    int32_t pad[2];
+};
+
 struct VoState {
     int32_t frame;        // index of the frame being processed
     int32_t status;       // VO_STATUS_* of the current frame
     int32_t mode;
-    int32_t cur, prev;    // descriptor / keypoint slots
-    int32_t n_kps[2];
+    int32_t cur, prev;    // keypoint/descriptor slots: prev always; cur only in stage mode
+                          // (frame mode: VoExt::slot[frame & 3])
     uint32_t cand_count;
     int32_t M;            // matches
     int32_t scored;       // T * floor(M / T)   (ransac.cpp:152-157)
@@ -92,9 +107,9 @@ struct VoDev {
     uint64_t* selbits;    // select: selected-key bitmap when it exceeds the LDS capacity
     int sel_lds;          // select: dynamic LDS bytes
     uint32_t* hist;
-    int2* kps[2];
-    uint64_t* desc[2];
-    uint32_t* pre[2];
+    int2* kps[VO_SLOTS];
+    uint64_t* desc[VO_SLOTS];
+    uint32_t* pre[VO_SLOTS];
     int32_t* match_j;
     int2* match_pairs;
     double* pts;
@@ -105,6 +120,7 @@ struct VoDev {
     const uint16_t* maxit_tab;
     const double* gt;
     VoState* st;
+    VoExt* ext;
     VoFrameOut* out;
     unsigned* ctr;        // in-launch arrival counters: [0] match, [1] ransac, [2] triangulate
     unsigned long long* dbg;   // diagnostic s_memtime stamps (VO_STAMPS builds only)
@@ -115,9 +131,12 @@ struct VoDev {
 namespace vo {
 void launch_frame_begin(const VoDev& d, int mode, hipStream_t s);
 void launch_stencil(const VoDev& d, const uint8_t* frame, int write_response, hipStream_t s);
-void launch_select(const VoDev& d, hipStream_t s);
+// fidx: frame index since vo_reset (frame pipeline; select picks the slot), or -1 for the
+// stage API (slot VO_STAGE_SLOT)
+void launch_select(const VoDev& d, int fidx, hipStream_t s);
 int select_lds_bytes(int W, int H, int* key_cap);     // sets the kernel attribute; <0 on failure
-void launch_describe(const VoDev& d, hipStream_t s);
+void launch_describe(const VoDev& d, int fidx, hipStream_t s);
+void launch_ext_missing(const VoDev& d, int fidx, hipStream_t s);   // extract side of a missing image
 void launch_match(const VoDev& d, hipStream_t s);          // + ordered compaction (last workgroup)
 void launch_ransac(const VoDev& d, int nhyp, hipStream_t s); // all hypotheses + replay (last workgroup)
 void launch_refit(const VoDev& d, int with_pose, hipStream_t s);

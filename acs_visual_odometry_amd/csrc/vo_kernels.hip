@@ -354,13 +354,9 @@ __global__ void __launch_bounds__(1024) k_frame_begin(VoDev d, int mode)
         for (int c = 0; c < 4; ++c) st->counts4[c] = 0;
         if (mode == VO_MODE_FRAME) {
             st->status = st->frame == 0 ? VO_STATUS_FIRST : VO_STATUS_OK;
-            st->cur = st->frame == 0 ? 0 : 1 - st->prev;
             st->frame_seed = mix64(d.seed + 0x632BE59BD9B4E019ULL * (uint64_t)(st->frame + 1));
         } else if (mode == VO_MODE_MISSING) {
             st->status = VO_STATUS_MISSING;
-        } else if (mode == VO_MODE_EXTRACT) {
-            st->status = VO_STATUS_OK;
-            st->cur = 0;
         } else {
             st->status = VO_STATUS_OK;
         }
@@ -392,7 +388,6 @@ __device__ __forceinline__ int refl101(int i, int n)
 
 __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restrict__ img, int write_response)
 {
-    if (d.st->status != VO_STATUS_OK && d.st->status != VO_STATUS_FIRST) return;
     __shared__ uint8_t s_src[ST_SH][ST_SW];
     __shared__ uint32_t s_hb[ST_SH][ST_BW];
     __shared__ float s_bl[ST_BH][ST_BW];
@@ -588,15 +583,25 @@ __device__ __forceinline__ uint32_t sel_bin(uint64_t key, uint32_t thr_bits)
 //   D  selected-key bitmap (ballots) + per-(row, tile) selected counts (u8, LDS atomics)
 //   E  chunked block scan over the (row, tile) segments in raster order
 //   F  each selected key computes its raster position directly and writes its keypoint
-__global__ void __launch_bounds__(1024) k_select(VoDev d)
+__device__ __forceinline__ int ext_slot(const VoDev& d, int fidx)
 {
-    VoState* st = d.st;
-    if (st->status != VO_STATUS_OK && st->status != VO_STATUS_FIRST) return;
+    return fidx < 0 ? VO_STAGE_SLOT : d.ext->slot[fidx & 3];
+}
+
+// the pose chain's current slot: frame mode reads the extract ring, stage mode st->cur
+__device__ __forceinline__ int cur_slot(const VoDev& d, const VoState* st)
+{
+    return st->mode == VO_MODE_FRAME ? d.ext->slot[st->frame & 3] : st->cur;
+}
+
+__global__ void __launch_bounds__(1024) k_select(VoDev d, int fidx)
+{
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ uint32_t s_hs[16];
     __shared__ int s_wsum[16];
     __shared__ int s_nbnd, s_b, s_above;
     __shared__ uint64_t s_tb;
+    __shared__ int s_slot;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int N = d.N;
     const int ntx = (d.W + ST_TW - 1) / ST_TW, nty = (d.H + ST_TH - 1) / ST_TH, ntiles = ntx * nty;
@@ -611,7 +616,19 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d)
     int* s_chunk = reinterpret_cast<int*>(smem + L.chunk);
     uint64_t* s_keys = reinterpret_cast<uint64_t*>(smem + L.keys);
     const size_t TCAP = ST_TW * ST_TH / 4;
-    if (tid == 0) { s_nbnd = 0; s_b = -1; s_above = 0; }
+    if (tid == 0) {
+        s_nbnd = 0; s_b = -1; s_above = 0;
+        // slot for this frame: neither frame f-1's slot nor its prev, the two slots frame
+        // f-1's pose chain (running concurrently) may read; frame f-2's chain is complete
+        int slot = VO_STAGE_SLOT;
+        if (fidx == 0) {
+            slot = 0;
+        } else if (fidx > 0) {
+            const int a = d.ext->slot[(fidx - 1) & 3], bb = d.ext->prev_for[(fidx - 1) & 3];
+            slot = (a != 0 && bb != 0) ? 0 : (a != 1 && bb != 1) ? 1 : 2;
+        }
+        s_slot = slot;
+    }
     VO_STAMP(d, 1990, 0);
     // A
     const int tpt = (ntiles + 1023) / 1024;            // tiles per thread (<= 2)
@@ -682,6 +699,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d)
     // C
     int b = -1;
     uint64_t Tb = 0ull;
+    bool ovf = false;
     if (C > N) {
         uint32_t h[4], hs = 0;
 #pragma unroll
@@ -720,13 +738,12 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d)
         VO_STAMP(d, 1990, 3);
         const int nb = s_nbnd;
         if (nb > BND_CAP) {            // boundary bin too large for LDS (never observed)
-            if (tid == 0) st->status = VO_STATUS_OVERFLOW;
-            return;
+            ovf = true;
         }
         // the need-th largest boundary key: the one with exactly need-1 larger keys
         const int need = N - s_above;
         Tb = ~0ull;
-        if (need > 0) {
+        if (need > 0 && !ovf) {
             for (int e = tid; e < nb; e += 1024) {
                 const uint64_t ke = s_bnd[e];
                 int rank = 0;
@@ -748,7 +765,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d)
         return bin > b || (bin == b && key >= Tb);
     };
     // D
-    const int nround = (C + 1023) / 1024;
+    const int nround = ovf ? 0 : (C + 1023) / 1024;
     for (int r0 = 0; r0 < nround; r0 += 4) {
         uint64_t v[4];
 #pragma unroll
@@ -806,7 +823,8 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d)
     __syncthreads();
     VO_STAMP(d, 1990, 5);
     // F
-    int2* out = d.kps[st->cur];
+    const int slot = s_slot;
+    int2* out = d.kps[slot];
     for (int r0 = 0; r0 < nround; r0 += 4) {
         uint64_t v[4];
 #pragma unroll
@@ -843,7 +861,24 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d)
         }
     }
     VO_STAMP(d, 1990, 6);
-    if (tid == 0) st->n_kps[st->cur] = C < N ? C : N;
+    // select is the histogram's only reader: leave it zeroed for the next frame's stencil
+    for (int i = tid; i < VO_HIST_BINS; i += 1024) d.hist[i] = 0u;
+    if (tid == 0) {
+        const int status = ovf ? VO_STATUS_OVERFLOW : VO_STATUS_OK;
+        d.ext->n_kps[slot] = ovf ? 0 : (C < N ? C : N);
+        if (fidx >= 0) { d.ext->slot[fidx & 3] = slot; d.ext->status[fidx & 3] = status; }
+        else d.ext->stage_status = status;
+    }
+}
+
+// extract side of a missing image (VisualOdometry.cpp:77-82): the frame owns no slot (-1);
+// its pose chain reads none, so the next frame's choice only has to avoid prev
+__global__ void k_ext_missing(VoDev d, int fidx)
+{
+    if (threadIdx.x == 0) {
+        d.ext->slot[fidx & 3] = -1;
+        d.ext->status[fidx & 3] = VO_STATUS_OK;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -854,12 +889,10 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d)
 #define DS_KPB 8
 #define DS_TSTRIDE 905
 
-__global__ void __launch_bounds__(256) k_describe(VoDev d)
+__global__ void __launch_bounds__(256) k_describe(VoDev d, int fidx)
 {
-    VoState* st = d.st;
-    if (st->status != VO_STATUS_OK && st->status != VO_STATUS_FIRST) return;
-    const int cur = st->cur;
-    const int n = st->n_kps[cur];
+    const int cur = ext_slot(d, fidx);
+    const int n = d.ext->n_kps[cur];
     const int base = blockIdx.x * DS_KPB;
     if (base >= n) return;
     const int nk = min(DS_KPB, n - base);
@@ -968,12 +1001,10 @@ __device__ __forceinline__ bool arrive_last(unsigned* ctr, unsigned total, unsig
 // seed, counters, histogram.  Run by the workgroup that finalizes the current frame.
 __device__ void setup_next_frame(const VoDev& d, VoState* st)
 {
-    for (int i = threadIdx.x; i < VO_HIST_BINS; i += blockDim.x) d.hist[i] = 0u;
     if (threadIdx.x == 0) {
         const int f = st->frame;        // already incremented
         st->mode = VO_MODE_FRAME;
         st->status = f == 0 ? VO_STATUS_FIRST : VO_STATUS_OK;
-        st->cur = f == 0 ? 0 : 1 - st->prev;
         st->frame_seed = mix64(d.seed + 0x632BE59BD9B4E019ULL * (uint64_t)(f + 1));
         st->cand_count = 0; st->M = 0; st->n_inl = 0; st->fitted = 0; st->degenerate = 0;
         st->bestk = -1; st->n_eval = 0; st->need_more = 0;
@@ -990,11 +1021,15 @@ __device__ void setup_next_frame(const VoDev& d, VoState* st)
 __global__ void __launch_bounds__(256) k_match(VoDev d)
 {
     VoState* st = d.st;
+    if (st->mode == VO_MODE_FRAME && d.ext->status[st->frame & 3] != VO_STATUS_OK) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) st->status = VO_STATUS_OVERFLOW;   // select capacity
+        return;
+    }
     if (st->status != VO_STATUS_OK) return;
     __shared__ unsigned s_last;
     __shared__ int s_wsum[4];
-    const int prev = st->prev, cur = st->cur;
-    const int n1 = st->n_kps[prev], n2 = st->n_kps[cur];
+    const int prev = st->prev, cur = cur_slot(d, st);
+    const int n1 = d.ext->n_kps[prev], n2 = d.ext->n_kps[cur];
     const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (q < n1) {
@@ -1708,11 +1743,13 @@ __device__ void finalize_frame(const VoDev& d, VoState* st)
             VoFrameOut* o = d.out;
             int flip = 1;
             if (status == VO_STATUS_FIRST || status == VO_STATUS_MISSING) flip = 0;
+            const int cur = cur_slot(d, st);
             if (status == VO_STATUS_OK || status == VO_STATUS_DEGENERATE) {
                 st->last_valid = st->frame;      // VisualOdometry.cpp:161-166 precede getPose
-                st->prev = st->cur;
+                st->prev = cur;
             }
-            if (status == VO_STATUS_FIRST) { st->prev = st->cur; st->last_valid = 0; }
+            if (status == VO_STATUS_FIRST) { st->prev = cur; st->last_valid = 0; }
+            d.ext->prev_for[(st->frame + 1) & 3] = st->prev;   // the extract stream's slot choice
             if (have_pose) {
                 double Trel[16] = {Rf[0], Rf[1], Rf[2], tf[0], Rf[3], Rf[4], Rf[5], tf[1],
                                    Rf[6], Rf[7], Rf[8], tf[2], 0, 0, 0, 1};
@@ -1721,7 +1758,7 @@ __device__ void finalize_frame(const VoDev& d, VoState* st)
             for (int r = 0; r < 3; ++r)
                 for (int c = 0; c < 4; ++c) o->pose[r * 4 + c] = (flip && r == 2) ? -Tc[r * 4 + c] : Tc[r * 4 + c];
             o->status = status;
-            o->n_kps = status == VO_STATUS_MISSING ? 0 : st->n_kps[st->cur];
+            o->n_kps = status == VO_STATUS_MISSING ? 0 : d.ext->n_kps[cur];
             o->n_matches = st->M;
             o->n_inl = st->n_inl;
             o->best_k = st->bestk;
@@ -1861,9 +1898,13 @@ void launch_stencil(const VoDev& d, const uint8_t* frame, int write_response, hi
     dim3 g((d.W + ST_TW - 1) / ST_TW, (d.H + ST_TH - 1) / ST_TH);
     hipLaunchKernelGGL(k_stencil, g, dim3(256), 0, s, d, frame, write_response);
 }
-void launch_select(const VoDev& d, hipStream_t s)
+void launch_select(const VoDev& d, int fidx, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(1024), (size_t)d.sel_lds, s, d);
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(1024), (size_t)d.sel_lds, s, d, fidx);
+}
+void launch_ext_missing(const VoDev& d, int fidx, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_ext_missing, dim3(1), dim3(64), 0, s, d, fidx);
 }
 int select_lds_bytes(int W, int H, int* key_cap)
 {
@@ -1876,9 +1917,9 @@ int select_lds_bytes(int W, int H, int* key_cap)
     if (key_cap) *key_cap = L.key_cap;
     return bytes;
 }
-void launch_describe(const VoDev& d, hipStream_t s)
+void launch_describe(const VoDev& d, int fidx, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_describe, dim3((d.N + DS_KPB - 1) / DS_KPB), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_describe, dim3((d.N + DS_KPB - 1) / DS_KPB), dim3(256), 0, s, d, fidx);
 }
 void launch_match(const VoDev& d, hipStream_t s)
 {
