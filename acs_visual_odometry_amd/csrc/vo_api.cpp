@@ -167,8 +167,12 @@ struct EvRec {
     std::vector<hipEvent_t>* pool;
     size_t used;
     int only;   // -1: all kernels
+    int frame;  // frame being enqueued; single-kernel mode brackets every VO_TIMING_STRIDE-th frame
     std::vector<std::pair<int, size_t>> spans;   // (kernel, index of its start event)
 };
+// An event pair costs ~6 us of queue time per bracketed launch (rocprofv3 kernel trace), so
+// the bench's live single-kernel timing samples one frame in VO_TIMING_STRIDE.
+#define VO_TIMING_STRIDE 8
 
 size_t ev_mark(EvRec* ev, hipStream_t st)
 {
@@ -184,7 +188,7 @@ size_t ev_mark(EvRec* ev, hipStream_t st)
 template <typename F>
 void timed(EvRec* ev, int k, hipStream_t st, F&& launch)
 {
-    const bool on = ev && (ev->only < 0 || ev->only == k);
+    const bool on = ev && (ev->only < 0 || (ev->only == k && ev->frame % VO_TIMING_STRIDE == 0));
     size_t b = on ? ev_mark(ev, st) : 0;
     launch();
     if (on) {
@@ -196,6 +200,7 @@ void timed(EvRec* ev, int k, hipStream_t st, F&& launch)
 void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev)
 {
     const int f = c->fidx++;
+    if (ev) ev->frame = f;
     VoDev d = c->d;
     d.out = out;
     // extract stream: frame f-2's pose chain must be done (its slots may be reused, and
@@ -627,7 +632,7 @@ int vo_process_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
     HIPCHK(hipSetDevice(c->cfg.device));
     int rc = ensure_out(c, std::max(nframes, 1));
     if (rc) return rc;
-    EvRec rec{&c->ev_pool, 0, c->timing >= 100 ? c->timing - 100 : -1, {}};
+    EvRec rec{&c->ev_pool, 0, c->timing >= 100 ? c->timing - 100 : -1, 0, {}};
     EvRec* evp = c->timing ? &rec : nullptr;
     for (int f = 0; f < nframes; ++f) enqueue_frame(c, d_frames + (size_t)f * frame_bytes, c->out_dev + f, evp);
     HIPCHK(hipGetLastError());

@@ -1018,6 +1018,39 @@ __device__ void setup_next_frame(const VoDev& d, VoState* st)
 // feature_matching_parallel.cpp:39-113; VisualOdometry.cpp:100-123.
 // key = dist<<16 | j, so the min key is (min dist, first j) and the 2nd key gives `second`
 // ---------------------------------------------------------------------------
+// branch-free top-2 update (keys are unique: the low 16 bits carry the candidate index)
+__device__ __forceinline__ void top2_insert(uint32_t key, uint32_t& m1, uint32_t& m2)
+{
+    m2 = min(m2, max(key, m1));
+    m1 = min(m1, key);
+}
+__device__ __forceinline__ void top2_wave(uint32_t& m1, uint32_t& m2)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        uint32_t o1 = __shfl_xor(m1, off), o2 = __shfl_xor(m2, off);
+        uint32_t n1v = min(m1, o1);
+        uint32_t n2v = min(max(m1, o1), min(m2, o2));
+        m1 = n1v; m2 = n2v;
+    }
+}
+// Lowe ratio test on the top-2 keys (feature_matching_parallel.cpp:90-99); needs 2 candidates
+__device__ __forceinline__ int ratio_accept(uint32_t m1, uint32_t m2, float ratio)
+{
+    if (m1 == 0xFFFFFFFFu || m2 == 0xFFFFFFFFu) return -1;
+    int d1 = (int)(m1 >> 16), d2 = (int)(m2 >> 16);
+    return ((float)d1 < ratio * (float)d2) ? (int)(m1 & 0xFFFF) : -1;
+}
+
+// 32-bit prefix mode: the cur frame's prefixes are staged once per workgroup in LDS
+// (16 KB at N = 4096), and each wave scores MT_QPW queries per candidate read.
+#define MT_QPW 4
+#define MT_QPB (4 * MT_QPW)
+__host__ __device__ inline int match_blocks(int N, int match_bits)
+{
+    return match_bits == 32 ? (N + MT_QPB - 1) / MT_QPB : (N + 3) / 4;
+}
+
 __global__ void __launch_bounds__(256) k_match(VoDev d)
 {
     VoState* st = d.st;
@@ -1028,20 +1061,47 @@ __global__ void __launch_bounds__(256) k_match(VoDev d)
     if (st->status != VO_STATUS_OK) return;
     __shared__ unsigned s_last;
     __shared__ int s_wsum[4];
+    __shared__ uint32_t s_cand[4096];
     const int prev = st->prev, cur = cur_slot(d, st);
     const int n1 = d.ext->n_kps[prev], n2 = d.ext->n_kps[cur];
-    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (q < n1) {
-        uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
-        if (d.match_bits == 32) {
-            const uint32_t qv = d.pre[prev][q];
+    if (d.match_bits == 32) {
+        if (blockIdx.x * MT_QPB < n1) {
             const uint32_t* cand = d.pre[cur];
-            for (int j = lane; j < n2; j += 64) {
-                uint32_t key = ((uint32_t)__popc(qv ^ cand[j]) << 16) | (uint32_t)j;
-                if (key < m1) { m2 = m1; m1 = key; } else if (key < m2) m2 = key;
+            for (int j0 = threadIdx.x; j0 < n2; j0 += 4 * 256) {
+                uint32_t v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = j0 + u * 256 < n2 ? cand[j0 + u * 256] : 0u;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (j0 + u * 256 < n2) s_cand[j0 + u * 256] = v[u];
             }
-        } else {
+            const int q0 = blockIdx.x * MT_QPB + (threadIdx.x >> 6) * MT_QPW;
+            uint32_t qv[MT_QPW], m1[MT_QPW], m2[MT_QPW];
+#pragma unroll
+            for (int u = 0; u < MT_QPW; ++u) {
+                qv[u] = q0 + u < n1 ? d.pre[prev][q0 + u] : 0u;
+                m1[u] = 0xFFFFFFFFu;
+                m2[u] = 0xFFFFFFFFu;
+            }
+            __syncthreads();
+#pragma unroll 4
+            for (int j = lane; j < n2; j += 64) {
+                const uint32_t c = s_cand[j];
+#pragma unroll
+                for (int u = 0; u < MT_QPW; ++u)
+                    top2_insert(((uint32_t)__popc(qv[u] ^ c) << 16) | (uint32_t)j, m1[u], m2[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < MT_QPW; ++u) {
+                top2_wave(m1[u], m2[u]);
+                if (lane == 0 && q0 + u < n1) st_sc1(d.match_j + q0 + u, ratio_accept(m1[u], m2[u], d.ratio));
+            }
+        }
+    } else {
+        const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+        if (q < n1) {
+            uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
             const uint64_t* qd = d.desc[prev] + (size_t)q * 8;
             uint64_t qw[8];
 #pragma unroll
@@ -1051,24 +1111,10 @@ __global__ void __launch_bounds__(256) k_match(VoDev d)
                 int dist = 0;
 #pragma unroll
                 for (int w = 0; w < 8; ++w) dist += __popcll(qw[w] ^ cd[(size_t)j * 8 + w]);
-                uint32_t key = ((uint32_t)dist << 16) | (uint32_t)j;
-                if (key < m1) { m2 = m1; m1 = key; } else if (key < m2) m2 = key;
+                top2_insert(((uint32_t)dist << 16) | (uint32_t)j, m1, m2);
             }
-        }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            uint32_t o1 = __shfl_xor(m1, off), o2 = __shfl_xor(m2, off);
-            uint32_t n1v = min(m1, o1);
-            uint32_t n2v = min(max(m1, o1), min(m2, o2));
-            m1 = n1v; m2 = n2v;
-        }
-        if (lane == 0) {
-            int res = -1;
-            if (m1 != 0xFFFFFFFFu && m2 != 0xFFFFFFFFu) {
-                int d1 = (int)(m1 >> 16), d2 = (int)(m2 >> 16);
-                if ((float)d1 < d.ratio * (float)d2) res = (int)(m1 & 0xFFFF);
-            }
-            st_sc1(d.match_j + q, res);
+            top2_wave(m1, m2);
+            if (lane == 0) st_sc1(d.match_j + q, ratio_accept(m1, m2, d.ratio));
         }
     }
     if (!arrive_last(d.ctr + 0, gridDim.x, &s_last)) return;
@@ -1477,7 +1523,7 @@ __device__ void pose_prep(const VoDev& d, VoState* st)
 
 // least-squares null vector: Cholesky (pivot floor) + inverse iteration, warm start x0
 // (mirror of oracle ls_nullvec9; S read from LDS, L kept in registers)
-__device__ void ls_nullvec9(const double* S, const double* x0, double* f)
+__device__ int ls_nullvec9(const double* S, const double* x0, double* f)
 {
     double L[45], invd[9];           // packed lower triangle, row i at i(i+1)/2
     double mx = 0.0;
@@ -1515,7 +1561,8 @@ __device__ void ls_nullvec9(const double* S, const double* x0, double* f)
 #pragma unroll
         for (int i = 0; i < 9; ++i) x[i] = 1.0 / 3.0;
     }
-    for (int it = 0; it < 32; ++it) {
+    int it = 0;
+    for (; it < 32; ++it) {
         double y[9], z[9];
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
@@ -1544,10 +1591,11 @@ __device__ void ls_nullvec9(const double* S, const double* x0, double* f)
             if (dd > diff) diff = dd;
             x[i] = xn;
         }
-        if (diff <= 4e-16) break;
+        if (diff <= 4e-16) { ++it; break; }
     }
 #pragma unroll
     for (int i = 0; i < 9; ++i) f[i] = x[i];
+    return it;
 }
 
 __device__ __forceinline__ void warm_start(const double* Fb, double s1, double mx1, double my1, double s2,
@@ -1589,6 +1637,7 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
     const int tid = threadIdx.x, lane = tid & 63;
     const int bestk = st->bestk;
     const int scored = st->scored;
+    VO_STAMP(d, 1995, 0);
     if (tid < 64) {                       // wave 0: ordered inlier compaction
         int n = 0;
         if (bestk >= 0) {
@@ -1613,6 +1662,7 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
     }
     __threadfence_block();
     __syncthreads();
+    VO_STAMP(d, 1995, 1);
     const int n = s_n;
     if (bestk >= 0 && n >= 8) {
         const int32_t* idx = d.inl;
@@ -1623,6 +1673,7 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
             for (int c = 0; c < 4; ++c) pm[c] = pm[c] + p[c];
         }
         refit_sums<4>(pm, s_part, s_sum);
+        VO_STAMP(d, 1995, 2);
         double mean[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) mean[c] = s_sum[c] / (double)n;
@@ -1636,6 +1687,7 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
             }
         }
         refit_sums<2>(ps, s_part, s_sum);
+        VO_STAMP(d, 1995, 3);
         const double sc1 = sqrt(2.0) / sqrt(s_sum[0] / (double)n);
         const double sc2 = sqrt(2.0) / sqrt(s_sum[1] / (double)n);
         const double o1x = -(sc1 * mean[0]), o1y = -(sc1 * mean[1]), o2x = -(sc2 * mean[2]), o2y = -(sc2 * mean[3]);
@@ -1653,6 +1705,7 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
                 for (int v = u; v < 9; ++v) { acc[e] = acc[e] + a[u] * a[v]; ++e; }
         }
         refit_sums<45>(acc, s_part, s_sum);
+        VO_STAMP(d, 1995, 4);
         if (tid < 45) {
             int u = 0, e = tid;
             while (e >= 9 - u) { e -= 9 - u; ++u; }
@@ -1669,11 +1722,19 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
         if (tid == 0) {
             double Fb[9], f0[9], f[9];
             for (int i = 0; i < 9; ++i) Fb[i] = d.hypF[(size_t)bestk * 9 + i];
+            VO_STAMP(d, 1995, 5);
             warm_start(Fb, sc1, mean[0], mean[1], sc2, mean[2], mean[3], f0);
-            ls_nullvec9(s_A, f0, f);
+            const int its = ls_nullvec9(s_A, f0, f);
+            VO_STAMP(d, 1995, 6);
+#ifdef VO_STAMPS
+            if (d.dbg) { d.dbg[1995 * 16 + 14] = (unsigned long long)its; d.dbg[1995 * 16 + 15] = (unsigned long long)n; }
+#else
+            (void)its;
+#endif
             double Fn[9];
             denormalize(f, sc1, mean[0], mean[1], sc2, mean[2], mean[3], Fn);
             rank2(Fn);
+            VO_STAMP(d, 1995, 7);
             for (int i = 0; i < 9; ++i) st->model_F[i] = Fn[i];
             st->fitted = 1;
             st->model_n = n;
@@ -1682,6 +1743,7 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
         st->fitted = 0;            // fit() returns early: the previous model stays (quirk 9)
     }
     if (with_pose && tid == 0) pose_prep(d, st);
+    if (tid == 0) VO_STAMP(d, 1995, 8);
 }
 
 __global__ void k_pose_prep(VoDev d)
@@ -1789,6 +1851,7 @@ __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d)
     const int n = st->model_n;
     const unsigned active = (unsigned)((4 * n + TRI_BLOCK - 1) / TRI_BLOCK);
     if (blockIdx.x >= active) return;
+    if (blockIdx.x == 0) VO_STAMP(d, 1996, 0);
     if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
     __syncthreads();
     const int g = blockIdx.x * TRI_BLOCK + threadIdx.x;   // (point, candidate) = (g >> 2, g & 3)
@@ -1837,6 +1900,7 @@ __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d)
             pos = (z1 > 0 && z2 > 0);
         }
     }
+    if (blockIdx.x == 0) VO_STAMP(d, 1996, 1);
     unsigned long long bal = ballot64(pos);
     const int lane = threadIdx.x & 63;
     if (lane < 4) {
@@ -1849,8 +1913,10 @@ __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d)
         __hip_atomic_fetch_add((gi32*)&st->counts4[threadIdx.x], s_cnt[threadIdx.x], __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     if (!arrive_last(d.ctr + 2, active, &s_last)) return;
+    VO_STAMP(d, 1996, 2);
     if (threadIdx.x == 0) d.ctr[2] = 0u;
     finalize_frame(d, st);
+    VO_STAMP(d, 1996, 3);
 }
 
 // a missing image (VisualOdometry.cpp:77-82): push T_curr, advance the frame counter
@@ -1923,7 +1989,7 @@ void launch_describe(const VoDev& d, int fidx, hipStream_t s)
 }
 void launch_match(const VoDev& d, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_match, dim3((d.N + 3) / 4), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_match, dim3(match_blocks(d.N, d.match_bits)), dim3(256), 0, s, d);
 }
 void launch_ransac(const VoDev& d, int nhyp, hipStream_t s)
 {

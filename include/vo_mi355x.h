@@ -135,9 +135,10 @@ int  vo_device_upload(vo_ctx* ctx, void* dptr, const void* src, size_t bytes);
 /* Reset the trajectory state (frame counter, T_curr, model, prev descriptors). */
 int  vo_reset(vo_ctx* ctx);
 
-/* Per-kernel timing of vo_process_frames_device (HIP events on the ctx stream).
- * on: 0 off, 1 every kernel, 100+k only kernel k (two events per frame).  times: average
- * ms per launch over the last call (-1 if not timed).  Returns the number written. */
+/* Per-kernel timing of vo_process_frames_device (HIP events on the stream each kernel runs on).
+ * on: 0 off, 1 every kernel of every frame, 100+k only kernel k, on every 8th frame (an event
+ * pair costs ~6 us of queue time, so the live timing samples).  times: average ms per timed
+ * launch over the last call (-1 if not timed).  Returns the number written. */
 int  vo_last_kernel_times(vo_ctx* ctx, const char** names, float* ms, int cap);
 int  vo_enable_kernel_timing(vo_ctx* ctx, int on);
 
