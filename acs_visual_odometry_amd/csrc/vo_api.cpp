@@ -33,7 +33,6 @@ struct vo_ctx {
     VoDev d;
     hipStream_t s = nullptr;          // pose chain (and stage APIs)
     hipStream_t se = nullptr;         // extract stream of the frame pipeline
-    hipEvent_t ev_ext[2] = {nullptr, nullptr}, ev_pose[2] = {nullptr, nullptr};
     int fidx = 0;                     // frames enqueued since vo_reset
     int max_hyp = VO_MAX_HYP;
     int gt_cap = 0;
@@ -156,7 +155,7 @@ void enqueue_extract(vo_ctx* c, const uint8_t* dframe, int write_response)
 int restore_state(vo_ctx* c, const VoState* saved)
 {
     HIPCHK(hipMemsetAsync(c->d.hist, 0, sizeof(uint32_t) * VO_HIST_BINS, c->s));
-    HIPCHK(hipMemsetAsync(c->d.ctr, 0, sizeof(unsigned) * 4, c->s));
+    HIPCHK(hipMemsetAsync(c->d.ctr, 0, sizeof(unsigned) * VO_CTR_COUNTERS, c->s));
     return write_state(c, saved);
 }
 
@@ -178,7 +177,9 @@ size_t ev_mark(EvRec* ev, hipStream_t st)
 {
     if (ev->used >= ev->pool->size()) {
         hipEvent_t e;
-        (void)hipEventCreate(&e);
+        // device-scope release: a system-scope fence (the default) writes back and invalidates
+        // the L2s at every record, which is most of an event's queue cost here
+        (void)hipEventCreateWithFlags(&e, hipEventReleaseToDevice);
         ev->pool->push_back(e);
     }
     (void)hipEventRecord((*ev->pool)[ev->used], st);
@@ -203,9 +204,17 @@ void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev)
     if (ev) ev->frame = f;
     VoDev d = c->d;
     d.out = out;
+    // Cross-queue order by frame counters the kernels publish (describe's last workgroup:
+    // extract done; finalize: pose chain done).  An event record + wait costs ~11-18 us of
+    // queue time per hop on MI355X (tools/evtest.hip); a stream-wait-value packet on a
+    // kernel-written counter ~1-6 us (ROCclr runs it as a small wait kernel); a poll inside
+    // the consuming kernel ~1 us.
+    const uint32_t seq = (uint32_t)f + 1u;
+    d.seqno = seq;
     // extract stream: frame f-2's pose chain must be done (its slots may be reused, and
     // finalize(f-2) wrote the prev slot select(f) avoids)
-    if (f >= 2) (void)hipStreamWaitEvent(c->se, c->ev_pose[f & 1], 0);
+    if (f >= 2)
+        (void)hipStreamWaitValue32(c->se, c->d.ctr + VO_SYNC_POSE, seq - 2u, hipStreamWaitValueGte, 0xFFFFFFFFu);
     if (dframe) {
         timed(ev, 0, c->se, [&] { vo::launch_stencil(d, dframe, 0, c->se); });
         timed(ev, 1, c->se, [&] { vo::launch_select(d, f, c->se); });
@@ -213,8 +222,7 @@ void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev)
     } else {
         vo::launch_ext_missing(d, f, c->se);
     }
-    (void)hipEventRecord(c->ev_ext[f & 1], c->se);
-    (void)hipStreamWaitEvent(c->s, c->ev_ext[f & 1], 0);
+    // the pose queue's wait for this frame's extract is in k_match (wait_seq)
     if (dframe) {
         timed(ev, 3, c->s, [&] { vo::launch_match(d, c->s); });
         timed(ev, 4, c->s, [&] { vo::launch_ransac(d, c->max_hyp, c->s); });
@@ -223,7 +231,6 @@ void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev)
     } else {
         vo::launch_missing(d, c->s);
     }
-    (void)hipEventRecord(c->ev_pose[f & 1], c->s);
 }
 
 int ensure_out(vo_ctx* c, int n)
@@ -331,10 +338,6 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     auto bail = [&](int r) { vo_destroy(c); return r; };
     if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipStreamCreateWithFlags(&c->se, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
-    for (int i = 0; i < 2; ++i) {
-        if (hip_ok(hipEventCreateWithFlags(&c->ev_ext[i], hipEventDisableTiming)) != VO_OK) return bail(VO_ERR_HIP);
-        if (hip_ok(hipEventCreateWithFlags(&c->ev_pose[i], hipEventDisableTiming)) != VO_OK) return bail(VO_ERR_HIP);
-    }
     d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
     if (d.sel_lds < 0) return bail(VO_ERR_HIP);
     rc |= dalloc(&d.frame_in, (size_t)W * H);
@@ -359,7 +362,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc(&d.model_p, (size_t)N * 4);
     rc |= dalloc(&d.st, 1);
     rc |= dalloc(&d.ext, 1);
-    rc |= dalloc(&d.ctr, 4);
+    rc |= dalloc(&d.ctr, VO_CTR_WORDS);
 #ifdef VO_STAMPS
     rc |= dalloc(&d.dbg, (size_t)c->max_hyp * 16);
 #endif
@@ -377,7 +380,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
         (void)hipMemset(d.pre[s], 0, sizeof(uint32_t) * N);
     }
     if (ensure_out(c, 16) != VO_OK) return bail(VO_ERR_HIP);
-    (void)hipMemset(d.ctr, 0, sizeof(unsigned) * 4);
+    (void)hipMemset(d.ctr, 0, sizeof(unsigned) * VO_CTR_WORDS);
     if (vo_reset(c) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipDeviceSynchronize()) != VO_OK) return bail(VO_ERR_HIP);
     *out = c;
@@ -404,10 +407,6 @@ void vo_destroy(vo_ctx* c)
     if (c->out_host) (void)hipHostFree(c->out_host);
     if (c->stage_host) (void)hipHostFree(c->stage_host);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
-    for (int i = 0; i < 2; ++i) {
-        if (c->ev_ext[i]) (void)hipEventDestroy(c->ev_ext[i]);
-        if (c->ev_pose[i]) (void)hipEventDestroy(c->ev_pose[i]);
-    }
     if (c->se) (void)hipStreamDestroy(c->se);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
@@ -428,7 +427,7 @@ int vo_reset(vo_ctx* c)
     HIPCHK(hipMemcpyAsync(c->d.ext, &e, sizeof(e), hipMemcpyHostToDevice, c->s));
     HIPCHK(hipMemsetAsync(c->d.hist, 0, sizeof(uint32_t) * VO_HIST_BINS, c->s));
     c->fidx = 0;
-    HIPCHK(hipMemsetAsync(c->d.ctr, 0, sizeof(unsigned) * 4, c->s));
+    HIPCHK(hipMemsetAsync(c->d.ctr, 0, sizeof(unsigned) * VO_CTR_WORDS, c->s));   // + frame counters
     vo::launch_frame_begin(c->d, VO_MODE_FRAME, c->s);     // frame 0 set up on the device
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->s));

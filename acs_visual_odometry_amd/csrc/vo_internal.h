@@ -31,6 +31,14 @@
 #define VO_PIPE_SLOTS 3        // keypoint/descriptor slots of the frame pipeline
 #define VO_STAGE_SLOT 3        // stage APIs (vo_extract / vo_match) use slots 3 and 4
 #define VO_SLOTS 5
+// ctr words: in-launch arrival counters [0, VO_CTR_COUNTERS), then the two cross-queue frame
+// counters on lines of their own (frames whose extract / pose chain is complete, 1-based,
+// read by the other queue's stream-wait-value packet)
+#define VO_CTR_COUNTERS 16
+#define VO_CTR_DESCRIBE 4
+#define VO_SYNC_EXT 32
+#define VO_SYNC_POSE 48
+#define VO_CTR_WORDS 64
 #define VO_MAX_HYP 2000
 #define VO_HYP_CHUNK0 256
 #define VO_RED_THREADS 256
@@ -122,7 +130,9 @@ struct VoDev {
     VoState* st;
     VoExt* ext;
     VoFrameOut* out;
-    unsigned* ctr;        // in-launch arrival counters: [0] match, [1] ransac, [2] triangulate
+    unsigned* ctr;        // in-launch arrival counters: [0] match, [1] ransac, [2] triangulate,
+                          // [3] ransac chunk 2, [4] describe; cross-queue counters (VO_SYNC_*)
+    uint32_t seqno;       // frame pipeline: 1 + frame index since vo_reset; 0 outside it
     unsigned long long* dbg;   // diagnostic s_memtime stamps (VO_STAMPS builds only)
 };
 

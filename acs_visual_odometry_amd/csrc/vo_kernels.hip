@@ -871,6 +871,50 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int fidx)
     }
 }
 
+// ---------------------------------------------------------------------------
+// in-launch hand-off: the last workgroup to arrive consumes what the others produced.
+// Valid form of MI355X_MICROARCH.md "Workgroup dispatch ... visibility" (table row 1):
+// payload stored sc1 (agent-scope relaxed atomic stores), every storing wave drains
+// vmcnt(0), one lane per workgroup adds to ONE unsharded counter, the workgroup whose
+// add returns total-1 loads the payload with sc1 loads only.  The counter is reset by
+// that last workgroup for the next launch (kernel boundary orders it).
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) int gi32;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+__device__ __forceinline__ void st_sc1(int* p, int v)
+{
+    __hip_atomic_store((gi32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_sc1(const int* p)
+{
+    return __hip_atomic_load((gi32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool arrive_last(unsigned* ctr, unsigned total, unsigned* s_flag)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned prev = __hip_atomic_fetch_add((gu32*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_flag = (prev == total - 1) ? 1u : 0u;
+    }
+    __syncthreads();
+    return *s_flag != 0u;
+}
+
+// Cross-queue hand-off to the other HIP queue's stream-wait-value packet (vo_api.cpp
+// enqueue_frame): every wave drains its stores, the workgroup meets, then one lane stores the
+// frame counter with a system-scope release (L2 write-back, then a write-through store the
+// command processor reads from memory).  Workgroups other than the caller must already have
+// published their stores at agent scope (release fence before arrive_last).
+__device__ __forceinline__ void publish_seq(unsigned* flag, unsigned v)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store((gu32*)flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // extract side of a missing image (VisualOdometry.cpp:77-82): the frame owns no slot (-1);
 // its pose chain reads none, so the next frame's choice only has to avoid prev
 __global__ void k_ext_missing(VoDev d, int fidx)
@@ -879,6 +923,7 @@ __global__ void k_ext_missing(VoDev d, int fidx)
         d.ext->slot[fidx & 3] = -1;
         d.ext->status[fidx & 3] = VO_STATUS_OK;
     }
+    if (d.seqno) publish_seq(d.ctr + VO_SYNC_EXT, d.seqno);
 }
 
 // ---------------------------------------------------------------------------
@@ -889,12 +934,8 @@ __global__ void k_ext_missing(VoDev d, int fidx)
 #define DS_KPB 8
 #define DS_TSTRIDE 905
 
-__global__ void __launch_bounds__(256) k_describe(VoDev d, int fidx)
+__device__ __forceinline__ void describe_block(const VoDev& d, int cur, int n, int base)
 {
-    const int cur = ext_slot(d, fidx);
-    const int n = d.ext->n_kps[cur];
-    const int base = blockIdx.x * DS_KPB;
-    if (base >= n) return;
     const int nk = min(DS_KPB, n - base);
     __shared__ float s_I0[DS_KPB][VO_FREAK_NPOINTS];
     __shared__ float s_term[DS_KPB * 2][DS_TSTRIDE];
@@ -965,36 +1006,21 @@ __global__ void __launch_bounds__(256) k_describe(VoDev d, int fidx)
     }
 }
 
-// ---------------------------------------------------------------------------
-// in-launch hand-off: the last workgroup to arrive consumes what the others produced.
-// Valid form of MI355X_MICROARCH.md "Workgroup dispatch ... visibility" (table row 1):
-// payload stored sc1 (agent-scope relaxed atomic stores), every storing wave drains
-// vmcnt(0), one lane per workgroup adds to ONE unsharded counter, the workgroup whose
-// add returns total-1 loads the payload with sc1 loads only.  The counter is reset by
-// that last workgroup for the next launch (kernel boundary orders it).
-// ---------------------------------------------------------------------------
-typedef __attribute__((address_space(1))) int gi32;
-typedef __attribute__((address_space(1))) unsigned gu32;
-
-__device__ __forceinline__ void st_sc1(int* p, int v)
+__global__ void __launch_bounds__(256) k_describe(VoDev d, int fidx)
 {
-    __hip_atomic_store((gi32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int ld_sc1(const int* p)
-{
-    return __hip_atomic_load((gi32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ bool arrive_last(unsigned* ctr, unsigned total, unsigned* s_flag)
-{
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // every storing wave drains its sc1 stores
+    const int cur = ext_slot(d, fidx);
+    const int n = d.ext->n_kps[cur];
+    const int base = blockIdx.x * DS_KPB;
+    if (base < n) describe_block(d, cur, n, base);
+    if (!d.seqno) return;
+    // frame pipeline: the last workgroup tells the pose queue this frame's descriptors are in
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned prev = __hip_atomic_fetch_add((gu32*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *s_flag = (prev == total - 1) ? 1u : 0u;
-    }
-    __syncthreads();
-    return *s_flag != 0u;
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __shared__ unsigned s_last;
+    if (!arrive_last(d.ctr + VO_CTR_DESCRIBE, gridDim.x, &s_last)) return;
+    if (threadIdx.x == 0) d.ctr[VO_CTR_DESCRIBE] = 0u;
+    publish_seq(d.ctr + VO_SYNC_EXT, d.seqno);
 }
 
 // next frame's bookkeeping (VisualOdometry.cpp:68-100 loop head): status, slot, sampler
@@ -1051,9 +1077,28 @@ __host__ __device__ inline int match_blocks(int N, int match_bits)
     return match_bits == 32 ? (N + MT_QPB - 1) / MT_QPB : (N + 3) / 4;
 }
 
+// frame pipeline: wait in-kernel for describe's counter (a ROCclr stream-wait-value packet
+// costs a ~5 us wait kernel on the critical queue).  Lane 0 polls with write-through loads,
+// then an agent-scope acquire + barrier before any load of extract-stream data.  The extract
+// queue never waits on this launch (it waits only for frame f-2's pose chain, which precedes
+// it on this queue), so the poll always ends; the bound only guards against a broken pipeline.
+__device__ __forceinline__ void wait_seq(const unsigned* flag, unsigned v)
+{
+    if (threadIdx.x == 0) {
+        for (unsigned spin = 0; spin < (1u << 24); ++spin) {
+            if (__hip_atomic_load((const gu32*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= v) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
 __global__ void __launch_bounds__(256) k_match(VoDev d)
 {
     VoState* st = d.st;
+    if (d.seqno) wait_seq(d.ctr + VO_SYNC_EXT, d.seqno);
     if (st->mode == VO_MODE_FRAME && d.ext->status[st->frame & 3] != VO_STATUS_OK) {
         if (blockIdx.x == 0 && threadIdx.x == 0) st->status = VO_STATUS_OVERFLOW;   // select capacity
         return;
@@ -1521,34 +1566,104 @@ __device__ void pose_prep(const VoDev& d, VoState* st)
     for (int c = 0; c < 4; ++c) st->counts4[c] = 0;
 }
 
-// least-squares null vector: Cholesky (pivot floor) + inverse iteration, warm start x0
-// (mirror of oracle ls_nullvec9; S read from LDS, L kept in registers)
-__device__ int ls_nullvec9(const double* S, const double* x0, double* f)
+// least-squares null vector (mirror of oracle ls_nullvec9): Cholesky with a pivot floor,
+// W = S^-1 from the column-wise inverse of L, six scaled squarings to W^64, then power
+// iteration from the warm start x0.  Called by the whole k_refit workgroup; each wave runs it
+// (wave 1 duplicates wave 0), lanes 0..8 own rows / columns, lanes 0..44 own the upper-
+// triangle entries of the squarings, and every sum runs in the oracle's ascending order.
+// Returns the number of power steps; f (unit) is valid in every lane.
+__constant__ unsigned char c_tri9[45][2] = {
+    {0, 0}, {0, 1}, {0, 2}, {0, 3}, {0, 4}, {0, 5}, {0, 6}, {0, 7}, {0, 8}, {1, 1}, {1, 2}, {1, 3},
+    {1, 4}, {1, 5}, {1, 6}, {1, 7}, {1, 8}, {2, 2}, {2, 3}, {2, 4}, {2, 5}, {2, 6}, {2, 7}, {2, 8},
+    {3, 3}, {3, 4}, {3, 5}, {3, 6}, {3, 7}, {3, 8}, {4, 4}, {4, 5}, {4, 6}, {4, 7}, {4, 8}, {5, 5},
+    {5, 6}, {5, 7}, {5, 8}, {6, 6}, {6, 7}, {6, 8}, {7, 7}, {7, 8}, {8, 8}};
+
+__device__ __forceinline__ double wave_max_d(double v)
 {
-    double L[45], invd[9];           // packed lower triangle, row i at i(i+1)/2
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmax(v, shfl_xor_d(v, off));
+    return v;
+}
+
+// B = A A scaled by 1/max|B_ij| (A, B symmetric 9x9 in LDS); lane e < 45 owns entry c_tri9[e]
+__device__ __forceinline__ void sym_square_scale9(const double* A, double* B, int lane)
+{
+    const int e = lane < 45 ? lane : 44;
+    const int i = c_tri9[e][0], j = c_tri9[e][1];
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) v = v + A[i * 9 + k] * A[k * 9 + j];
+    const double m = wave_max_d(lane < 45 ? fabs(v) : 0.0);
+    v = v * (1.0 / m);
+    if (lane < 45) { B[i * 9 + j] = v; B[j * 9 + i] = v; }
+    __syncthreads();
+}
+
+__device__ int ls_nullvec9_par(const double* S, const double* x0, double* f, double* s_L, double* s_W,
+                               double* s_W2)
+{
+    const int lane = threadIdx.x & 63;
+    const int r = lane < 9 ? lane : 8;          // row / column owned by this lane
     double mx = 0.0;
 #pragma unroll
     for (int i = 0; i < 9; ++i)
         if (S[i * 9 + i] > mx) mx = S[i * 9 + i];
     double fl = 1e-15 * mx;
     if (!(fl > 0.0)) fl = 1e-300;
+    // Cholesky, column j: lane i computes S_ij - sum_k L_ik L_jk (lane j: the pivot)
+    double Lr[9], invd[9];
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
-        double sj = S[j * 9 + j];
+        double v = S[r * 9 + j];
 #pragma unroll
-        for (int k = 0; k < j; ++k) sj = sj - L[j * (j + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+        for (int k = 0; k < j; ++k) v = v - Lr[k] * shfl_d(Lr[k], j);
+        double sj = shfl_d(v, j);
         if (!(sj > fl)) sj = fl;
-        double dj = sqrt(sj);
-        L[j * (j + 1) / 2 + j] = dj;
+        const double dj = sqrt(sj);
         invd[j] = 1.0 / dj;
+        Lr[j] = r == j ? dj : (r > j ? v * invd[j] : 0.0);
+    }
+    if (lane < 9) {
 #pragma unroll
-        for (int i = j + 1; i < 9; ++i) {
-            double v = S[i * 9 + j];
+        for (int k = 0; k < 9; ++k) s_L[lane * 9 + k] = Lr[k];
+    }
+    __syncthreads();
+    // column c = r of L^-1 by forward substitution; the k < c terms are exact zeros
+    {
+        double Li[9];
 #pragma unroll
-            for (int k = 0; k < j; ++k) v = v - L[i * (i + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
-            L[i * (i + 1) / 2 + j] = v * invd[j];
+        for (int i = 0; i < 9; ++i) {
+            double v = 0.0;
+#pragma unroll
+            for (int k = 0; k < i; ++k) v = v + s_L[i * 9 + k] * Li[k];
+            Li[i] = i < r ? 0.0 : (i == r ? invd[i] : -(v * invd[i]));
+        }
+        // W = L^-T L^-1 needs rows of L^-1 per entry: stage L^-1 in s_W2 (row-major)
+        if (lane < 9) {
+#pragma unroll
+            for (int i = 0; i < 9; ++i) s_W2[i * 9 + lane] = Li[i];
         }
     }
+    __syncthreads();
+    {
+        const int e = lane < 45 ? lane : 44;
+        const int i = c_tri9[e][0], j = c_tri9[e][1];
+        double v = 0.0;
+        for (int k = j; k < 9; ++k) v = v + s_W2[k * 9 + i] * s_W2[k * 9 + j];
+        const double m = wave_max_d(lane < 45 ? fabs(v) : 0.0);
+        v = v * (1.0 / m);
+        __syncthreads();                        // all reads of L^-1 done before s_W2 is reused
+        if (lane < 45) { s_W[i * 9 + j] = v; s_W[j * 9 + i] = v; }
+        __syncthreads();
+    }
+#pragma unroll 1
+    for (int q = 0; q < 3; ++q) {
+        sym_square_scale9(s_W, s_W2, lane);
+        sym_square_scale9(s_W2, s_W, lane);
+    }
+    double Wr[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) Wr[j] = s_W[r * 9 + j];
     double x[9];
     double n0 = 0.0;
 #pragma unroll
@@ -1563,31 +1678,22 @@ __device__ int ls_nullvec9(const double* S, const double* x0, double* f)
     }
     int it = 0;
     for (; it < 32; ++it) {
-        double y[9], z[9];
+        double zi = 0.0;
 #pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            double v = x[i];
+        for (int j = 0; j < 9; ++j) zi = zi + Wr[j] * x[j];
+        double z[9];
 #pragma unroll
-            for (int k = 0; k < i; ++k) v = v - L[i * (i + 1) / 2 + k] * y[k];
-            y[i] = v * invd[i];
-        }
-#pragma unroll
-        for (int i = 8; i >= 0; --i) {
-            double v = y[i];
-#pragma unroll
-            for (int k = i + 1; k < 9; ++k) v = v - L[k * (k + 1) / 2 + i] * z[k];
-            z[i] = v * invd[i];
-        }
+        for (int i = 0; i < 9; ++i) z[i] = shfl_d(zi, i);
         double nn = 0.0, dot = 0.0;
 #pragma unroll
         for (int i = 0; i < 9; ++i) { nn = nn + z[i] * z[i]; dot = dot + z[i] * x[i]; }
         nn = sqrt(nn);
-        double sg = dot < 0.0 ? -1.0 : 1.0;
+        const double rs = (dot < 0.0 ? -1.0 : 1.0) / nn;
         double diff = 0.0;
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
-            double xn = (z[i] / nn) * sg;
-            double dd = fabs(xn - x[i]);
+            const double xn = z[i] * rs;
+            const double dd = fabs(xn - x[i]);
             if (dd > diff) diff = dd;
             x[i] = xn;
         }
@@ -1719,12 +1825,12 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
             float4 o = make_float4((float)p[0], (float)p[1], (float)p[2], (float)p[3]);
             reinterpret_cast<float4*>(d.model_p)[i] = o;
         }
+        double Fb[9], f0[9], f[9];
+        for (int i = 0; i < 9; ++i) Fb[i] = d.hypF[(size_t)bestk * 9 + i];
+        VO_STAMP(d, 1995, 5);
+        warm_start(Fb, sc1, mean[0], mean[1], sc2, mean[2], mean[3], f0);
+        const int its = ls_nullvec9_par(s_A, f0, f, &s_part[0][0], &s_part[9][0], &s_part[18][0]);
         if (tid == 0) {
-            double Fb[9], f0[9], f[9];
-            for (int i = 0; i < 9; ++i) Fb[i] = d.hypF[(size_t)bestk * 9 + i];
-            VO_STAMP(d, 1995, 5);
-            warm_start(Fb, sc1, mean[0], mean[1], sc2, mean[2], mean[3], f0);
-            const int its = ls_nullvec9(s_A, f0, f);
             VO_STAMP(d, 1995, 6);
 #ifdef VO_STAMPS
             if (d.dbg) { d.dbg[1995 * 16 + 14] = (unsigned long long)its; d.dbg[1995 * 16 + 15] = (unsigned long long)n; }
@@ -1832,6 +1938,7 @@ __device__ void finalize_frame(const VoDev& d, VoState* st)
     }
     __syncthreads();
     if (s_mode == VO_MODE_FRAME || s_mode == VO_MODE_MISSING) setup_next_frame(d, st);
+    if (d.seqno) publish_seq(d.ctr + VO_SYNC_POSE, d.seqno);   // the extract queue may reuse slots
 }
 
 // cheirality test of the 4 (R, t) candidates, one thread per (model inlier, candidate)

@@ -225,19 +225,41 @@ static void mm3(const double* A, const double* B, double* C);
 static void mtm3(const double* A, const double* B, double* C);
 
 /* Least-squares null vector of the refit's design matrix: the smallest eigenvector of the
- * 9x9 PSD S = A^T A (Eigen::JacobiSVD V.col(8), ransac.cpp:77-78).  Cholesky S = L L^T with a
- * pivot floor of 1e-15 * max diag (an exactly singular S -- e.g. 8 inliers -- has its null
- * vector as the fixed point), then inverse iteration from the warm start x0 until the unit
- * iterate moves by <= 4e-16 (at most 32 steps).  Same operation order as k_refit. */
+ * 9x9 PSD S = A^T A (Eigen::JacobiSVD V.col(8), ransac.cpp:77-78).
+ *   1. Cholesky S = L L^T with a pivot floor of 1e-15 * max diag (an exactly singular S --
+ *      e.g. 8 inliers -- has its null vector as the dominant direction of S^-1);
+ *   2. W = S^-1 = L^-T L^-1 from the column-wise inverse of L, squared six times to W^64, each
+ *      power scaled by the reciprocal of its largest |entry| (eigenvectors unchanged);
+ *   3. power iteration x <- W64 x / |W64 x| (sign kept towards x) from the warm start x0 until
+ *      the unit iterate moves by <= 4e-16 (at most 32 steps; one step = 64 inverse iterations).
+ * Every entry's sum runs in ascending index order; k_refit computes the same entries lane-
+ * parallel in that order, so the two agree bit for bit. */
+int voo_dbg_nullvec_iters;
+static void sym_scale9(double* W)
+{
+    double m = 0.0;
+    for (int i = 0; i < 81; ++i) if (fabs(W[i]) > m) m = fabs(W[i]);
+    double r = 1.0 / m;
+    for (int i = 0; i < 81; ++i) W[i] = W[i] * r;
+}
+static void sym_square9(const double* A, double* B)   /* B = A A (A symmetric), entry sums k-ascending */
+{
+    for (int i = 0; i < 9; ++i)
+        for (int j = i; j < 9; ++j) {
+            double v = 0.0;
+            for (int k = 0; k < 9; ++k) v = v + A[i * 9 + k] * A[k * 9 + j];
+            B[i * 9 + j] = v; B[j * 9 + i] = v;
+        }
+}
 static void ls_nullvec9(const double* S, const double* x0, double* f)
 {
-    double L[81], invd[9];
+    double L[81], invd[9], Li[81], W[81], W2[81];
     double mx = 0.0;
     for (int i = 0; i < 9; ++i)
         if (S[i * 9 + i] > mx) mx = S[i * 9 + i];
     double fl = 1e-15 * mx;
     if (!(fl > 0.0)) fl = 1e-300;
-    for (int i = 0; i < 81; ++i) L[i] = 0.0;
+    for (int i = 0; i < 81; ++i) { L[i] = 0.0; Li[i] = 0.0; }
     for (int j = 0; j < 9; ++j) {
         double sj = S[j * 9 + j];
         for (int k = 0; k < j; ++k) sj = sj - L[j * 9 + k] * L[j * 9 + k];
@@ -251,37 +273,57 @@ static void ls_nullvec9(const double* S, const double* x0, double* f)
             L[i * 9 + j] = v * invd[j];
         }
     }
+    for (int c = 0; c < 9; ++c) {             /* column c of L^-1 by forward substitution */
+        Li[c * 9 + c] = invd[c];
+        for (int i = c + 1; i < 9; ++i) {
+            double v = 0.0;
+            for (int k = c; k < i; ++k) v = v + L[i * 9 + k] * Li[k * 9 + c];
+            Li[i * 9 + c] = -(v * invd[i]);
+        }
+    }
+    for (int i = 0; i < 9; ++i)               /* W = L^-T L^-1: W_ij = sum_{k>=j} Li_ki Li_kj, i <= j */
+        for (int j = i; j < 9; ++j) {
+            double v = 0.0;
+            for (int k = j; k < 9; ++k) v = v + Li[k * 9 + i] * Li[k * 9 + j];
+            W[i * 9 + j] = v; W[j * 9 + i] = v;
+        }
+    sym_scale9(W);
+    sym_square9(W, W2);
+    sym_scale9(W2);
+    for (int q = 0; q < 3; ++q) {              /* W <- W^64 */
+        sym_square9(W, W2);
+        sym_scale9(W2);
+        sym_square9(W2, W);
+        sym_scale9(W);
+    }
     double x[9];
     double n0 = 0.0;
     for (int i = 0; i < 9; ++i) n0 = n0 + x0[i] * x0[i];
     n0 = sqrt(n0);
     if (n0 > 0.0 && n0 < 1e300) { for (int i = 0; i < 9; ++i) x[i] = x0[i] / n0; }
     else { for (int i = 0; i < 9; ++i) x[i] = 1.0 / 3.0; }
-    for (int it = 0; it < 32; ++it) {
-        double y[9], z[9];
+    int it = 0;
+    for (; it < 32; ++it) {
+        double z[9];
         for (int i = 0; i < 9; ++i) {
-            double v = x[i];
-            for (int k = 0; k < i; ++k) v = v - L[i * 9 + k] * y[k];
-            y[i] = v * invd[i];
-        }
-        for (int i = 8; i >= 0; --i) {
-            double v = y[i];
-            for (int k = i + 1; k < 9; ++k) v = v - L[k * 9 + i] * z[k];
-            z[i] = v * invd[i];
+            double v = 0.0;
+            for (int j = 0; j < 9; ++j) v = v + W[i * 9 + j] * x[j];
+            z[i] = v;
         }
         double nn = 0.0, dot = 0.0;
         for (int i = 0; i < 9; ++i) { nn = nn + z[i] * z[i]; dot = dot + z[i] * x[i]; }
         nn = sqrt(nn);
-        double sg = dot < 0.0 ? -1.0 : 1.0;
+        double r = (dot < 0.0 ? -1.0 : 1.0) / nn;
         double diff = 0.0;
         for (int i = 0; i < 9; ++i) {
-            double xn = (z[i] / nn) * sg;
+            double xn = z[i] * r;
             double dd = fabs(xn - x[i]);
             if (dd > diff) diff = dd;
             x[i] = xn;
         }
-        if (diff <= 4e-16) break;
+        if (diff <= 4e-16) { ++it; break; }
     }
+    voo_dbg_nullvec_iters = it;
     for (int i = 0; i < 9; ++i) f[i] = x[i];
 }
 
