@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <climits>
 #include <map>
 #include <mutex>
@@ -336,8 +337,27 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     d.cand_cap = (uint32_t)ntiles * 256u;
     int rc = VO_OK;
     auto bail = [&](int r) { vo_destroy(c); return r; };
-    if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
-    if (hip_ok(hipStreamCreateWithFlags(&c->se, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
+    // the pose chain is the frame pipeline's critical path: its queue gets the higher
+    // dispatch priority, so the extract queue's wide launches fill in around it
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    const char* cu_env = getenv("VO_CU_POSE");
+    const int cu_pose = cu_env ? atoi(cu_env) : 0;
+    int ncu = 0;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, k.device);
+    if (cu_pose > 0 && cu_pose < ncu && ncu <= 1024) {
+        // experimental: disjoint CU sets for the two queues (CU ids spread evenly)
+        std::vector<uint32_t> mp((ncu + 31) / 32, 0u), me((ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; ++i) {
+            const bool pose = (long)(i + 1) * cu_pose / ncu != (long)i * cu_pose / ncu;
+            (pose ? mp : me)[i >> 5] |= 1u << (i & 31);
+        }
+        if (hip_ok(hipExtStreamCreateWithCUMask(&c->s, (uint32_t)mp.size(), mp.data())) != VO_OK) return bail(VO_ERR_HIP);
+        if (hip_ok(hipExtStreamCreateWithCUMask(&c->se, (uint32_t)me.size(), me.data())) != VO_OK) return bail(VO_ERR_HIP);
+    } else {
+        if (hip_ok(hipStreamCreateWithPriority(&c->s, hipStreamNonBlocking, prio_hi)) != VO_OK) return bail(VO_ERR_HIP);
+        if (hip_ok(hipStreamCreateWithPriority(&c->se, hipStreamNonBlocking, prio_lo)) != VO_OK) return bail(VO_ERR_HIP);
+    }
     d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
     if (d.sel_lds < 0) return bail(VO_ERR_HIP);
     rc |= dalloc(&d.frame_in, (size_t)W * H);

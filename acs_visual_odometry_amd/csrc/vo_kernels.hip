@@ -193,7 +193,7 @@ __device__ void jacobi_eig(double* A, double* V)
 #pragma unroll
             for (int q = p + 1; q < n; ++q) off = off + A[p * n + q] * A[p * n + q];
         }
-        if (off == 0.0 || off <= 1e-30 * dia) break;
+        if (!(off > 1e-30 * dia)) break;   // converged, zero, or NaN input (a degenerate sample)
 #pragma unroll
         for (int p = 0; p < n - 1; ++p) {
 #pragma unroll
@@ -1501,7 +1501,10 @@ __global__ void __launch_bounds__(64) k_ransac_hyp(VoDev d, int k0, int k1, int 
     }
     unsigned* ctr = d.ctr + (k0 == 0 ? 1 : 3);
     if (!arrive_last(ctr, gridDim.x, &s_last)) return;
-    // ---- last workgroup (one wave): replay of ransac.cpp:139-190 over [kk, k1), 64 per step ----
+    VO_STAMP(d, 1997 + (k0 > 0), 0);
+    // ---- last workgroup (one wave): replay of ransac.cpp:139-190 over [kk, k1) ----
+    // 64 hypotheses at a time: their counts and adaptive-table entries are loaded once, then
+    // every improvement inside the window is a ballot + two shuffles (no memory round trip)
     const uint16_t* tab = d.maxit_tab + (size_t)M * (M + 1) / 2;
     int kk, maxit, best, bestk;
     if (k0 == 0) { kk = 0; maxit = d.maxit_initial; best = 0; bestk = -1; }
@@ -1509,20 +1512,25 @@ __global__ void __launch_bounds__(64) k_ransac_hyp(VoDev d, int k0, int k1, int 
     if (maxit > nhyp) maxit = nhyp;
     const int lim = k1;
     while (kk < maxit && kk < lim) {
-        int idx = kk + lane;
-        int c = (idx < maxit && idx < lim) ? ld_sc1(d.counts + idx) : -1;
-        unsigned long long bal = ballot64(c > best);
-        if (bal == 0ull) {
-            kk = min(min(kk + 64, maxit), lim);
-            continue;
+        const int base = kk, idx = base + lane;
+        const int c = idx < lim ? ld_sc1(d.counts + idx) : -1;
+        const int u = c >= 0 ? (int)tab[c] : 0xFFFF;
+        for (;;) {
+            const unsigned long long bal = ballot64(idx >= kk && idx < maxit && idx < lim && c > best);
+            if (bal == 0ull) {
+                kk = min(min(base + 64, maxit), lim);
+                break;
+            }
+            const int j = __ffsll((long long)bal) - 1;
+            best = __shfl(c, j);
+            bestk = base + j;
+            const int uj = __shfl(u, j);
+            if (uj != 0xFFFF) maxit = min(uj, nhyp);
+            kk = bestk + 1;
+            if (!(kk < maxit && kk < lim)) break;
         }
-        int j = __ffsll((long long)bal) - 1;
-        best = __shfl(c, j);
-        bestk = kk + j;
-        uint16_t u = tab[best];
-        if (u != 0xFFFFu) maxit = min((int)u, nhyp);
-        kk = bestk + 1;
     }
+    VO_STAMP(d, 1997 + (k0 > 0), 1);
     if (lane == 0) {
         st->k_done = kk; st->maxit = maxit; st->best = best; st->bestk = bestk;
         st->need_more = kk < maxit ? 1 : 0;
@@ -1567,7 +1575,7 @@ __device__ void pose_prep(const VoDev& d, VoState* st)
 }
 
 // least-squares null vector (mirror of oracle ls_nullvec9): Cholesky with a pivot floor,
-// W = S^-1 from the column-wise inverse of L, six scaled squarings to W^64, then power
+// W = S^-1 from the column-wise inverse of L, six power-of-two-scaled squarings to W^64, then power
 // iteration from the warm start x0.  Called by the whole k_refit workgroup; each wave runs it
 // (wave 1 duplicates wave 0), lanes 0..8 own rows / columns, lanes 0..44 own the upper-
 // triangle entries of the squarings, and every sum runs in the oracle's ascending order.
@@ -1578,23 +1586,27 @@ __constant__ unsigned char c_tri9[45][2] = {
     {3, 3}, {3, 4}, {3, 5}, {3, 6}, {3, 7}, {3, 8}, {4, 4}, {4, 5}, {4, 6}, {4, 7}, {4, 8}, {5, 5},
     {5, 6}, {5, 7}, {5, 8}, {6, 6}, {6, 7}, {6, 8}, {7, 7}, {7, 8}, {8, 8}};
 
-__device__ __forceinline__ double wave_max_d(double v)
+// power of two r with max_i A_ii * r in [0.5, 1) (A symmetric PSD: |A_ij| <= max_i A_ii)
+__device__ __forceinline__ double pow2_scale9(const double* A)
 {
+    double m = 0.0;
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = fmax(v, shfl_xor_d(v, off));
-    return v;
+    for (int i = 0; i < 9; ++i) m = A[i * 9 + i] > m ? A[i * 9 + i] : m;
+    int e;
+    (void)frexp(m, &e);
+    return ldexp(1.0, -e);
 }
 
-// B = A A scaled by 1/max|B_ij| (A, B symmetric 9x9 in LDS); lane e < 45 owns entry c_tri9[e]
-__device__ __forceinline__ void sym_square_scale9(const double* A, double* B, int lane)
+// B = (rA)(rA) with r = pow2_scale9(A) (A, B symmetric 9x9 in LDS); lane e < 45 owns entry
+// c_tri9[e]
+__device__ __forceinline__ void sym_square9(const double* A, double* B, int lane)
 {
+    const double r = pow2_scale9(A);
     const int e = lane < 45 ? lane : 44;
     const int i = c_tri9[e][0], j = c_tri9[e][1];
     double v = 0.0;
 #pragma unroll
-    for (int k = 0; k < 9; ++k) v = v + A[i * 9 + k] * A[k * 9 + j];
-    const double m = wave_max_d(lane < 45 ? fabs(v) : 0.0);
-    v = v * (1.0 / m);
+    for (int k = 0; k < 9; ++k) v = v + (A[i * 9 + k] * r) * (A[k * 9 + j] * r);
     if (lane < 45) { B[i * 9 + j] = v; B[j * 9 + i] = v; }
     __syncthreads();
 }
@@ -1650,16 +1662,14 @@ __device__ int ls_nullvec9_par(const double* S, const double* x0, double* f, dou
         const int i = c_tri9[e][0], j = c_tri9[e][1];
         double v = 0.0;
         for (int k = j; k < 9; ++k) v = v + s_W2[k * 9 + i] * s_W2[k * 9 + j];
-        const double m = wave_max_d(lane < 45 ? fabs(v) : 0.0);
-        v = v * (1.0 / m);
         __syncthreads();                        // all reads of L^-1 done before s_W2 is reused
         if (lane < 45) { s_W[i * 9 + j] = v; s_W[j * 9 + i] = v; }
         __syncthreads();
     }
 #pragma unroll 1
     for (int q = 0; q < 3; ++q) {
-        sym_square_scale9(s_W, s_W2, lane);
-        sym_square_scale9(s_W2, s_W, lane);
+        sym_square9(s_W, s_W2, lane);
+        sym_square9(s_W2, s_W, lane);
     }
     double Wr[9];
 #pragma unroll

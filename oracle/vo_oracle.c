@@ -188,7 +188,7 @@ static void jacobi_eig(double* A, int n, double* V)
             dia = dia + A[p * n + p] * A[p * n + p];
             for (int q = p + 1; q < n; ++q) off = off + A[p * n + q] * A[p * n + q];
         }
-        if (off == 0.0 || off <= 1e-30 * dia) break;
+        if (!(off > 1e-30 * dia)) break;   // converged, zero, or NaN input (a degenerate sample)
         for (int p = 0; p < n - 1; ++p) {
             for (int q = p + 1; q < n; ++q) {
                 double apq = A[p * n + q];
@@ -229,25 +229,29 @@ static void mtm3(const double* A, const double* B, double* C);
  *   1. Cholesky S = L L^T with a pivot floor of 1e-15 * max diag (an exactly singular S --
  *      e.g. 8 inliers -- has its null vector as the dominant direction of S^-1);
  *   2. W = S^-1 = L^-T L^-1 from the column-wise inverse of L, squared six times to W^64, each
- *      power scaled by the reciprocal of its largest |entry| (eigenvectors unchanged);
+ *      power first scaled by the power of two that brings its largest diagonal entry into
+ *      [0.5, 1) (exact; eigenvectors unchanged);
  *   3. power iteration x <- W64 x / |W64 x| (sign kept towards x) from the warm start x0 until
  *      the unit iterate moves by <= 4e-16 (at most 32 steps; one step = 64 inverse iterations).
  * Every entry's sum runs in ascending index order; k_refit computes the same entries lane-
  * parallel in that order, so the two agree bit for bit. */
 int voo_dbg_nullvec_iters;
-static void sym_scale9(double* W)
+/* power of two r with max_i W_ii * r in [0.5, 1): W is symmetric PSD, so |W_ij| <= max_i W_ii,
+ * and scaling by r is exact (the squarings only need it to keep clear of overflow) */
+static double pow2_scale9(const double* W)
 {
     double m = 0.0;
-    for (int i = 0; i < 81; ++i) if (fabs(W[i]) > m) m = fabs(W[i]);
-    double r = 1.0 / m;
-    for (int i = 0; i < 81; ++i) W[i] = W[i] * r;
+    for (int i = 0; i < 9; ++i) if (W[i * 9 + i] > m) m = W[i * 9 + i];
+    int e;
+    (void)frexp(m, &e);
+    return ldexp(1.0, -e);
 }
-static void sym_square9(const double* A, double* B)   /* B = A A (A symmetric), entry sums k-ascending */
+static void sym_square9(const double* A, double r, double* B)   /* B = (rA)(rA), A symmetric, sums k-ascending */
 {
     for (int i = 0; i < 9; ++i)
         for (int j = i; j < 9; ++j) {
             double v = 0.0;
-            for (int k = 0; k < 9; ++k) v = v + A[i * 9 + k] * A[k * 9 + j];
+            for (int k = 0; k < 9; ++k) v = v + (A[i * 9 + k] * r) * (A[k * 9 + j] * r);
             B[i * 9 + j] = v; B[j * 9 + i] = v;
         }
 }
@@ -287,14 +291,9 @@ static void ls_nullvec9(const double* S, const double* x0, double* f)
             for (int k = j; k < 9; ++k) v = v + Li[k * 9 + i] * Li[k * 9 + j];
             W[i * 9 + j] = v; W[j * 9 + i] = v;
         }
-    sym_scale9(W);
-    sym_square9(W, W2);
-    sym_scale9(W2);
     for (int q = 0; q < 3; ++q) {              /* W <- W^64 */
-        sym_square9(W, W2);
-        sym_scale9(W2);
-        sym_square9(W2, W);
-        sym_scale9(W);
+        sym_square9(W, pow2_scale9(W), W2);
+        sym_square9(W2, pow2_scale9(W2), W);
     }
     double x[9];
     double n0 = 0.0;
