@@ -1951,6 +1951,105 @@ __device__ void finalize_frame(const VoDev& d, VoState* st)
     if (d.seqno) publish_seq(d.ctr + VO_SYNC_POSE, d.seqno);   // the extract queue may reuse slots
 }
 
+// smallest right singular vector of the 4x4 triangulation matrix (mirror of oracle nullvec4):
+// dominant eigenvector of adj(A^T A), squared four times with power-of-two scaling, then
+// power-iterated from its largest-diagonal column.  One thread, no divisions but one 1/sqrt.
+__device__ __forceinline__ void cof4_sym(const double* S, double* B)
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = i; j < 4; ++j) {
+            double m[9];
+            int e = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (r == j) continue;
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (c != i) m[e++] = S[r * 4 + c];
+            }
+            double v = det3(m);
+            if ((i + j) & 1) v = -v;
+            B[i * 4 + j] = v; B[j * 4 + i] = v;
+        }
+}
+__device__ __forceinline__ double pow2_scale4(const double* B)
+{
+    double m = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m = B[i * 4 + i] > m ? B[i * 4 + i] : m;
+    int e;
+    (void)frexp(m, &e);
+    return ldexp(1.0, -e);
+}
+__device__ __forceinline__ void nullvec4(const double* A, double* x)
+{
+    double S[16], B[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            S[i * 4 + j] = ((A[0 * 4 + i] * A[0 * 4 + j] + A[1 * 4 + i] * A[1 * 4 + j]) + A[2 * 4 + i] * A[2 * 4 + j]) +
+                           A[3 * 4 + i] * A[3 * 4 + j];
+    cof4_sym(S, B);
+    double bmax = B[0];
+#pragma unroll
+    for (int i = 1; i < 4; ++i) bmax = B[i * 4 + i] > bmax ? B[i * 4 + i] : bmax;
+    if (!(bmax > 0.0)) { x[0] = 0.0; x[1] = 0.0; x[2] = 0.0; x[3] = 1.0; return; }
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) {
+        const double r = pow2_scale4(B);
+        double B2[16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = i; j < 4; ++j) {
+                double v = 0.0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) v = v + (B[i * 4 + t] * r) * (B[t * 4 + j] * r);
+                B2[i * 4 + j] = v; B2[j * 4 + i] = v;
+            }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) B[i] = B2[i];
+    }
+    int k = 0;
+#pragma unroll
+    for (int i = 1; i < 4; ++i) if (B[i * 4 + i] > B[k * 4 + k]) k = i;
+    double y[4], nn = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        double v = B[i * 4 + 0];
+#pragma unroll
+        for (int c = 1; c < 4; ++c) if (c == k) v = B[i * 4 + c];
+        y[i] = v;
+        nn = nn + y[i] * y[i];
+    }
+    const double rn = 1.0 / sqrt(nn);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = y[i] * rn;
+    for (int it = 0; it < 16; ++it) {
+        double z[4], dot = 0.0;
+        nn = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            z[i] = ((B[i * 4 + 0] * x[0] + B[i * 4 + 1] * x[1]) + B[i * 4 + 2] * x[2]) + B[i * 4 + 3] * x[3];
+            nn = nn + z[i] * z[i];
+            dot = dot + z[i] * x[i];
+        }
+        const double rs = (dot < 0.0 ? -1.0 : 1.0) / sqrt(nn);
+        double diff = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const double xn = z[i] * rs;
+            const double dd = fabs(xn - x[i]);
+            if (dd > diff) diff = dd;
+            x[i] = xn;
+        }
+        if (diff <= 4e-16) break;
+    }
+}
+
 // cheirality test of the 4 (R, t) candidates, one thread per (model inlier, candidate)
 // (cv::undistortPoints + cv::triangulatePoints + depth test, PoseUpdate.hpp:101-147);
 // the last workgroup finalizes the frame.  On a skipped frame workgroup 0 finalizes.
@@ -1994,19 +2093,8 @@ __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d)
             A[2 * 4 + k] = X2 * P2[8 + k] - P2[0 + k];
             A[3 * 4 + k] = Y2 * P2[8 + k] - P2[4 + k];
         }
-        double AtA[16], V[16];
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                AtA[a * 4 + b] = ((A[0 * 4 + a] * A[0 * 4 + b] + A[1 * 4 + a] * A[1 * 4 + b]) + A[2 * 4 + a] * A[2 * 4 + b]) +
-                                 A[3 * 4 + a] * A[3 * 4 + b];
-        jacobi_eig<4>(AtA, V);
-        int km = argmin_diag<4>(AtA);
-        double X[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-            if (c == km) { X[0] = V[0 * 4 + c]; X[1] = V[1 * 4 + c]; X[2] = V[2 * 4 + c]; X[3] = V[3 * 4 + c]; }
+        double X[4];
+        nullvec4(A, X);
         double h0 = (double)(float)X[0], h1 = (double)(float)X[1], h2 = (double)(float)X[2], h3 = (double)(float)X[3];
         double w = h3;
         if (!(fabs(w) < 1e-6)) {

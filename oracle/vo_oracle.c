@@ -937,17 +937,83 @@ static void svd3(const double* A, double* U, double* S, double* Vt)
         }
 }
 
-/* smallest right singular vector of a 4x4 A (cv::triangulatePoints' SVD, last row of V^T). */
+/* smallest right singular vector of a 4x4 A (cv::triangulatePoints' SVD, last row of V^T):
+ * the dominant eigenvector of adj(S), S = A^T A (the adjugate of a PSD S has S's
+ * eigenvectors, eigenvalue of the smallest one the largest).  adj(S) is squared four times
+ * (each power first scaled by the power of two bringing its largest diagonal entry into
+ * [0.5, 1)), started from its column with the largest diagonal entry, power-iterated until
+ * the unit iterate moves by <= 4e-16 (at most 16 steps).  k_triangulate runs the same code
+ * per thread.  S of rank <= 2 (adj(S) = 0: no unique point) gives (0,0,0,1), a point that
+ * fails the depth test. */
+static void cof4_sym(const double* S, double* B)   /* B = adj(S), S symmetric: cofactors C_ij, i <= j */
+{
+    for (int i = 0; i < 4; ++i)
+        for (int j = i; j < 4; ++j) {
+            double m[9];
+            int e = 0;
+            for (int r = 0; r < 4; ++r) {
+                if (r == j) continue;              /* adj = C^T: row j, column i of S removed */
+                for (int c = 0; c < 4; ++c)
+                    if (c != i) m[e++] = S[r * 4 + c];
+            }
+            double v = det3(m);
+            if ((i + j) & 1) v = -v;
+            B[i * 4 + j] = v; B[j * 4 + i] = v;
+        }
+}
+static double pow2_scale4(const double* B)
+{
+    double m = 0.0;
+    for (int i = 0; i < 4; ++i) if (B[i * 4 + i] > m) m = B[i * 4 + i];
+    int e;
+    (void)frexp(m, &e);
+    return ldexp(1.0, -e);
+}
 static void nullvec4(const double* A, double* x)
 {
-    double AtA[16], V[16];
+    double S[16], B[16], B2[16];
     for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j)
-            AtA[i * 4 + j] = ((A[0 * 4 + i] * A[0 * 4 + j] + A[1 * 4 + i] * A[1 * 4 + j]) + A[2 * 4 + i] * A[2 * 4 + j]) +
-                             A[3 * 4 + i] * A[3 * 4 + j];
-    jacobi_eig(AtA, 4, V);
-    int k = argmin_diag(AtA, 4);
-    for (int i = 0; i < 4; ++i) x[i] = V[i * 4 + k];
+            S[i * 4 + j] = ((A[0 * 4 + i] * A[0 * 4 + j] + A[1 * 4 + i] * A[1 * 4 + j]) + A[2 * 4 + i] * A[2 * 4 + j]) +
+                           A[3 * 4 + i] * A[3 * 4 + j];
+    cof4_sym(S, B);
+    int k = 0;
+    for (int i = 1; i < 4; ++i) if (B[i * 4 + i] > B[k * 4 + k]) k = i;
+    if (!(B[k * 4 + k] > 0.0)) { x[0] = 0.0; x[1] = 0.0; x[2] = 0.0; x[3] = 1.0; return; }
+    for (int q = 0; q < 4; ++q) {
+        double r = pow2_scale4(B);
+        for (int i = 0; i < 4; ++i)
+            for (int j = i; j < 4; ++j) {
+                double v = 0.0;
+                for (int t = 0; t < 4; ++t) v = v + (B[i * 4 + t] * r) * (B[t * 4 + j] * r);
+                B2[i * 4 + j] = v; B2[j * 4 + i] = v;
+            }
+        memcpy(B, B2, sizeof(B2));
+    }
+    k = 0;
+    for (int i = 1; i < 4; ++i) if (B[i * 4 + i] > B[k * 4 + k]) k = i;
+    double y[4], nn = 0.0;
+    for (int i = 0; i < 4; ++i) { y[i] = B[i * 4 + k]; nn = nn + y[i] * y[i]; }
+    double rn = 1.0 / sqrt(nn);
+    for (int i = 0; i < 4; ++i) x[i] = y[i] * rn;
+    for (int it = 0; it < 16; ++it) {
+        double z[4], dot = 0.0;
+        nn = 0.0;
+        for (int i = 0; i < 4; ++i) {
+            z[i] = ((B[i * 4 + 0] * x[0] + B[i * 4 + 1] * x[1]) + B[i * 4 + 2] * x[2]) + B[i * 4 + 3] * x[3];
+            nn = nn + z[i] * z[i];
+            dot = dot + z[i] * x[i];
+        }
+        double rs = (dot < 0.0 ? -1.0 : 1.0) / sqrt(nn);
+        double diff = 0.0;
+        for (int i = 0; i < 4; ++i) {
+            double xn = z[i] * rs;
+            double dd = fabs(xn - x[i]);
+            if (dd > diff) diff = dd;
+            x[i] = xn;
+        }
+        if (diff <= 4e-16) break;
+    }
 }
 
 /* PoseUpdate::getPose (PoseUpdate.hpp:61-179). p1/p2: n x 2 f32 (cv::Point2f inliers). */
