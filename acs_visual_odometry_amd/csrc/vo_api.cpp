@@ -33,7 +33,15 @@ struct vo_ctx {
     vo_config cfg;
     VoDev d;
     hipStream_t s = nullptr;          // pose chain (and stage APIs)
-    hipStream_t se = nullptr;         // extract stream of the frame pipeline
+    hipStream_t se[VO_EXT_QUEUES] = {};   // extract queues of the frame pipeline
+    struct Scratch {                  // per extract queue (queue 0 uses VoDev's own buffers)
+        uint8_t* blurred = nullptr;
+        uint64_t* cand = nullptr;
+        uint8_t* tilerows = nullptr;
+        uint64_t* ckeys = nullptr;
+        uint64_t* selbits = nullptr;
+        uint32_t* hist = nullptr;
+    } xs[VO_EXT_QUEUES];
     int fidx = 0;                     // frames enqueued since vo_reset
     int max_hyp = VO_MAX_HYP;
     int gt_cap = 0;
@@ -105,9 +113,21 @@ int dalloc(T** p, size_t n)
     return hip_ok(hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T)));
 }
 
+int sync_ext(vo_ctx* c)
+{
+    for (hipStream_t q : c->se)
+        if (q) HIPCHK(hipStreamSynchronize(q));
+    return VO_OK;
+}
+#define SYNC_EXT(c)                        \
+    do {                                   \
+        int _rc = sync_ext(c);             \
+        if (_rc != VO_OK) return _rc;      \
+    } while (0)
+
 int read_state(vo_ctx* c, VoState* h)
 {
-    HIPCHK(hipStreamSynchronize(c->se));
+    SYNC_EXT(c);
     HIPCHK(hipMemcpyAsync(h, c->d.st, sizeof(VoState), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
     return VO_OK;
@@ -121,7 +141,7 @@ int write_state(vo_ctx* c, const VoState* h)
 
 int read_ext(vo_ctx* c, VoExt* h)
 {
-    HIPCHK(hipStreamSynchronize(c->se));
+    SYNC_EXT(c);
     HIPCHK(hipMemcpyAsync(h, c->d.ext, sizeof(VoExt), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
     return VO_OK;
@@ -133,7 +153,7 @@ int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride, hipStream_t st)
     const int W = c->cfg.width, H = c->cfg.height;
     if (stride == 0) stride = (size_t)W;
     HIPCHK(hipStreamSynchronize(c->s));   // staging buffer / frame_in may still be in use
-    HIPCHK(hipStreamSynchronize(c->se));
+    SYNC_EXT(c);
     if (stride == (size_t)W) {
         std::memcpy(c->stage_host, gray, (size_t)W * H);
     } else {
@@ -155,7 +175,7 @@ void enqueue_extract(vo_ctx* c, const uint8_t* dframe, int write_response)
 // histogram / arrival counters the next frame expects) afterwards
 int restore_state(vo_ctx* c, const VoState* saved)
 {
-    HIPCHK(hipMemsetAsync(c->d.hist, 0, sizeof(uint32_t) * VO_HIST_BINS, c->s));
+    HIPCHK(hipMemsetAsync(c->d.hist, 0, sizeof(uint32_t) * VO_HIST_BINS, c->s));   // queue 0's
     HIPCHK(hipMemsetAsync(c->d.ctr, 0, sizeof(unsigned) * VO_CTR_COUNTERS, c->s));
     return write_state(c, saved);
 }
@@ -206,22 +226,32 @@ void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev)
     VoDev d = c->d;
     d.out = out;
     // Cross-queue order by frame counters the kernels publish (describe's last workgroup:
-    // extract done; finalize: pose chain done).  An event record + wait costs ~11-18 us of
-    // queue time per hop on MI355X (tools/evtest.hip); a stream-wait-value packet on a
+    // frame f extracted; finalize: pose chain done).  An event record + wait costs ~11-18 us
+    // of queue time per hop on MI355X (tools/evtest.hip); a stream-wait-value packet on a
     // kernel-written counter ~1-6 us (ROCclr runs it as a small wait kernel); a poll inside
     // the consuming kernel ~1 us.
     const uint32_t seq = (uint32_t)f + 1u;
     d.seqno = seq;
-    // extract stream: frame f-2's pose chain must be done (its slots may be reused, and
-    // finalize(f-2) wrote the prev slot select(f) avoids)
-    if (f >= 2)
-        (void)hipStreamWaitValue32(c->se, c->d.ctr + VO_SYNC_POSE, seq - 2u, hipStreamWaitValueGte, 0xFFFFFFFFu);
+    // extract queue q = f % E with its own scratch; frames on different queues overlap
+    const int q = f % VO_EXT_QUEUES;
+    hipStream_t se = c->se[q];
+    d.eq = q;
+    if (q > 0) {
+        const vo_ctx::Scratch& x = c->xs[q];
+        d.blurred = x.blurred; d.cand = x.cand; d.tilerows = x.tilerows;
+        d.ckeys = x.ckeys; d.selbits = x.selbits; d.hist = x.hist;
+    }
+    // ring slot f % R is read by the pose chains of frames f - R (cur) and f - R + 1 (prev,
+    // or the carry copy finalize(f - R + 1) makes): frame f - R + 1's chain must be done
+    if (f >= VO_RING_SLOTS - 1)
+        (void)hipStreamWaitValue32(se, c->d.ctr + VO_SYNC_POSE, seq - (uint32_t)(VO_RING_SLOTS - 1),
+                                   hipStreamWaitValueGte, 0xFFFFFFFFu);
     if (dframe) {
-        timed(ev, 0, c->se, [&] { vo::launch_stencil(d, dframe, 0, c->se); });
-        timed(ev, 1, c->se, [&] { vo::launch_select(d, f, c->se); });
-        timed(ev, 2, c->se, [&] { vo::launch_describe(d, f, c->se); });
+        timed(ev, 0, se, [&] { vo::launch_stencil(d, dframe, 0, se); });
+        timed(ev, 1, se, [&] { vo::launch_select(d, f, se); });
+        timed(ev, 2, se, [&] { vo::launch_describe(d, f, se); });
     } else {
-        vo::launch_ext_missing(d, f, c->se);
+        vo::launch_ext_missing(d, f, se);
     }
     // the pose queue's wait for this frame's extract is in k_match (wait_seq)
     if (dframe) {
@@ -353,10 +383,12 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
             (pose ? mp : me)[i >> 5] |= 1u << (i & 31);
         }
         if (hip_ok(hipExtStreamCreateWithCUMask(&c->s, (uint32_t)mp.size(), mp.data())) != VO_OK) return bail(VO_ERR_HIP);
-        if (hip_ok(hipExtStreamCreateWithCUMask(&c->se, (uint32_t)me.size(), me.data())) != VO_OK) return bail(VO_ERR_HIP);
+        for (hipStream_t& q : c->se)
+            if (hip_ok(hipExtStreamCreateWithCUMask(&q, (uint32_t)me.size(), me.data())) != VO_OK) return bail(VO_ERR_HIP);
     } else {
         if (hip_ok(hipStreamCreateWithPriority(&c->s, hipStreamNonBlocking, prio_hi)) != VO_OK) return bail(VO_ERR_HIP);
-        if (hip_ok(hipStreamCreateWithPriority(&c->se, hipStreamNonBlocking, prio_lo)) != VO_OK) return bail(VO_ERR_HIP);
+        for (hipStream_t& q : c->se)
+            if (hip_ok(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, prio_lo)) != VO_OK) return bail(VO_ERR_HIP);
     }
     d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
     if (d.sel_lds < 0) return bail(VO_ERR_HIP);
@@ -368,6 +400,15 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc(&d.ckeys, d.cand_cap);
     rc |= dalloc(&d.selbits, d.cand_cap / 64 + 1);
     rc |= dalloc(&d.hist, VO_HIST_BINS);
+    for (int q = 1; q < VO_EXT_QUEUES; ++q) {
+        vo_ctx::Scratch& x = c->xs[q];
+        rc |= dalloc(&x.blurred, (size_t)W * H);
+        rc |= dalloc(&x.cand, d.cand_cap);
+        rc |= dalloc(&x.tilerows, (size_t)ntiles * 16);
+        rc |= dalloc(&x.ckeys, d.cand_cap);
+        rc |= dalloc(&x.selbits, d.cand_cap / 64 + 1);
+        rc |= dalloc(&x.hist, VO_HIST_BINS);
+    }
     for (int s = 0; s < VO_SLOTS; ++s) {
         rc |= dalloc(&d.kps[s], N);
         rc |= dalloc(&d.desc[s], (size_t)N * 8);
@@ -411,7 +452,8 @@ void vo_destroy(vo_ctx* c)
 {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
-    if (c->se) (void)hipStreamSynchronize(c->se);
+    for (hipStream_t q : c->se)
+        if (q) (void)hipStreamSynchronize(q);
     if (c->s) (void)hipStreamSynchronize(c->s);
     VoDev& d = c->d;
     for (int s = 0; s < VO_SLOTS; ++s) {
@@ -424,10 +466,16 @@ void vo_destroy(vo_ctx* c)
                     d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr, d.dbg};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    for (const vo_ctx::Scratch& x : c->xs) {
+        void* xp[] = {x.blurred, x.cand, x.tilerows, x.ckeys, x.selbits, x.hist};
+        for (void* p : xp)
+            if (p) (void)hipFree(p);
+    }
     if (c->out_host) (void)hipHostFree(c->out_host);
     if (c->stage_host) (void)hipHostFree(c->stage_host);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
-    if (c->se) (void)hipStreamDestroy(c->se);
+    for (hipStream_t q : c->se)
+        if (q) (void)hipStreamDestroy(q);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
 }
@@ -436,16 +484,18 @@ int vo_reset(vo_ctx* c)
 {
     if (!c) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    HIPCHK(hipStreamSynchronize(c->se));
+    SYNC_EXT(c);
     VoState h;
     init_state(c, &h);
     int rc = write_state(c, &h);
     if (rc) return rc;
     VoExt e;
     std::memset(&e, 0, sizeof(e));
-    for (int i = 0; i < 4; ++i) { e.slot[i] = -1; e.prev_for[i] = -1; e.status[i] = VO_STATUS_OK; }
+    for (int i = 0; i < VO_EXT_RING; ++i) { e.slot[i] = -1; e.status[i] = VO_STATUS_OK; }
     HIPCHK(hipMemcpyAsync(c->d.ext, &e, sizeof(e), hipMemcpyHostToDevice, c->s));
     HIPCHK(hipMemsetAsync(c->d.hist, 0, sizeof(uint32_t) * VO_HIST_BINS, c->s));
+    for (int q = 1; q < VO_EXT_QUEUES; ++q)
+        HIPCHK(hipMemsetAsync(c->xs[q].hist, 0, sizeof(uint32_t) * VO_HIST_BINS, c->s));
     c->fidx = 0;
     HIPCHK(hipMemsetAsync(c->d.ctr, 0, sizeof(unsigned) * VO_CTR_WORDS, c->s));   // + frame counters
     vo::launch_frame_begin(c->d, VO_MODE_FRAME, c->s);     // frame 0 set up on the device
@@ -519,7 +569,7 @@ int vo_match(vo_ctx* c, const uint64_t* d_prev, int n_prev, const uint64_t* d_cu
     std::vector<uint32_t> p0(n_prev), p1(n_cur);
     for (int i = 0; i < n_prev; ++i) p0[i] = (uint32_t)d_prev[8 * (size_t)i];
     for (int i = 0; i < n_cur; ++i) p1[i] = (uint32_t)d_cur[8 * (size_t)i];
-    HIPCHK(hipStreamSynchronize(c->se));
+    SYNC_EXT(c);
     HIPCHK(hipStreamSynchronize(c->s));
     const int a = VO_STAGE_SLOT, b = VO_STAGE_SLOT + 1;     // stage slots: the trajectory's stay intact
     HIPCHK(hipMemcpy(c->d.desc[a], d_prev, sizeof(uint64_t) * 8 * n_prev, hipMemcpyHostToDevice));
@@ -626,7 +676,7 @@ int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_
     if (!c) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
     if (gray) {
-        int rc = upload_frame(c, gray, stride, c->se);
+        int rc = upload_frame(c, gray, stride, c->se[c->fidx % VO_EXT_QUEUES]);
         if (rc) return rc;
     }
     enqueue_frame(c, gray ? c->d.frame_in : nullptr, c->out_dev, nullptr);

@@ -28,17 +28,23 @@
 #include <stdint.h>
 
 #define VO_HIST_BINS 4096
-#define VO_PIPE_SLOTS 3        // keypoint/descriptor slots of the frame pipeline
-#define VO_STAGE_SLOT 3        // stage APIs (vo_extract / vo_match) use slots 3 and 4
-#define VO_SLOTS 5
-// ctr words: in-launch arrival counters [0, VO_CTR_COUNTERS), then the two cross-queue frame
-// counters on lines of their own (frames whose extract / pose chain is complete, 1-based,
-// read by the other queue's stream-wait-value packet)
+// keypoint/descriptor slots: frame f of the pipeline extracts into ring slot f % VO_RING_SLOTS;
+// a prev that must outlive its ring slot (frames skipped after it) is copied to the carry
+// slot; the stage APIs (vo_extract / vo_match) use their own two slots
+#define VO_RING_SLOTS 8
+#define VO_CARRY_SLOT 8
+#define VO_STAGE_SLOT 9
+#define VO_SLOTS 11
+#define VO_EXT_RING 16         // per-frame extract results, indexed f & (VO_EXT_RING - 1)
+#define VO_EXT_QUEUES 2        // extract queues: frame f on queue f % VO_EXT_QUEUES
+// ctr words: in-launch arrival counters [0, VO_CTR_COUNTERS), then the cross-queue frame
+// counters on lines of their own: the pose chain's (monotonic, read by the extract queues'
+// stream-wait-value packets) and one extract-done word per ring entry (polled by k_match)
 #define VO_CTR_COUNTERS 16
-#define VO_CTR_DESCRIBE 4
-#define VO_SYNC_EXT 32
-#define VO_SYNC_POSE 48
-#define VO_CTR_WORDS 64
+#define VO_CTR_DESCRIBE 4      // + extract queue
+#define VO_SYNC_POSE 48        // frames whose pose chain is complete
+#define VO_SYNC_EXT 64         // + (f & (VO_EXT_RING - 1)): f + 1 once frame f is extracted
+#define VO_CTR_WORDS 96
 #define VO_MAX_HYP 2000
 #define VO_HYP_CHUNK0 256
 #define VO_RED_THREADS 256
@@ -54,13 +60,13 @@ struct VoFrameOut {
     double pose[12];
 };
 
-// Extract-side state.  The extract kernels of frame f+1 run on their own stream while frame
-// f's match -> pose chain runs; they never touch VoState, and the pose chain only reads
-// the ring entries of its own frame here, so the two streams never write the same field.
+// Extract-side state.  The extract kernels of frames f+1, f+2, ... run on their own queues
+// while frame f's match -> pose chain runs; they never touch VoState, and the pose chain only
+// reads the ring entries of its own frame here (the carry copy in finalize reads a slot no
+// extract in flight writes), so the queues never write the same field.
 struct VoExt {
-    int32_t slot[4];       // slot extracted for frame f (ring f & 3), chosen by k_select
-    int32_t status[4];     // VO_STATUS_OK, or VO_STATUS_OVERFLOW (select capacity) for frame f
-    int32_t prev_for[4];   // prev slot of frame f, written by finalize(f-1); -1: none
+    int32_t slot[VO_EXT_RING];    // slot extracted for frame f (ring f & 15); -1: image missing
+    int32_t status[VO_EXT_RING];  // VO_STATUS_OK, or VO_STATUS_OVERFLOW (select capacity)
     int32_t n_kps[VO_SLOTS];
     int32_t stage_status;  // status of the last stage extract (vo_extract)
     int32_t pad[2];
@@ -71,7 +77,7 @@ struct VoState {
     int32_t status;       // VO_STATUS_* of the current frame
     int32_t mode;
     int32_t cur, prev;    // keypoint/descriptor slots: prev always; cur only in stage mode
-                          // (frame mode: VoExt::slot[frame & 3])
+                          // (frame mode: VoExt::slot[frame & (VO_EXT_RING - 1)])
     uint32_t cand_count;
     int32_t M;            // matches
     int32_t scored;       // T * floor(M / T)   (ransac.cpp:152-157)
@@ -133,6 +139,7 @@ struct VoDev {
     unsigned* ctr;        // in-launch arrival counters: [0] match, [1] ransac, [2] triangulate,
                           // [3] ransac chunk 2, [4] describe; cross-queue counters (VO_SYNC_*)
     uint32_t seqno;       // frame pipeline: 1 + frame index since vo_reset; 0 outside it
+    int eq;               // extract queue of this frame (its scratch: blurred .. hist)
     unsigned long long* dbg;   // diagnostic s_memtime stamps (VO_STAMPS builds only)
 };
 

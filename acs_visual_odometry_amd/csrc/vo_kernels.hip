@@ -585,13 +585,13 @@ __device__ __forceinline__ uint32_t sel_bin(uint64_t key, uint32_t thr_bits)
 //   F  each selected key computes its raster position directly and writes its keypoint
 __device__ __forceinline__ int ext_slot(const VoDev& d, int fidx)
 {
-    return fidx < 0 ? VO_STAGE_SLOT : d.ext->slot[fidx & 3];
+    return fidx < 0 ? VO_STAGE_SLOT : fidx % VO_RING_SLOTS;
 }
 
 // the pose chain's current slot: frame mode reads the extract ring, stage mode st->cur
 __device__ __forceinline__ int cur_slot(const VoDev& d, const VoState* st)
 {
-    return st->mode == VO_MODE_FRAME ? d.ext->slot[st->frame & 3] : st->cur;
+    return st->mode == VO_MODE_FRAME ? d.ext->slot[st->frame & (VO_EXT_RING - 1)] : st->cur;
 }
 
 __global__ void __launch_bounds__(1024) k_select(VoDev d, int fidx)
@@ -618,15 +618,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int fidx)
     const size_t TCAP = ST_TW * ST_TH / 4;
     if (tid == 0) {
         s_nbnd = 0; s_b = -1; s_above = 0;
-        // slot for this frame: neither frame f-1's slot nor its prev, the two slots frame
-        // f-1's pose chain (running concurrently) may read; frame f-2's chain is complete
-        int slot = VO_STAGE_SLOT;
-        if (fidx == 0) {
-            slot = 0;
-        } else if (fidx > 0) {
-            const int a = d.ext->slot[(fidx - 1) & 3], bb = d.ext->prev_for[(fidx - 1) & 3];
-            slot = (a != 0 && bb != 0) ? 0 : (a != 1 && bb != 1) ? 1 : 2;
-        }
+        const int slot = ext_slot(d, fidx);    // ring slot f % R (vo_api.cpp enqueue_frame)
         s_slot = slot;
     }
     VO_STAMP(d, 1990, 0);
@@ -866,7 +858,10 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int fidx)
     if (tid == 0) {
         const int status = ovf ? VO_STATUS_OVERFLOW : VO_STATUS_OK;
         d.ext->n_kps[slot] = ovf ? 0 : (C < N ? C : N);
-        if (fidx >= 0) { d.ext->slot[fidx & 3] = slot; d.ext->status[fidx & 3] = status; }
+        if (fidx >= 0) {
+            d.ext->slot[fidx & (VO_EXT_RING - 1)] = slot;
+            d.ext->status[fidx & (VO_EXT_RING - 1)] = status;
+        }
         else d.ext->stage_status = status;
     }
 }
@@ -920,10 +915,10 @@ __device__ __forceinline__ void publish_seq(unsigned* flag, unsigned v)
 __global__ void k_ext_missing(VoDev d, int fidx)
 {
     if (threadIdx.x == 0) {
-        d.ext->slot[fidx & 3] = -1;
-        d.ext->status[fidx & 3] = VO_STATUS_OK;
+        d.ext->slot[fidx & (VO_EXT_RING - 1)] = -1;
+        d.ext->status[fidx & (VO_EXT_RING - 1)] = VO_STATUS_OK;
     }
-    if (d.seqno) publish_seq(d.ctr + VO_SYNC_EXT, d.seqno);
+    if (d.seqno) publish_seq(d.ctr + VO_SYNC_EXT + (fidx & (VO_EXT_RING - 1)), d.seqno);
 }
 
 // ---------------------------------------------------------------------------
@@ -1018,9 +1013,9 @@ __global__ void __launch_bounds__(256) k_describe(VoDev d, int fidx)
     __syncthreads();
     if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __shared__ unsigned s_last;
-    if (!arrive_last(d.ctr + VO_CTR_DESCRIBE, gridDim.x, &s_last)) return;
-    if (threadIdx.x == 0) d.ctr[VO_CTR_DESCRIBE] = 0u;
-    publish_seq(d.ctr + VO_SYNC_EXT, d.seqno);
+    if (!arrive_last(d.ctr + VO_CTR_DESCRIBE + d.eq, gridDim.x, &s_last)) return;
+    if (threadIdx.x == 0) d.ctr[VO_CTR_DESCRIBE + d.eq] = 0u;
+    publish_seq(d.ctr + VO_SYNC_EXT + (fidx & (VO_EXT_RING - 1)), d.seqno);
 }
 
 // next frame's bookkeeping (VisualOdometry.cpp:68-100 loop head): status, slot, sampler
@@ -1098,8 +1093,8 @@ __device__ __forceinline__ void wait_seq(const unsigned* flag, unsigned v)
 __global__ void __launch_bounds__(256) k_match(VoDev d)
 {
     VoState* st = d.st;
-    if (d.seqno) wait_seq(d.ctr + VO_SYNC_EXT, d.seqno);
-    if (st->mode == VO_MODE_FRAME && d.ext->status[st->frame & 3] != VO_STATUS_OK) {
+    if (d.seqno) wait_seq(d.ctr + VO_SYNC_EXT + ((d.seqno - 1u) & (VO_EXT_RING - 1)), d.seqno);
+    if (st->mode == VO_MODE_FRAME && d.ext->status[st->frame & (VO_EXT_RING - 1)] != VO_STATUS_OK) {
         if (blockIdx.x == 0 && threadIdx.x == 0) st->status = VO_STATUS_OVERFLOW;   // select capacity
         return;
     }
@@ -1874,7 +1869,9 @@ __global__ void k_pose_prep(VoDev d)
 // whole workgroup zeroes the next frame's histogram.
 __device__ void finalize_frame(const VoDev& d, VoState* st)
 {
-    __shared__ int s_mode;
+    __shared__ int s_mode, s_copy;
+    if (threadIdx.x == 0) s_copy = -1;
+    __syncthreads();
     if (threadIdx.x == 0) {
         const int status = st->status;
         const int mode = st->mode;
@@ -1927,7 +1924,13 @@ __device__ void finalize_frame(const VoDev& d, VoState* st)
                 st->prev = cur;
             }
             if (status == VO_STATUS_FIRST) { st->prev = cur; st->last_valid = 0; }
-            d.ext->prev_for[(st->frame + 1) & 3] = st->prev;   // the extract stream's slot choice
+            // a skipped frame keeps prev (quirk 10); its ring slot is rewritten R frames on, so
+            // the descriptors move to the carry slot now (rare: one copy per skip run)
+            if (st->prev >= 0 && st->prev < VO_RING_SLOTS && status != VO_STATUS_OK &&
+                status != VO_STATUS_DEGENERATE && status != VO_STATUS_FIRST) {
+                s_copy = st->prev;
+                st->prev = VO_CARRY_SLOT;
+            }
             if (have_pose) {
                 double Trel[16] = {Rf[0], Rf[1], Rf[2], tf[0], Rf[3], Rf[4], Rf[5], tf[1],
                                    Rf[6], Rf[7], Rf[8], tf[2], 0, 0, 0, 1};
@@ -1948,7 +1951,16 @@ __device__ void finalize_frame(const VoDev& d, VoState* st)
     }
     __syncthreads();
     if (s_mode == VO_MODE_FRAME || s_mode == VO_MODE_MISSING) setup_next_frame(d, st);
-    if (d.seqno) publish_seq(d.ctr + VO_SYNC_POSE, d.seqno);   // the extract queue may reuse slots
+    if (s_copy >= 0) {
+        const int src = s_copy, n = d.ext->n_kps[src];
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            d.kps[VO_CARRY_SLOT][i] = d.kps[src][i];
+            d.pre[VO_CARRY_SLOT][i] = d.pre[src][i];
+        }
+        for (int i = threadIdx.x; i < 8 * n; i += blockDim.x) d.desc[VO_CARRY_SLOT][i] = d.desc[src][i];
+        if (threadIdx.x == 0) d.ext->n_kps[VO_CARRY_SLOT] = n;
+    }
+    if (d.seqno) publish_seq(d.ctr + VO_SYNC_POSE, d.seqno);   // the extract queues may reuse slots
 }
 
 // smallest right singular vector of the 4x4 triangulation matrix (mirror of oracle nullvec4):

@@ -272,3 +272,30 @@ def test_skip_few_matches_keeps_previous_descriptors():
         pr, sr, ir = vo.process(frames[f])
         assert sg == sr and np.array_equal(pg, pr) and np.array_equal(ig[:6], ir[:6]), (f, sg, sr, ig, ir)
     ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("blank", [(), tuple(range(10, 21)), (3, 4, 9, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26)])
+def test_pipelined_batch_matches_oracle_across_ring_wraps(blank):
+    """The device batch path runs extract on VO_EXT_QUEUES queues, up to R-1 = 7 frames ahead
+    of the pose chain, over a ring of 8 keypoint/descriptor slots.  40 frames wrap the ring
+    five times; a skip run longer than the ring (blank frames -> < 8 matches) must keep the
+    last good frame's descriptors (quirk 10) through the carry slot."""
+    seq = SceneSequence(nframes=40, step=0.05)
+    frames = seq.frames()
+    for b in blank:
+        frames[b] = 128
+    cfg = O.config(seq.W, seq.H, K=seq.K.reshape(9))
+    vo = O.VO(cfg, gt=seq.gt())
+    ref = [vo.process(frames[f]) for f in range(seq.n)]
+    ctx = Context(seq.W, seq.H, K=seq.K)
+    ctx.set_ground_truth(seq.gt())
+    df = ctx.device_frames(frames)
+    poses, st, info = ctx.process_frames_device(df)
+    for f in range(seq.n):
+        pr, sr, ir = ref[f]
+        assert st[f] == sr, (f, st[f], sr)
+        assert np.array_equal(info[f, :6], ir[:6]), (f, info[f], ir)
+        assert np.array_equal(poses[f], pr), f
+    df.free()
+    ctx.close()
