@@ -420,6 +420,8 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc(&d.hypF, (size_t)c->max_hyp * 9);
     rc |= dalloc(&d.counts, c->max_hyp);
     rc |= dalloc(&d.inl, N);
+    d.mask_words = (N + 63) / 64;
+    rc |= dalloc(&d.inlmask, (size_t)c->max_hyp * d.mask_words);
     rc |= dalloc(&d.model_p, (size_t)N * 4);
     rc |= dalloc(&d.st, 1);
     rc |= dalloc(&d.ext, 1);
@@ -462,7 +464,7 @@ void vo_destroy(vo_ctx* c)
             if (p) (void)hipFree(p);
     }
     void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.tilerows, d.ckeys, d.selbits, d.hist, d.ext,
-                    d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.model_p,
+                    d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.inlmask, d.model_p,
                     d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr, d.dbg};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);

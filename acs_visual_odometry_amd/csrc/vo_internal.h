@@ -130,6 +130,8 @@ struct VoDev {
     double* hypF;
     int32_t* counts;
     int32_t* inl;
+    uint64_t* inlmask;    // per hypothesis: Sampson inlier bits of the scored matches
+    int mask_words;       // (N + 63) / 64
     float* model_p;
     const uint16_t* maxit_tab;
     const double* gt;

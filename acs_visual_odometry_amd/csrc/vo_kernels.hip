@@ -180,55 +180,6 @@ __device__ void sample8(uint64_t seed, int k, int m, int out[8])
 // ---------------------------------------------------------------------------
 // small dense linear algebra (mirror of oracle/vo_oracle.c)
 // ---------------------------------------------------------------------------
-template <int n>
-__device__ void jacobi_eig(double* A, double* V)
-{
-    for (int i = 0; i < n * n; ++i) V[i] = 0.0;
-    for (int i = 0; i < n; ++i) V[i * n + i] = 1.0;
-    for (int sweep = 0; sweep < 50; ++sweep) {
-        double off = 0.0, dia = 0.0;
-#pragma unroll
-        for (int p = 0; p < n; ++p) {
-            dia = dia + A[p * n + p] * A[p * n + p];
-#pragma unroll
-            for (int q = p + 1; q < n; ++q) off = off + A[p * n + q] * A[p * n + q];
-        }
-        if (!(off > 1e-30 * dia)) break;   // converged, zero, or NaN input (a degenerate sample)
-#pragma unroll
-        for (int p = 0; p < n - 1; ++p) {
-#pragma unroll
-            for (int q = p + 1; q < n; ++q) {
-                double apq = A[p * n + q];
-                if (apq == 0.0) continue;
-                double app = A[p * n + p], aqq = A[q * n + q];
-                double theta = (aqq - app) / (2.0 * apq);
-                double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
-                if (theta < 0.0) t = -t;
-                double c = 1.0 / sqrt(t * t + 1.0);
-                double s = t * c;
-                A[p * n + p] = app - t * apq;
-                A[q * n + q] = aqq + t * apq;
-                A[p * n + q] = 0.0;
-                A[q * n + p] = 0.0;
-#pragma unroll
-                for (int k = 0; k < n; ++k) {
-                    if (k == p || k == q) continue;
-                    double akp = A[k * n + p], akq = A[k * n + q];
-                    double nkp = c * akp - s * akq;
-                    double nkq = s * akp + c * akq;
-                    A[k * n + p] = nkp; A[p * n + k] = nkp;
-                    A[k * n + q] = nkq; A[q * n + k] = nkq;
-                }
-#pragma unroll
-                for (int k = 0; k < n; ++k) {
-                    double vkp = V[k * n + p], vkq = V[k * n + q];
-                    V[k * n + p] = c * vkp - s * vkq;
-                    V[k * n + q] = s * vkp + c * vkq;
-                }
-            }
-        }
-    }
-}
 
 template <int n>
 __device__ __forceinline__ int argmin_diag(const double* A)
@@ -268,16 +219,74 @@ __device__ __forceinline__ double det3(const double* M)
            M[2] * (M[3] * M[7] - M[4] * M[6]);
 }
 
+// smallest eigenvector of a 3x3 symmetric PSD S via adj(S) (mirror of oracle min_eigvec3)
+__device__ void min_eigvec3(const double* S, double* v)
+{
+    double B[9];
+    B[0] = S[4] * S[8] - S[5] * S[7];
+    B[4] = S[0] * S[8] - S[2] * S[6];
+    B[8] = S[0] * S[4] - S[1] * S[3];
+    B[1] = -(S[3] * S[8] - S[5] * S[6]); B[3] = B[1];
+    B[2] = S[3] * S[7] - S[4] * S[6];    B[6] = B[2];
+    B[5] = -(S[0] * S[7] - S[1] * S[6]); B[7] = B[5];
+    double bmax = B[0];
+    bmax = B[4] > bmax ? B[4] : bmax;
+    bmax = B[8] > bmax ? B[8] : bmax;
+    if (!(bmax > 0.0)) { v[0] = 0.0; v[1] = 0.0; v[2] = 1.0; return; }
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) {
+        double m = 0.0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) m = B[i * 3 + i] > m ? B[i * 3 + i] : m;
+        int e;
+        (void)frexp(m, &e);
+        const double r = ldexp(1.0, -e);
+        double B2[9];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = i; j < 3; ++j) {
+                const double x = ((B[i * 3 + 0] * r) * (B[0 * 3 + j] * r) + (B[i * 3 + 1] * r) * (B[1 * 3 + j] * r)) +
+                                 (B[i * 3 + 2] * r) * (B[2 * 3 + j] * r);
+                B2[i * 3 + j] = x; B2[j * 3 + i] = x;
+            }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) B[i] = B2[i];
+    }
+    int k = 0;
+#pragma unroll
+    for (int i = 1; i < 3; ++i) if (B[i * 3 + i] > B[k * 3 + k]) k = i;
+    double c0 = B[0], c1 = B[3], c2 = B[6];
+    if (k == 1) { c0 = B[1]; c1 = B[4]; c2 = B[7]; }
+    if (k == 2) { c0 = B[2]; c1 = B[5]; c2 = B[8]; }
+    const double nn = (c0 * c0 + c1 * c1) + c2 * c2;
+    const double rn = 1.0 / sqrt(nn);
+    v[0] = c0 * rn; v[1] = c1 * rn; v[2] = c2 * rn;
+    for (int it = 0; it < 32; ++it) {
+        double z[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) z[i] = (B[i * 3 + 0] * v[0] + B[i * 3 + 1] * v[1]) + B[i * 3 + 2] * v[2];
+        const double zz = (z[0] * z[0] + z[1] * z[1]) + z[2] * z[2];
+        const double dot = (z[0] * v[0] + z[1] * v[1]) + z[2] * v[2];
+        const double rs = (dot < 0.0 ? -1.0 : 1.0) / sqrt(zz);
+        double diff = 0.0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const double xn = z[i] * rs;
+            const double dd = fabs(xn - v[i]);
+            if (dd > diff) diff = dd;
+            v[i] = xn;
+        }
+        if (diff <= 4e-16) break;
+    }
+}
+
 __device__ void rank2(double* F)
 {
-    double FtF[9], V[9];
+    double FtF[9], v[3];
     mtm3(F, F, FtF);
-    jacobi_eig<3>(FtF, V);
-    int k = argmin_diag<3>(FtF);
-    double v0 = 0, v1 = 0, v2 = 0;
-#pragma unroll
-    for (int c = 0; c < 3; ++c)
-        if (c == k) { v0 = V[0 * 3 + c]; v1 = V[1 * 3 + c]; v2 = V[2 * 3 + c]; }
+    min_eigvec3(FtF, v);
+    const double v0 = v[0], v1 = v[1], v2 = v[2];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         double fv = (F[i * 3 + 0] * v0 + F[i * 3 + 1] * v1) + F[i * 3 + 2] * v2;
@@ -1366,17 +1375,22 @@ __device__ __forceinline__ bool sampson_inlier(const double* F, double x, double
     return thr_is_one ? (num < den) : (num / den < thr);
 }
 
-// inliers of F among the first `scored` matches, counted by ballot; loads 4 steps ahead
+// inliers of F among the first `scored` matches, counted by ballot; loads 4 words ahead.
+// WPH waves share a hypothesis: sub-wave sw takes the 64-match words w = sw (mod WPH).  The
+// ballots go to `mask` (bit i = match i), from which k_refit compacts the best set.
+template <int WPH>
 __device__ __forceinline__ int count_inliers(const double* __restrict__ pts, int scored, const double* F,
-                                             double thr, int lane)
+                                             double thr, int lane, int sw, uint64_t* __restrict__ mask)
 {
     const bool one = thr == 1.0;
-    int cnt = 0;
-    for (int b = 0; b < scored; b += 256) {
+    const int nw = (scored + 63) >> 6;
+    int cnt = 0, j = 0;
+    unsigned long long myword = 0ull;            // lane j keeps word sw + WPH * j (scored <= 4096)
+    for (int w0 = sw; w0 < nw; w0 += 4 * WPH) {
         double2 a[4], c[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            int i = b + 64 * u + lane;
+            const int i = (w0 + u * WPH) * 64 + lane;
             if (i < scored) {
                 const double2* p = reinterpret_cast<const double2*>(pts + 4 * (size_t)i);
                 a[u] = p[0]; c[u] = p[1];
@@ -1384,54 +1398,88 @@ __device__ __forceinline__ int count_inliers(const double* __restrict__ pts, int
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            int i = b + 64 * u + lane;
-            bool in = i < scored && sampson_inlier(F, a[u].x, a[u].y, c[u].x, c[u].y, thr, one);
-            cnt += __popcll(ballot64(in));
+            const int i = (w0 + u * WPH) * 64 + lane;
+            const bool in = i < scored && sampson_inlier(F, a[u].x, a[u].y, c[u].x, c[u].y, thr, one);
+            const unsigned long long bal = ballot64(in);
+            myword = lane == j + u ? bal : myword;
+            cnt += __popcll(bal);
         }
+        j += 4;
     }
+    if (sw + WPH * lane < nw) mask[sw + WPH * lane] = myword;
     return cnt;
 }
 
+// SVD of a 3x3 A (mirror of oracle svd3): min_eigvec3 + one 2x2 Jacobi rotation
 __device__ void svd3(const double* A, double* U, double* S, double* Vt)
 {
-    double AtA[9], V[9];
+    double AtA[9], v3[3];
     mtm3(A, A, AtA);
-    jacobi_eig<3>(AtA, V);
-    int o0 = 0, o1 = 1, o2 = 2;
-    // stable insertion sort of {0,1,2} by eigenvalue descending (oracle svd3)
-    double e0 = AtA[0], e1 = AtA[4], e2 = AtA[8];
-    double ev[3] = {e0, e1, e2};
-    int o[3] = {o0, o1, o2};
-    for (int i = 1; i < 3; ++i) {
-        int v = o[i], j = i - 1;
-        while (j >= 0 && ev[o[j]] < ev[v]) { o[j + 1] = o[j]; --j; }
-        o[j + 1] = v;
+    min_eigvec3(AtA, v3);
+    /* orthonormal basis (p, q) of the plane orthogonal to v3: p = e_m x v3 / |.|, m the first
+     * index of the smallest |v3_m|; q = v3 x p */
+    int m = 0;
+    if (fabs(v3[1]) < fabs(v3[m])) m = 1;
+    if (fabs(v3[2]) < fabs(v3[m])) m = 2;
+    double p[3];
+    if (m == 0) { p[0] = 0.0; p[1] = -v3[2]; p[2] = v3[1]; }
+    else if (m == 1) { p[0] = v3[2]; p[1] = 0.0; p[2] = -v3[0]; }
+    else { p[0] = -v3[1]; p[1] = v3[0]; p[2] = 0.0; }
+    const double rp = 1.0 / sqrt((p[0] * p[0] + p[1] * p[1]) + p[2] * p[2]);
+    p[0] = p[0] * rp; p[1] = p[1] * rp; p[2] = p[2] * rp;
+    double q[3] = {v3[1] * p[2] - v3[2] * p[1], v3[2] * p[0] - v3[0] * p[2], v3[0] * p[1] - v3[1] * p[0]};
+    /* the 2x2 restriction of A^T A to that plane, diagonalized by one Jacobi rotation (the
+     * rotation of the classic Jacobi eigenvalue method) */
+    double Sp[3], Sq[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        Sp[i] = (AtA[i * 3 + 0] * p[0] + AtA[i * 3 + 1] * p[1]) + AtA[i * 3 + 2] * p[2];
+        Sq[i] = (AtA[i * 3 + 0] * q[0] + AtA[i * 3 + 1] * q[1]) + AtA[i * 3 + 2] * q[2];
     }
+    const double m00 = (p[0] * Sp[0] + p[1] * Sp[1]) + p[2] * Sp[2];
+    const double m01 = (p[0] * Sq[0] + p[1] * Sq[1]) + p[2] * Sq[2];
+    const double m11 = (q[0] * Sq[0] + q[1] * Sq[1]) + q[2] * Sq[2];
+    double c = 1.0, s = 0.0, t = 0.0;
+    if (m01 != 0.0) {
+        const double theta = (m11 - m00) / (2.0 * m01);
+        t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+        if (theta < 0.0) t = -t;
+        c = 1.0 / sqrt(t * t + 1.0);
+        s = t * c;
+    }
+    const double l1 = m00 - t * m01, l2 = m11 + t * m01;
+    double w1[3], w2[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { w1[i] = c * p[i] - s * q[i]; w2[i] = s * p[i] + c * q[i]; }
+    double V[9];                               /* columns: descending eigenvalue, then v3 */
+    const double* va = l2 > l1 ? w2 : w1;
+    const double* vb = l2 > l1 ? w1 : w2;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { V[i * 3 + 0] = va[i]; V[i * 3 + 1] = vb[i]; V[i * 3 + 2] = v3[i]; }
     double u[3][3];
-    for (int c = 0; c < 2; ++c) {
-        double v0 = V[0 * 3 + o[c]], v1 = V[1 * 3 + o[c]], v2 = V[2 * 3 + o[c]];
+    for (int cc = 0; cc < 2; ++cc) {
+        double v0 = V[0 * 3 + cc], v1 = V[1 * 3 + cc], v2 = V[2 * 3 + cc];
         double a0 = (A[0] * v0 + A[1] * v1) + A[2] * v2;
         double a1 = (A[3] * v0 + A[4] * v1) + A[5] * v2;
         double a2 = (A[6] * v0 + A[7] * v1) + A[8] * v2;
-        double s = sqrt((a0 * a0 + a1 * a1) + a2 * a2);
-        S[c] = s;
-        if (s > 0.0) { u[c][0] = a0 / s; u[c][1] = a1 / s; u[c][2] = a2 / s; }
-        else { u[c][0] = c == 0 ? 1.0 : 0.0; u[c][1] = c == 1 ? 1.0 : 0.0; u[c][2] = 0.0; }
+        double sv = sqrt((a0 * a0 + a1 * a1) + a2 * a2);
+        S[cc] = sv;
+        if (sv > 0.0) { u[cc][0] = a0 / sv; u[cc][1] = a1 / sv; u[cc][2] = a2 / sv; }
+        else { u[cc][0] = cc == 0 ? 1.0 : 0.0; u[cc][1] = cc == 1 ? 1.0 : 0.0; u[cc][2] = 0.0; }
     }
     {
-        double v0 = V[0 * 3 + o[2]], v1 = V[1 * 3 + o[2]], v2 = V[2 * 3 + o[2]];
-        double a0 = (A[0] * v0 + A[1] * v1) + A[2] * v2;
-        double a1 = (A[3] * v0 + A[4] * v1) + A[5] * v2;
-        double a2 = (A[6] * v0 + A[7] * v1) + A[8] * v2;
+        double a0 = (A[0] * v3[0] + A[1] * v3[1]) + A[2] * v3[2];
+        double a1 = (A[3] * v3[0] + A[4] * v3[1]) + A[5] * v3[2];
+        double a2 = (A[6] * v3[0] + A[7] * v3[1]) + A[8] * v3[2];
         S[2] = sqrt((a0 * a0 + a1 * a1) + a2 * a2);
     }
     u[2][0] = u[0][1] * u[1][2] - u[0][2] * u[1][1];
     u[2][1] = u[0][2] * u[1][0] - u[0][0] * u[1][2];
     u[2][2] = u[0][0] * u[1][1] - u[0][1] * u[1][0];
     for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) {
-            U[r * 3 + c] = u[c][r];
-            Vt[c * 3 + r] = V[r * 3 + o[c]];
+        for (int cc = 0; cc < 3; ++cc) {
+            U[r * 3 + cc] = u[cc][r];
+            Vt[cc * 3 + r] = V[r * 3 + cc];
         }
 }
 
@@ -1467,16 +1515,23 @@ __device__ void inv4(const double* M, double* Inv)
         for (int j = 0; j < 4; ++j) Inv[i * 4 + j] = a[i][j + 4];
 }
 
-__global__ void __launch_bounds__(64) k_ransac_hyp(VoDev d, int k0, int k1, int nhyp)
+// HPB hypotheses per workgroup, WPH waves per hypothesis.  First chunk: one hypothesis per
+// 4-wave workgroup (each wave fits the same F, the four split the Sampson count: the latency
+// path); second chunk: four single-wave hypotheses per workgroup, since it usually exits at
+// once (fewer workgroups to dispatch).
+template <int WPH, int HPB>
+__global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, int k1, int nhyp)
 {
     VoState* st = d.st;
     if (st->status != VO_STATUS_OK) return;
     if (k0 > 0 && !st->need_more) return;          // the replay of [0, k0) already stopped
     __shared__ unsigned s_last;
-    const int k = k0 + blockIdx.x;
+    __shared__ int s_cnt[HPB][WPH];
+    const int wave = threadIdx.x >> 6, h = wave / WPH, sw = wave - h * WPH;
+    const int k = k0 + blockIdx.x * HPB + h;
     const int lane = threadIdx.x & 63;
     const int M = st->M, scored = st->scored;
-    {
+    if (k < k1) {
         VO_STAMP(d, k, 0);
         int s8[8];
         sample8(st->frame_seed, k, M, s8);
@@ -1484,18 +1539,33 @@ __global__ void __launch_bounds__(64) k_ransac_hyp(VoDev d, int k0, int k1, int 
         double F[9];
         fit_F8_wave(d, d.pts, s8, lane, F, k);
         VO_STAMP(d, k, 5);
-        if (lane < 9) {
+        if (sw == 0 && lane < 9) {
             double v = 0.0;
 #pragma unroll
             for (int c = 0; c < 9; ++c) if (c == lane) v = F[c];
             d.hypF[(size_t)k * 9 + lane] = v;
         }
-        const int cnt = count_inliers(d.pts, scored, F, d.sampson_thr, lane);
-        if (lane == 0) st_sc1(d.counts + k, cnt);
+        const int cnt =
+            count_inliers<WPH>(d.pts, scored, F, d.sampson_thr, lane, sw, d.inlmask + (size_t)k * d.mask_words);
+        if (WPH == 1) {
+            if (lane == 0) st_sc1(d.counts + k, cnt);
+        } else if (lane == 0) {
+            s_cnt[h][sw] = cnt;
+        }
         VO_STAMP(d, k, 6);
+    }
+    if (WPH > 1) {
+        __syncthreads();
+        if (k < k1 && sw == 0 && lane == 0) {
+            int t = 0;
+#pragma unroll
+            for (int w = 0; w < WPH; ++w) t += s_cnt[h][w];
+            st_sc1(d.counts + k, t);
+        }
     }
     unsigned* ctr = d.ctr + (k0 == 0 ? 1 : 3);
     if (!arrive_last(ctr, gridDim.x, &s_last)) return;
+    if (threadIdx.x >= 64) return;                 // the replay is one wave's
     VO_STAMP(d, 1997 + (k0 > 0), 0);
     // ---- last workgroup (one wave): replay of ransac.cpp:139-190 over [kk, k1) ----
     // 64 hypotheses at a time: their counts and adaptive-table entries are loaded once, then
@@ -1606,9 +1676,10 @@ __device__ __forceinline__ void sym_square9(const double* A, double* B, int lane
     __syncthreads();
 }
 
-__device__ int ls_nullvec9_par(const double* S, const double* x0, double* f, double* s_L, double* s_W,
-                               double* s_W2)
+__device__ int ls_nullvec9_par(const VoDev& d, const double* S, const double* x0, double* f, double* s_L,
+                               double* s_W, double* s_W2)
 {
+    VO_STAMP(d, 1994, 0);
     const int lane = threadIdx.x & 63;
     const int r = lane < 9 ? lane : 8;          // row / column owned by this lane
     double mx = 0.0;
@@ -1623,8 +1694,8 @@ __device__ int ls_nullvec9_par(const double* S, const double* x0, double* f, dou
     for (int j = 0; j < 9; ++j) {
         double v = S[r * 9 + j];
 #pragma unroll
-        for (int k = 0; k < j; ++k) v = v - Lr[k] * shfl_d(Lr[k], j);
-        double sj = shfl_d(v, j);
+        for (int k = 0; k < j; ++k) v = v - Lr[k] * rdlane(Lr[k], j);
+        double sj = rdlane(v, j);
         if (!(sj > fl)) sj = fl;
         const double dj = sqrt(sj);
         invd[j] = 1.0 / dj;
@@ -1635,6 +1706,7 @@ __device__ int ls_nullvec9_par(const double* S, const double* x0, double* f, dou
         for (int k = 0; k < 9; ++k) s_L[lane * 9 + k] = Lr[k];
     }
     __syncthreads();
+    VO_STAMP(d, 1994, 1);
     // column c = r of L^-1 by forward substitution; the k < c terms are exact zeros
     {
         double Li[9];
@@ -1661,11 +1733,13 @@ __device__ int ls_nullvec9_par(const double* S, const double* x0, double* f, dou
         if (lane < 45) { s_W[i * 9 + j] = v; s_W[j * 9 + i] = v; }
         __syncthreads();
     }
+    VO_STAMP(d, 1994, 2);
 #pragma unroll 1
     for (int q = 0; q < 3; ++q) {
         sym_square9(s_W, s_W2, lane);
         sym_square9(s_W2, s_W, lane);
     }
+    VO_STAMP(d, 1994, 3);
     double Wr[9];
 #pragma unroll
     for (int j = 0; j < 9; ++j) Wr[j] = s_W[r * 9 + j];
@@ -1688,7 +1762,7 @@ __device__ int ls_nullvec9_par(const double* S, const double* x0, double* f, dou
         for (int j = 0; j < 9; ++j) zi = zi + Wr[j] * x[j];
         double z[9];
 #pragma unroll
-        for (int i = 0; i < 9; ++i) z[i] = shfl_d(zi, i);
+        for (int i = 0; i < 9; ++i) z[i] = rdlane(zi, i);
         double nn = 0.0, dot = 0.0;
 #pragma unroll
         for (int i = 0; i < 9; ++i) { nn = nn + z[i] * z[i]; dot = dot + z[i] * x[i]; }
@@ -1706,6 +1780,7 @@ __device__ int ls_nullvec9_par(const double* S, const double* x0, double* f, dou
     }
 #pragma unroll
     for (int i = 0; i < 9; ++i) f[i] = x[i];
+    VO_STAMP(d, 1994, 4);
     return it;
 }
 
@@ -1720,8 +1795,10 @@ __device__ __forceinline__ void warm_start(const double* Fb, double s1, double m
 }
 
 #define RF_T 128
+#define RF_PCAP 2048     // inlier points staged in LDS as f64 (beyond: read from HBM)
 // one sum over the refit threads in the oracle's order (red_finish): per-thread partials
-// -> LDS -> thread e sums the RF_T partials of quantity e sequentially
+// -> LDS -> thread e sums the RF_T partials of quantity e as 8 sequential chains of 16,
+// combined pairwise
 template <int NS>
 __device__ __forceinline__ void refit_sums(const double (&part)[NS], double (*s_part)[RF_T + 1], double* s_out)
 {
@@ -1730,11 +1807,28 @@ __device__ __forceinline__ void refit_sums(const double (&part)[NS], double (*s_
     for (int e = 0; e < NS; ++e) s_part[e][tid] = part[e];
     __syncthreads();
     if (tid < NS) {
-        double s = 0.0;
-        for (int t = 0; t < RF_T; ++t) s = s + s_part[tid][t];
-        s_out[tid] = s;
+        double c[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) c[j] = 0.0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) c[j] = c[j] + s_part[tid][16 * j + t];
+        s_out[tid] = ((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7]));
     }
     __syncthreads();
+}
+
+// inlier point i of the refit: LDS for i < RF_PCAP, HBM beyond
+__device__ __forceinline__ void refit_pt(const double2* s_p, const VoDev& d, int i, double* p)
+{
+    double2 a, b;
+    if (i < RF_PCAP) { a = s_p[2 * i]; b = s_p[2 * i + 1]; }
+    else {
+        const double2* g = reinterpret_cast<const double2*>(d.pts + 4 * (size_t)d.inl[i]);
+        a = g[0]; b = g[1];
+    }
+    p[0] = a.x; p[1] = a.y; p[2] = b.x; p[3] = b.y;
 }
 
 __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
@@ -1745,41 +1839,50 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
     __shared__ double s_sum[45];
     __shared__ double s_A[81];
     __shared__ int s_n;
+    __shared__ double2 s_p[2 * RF_PCAP];
+    __shared__ uint64_t s_w[64];
+    __shared__ int s_woff[64];
     const int tid = threadIdx.x, lane = tid & 63;
     const int bestk = st->bestk;
     const int scored = st->scored;
     VO_STAMP(d, 1995, 0);
-    if (tid < 64) {                       // wave 0: ordered inlier compaction
-        int n = 0;
-        if (bestk >= 0) {
-            double F[9];
+    // ordered compaction of the best hypothesis' inliers from its Sampson mask (written by
+    // k_ransac_hyp with the same F and test): word offsets by a wave scan, then every thread
+    // places its bits; the points are staged in LDS for the three passes below
+    const int nw = bestk >= 0 ? (scored + 63) >> 6 : 0;
+    if (tid < 64) {
+        const uint64_t w = lane < nw ? d.inlmask[(size_t)bestk * d.mask_words + lane] : 0ull;
+        const int c = __popcll(w);
+        int x = c;
 #pragma unroll
-            for (int c = 0; c < 9; ++c) F[c] = d.hypF[(size_t)bestk * 9 + c];
-            const double thr = d.sampson_thr;
-            const bool one = thr == 1.0;
-            for (int b0 = 0; b0 < scored; b0 += 64) {
-                int i = b0 + lane;
-                bool in = false;
-                if (i < scored) {
-                    const double* p = d.pts + 4 * (size_t)i;
-                    in = sampson_inlier(F, p[0], p[1], p[2], p[3], thr, one);
-                }
-                unsigned long long bal = ballot64(in);
-                if (in) d.inl[n + __popcll(bal & ((1ull << lane) - 1ull))] = i;
-                n += __popcll(bal);
-            }
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(x, off);
+            if (lane >= off) x += y;
         }
-        if (lane == 0) { s_n = n; st->n_inl = n; }
+        s_w[lane] = w;
+        s_woff[lane] = x - c;
+        if (lane == 63) { s_n = x; st->n_inl = x; }
     }
-    __threadfence_block();
     __syncthreads();
     VO_STAMP(d, 1995, 1);
     const int n = s_n;
+    for (int i = tid; i < nw * 64; i += RF_T) {
+        const uint64_t w = s_w[i >> 6];
+        if ((w >> (i & 63)) & 1ull) {
+            const int pos = s_woff[i >> 6] + __popcll(w & ((1ull << (i & 63)) - 1ull));
+            const double2* g = reinterpret_cast<const double2*>(d.pts + 4 * (size_t)i);
+            const double2 a = g[0], b = g[1];
+            if (pos < RF_PCAP) { s_p[2 * pos] = a; s_p[2 * pos + 1] = b; }
+            d.inl[pos] = i;
+            reinterpret_cast<float4*>(d.model_p)[pos] = make_float4((float)a.x, (float)a.y, (float)b.x, (float)b.y);
+        }
+    }
+    __syncthreads();
     if (bestk >= 0 && n >= 8) {
-        const int32_t* idx = d.inl;
         double pm[4] = {0.0, 0.0, 0.0, 0.0};
         for (int i = tid; i < n; i += RF_T) {
-            const double* p = d.pts + 4 * (size_t)idx[i];
+            double p[4];
+            refit_pt(s_p, d, i, p);
 #pragma unroll
             for (int c = 0; c < 4; ++c) pm[c] = pm[c] + p[c];
         }
@@ -1790,7 +1893,8 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
         for (int c = 0; c < 4; ++c) mean[c] = s_sum[c] / (double)n;
         double ps[2] = {0.0, 0.0};
         for (int i = tid; i < n; i += RF_T) {
-            const double* p = d.pts + 4 * (size_t)idx[i];
+            double p[4];
+            refit_pt(s_p, d, i, p);
 #pragma unroll
             for (int g = 0; g < 2; ++g) {
                 double a = p[2 * g] - mean[2 * g], b = p[2 * g + 1] - mean[2 * g + 1];
@@ -1806,7 +1910,8 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
 #pragma unroll
         for (int e = 0; e < 45; ++e) acc[e] = 0.0;
         for (int i = tid; i < n; i += RF_T) {
-            const double* p = d.pts + 4 * (size_t)idx[i];
+            double p[4];
+            refit_pt(s_p, d, i, p);
             double a[9];
             design_row(sc1 * p[0] + o1x, sc1 * p[1] + o1y, sc2 * p[2] + o2x, sc2 * p[3] + o2y, a);
             int e = 0;
@@ -1825,16 +1930,11 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
             s_A[v * 9 + u] = s_sum[tid];
         }
         __syncthreads();
-        for (int i = tid; i < n; i += RF_T) {
-            const double* p = d.pts + 4 * (size_t)idx[i];
-            float4 o = make_float4((float)p[0], (float)p[1], (float)p[2], (float)p[3]);
-            reinterpret_cast<float4*>(d.model_p)[i] = o;
-        }
         double Fb[9], f0[9], f[9];
         for (int i = 0; i < 9; ++i) Fb[i] = d.hypF[(size_t)bestk * 9 + i];
         VO_STAMP(d, 1995, 5);
         warm_start(Fb, sc1, mean[0], mean[1], sc2, mean[2], mean[3], f0);
-        const int its = ls_nullvec9_par(s_A, f0, f, &s_part[0][0], &s_part[9][0], &s_part[18][0]);
+        const int its = ls_nullvec9_par(d, s_A, f0, f, &s_part[0][0], &s_part[9][0], &s_part[18][0]);
         if (tid == 0) {
             VO_STAMP(d, 1995, 6);
 #ifdef VO_STAMPS
@@ -1870,35 +1970,59 @@ __global__ void k_pose_prep(VoDev d)
 __device__ void finalize_frame(const VoDev& d, VoState* st)
 {
     __shared__ int s_mode, s_copy;
-    if (threadIdx.x == 0) s_copy = -1;
+    __shared__ VoState sv;                 // snapshot: one round of parallel loads, not a chain
+    __shared__ double s_gt[24];
+    __shared__ int s_cur, s_ncur;
+    {
+        // agent-scope loads: counts4 arrived by atomics from the other workgroups
+        const int nwd = (int)(sizeof(VoState) / 8);
+        for (int i = threadIdx.x; i < nwd; i += blockDim.x)
+            reinterpret_cast<unsigned long long*>(&sv)[i] = __hip_atomic_load(
+                reinterpret_cast<unsigned long long*>(st) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) s_copy = -1;
+    }
+    __syncthreads();
+    {
+        const int fi = sv.frame, last = sv.last_valid;
+        const bool want_gt = sv.mode == VO_MODE_FRAME && sv.status == VO_STATUS_OK && d.gt_n > 0 && fi < d.gt_n &&
+                             last < d.gt_n;
+        const int t = threadIdx.x;
+        if (want_gt && t < 24) s_gt[t] = d.gt[12 * (size_t)(t < 12 ? fi : last) + (t < 12 ? t : t - 12)];
+        if (t == 32) {
+            const int cur = sv.mode == VO_MODE_FRAME ? d.ext->slot[fi & (VO_EXT_RING - 1)] : sv.cur;
+            s_cur = cur;
+            s_ncur = cur >= 0 ? d.ext->n_kps[cur] : 0;
+        }
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int status = st->status;
-        const int mode = st->mode;
+        const int status = sv.status;
+        const int mode = sv.mode;
         s_mode = mode;
-        double* Tc = st->Tcurr;
+        double Tc[16];
+        for (int i = 0; i < 16; ++i) Tc[i] = sv.Tcurr[i];
         double Rf[9], tf[3];
         bool have_pose = false;
         if (status == VO_STATUS_OK) {
             int maxPos = -1, bestc = 0;
             for (int c = 0; c < 4; ++c) {
-                int v = __hip_atomic_load((gi32*)&st->counts4[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int v = sv.counts4[c];
                 if (v > maxPos) { maxPos = v; bestc = c; }
             }
-            const double* R = bestc < 2 ? st->R1 : st->R2;
+            const double* R = bestc < 2 ? sv.R1 : sv.R2;
             double sg = (bestc & 1) ? -1.0 : 1.0;
             for (int i = 0; i < 9; ++i) Rf[i] = R[i];
             if (det3(Rf) < 0) for (int i = 0; i < 9; ++i) Rf[i] = -Rf[i];
-            tf[0] = st->t[0] * sg; tf[1] = st->t[1] * sg; tf[2] = st->t[2] * sg;
-            double scale = st->scale_override;
+            tf[0] = sv.t[0] * sg; tf[1] = sv.t[1] * sg; tf[2] = sv.t[2] * sg;
+            double scale = sv.scale_override;
             if (mode == VO_MODE_FRAME) {
                 scale = 1.0;
-                const int fi = st->frame, last = st->last_valid;
+                const int fi = sv.frame, last = sv.last_valid;
                 if (d.gt_n > 0 && fi < d.gt_n && last < d.gt_n) {
                     double Gi[16], Gl[16], Ii[16], Tr[16];
                     for (int r = 0; r < 16; ++r) {
-                        Gi[r] = r < 12 ? d.gt[12 * (size_t)fi + r] : (r == 15 ? 1.0 : 0.0);
-                        Gl[r] = r < 12 ? d.gt[12 * (size_t)last + r] : (r == 15 ? 1.0 : 0.0);
+                        Gi[r] = r < 12 ? s_gt[r] : (r == 15 ? 1.0 : 0.0);
+                        Gl[r] = r < 12 ? s_gt[12 + r] : (r == 15 ? 1.0 : 0.0);
                     }
                     inv4(Gi, Ii);
                     mm4(Ii, Gl, Tr);
@@ -1918,35 +2042,38 @@ __device__ void finalize_frame(const VoDev& d, VoState* st)
             VoFrameOut* o = d.out;
             int flip = 1;
             if (status == VO_STATUS_FIRST || status == VO_STATUS_MISSING) flip = 0;
-            const int cur = cur_slot(d, st);
+            const int cur = s_cur;
+            int prev = sv.prev;
             if (status == VO_STATUS_OK || status == VO_STATUS_DEGENERATE) {
-                st->last_valid = st->frame;      // VisualOdometry.cpp:161-166 precede getPose
-                st->prev = cur;
+                st->last_valid = sv.frame;      // VisualOdometry.cpp:161-166 precede getPose
+                prev = cur;
             }
-            if (status == VO_STATUS_FIRST) { st->prev = cur; st->last_valid = 0; }
+            if (status == VO_STATUS_FIRST) { prev = cur; st->last_valid = 0; }
             // a skipped frame keeps prev (quirk 10); its ring slot is rewritten R frames on, so
             // the descriptors move to the carry slot now (rare: one copy per skip run)
-            if (st->prev >= 0 && st->prev < VO_RING_SLOTS && status != VO_STATUS_OK &&
-                status != VO_STATUS_DEGENERATE && status != VO_STATUS_FIRST) {
-                s_copy = st->prev;
-                st->prev = VO_CARRY_SLOT;
+            if (prev >= 0 && prev < VO_RING_SLOTS && status != VO_STATUS_OK && status != VO_STATUS_DEGENERATE &&
+                status != VO_STATUS_FIRST) {
+                s_copy = prev;
+                prev = VO_CARRY_SLOT;
             }
+            st->prev = prev;
             if (have_pose) {
                 double Trel[16] = {Rf[0], Rf[1], Rf[2], tf[0], Rf[3], Rf[4], Rf[5], tf[1],
                                    Rf[6], Rf[7], Rf[8], tf[2], 0, 0, 0, 1};
                 mm4(Tc, Trel, Tc);
+                for (int i = 0; i < 16; ++i) st->Tcurr[i] = Tc[i];
             }
             for (int r = 0; r < 3; ++r)
                 for (int c = 0; c < 4; ++c) o->pose[r * 4 + c] = (flip && r == 2) ? -Tc[r * 4 + c] : Tc[r * 4 + c];
             o->status = status;
-            o->n_kps = status == VO_STATUS_MISSING ? 0 : d.ext->n_kps[cur];
-            o->n_matches = st->M;
-            o->n_inl = st->n_inl;
-            o->best_k = st->bestk;
-            o->n_eval = st->n_eval;
-            o->fitted = st->fitted;
-            o->frame = st->frame;
-            st->frame = st->frame + 1;
+            o->n_kps = status == VO_STATUS_MISSING ? 0 : s_ncur;
+            o->n_matches = sv.M;
+            o->n_inl = sv.n_inl;
+            o->best_k = sv.bestk;
+            o->n_eval = sv.n_eval;
+            o->fitted = sv.fitted;
+            o->frame = sv.frame;
+            st->frame = sv.frame + 1;
         }
     }
     __syncthreads();
@@ -2211,8 +2338,9 @@ void launch_match(const VoDev& d, hipStream_t s)
 void launch_ransac(const VoDev& d, int nhyp, hipStream_t s)
 {
     const int k0 = nhyp < VO_HYP_CHUNK0 ? nhyp : VO_HYP_CHUNK0;
-    hipLaunchKernelGGL(k_ransac_hyp, dim3(k0), dim3(64), 0, s, d, 0, k0, nhyp);
-    if (nhyp > k0) hipLaunchKernelGGL(k_ransac_hyp, dim3(nhyp - k0), dim3(64), 0, s, d, k0, nhyp, nhyp);
+    hipLaunchKernelGGL((k_ransac_hyp<4, 1>), dim3(k0), dim3(256), 0, s, d, 0, k0, nhyp);
+    if (nhyp > k0)
+        hipLaunchKernelGGL((k_ransac_hyp<1, 4>), dim3((nhyp - k0 + 3) / 4), dim3(256), 0, s, d, k0, nhyp, nhyp);
 }
 void launch_refit(const VoDev& d, int with_pose, hipStream_t s)
 {

@@ -176,50 +176,6 @@ int voo_ransac_maxit_update(int best, int n, double prob)
 /* small dense linear algebra (f64, fixed operation order)                      */
 /* ========================================================================== */
 
-/* Cyclic Jacobi eigen-decomposition of a symmetric n x n matrix (n <= 9).
- * A is overwritten (eigenvalues on the diagonal), V receives eigenvectors as columns. */
-static void jacobi_eig(double* A, int n, double* V)
-{
-    for (int i = 0; i < n * n; ++i) V[i] = 0.0;
-    for (int i = 0; i < n; ++i) V[i * n + i] = 1.0;
-    for (int sweep = 0; sweep < 50; ++sweep) {
-        double off = 0.0, dia = 0.0;
-        for (int p = 0; p < n; ++p) {
-            dia = dia + A[p * n + p] * A[p * n + p];
-            for (int q = p + 1; q < n; ++q) off = off + A[p * n + q] * A[p * n + q];
-        }
-        if (!(off > 1e-30 * dia)) break;   // converged, zero, or NaN input (a degenerate sample)
-        for (int p = 0; p < n - 1; ++p) {
-            for (int q = p + 1; q < n; ++q) {
-                double apq = A[p * n + q];
-                if (apq == 0.0) continue;
-                double app = A[p * n + p], aqq = A[q * n + q];
-                double theta = (aqq - app) / (2.0 * apq);
-                double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
-                if (theta < 0.0) t = -t;
-                double c = 1.0 / sqrt(t * t + 1.0);
-                double s = t * c;
-                A[p * n + p] = app - t * apq;
-                A[q * n + q] = aqq + t * apq;
-                A[p * n + q] = 0.0;
-                A[q * n + p] = 0.0;
-                for (int k = 0; k < n; ++k) {
-                    if (k == p || k == q) continue;
-                    double akp = A[k * n + p], akq = A[k * n + q];
-                    double nkp = c * akp - s * akq;
-                    double nkq = s * akp + c * akq;
-                    A[k * n + p] = nkp; A[p * n + k] = nkp;
-                    A[k * n + q] = nkq; A[q * n + k] = nkq;
-                }
-                for (int k = 0; k < n; ++k) {
-                    double vkp = V[k * n + p], vkq = V[k * n + q];
-                    V[k * n + p] = c * vkp - s * vkq;
-                    V[k * n + q] = s * vkp + c * vkq;
-                }
-            }
-        }
-    }
-}
 
 static void mm3(const double* A, const double* B, double* C);
 static void mtm3(const double* A, const double* B, double* C);
@@ -338,13 +294,6 @@ static void warm_start(const double* Fb, double s1, double mx1, double my1, doub
     mm3(G, T1i, f0);
 }
 
-static int argmin_diag(const double* A, int n)
-{
-    int b = 0;
-    for (int i = 1; i < n; ++i)
-        if (A[i * n + i] < A[b * n + b]) b = i;
-    return b;
-}
 
 /* C = A(3x3) * B(3x3), sums in k order. */
 static void mm3(const double* A, const double* B, double* C)
@@ -369,14 +318,67 @@ static double det3(const double* M)
            M[2] * (M[3] * M[7] - M[4] * M[6]);
 }
 
-/* Rank-2 projection F <- U diag(s1,s2,0) V^T == F (I - v3 v3^T)  (ransac.cpp:87-90). */
+/* Unit eigenvector of the smallest eigenvalue of a 3x3 symmetric PSD S: the dominant
+ * eigenvector of adj(S) (eigenvalues l2 l3, l1 l3, l1 l2), squared four times (each power
+ * first scaled by the power of two bringing its largest diagonal entry into [0.5, 1)),
+ * started from its largest-diagonal column and power-iterated until the unit iterate moves
+ * by <= 4e-16 (at most 32 steps).  adj(S) = 0 (rank <= 1) gives e3. */
+static void min_eigvec3(const double* S, double* v)
+{
+    double B[9], B2[9];
+    B[0] = S[4] * S[8] - S[5] * S[7];
+    B[4] = S[0] * S[8] - S[2] * S[6];
+    B[8] = S[0] * S[4] - S[1] * S[3];
+    B[1] = -(S[3] * S[8] - S[5] * S[6]); B[3] = B[1];
+    B[2] = S[3] * S[7] - S[4] * S[6];    B[6] = B[2];
+    B[5] = -(S[0] * S[7] - S[1] * S[6]); B[7] = B[5];
+    int k = 0;
+    for (int i = 1; i < 3; ++i) if (B[i * 3 + i] > B[k * 3 + k]) k = i;
+    if (!(B[k * 3 + k] > 0.0)) { v[0] = 0.0; v[1] = 0.0; v[2] = 1.0; return; }
+    for (int q = 0; q < 4; ++q) {
+        double m = 0.0;
+        for (int i = 0; i < 3; ++i) if (B[i * 3 + i] > m) m = B[i * 3 + i];
+        int e;
+        (void)frexp(m, &e);
+        double r = ldexp(1.0, -e);
+        for (int i = 0; i < 3; ++i)
+            for (int j = i; j < 3; ++j) {
+                double x = ((B[i * 3 + 0] * r) * (B[0 * 3 + j] * r) + (B[i * 3 + 1] * r) * (B[1 * 3 + j] * r)) +
+                           (B[i * 3 + 2] * r) * (B[2 * 3 + j] * r);
+                B2[i * 3 + j] = x; B2[j * 3 + i] = x;
+            }
+        memcpy(B, B2, sizeof(B2));
+    }
+    k = 0;
+    for (int i = 1; i < 3; ++i) if (B[i * 3 + i] > B[k * 3 + k]) k = i;
+    double nn = (B[0 * 3 + k] * B[0 * 3 + k] + B[1 * 3 + k] * B[1 * 3 + k]) + B[2 * 3 + k] * B[2 * 3 + k];
+    double rn = 1.0 / sqrt(nn);
+    for (int i = 0; i < 3; ++i) v[i] = B[i * 3 + k] * rn;
+    for (int it = 0; it < 32; ++it) {
+        double z[3];
+        for (int i = 0; i < 3; ++i) z[i] = (B[i * 3 + 0] * v[0] + B[i * 3 + 1] * v[1]) + B[i * 3 + 2] * v[2];
+        double zz = (z[0] * z[0] + z[1] * z[1]) + z[2] * z[2];
+        double dot = (z[0] * v[0] + z[1] * v[1]) + z[2] * v[2];
+        double rs = (dot < 0.0 ? -1.0 : 1.0) / sqrt(zz);
+        double diff = 0.0;
+        for (int i = 0; i < 3; ++i) {
+            double xn = z[i] * rs;
+            double dd = fabs(xn - v[i]);
+            if (dd > diff) diff = dd;
+            v[i] = xn;
+        }
+        if (diff <= 4e-16) break;
+    }
+}
+
+/* Rank-2 projection F <- U diag(s1,s2,0) V^T == F (I - v3 v3^T)  (ransac.cpp:87-90), v3 the
+ * smallest eigenvector of F^T F (min_eigvec3). */
 static void rank2(double* F)
 {
-    double FtF[9], V[9];
+    double FtF[9], v[3];
     mtm3(F, F, FtF);
-    jacobi_eig(FtF, 3, V);
-    int k = argmin_diag(FtF, 3);
-    double v0 = V[0 * 3 + k], v1 = V[1 * 3 + k], v2 = V[2 * 3 + k];
+    min_eigvec3(FtF, v);
+    double v0 = v[0], v1 = v[1], v2 = v[2];
     for (int i = 0; i < 3; ++i) {
         double fv = (F[i * 3 + 0] * v0 + F[i * 3 + 1] * v1) + F[i * 3 + 2] * v2;
         F[i * 3 + 0] = F[i * 3 + 0] - fv * v0;
@@ -443,15 +445,19 @@ static void nullvec_8x9(double M[8][9], double f[9])
 }
 
 /* Fixed-order parallel sum used by the device refit (128 threads): thread t accumulates
- * elements t, t+128, ... in order; the total is the sequential sum of the 128 partials in
- * thread order.  The oracle reproduces that order so refit outputs compare bit for bit. */
+ * elements t, t+128, ... in order; the total sums the 128 partials in thread order as 8
+ * sequential chains of 16, combined pairwise.  The oracle reproduces that order so refit
+ * outputs compare bit for bit. */
 #define VOO_RED_THREADS 128
 typedef struct { double v[VOO_RED_THREADS]; } red256;
 static double red_finish(red256* r)
 {
-    double s = 0.0;
-    for (int t = 0; t < VOO_RED_THREADS; ++t) s = s + r->v[t];
-    return s;
+    double c[8];
+    for (int j = 0; j < 8; ++j) {
+        c[j] = 0.0;
+        for (int t = 0; t < 16; ++t) c[j] = c[j] + r->v[16 * j + t];
+    }
+    return ((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7]));
 }
 
 /* ========================================================================== */
@@ -897,43 +903,75 @@ int voo_ransac(const double* pts, int m, double prob, double thr, int T, uint64_
 /* pose                                                                         */
 /* ========================================================================== */
 
-/* 3x3 SVD A = U diag(S) V^T, S descending, via Jacobi on A^T A; u2 = u0 x u1. */
+/* SVD of a 3x3 A (cv::SVD::compute of E, PoseUpdate.hpp:75-77): v3 = the smallest
+ * eigenvector of A^T A (min_eigvec3), the other two from one 2x2 Jacobi rotation in the plane
+ * orthogonal to v3; u_i = A v_i / s_i (i = 1, 2), u3 = u1 x u2.  Same code as k_refit. */
 static void svd3(const double* A, double* U, double* S, double* Vt)
 {
-    double AtA[9], V[9];
+    double AtA[9], v3[3];
     mtm3(A, A, AtA);
-    jacobi_eig(AtA, 3, V);
-    int o[3] = {0, 1, 2};
-    for (int i = 1; i < 3; ++i) {            /* stable insertion sort, eigenvalue descending */
-        int v = o[i], j = i - 1;
-        while (j >= 0 && AtA[o[j] * 3 + o[j]] < AtA[v * 3 + v]) { o[j + 1] = o[j]; --j; }
-        o[j + 1] = v;
+    min_eigvec3(AtA, v3);
+    /* orthonormal basis (p, q) of the plane orthogonal to v3: p = e_m x v3 / |.|, m the first
+     * index of the smallest |v3_m|; q = v3 x p */
+    int m = 0;
+    if (fabs(v3[1]) < fabs(v3[m])) m = 1;
+    if (fabs(v3[2]) < fabs(v3[m])) m = 2;
+    double p[3];
+    if (m == 0) { p[0] = 0.0; p[1] = -v3[2]; p[2] = v3[1]; }
+    else if (m == 1) { p[0] = v3[2]; p[1] = 0.0; p[2] = -v3[0]; }
+    else { p[0] = -v3[1]; p[1] = v3[0]; p[2] = 0.0; }
+    const double rp = 1.0 / sqrt((p[0] * p[0] + p[1] * p[1]) + p[2] * p[2]);
+    p[0] = p[0] * rp; p[1] = p[1] * rp; p[2] = p[2] * rp;
+    double q[3] = {v3[1] * p[2] - v3[2] * p[1], v3[2] * p[0] - v3[0] * p[2], v3[0] * p[1] - v3[1] * p[0]};
+    /* the 2x2 restriction of A^T A to that plane, diagonalized by one Jacobi rotation (the
+     * rotation of the classic Jacobi eigenvalue method) */
+    double Sp[3], Sq[3];
+    for (int i = 0; i < 3; ++i) {
+        Sp[i] = (AtA[i * 3 + 0] * p[0] + AtA[i * 3 + 1] * p[1]) + AtA[i * 3 + 2] * p[2];
+        Sq[i] = (AtA[i * 3 + 0] * q[0] + AtA[i * 3 + 1] * q[1]) + AtA[i * 3 + 2] * q[2];
     }
+    const double m00 = (p[0] * Sp[0] + p[1] * Sp[1]) + p[2] * Sp[2];
+    const double m01 = (p[0] * Sq[0] + p[1] * Sq[1]) + p[2] * Sq[2];
+    const double m11 = (q[0] * Sq[0] + q[1] * Sq[1]) + q[2] * Sq[2];
+    double c = 1.0, s = 0.0, t = 0.0;
+    if (m01 != 0.0) {
+        const double theta = (m11 - m00) / (2.0 * m01);
+        t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+        if (theta < 0.0) t = -t;
+        c = 1.0 / sqrt(t * t + 1.0);
+        s = t * c;
+    }
+    const double l1 = m00 - t * m01, l2 = m11 + t * m01;
+    double w1[3], w2[3];
+    for (int i = 0; i < 3; ++i) { w1[i] = c * p[i] - s * q[i]; w2[i] = s * p[i] + c * q[i]; }
+    double V[9];                               /* columns: descending eigenvalue, then v3 */
+    const double* va = l2 > l1 ? w2 : w1;
+    const double* vb = l2 > l1 ? w1 : w2;
+    for (int i = 0; i < 3; ++i) { V[i * 3 + 0] = va[i]; V[i * 3 + 1] = vb[i]; V[i * 3 + 2] = v3[i]; }
     double u[3][3];
-    for (int c = 0; c < 2; ++c) {
-        double v0 = V[0 * 3 + o[c]], v1 = V[1 * 3 + o[c]], v2 = V[2 * 3 + o[c]];
+    for (int cc = 0; cc < 2; ++cc) {
+        double v0 = V[0 * 3 + cc], v1 = V[1 * 3 + cc], v2 = V[2 * 3 + cc];
         double a0 = (A[0] * v0 + A[1] * v1) + A[2] * v2;
         double a1 = (A[3] * v0 + A[4] * v1) + A[5] * v2;
         double a2 = (A[6] * v0 + A[7] * v1) + A[8] * v2;
-        double s = sqrt((a0 * a0 + a1 * a1) + a2 * a2);
-        S[c] = s;
-        if (s > 0.0) { u[c][0] = a0 / s; u[c][1] = a1 / s; u[c][2] = a2 / s; }
-        else { u[c][0] = c == 0 ? 1.0 : 0.0; u[c][1] = c == 1 ? 1.0 : 0.0; u[c][2] = 0.0; }
+        double sv = sqrt((a0 * a0 + a1 * a1) + a2 * a2);
+        S[cc] = sv;
+        if (sv > 0.0) { u[cc][0] = a0 / sv; u[cc][1] = a1 / sv; u[cc][2] = a2 / sv; }
+        else { u[cc][0] = cc == 0 ? 1.0 : 0.0; u[cc][1] = cc == 1 ? 1.0 : 0.0; u[cc][2] = 0.0; }
     }
     {
-        double v0 = V[0 * 3 + o[2]], v1 = V[1 * 3 + o[2]], v2 = V[2 * 3 + o[2]];
-        double a0 = (A[0] * v0 + A[1] * v1) + A[2] * v2;
-        double a1 = (A[3] * v0 + A[4] * v1) + A[5] * v2;
-        double a2 = (A[6] * v0 + A[7] * v1) + A[8] * v2;
+        double a0 = (A[0] * v3[0] + A[1] * v3[1]) + A[2] * v3[2];
+        double a1 = (A[3] * v3[0] + A[4] * v3[1]) + A[5] * v3[2];
+        double a2 = (A[6] * v3[0] + A[7] * v3[1]) + A[8] * v3[2];
         S[2] = sqrt((a0 * a0 + a1 * a1) + a2 * a2);
     }
     u[2][0] = u[0][1] * u[1][2] - u[0][2] * u[1][1];
     u[2][1] = u[0][2] * u[1][0] - u[0][0] * u[1][2];
     u[2][2] = u[0][0] * u[1][1] - u[0][1] * u[1][0];
     for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) {
-            U[r * 3 + c] = u[c][r];
-            Vt[c * 3 + r] = V[r * 3 + o[c]];
+        for (int cc = 0; cc < 3; ++cc) {
+            U[r * 3 + cc] = u[cc][r];
+            Vt[cc * 3 + r] = V[r * 3 + cc];
         }
 }
 

@@ -14,7 +14,7 @@ import numpy as np
 
 
 def short(n):
-    m = re.match(r"(?:vo::)?(\w+)", n)
+    m = re.match(r"(?:void\s+)?(?:vo::)?(\w+)", n)
     return m.group(1) if m else n
 
 
