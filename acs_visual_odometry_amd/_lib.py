@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("VO_LIB_PATH") or os.path.join(_HERE, "libvo_mi355x.so
 VO_OK = 0
 VO_ERR_DEGENERATE_E = -10
 STATUS = {0: "OK", 1: "FIRST", 2: "MISSING", 3: "FEW_MATCHES", 4: "FEW_INLIERS", 5: "DEGENERATE",
-          6: "OVERFLOW"}
+          6: "OVERFLOW", 7: "STALLED"}
 
 # every symbol include/vo_mi355x.h declares (checked by tests/test_abi.py)
 EXPORTS = [

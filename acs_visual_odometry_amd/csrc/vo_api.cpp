@@ -43,6 +43,7 @@ struct vo_ctx {
         uint32_t* hist = nullptr;
     } xs[VO_EXT_QUEUES];
     int fidx = 0;                     // frames enqueued since vo_reset
+    uint32_t ext_ready = 0;           // extract seq the last enqueued finalize waits for
     int max_hyp = VO_MAX_HYP;
     int gt_cap = 0;
     VoFrameOut* out_dev = nullptr;
@@ -219,7 +220,8 @@ void timed(EvRec* ev, int k, hipStream_t st, F&& launch)
     }
 }
 
-void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev)
+// more: the caller enqueues frame f+1 right after this one (the batch path)
+void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev, bool more)
 {
     const int f = c->fidx++;
     if (ev) ev->frame = f;
@@ -253,7 +255,16 @@ void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev)
     } else {
         vo::launch_ext_missing(d, f, se);
     }
-    // the pose queue's wait for this frame's extract is in k_match (wait_seq)
+    // The pose queue needs frame f's extract before k_match.  Inside a batch the previous
+    // frame's finalize (one workgroup) waited for it at its end, so k_match starts behind a
+    // kernel boundary with the descriptors in place; otherwise a stream-wait-value packet.
+    // (A poll inside k_match itself can deadlock: 250 spinning workgroups can hold the CUs
+    // the extract's single 1024-thread select workgroup needs.)
+    if (c->ext_ready != seq)
+        (void)hipStreamWaitValue32(c->s, c->d.ctr + VO_SYNC_EXT + (f & (VO_EXT_RING - 1)), seq, hipStreamWaitValueGte,
+                                   0xFFFFFFFFu);
+    d.wait_next = more ? seq + 1u : 0u;
+    c->ext_ready = d.wait_next;
     if (dframe) {
         timed(ev, 3, c->s, [&] { vo::launch_match(d, c->s); });
         timed(ev, 4, c->s, [&] { vo::launch_ransac(d, c->max_hyp, c->s); });
@@ -367,10 +378,9 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     d.cand_cap = (uint32_t)ntiles * 256u;
     int rc = VO_OK;
     auto bail = [&](int r) { vo_destroy(c); return r; };
-    // the pose chain is the frame pipeline's critical path: its queue gets the higher
-    // dispatch priority, so the extract queue's wide launches fill in around it
-    int prio_lo = 0, prio_hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    // no stream priorities: k_match waits inside the kernel for the extract queue, and a
+    // high-priority queue spinning on low-priority work can starve it (observed: the wait ran
+    // into its timeout when 250 match workgroups were pending at high priority)
     const char* cu_env = getenv("VO_CU_POSE");
     const int cu_pose = cu_env ? atoi(cu_env) : 0;
     int ncu = 0;
@@ -386,9 +396,9 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
         for (hipStream_t& q : c->se)
             if (hip_ok(hipExtStreamCreateWithCUMask(&q, (uint32_t)me.size(), me.data())) != VO_OK) return bail(VO_ERR_HIP);
     } else {
-        if (hip_ok(hipStreamCreateWithPriority(&c->s, hipStreamNonBlocking, prio_hi)) != VO_OK) return bail(VO_ERR_HIP);
+        if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
         for (hipStream_t& q : c->se)
-            if (hip_ok(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, prio_lo)) != VO_OK) return bail(VO_ERR_HIP);
+            if (hip_ok(hipStreamCreateWithFlags(&q, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
     }
     d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
     if (d.sel_lds < 0) return bail(VO_ERR_HIP);
@@ -499,6 +509,7 @@ int vo_reset(vo_ctx* c)
     for (int q = 1; q < VO_EXT_QUEUES; ++q)
         HIPCHK(hipMemsetAsync(c->xs[q].hist, 0, sizeof(uint32_t) * VO_HIST_BINS, c->s));
     c->fidx = 0;
+    c->ext_ready = 0;
     HIPCHK(hipMemsetAsync(c->d.ctr, 0, sizeof(unsigned) * VO_CTR_WORDS, c->s));   // + frame counters
     vo::launch_frame_begin(c->d, VO_MODE_FRAME, c->s);     // frame 0 set up on the device
     HIPCHK(hipGetLastError());
@@ -681,7 +692,7 @@ int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_
         int rc = upload_frame(c, gray, stride, c->se[c->fidx % VO_EXT_QUEUES]);
         if (rc) return rc;
     }
-    enqueue_frame(c, gray ? c->d.frame_in : nullptr, c->out_dev, nullptr);
+    enqueue_frame(c, gray ? c->d.frame_in : nullptr, c->out_dev, nullptr, false);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->out_host, c->out_dev, sizeof(VoFrameOut), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
@@ -705,7 +716,8 @@ int vo_process_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
     if (rc) return rc;
     EvRec rec{&c->ev_pool, 0, c->timing >= 100 ? c->timing - 100 : -1, 0, {}};
     EvRec* evp = c->timing ? &rec : nullptr;
-    for (int f = 0; f < nframes; ++f) enqueue_frame(c, d_frames + (size_t)f * frame_bytes, c->out_dev + f, evp);
+    for (int f = 0; f < nframes; ++f)
+        enqueue_frame(c, d_frames + (size_t)f * frame_bytes, c->out_dev + f, evp, f + 1 < nframes);
     HIPCHK(hipGetLastError());
     if (nframes)
         HIPCHK(hipMemcpyAsync(c->out_host, c->out_dev, sizeof(VoFrameOut) * nframes, hipMemcpyDeviceToHost, c->s));

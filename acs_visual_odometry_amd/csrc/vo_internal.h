@@ -141,6 +141,7 @@ struct VoDev {
     unsigned* ctr;        // in-launch arrival counters: [0] match, [1] ransac, [2] triangulate,
                           // [3] ransac chunk 2, [4] describe; cross-queue counters (VO_SYNC_*)
     uint32_t seqno;       // frame pipeline: 1 + frame index since vo_reset; 0 outside it
+    uint32_t wait_next;   // finalize then waits for this frame's extract (seqno + 1), or 0
     int eq;               // extract queue of this frame (its scratch: blurred .. hist)
     unsigned long long* dbg;   // diagnostic s_memtime stamps (VO_STAMPS builds only)
 };

@@ -1029,10 +1029,9 @@ __global__ void __launch_bounds__(256) k_describe(VoDev d, int fidx)
 
 // next frame's bookkeeping (VisualOdometry.cpp:68-100 loop head): status, slot, sampler
 // seed, counters, histogram.  Run by the workgroup that finalizes the current frame.
-__device__ void setup_next_frame(const VoDev& d, VoState* st)
+__device__ void setup_next_frame(const VoDev& d, VoState* st, int f)
 {
     if (threadIdx.x == 0) {
-        const int f = st->frame;        // already incremented
         st->mode = VO_MODE_FRAME;
         st->status = f == 0 ? VO_STATUS_FIRST : VO_STATUS_OK;
         st->frame_seed = mix64(d.seed + 0x632BE59BD9B4E019ULL * (uint64_t)(f + 1));
@@ -1074,35 +1073,41 @@ __device__ __forceinline__ int ratio_accept(uint32_t m1, uint32_t m2, float rati
 
 // 32-bit prefix mode: the cur frame's prefixes are staged once per workgroup in LDS
 // (16 KB at N = 4096), and each wave scores MT_QPW queries per candidate read.
-#define MT_QPW 4
+#define MT_QPW 2
 #define MT_QPB (4 * MT_QPW)
 __host__ __device__ inline int match_blocks(int N, int match_bits)
 {
     return match_bits == 32 ? (N + MT_QPB - 1) / MT_QPB : (N + 3) / 4;
 }
 
-// frame pipeline: wait in-kernel for describe's counter (a ROCclr stream-wait-value packet
-// costs a ~5 us wait kernel on the critical queue).  Lane 0 polls with write-through loads,
-// then an agent-scope acquire + barrier before any load of extract-stream data.  The extract
-// queue never waits on this launch (it waits only for frame f-2's pose chain, which precedes
-// it on this queue), so the poll always ends; the bound only guards against a broken pipeline.
-__device__ __forceinline__ void wait_seq(const unsigned* flag, unsigned v)
+// Frame pipeline: one workgroup waits for the extract queue's counter of the next frame
+// (finalize_frame, at the end of the previous frame's chain), so k_match always starts behind
+// a kernel boundary.  Lane 0 polls, then an agent-scope acquire + barrier.  The extract of
+// frame f+1 waits only for frame f-6's chain, long complete, so the poll ends; the bound
+// (~1 s) only guards against a broken pipeline: the caller then marks the frame STALLED.
+__device__ __forceinline__ bool wait_seq(unsigned* flag, unsigned v)
 {
+    __shared__ int s_ok;
     if (threadIdx.x == 0) {
+        int ok = 0;
         for (unsigned spin = 0; spin < (1u << 24); ++spin) {
-            if (__hip_atomic_load((const gu32*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= v) break;
+            // an atomic read-modify-write, not a load: a polled line can stay cached in this
+            // XCD's L2 and miss the producer's write-through store from another XCD
+            if (__hip_atomic_fetch_or((gu32*)flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= v) { ok = 1; break; }
             __builtin_amdgcn_s_sleep(2);
         }
+        s_ok = ok;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+    return s_ok != 0;
 }
 
 __global__ void __launch_bounds__(256) k_match(VoDev d)
 {
     VoState* st = d.st;
-    if (d.seqno) wait_seq(d.ctr + VO_SYNC_EXT + ((d.seqno - 1u) & (VO_EXT_RING - 1)), d.seqno);
+    if (blockIdx.x == 0) VO_STAMP(d, 1993, 0);
     if (st->mode == VO_MODE_FRAME && d.ext->status[st->frame & (VO_EXT_RING - 1)] != VO_STATUS_OK) {
         if (blockIdx.x == 0 && threadIdx.x == 0) st->status = VO_STATUS_OVERFLOW;   // select capacity
         return;
@@ -1166,6 +1171,7 @@ __global__ void __launch_bounds__(256) k_match(VoDev d)
             if (lane == 0) st_sc1(d.match_j + q, ratio_accept(m1, m2, d.ratio));
         }
     }
+    if (blockIdx.x == 0) VO_STAMP(d, 1993, 1);
     if (!arrive_last(d.ctr + 0, gridDim.x, &s_last)) return;
     // ---- last workgroup: ordered compaction, thread t owns queries [t*per, (t+1)*per) ----
     const int tid = threadIdx.x, wave = tid >> 6;
@@ -1173,13 +1179,21 @@ __global__ void __launch_bounds__(256) k_match(VoDev d)
     const int2* kp2 = d.kps[cur];
     const int per = (n1 + 255) / 256;            // <= 16 (N <= 4096)
     const int q0 = tid * per;
+    VO_STAMP(d, 1993, 2);
     int js[16];
+    int2 ka[16], kb[16];
     int cnt = 0;
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
         int i = q0 + u;
         js[u] = (u < per && i < n1) ? ld_sc1(d.match_j + i) : -1;
         cnt += js[u] >= 0;
+    }
+    // all keypoint gathers in flight before the scan (no load-use chain per match)
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        ka[u] = make_int2(0, 0); kb[u] = make_int2(0, 0);
+        if (js[u] >= 0) { ka[u] = kp1[q0 + u]; kb[u] = kp2[js[u]]; }
     }
     // block exclusive scan of cnt (wave inclusive scan + wave totals)
     int incl = cnt;
@@ -1197,7 +1211,7 @@ __global__ void __launch_bounds__(256) k_match(VoDev d)
         if (js[u] >= 0) {
             int i = q0 + u, j = js[u];
             d.match_pairs[pos] = make_int2(i, j);
-            int2 a = kp1[i], b = kp2[j];
+            const int2 a = ka[u], b = kb[u];
             double2* p = reinterpret_cast<double2*>(d.pts + 4 * (size_t)pos);
             p[0] = make_double2((double)a.x, (double)a.y);
             p[1] = make_double2((double)b.x, (double)b.y);
@@ -1211,6 +1225,7 @@ __global__ void __launch_bounds__(256) k_match(VoDev d)
         if (M < 8) st->status = VO_STATUS_FEW_MATCHES;
         d.ctr[0] = 0u;
     }
+    VO_STAMP(d, 1993, 3);
 }
 
 // ---------------------------------------------------------------------------
@@ -1972,7 +1987,7 @@ __device__ void finalize_frame(const VoDev& d, VoState* st)
     __shared__ int s_mode, s_copy;
     __shared__ VoState sv;                 // snapshot: one round of parallel loads, not a chain
     __shared__ double s_gt[24];
-    __shared__ int s_cur, s_ncur;
+    __shared__ int s_cur, s_ncur, s_next;
     {
         // agent-scope loads: counts4 arrived by atomics from the other workgroups
         const int nwd = (int)(sizeof(VoState) / 8);
@@ -2074,10 +2089,11 @@ __device__ void finalize_frame(const VoDev& d, VoState* st)
             o->fitted = sv.fitted;
             o->frame = sv.frame;
             st->frame = sv.frame + 1;
+            s_next = sv.frame + 1;
         }
     }
     __syncthreads();
-    if (s_mode == VO_MODE_FRAME || s_mode == VO_MODE_MISSING) setup_next_frame(d, st);
+    if (s_mode == VO_MODE_FRAME || s_mode == VO_MODE_MISSING) setup_next_frame(d, st, s_next);
     if (s_copy >= 0) {
         const int src = s_copy, n = d.ext->n_kps[src];
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -2087,7 +2103,21 @@ __device__ void finalize_frame(const VoDev& d, VoState* st)
         for (int i = threadIdx.x; i < 8 * n; i += blockDim.x) d.desc[VO_CARRY_SLOT][i] = d.desc[src][i];
         if (threadIdx.x == 0) d.ext->n_kps[VO_CARRY_SLOT] = n;
     }
-    if (d.seqno) publish_seq(d.ctr + VO_SYNC_POSE, d.seqno);   // the extract queues may reuse slots
+    // the extract queues may now rewrite the ring slots this chain read.  They read nothing
+    // the chain wrote, so the counter needs no release of data (no L2 write-back on the
+    // critical path): every load of this workgroup (the carry copy) has returned, then one
+    // write-through store the command processor reads from memory
+    if (d.seqno) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store((gu32*)(d.ctr + VO_SYNC_POSE), d.seqno, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // the next frame's k_match follows this kernel: hold it until that frame's descriptors
+    // are published (one workgroup spinning cannot starve the extract queues)
+    if (d.wait_next && !wait_seq(d.ctr + VO_SYNC_EXT + ((d.wait_next - 1u) & (VO_EXT_RING - 1)), d.wait_next)) {
+        if (threadIdx.x == 0 && st->status == VO_STATUS_OK) st->status = VO_STATUS_STALLED;
+    }
 }
 
 // smallest right singular vector of the 4x4 triangulation matrix (mirror of oracle nullvec4):

@@ -46,6 +46,7 @@ extern "C" {
 #define VO_STATUS_FEW_INLIERS   4   /* < 8 model inliers (:147-153)                  */
 #define VO_STATUS_DEGENERATE    5   /* getPose threw (countNonZero(E) < 5)           */
 #define VO_STATUS_OVERFLOW      6   /* top-N boundary bin exceeded the LDS select buffer */
+#define VO_STATUS_STALLED       7   /* frame pipeline: this frame's extract never signalled */
 
 typedef struct vo_ctx vo_ctx;
 

@@ -17,7 +17,7 @@ ctx = Context(seq.W, seq.H, K=seq.K)
 ctx.set_ground_truth(seq.gt())
 L = load()
 L.vo_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
-rows_r, rows_t, rows_n = [], [], []
+rows_r, rows_t, rows_n, rows_m = [], [], [], []
 for f in range(seq.n):
     _, st, info = ctx.process_frame(fr[f])
     buf = np.zeros(2000 * 16, np.uint64)
@@ -29,6 +29,8 @@ for f in range(seq.n):
         rows_t.append(np.diff(t[:4]))
         nv = buf[1994 * 16:1994 * 16 + 16].astype(np.int64)
         rows_n.append(np.diff(nv[:5]))
+        mt = buf[1993 * 16:1993 * 16 + 16].astype(np.int64)
+        rows_m.append(np.diff(mt[:4]))
 R = np.array(rows_r)
 T = np.array(rows_t)
 names = ["compaction", "means", "spread", "moments", "modelp+sync", "nullvec9", "denorm+rank2", "pose_prep"]
@@ -41,3 +43,5 @@ print("k_triangulate (block 0): cheirality", int(np.median(T[:, 0])), " arrive",
       " finalize", int(np.median(T[:, 2])))
 NV = np.median(np.array(rows_n), axis=0)
 print("nullvec9 phases: cholesky", int(NV[0]), " inverse+W", int(NV[1]), " squarings", int(NV[2]), " power", int(NV[3]))
+MT = np.median(np.array(rows_m), axis=0)
+print("k_match (block 0 / last block): scoring", int(MT[0]), " arrive", int(MT[1]), " compaction", int(MT[2]))
