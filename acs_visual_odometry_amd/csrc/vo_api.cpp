@@ -44,6 +44,8 @@ struct vo_ctx {
     } xs[VO_EXT_QUEUES];
     int fidx = 0;                     // frames enqueued since vo_reset
     uint32_t ext_ready = 0;           // extract seq the last enqueued finalize waits for
+    bool serial = false;              // VO_SERIAL=1: every kernel on one queue, no cross-queue
+                                      // waits (for profilers that serialize dispatches: PMC passes)
     int max_hyp = VO_MAX_HYP;
     int gt_cap = 0;
     VoFrameOut* out_dev = nullptr;
@@ -236,7 +238,7 @@ void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev,
     d.seqno = seq;
     // extract queue q = f % E with its own scratch; frames on different queues overlap
     const int q = f % VO_EXT_QUEUES;
-    hipStream_t se = c->se[q];
+    hipStream_t se = c->serial ? c->s : c->se[q];
     d.eq = q;
     if (q > 0) {
         const vo_ctx::Scratch& x = c->xs[q];
@@ -245,7 +247,7 @@ void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev,
     }
     // ring slot f % R is read by the pose chains of frames f - R (cur) and f - R + 1 (prev,
     // or the carry copy finalize(f - R + 1) makes): frame f - R + 1's chain must be done
-    if (f >= VO_RING_SLOTS - 1)
+    if (f >= VO_RING_SLOTS - 1 && !c->serial)
         (void)hipStreamWaitValue32(se, c->d.ctr + VO_SYNC_POSE, seq - (uint32_t)(VO_RING_SLOTS - 1),
                                    hipStreamWaitValueGte, 0xFFFFFFFFu);
     if (dframe) {
@@ -260,10 +262,10 @@ void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev,
     // kernel boundary with the descriptors in place; otherwise a stream-wait-value packet.
     // (A poll inside k_match itself can deadlock: 250 spinning workgroups can hold the CUs
     // the extract's single 1024-thread select workgroup needs.)
-    if (c->ext_ready != seq)
+    if (c->ext_ready != seq && !c->serial)
         (void)hipStreamWaitValue32(c->s, c->d.ctr + VO_SYNC_EXT + (f & (VO_EXT_RING - 1)), seq, hipStreamWaitValueGte,
                                    0xFFFFFFFFu);
-    d.wait_next = more ? seq + 1u : 0u;
+    d.wait_next = more && !c->serial ? seq + 1u : 0u;
     c->ext_ready = d.wait_next;
     if (dframe) {
         timed(ev, 3, c->s, [&] { vo::launch_match(d, c->s); });
@@ -381,6 +383,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     // no stream priorities: k_match waits inside the kernel for the extract queue, and a
     // high-priority queue spinning on low-priority work can starve it (observed: the wait ran
     // into its timeout when 250 match workgroups were pending at high priority)
+    c->serial = getenv("VO_SERIAL") && atoi(getenv("VO_SERIAL")) != 0;
     const char* cu_env = getenv("VO_CU_POSE");
     const int cu_pose = cu_env ? atoi(cu_env) : 0;
     int ncu = 0;
@@ -689,7 +692,7 @@ int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_
     if (!c) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
     if (gray) {
-        int rc = upload_frame(c, gray, stride, c->se[c->fidx % VO_EXT_QUEUES]);
+        int rc = upload_frame(c, gray, stride, c->serial ? c->s : c->se[c->fidx % VO_EXT_QUEUES]);
         if (rc) return rc;
     }
     enqueue_frame(c, gray ? c->d.frame_in : nullptr, c->out_dev, nullptr, false);

@@ -35,7 +35,7 @@ import numpy as np  # noqa: E402
 METRIC = "VO frames/sec (extract+match+pose), 1241×376 mono, 2000 kpts/frame"
 # committed rocprofv3 FETCH_SIZE / WRITE_SIZE summary of this workload (tools/profile.sh ->
 # tools/rocprof_summary.py --fetch-x2 --json): source of roofline.traffic
-PMC_PROFILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1_select_kernels.json")
+PMC_PROFILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1_pipeline_kernels.json")
 ROCPROF_NAME = {"stencil": "k_stencil", "select": "k_select", "describe": "k_describe", "match": "k_match",
                 "ransac": "k_ransac_hyp", "refit": "k_refit", "triangulate": "k_triangulate"}
 HBM_PEAK_GBS = 8000.0
@@ -70,9 +70,10 @@ def pmc_traffic(kernel: str):
     """HBM bytes per frame of `kernel` from the committed PMC profile (None if absent)."""
     try:
         prof = json.load(open(PMC_PROFILE))["kernels"]
-        row = prof[ROCPROF_NAME[kernel]]
+        rows = [r for k, r in prof.items() if k.split("<")[0] == ROCPROF_NAME[kernel]]   # template instances
         frames = prof["k_stencil"]["calls"]
-        return row["hbm_bytes_per_launch"] * row["calls"] / frames, os.path.relpath(PMC_PROFILE, ROOT)
+        total = sum(r["hbm_bytes_per_launch"] * r["calls"] for r in rows)
+        return (total / frames if rows else None), os.path.relpath(PMC_PROFILE, ROOT)
     except (OSError, KeyError, TypeError, ZeroDivisionError, ValueError):
         return None, None
 

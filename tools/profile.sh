@@ -12,6 +12,10 @@ export TMPDIR=/tmp
 cd "$ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o stats -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu "$@" > "$OUT/bench_stats.json"
+# PMC collection serializes dispatches, so the frame pipeline's cross-queue waits would spin
+# into their timeouts: the counter passes run every kernel on one queue (same kernels, same
+# bytes; VO_SERIAL=1)
+export VO_SERIAL=1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT" -o fetch -- \
     python3 bench.py --steps 1 --warmup 1 --no-cpu "$@" > "$OUT/bench_fetch.json"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT" -o write -- \

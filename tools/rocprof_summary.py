@@ -16,8 +16,8 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.match(r"(?:void\s+)?(?:vo::)?(\w+)", name)
-    return m.group(1) if m else name[:40]
+    m = re.match(r"(?:void\s+)?(?:vo::)?(\w+(?:<[^>]*>)?)", name)
+    return m.group(1).replace(" ", "") if m else name[:40]
 
 
 def pmc(d, prefix, counter):
