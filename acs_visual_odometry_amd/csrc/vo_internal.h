@@ -36,7 +36,7 @@
 #define VO_STAGE_SLOT 9
 #define VO_SLOTS 11
 #define VO_EXT_RING 16         // per-frame extract results, indexed f & (VO_EXT_RING - 1)
-#define VO_EXT_QUEUES 2        // extract queues: frame f on queue f % VO_EXT_QUEUES
+#define VO_EXT_QUEUES 3        // extract queues: frame f on queue f % VO_EXT_QUEUES (+1 pose queue = 4 HW queues)
 // ctr words: in-launch arrival counters [0, VO_CTR_COUNTERS), then the cross-queue frame
 // counters on lines of their own: the pose chain's (monotonic, read by the extract queues'
 // stream-wait-value packets) and one extract-done word per ring entry (polled by k_match)
