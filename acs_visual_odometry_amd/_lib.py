@@ -20,7 +20,7 @@ EXPORTS = [
     "vo_config_default", "vo_create", "vo_destroy", "vo_strerror", "vo_abi_version", "vo_extract",
     "vo_response", "vo_match", "vo_ransac_F", "vo_pose", "vo_set_ground_truth", "vo_process_frame",
     "vo_process_frames_device", "vo_device_alloc", "vo_device_free", "vo_device_upload", "vo_reset",
-    "vo_last_kernel_times", "vo_enable_kernel_timing", "vo_unpack_descriptor",
+    "vo_last_kernel_times", "vo_last_kernel_stats", "vo_enable_kernel_timing", "vo_unpack_descriptor",
 ]
 
 
@@ -30,7 +30,7 @@ class VoConfig(C.Structure):
         ("resp_thr", C.c_float), ("border_row", C.c_int), ("border_col", C.c_int),
         ("ratio", C.c_float), ("match_bits", C.c_int), ("ransac_p", C.c_double),
         ("sampson_thr", C.c_double), ("ransac_chunk_threads", C.c_int), ("seed", C.c_uint64),
-        ("K", C.c_double * 9), ("device", C.c_int),
+        ("K", C.c_double * 9), ("device", C.c_int), ("frame_batch", C.c_int),
     ]
 
 
@@ -68,6 +68,7 @@ def load():
     L.vo_device_upload.argtypes = [P, P, P, C.c_size_t]
     L.vo_reset.argtypes = [P]
     L.vo_last_kernel_times.argtypes = [P, C.POINTER(C.c_char_p), C.POINTER(C.c_float), I]
+    L.vo_last_kernel_stats.argtypes = [P, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.POINTER(C.c_float), I]
     L.vo_enable_kernel_timing.argtypes = [P, I]
     L.vo_unpack_descriptor.argtypes = [P, P]
     L.vo_unpack_descriptor.restype = None

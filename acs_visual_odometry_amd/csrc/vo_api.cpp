@@ -6,11 +6,13 @@
 // inliers, descriptor carry-forward, RANSAC model leak, GT scale) are taken on the
 // device from VoState, so frames can be enqueued back to back with no host sync.
 //
-// Frame pipeline: extract(f) (stencil, select, describe) runs on stream `se` and waits
-// only for frame f-2's pose chain; the pose chain of frame f (match, RANSAC, refit,
-// triangulate + finalize) runs on stream `s` after extract(f).  So extract(f+1)
-// overlaps pose(f).  Three keypoint/descriptor slots make that safe: select(f) picks a
-// slot that is neither frame f-1's nor its prev (VoExt, k_select).
+// Frame pipeline (vo_process_frames_device): frames are extracted B per launch on stream
+// `se` into a ring of VO_RING keypoint/descriptor slots; pose passes on stream `s` each take
+// the window of the next B uncommitted frames (match, RANSAC, refit, triangulate: one
+// launch each for the whole window; finalize commits in frame order, vo_internal.h).  The
+// pose queue waits for the extract counter with a stream-wait-value packet; a chunk of at
+// most VO_CHUNK frames never rewrites a slot its passes still read, so the extract queue
+// runs ahead freely.  One host sync per chunk reads how far the passes committed.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -32,31 +34,26 @@
 struct vo_ctx {
     vo_config cfg;
     VoDev d;
-    hipStream_t s = nullptr;          // pose chain (and stage APIs)
-    hipStream_t se[VO_EXT_QUEUES] = {};   // extract queues of the frame pipeline
-    struct Scratch {                  // per extract queue (queue 0 uses VoDev's own buffers)
-        uint8_t* blurred = nullptr;
-        uint64_t* cand = nullptr;
-        uint8_t* tilerows = nullptr;
-        uint64_t* ckeys = nullptr;
-        uint64_t* selbits = nullptr;
-        uint32_t* hist = nullptr;
-    } xs[VO_EXT_QUEUES];
+    hipStream_t s = nullptr;          // pose passes, stage APIs, the single-frame path
+    hipStream_t se = nullptr;         // extract batches of the device path
+    int B = VO_DEFAULT_BATCH;         // frames per extract batch / pose-pass window
     int fidx = 0;                     // frames enqueued since vo_reset
-    uint32_t ext_ready = 0;           // extract seq the last enqueued finalize waits for
     bool serial = false;              // VO_SERIAL=1: every kernel on one queue, no cross-queue
                                       // waits (for profilers that serialize dispatches: PMC passes)
-    int max_hyp = VO_MAX_HYP;
     int gt_cap = 0;
     VoFrameOut* out_dev = nullptr;
     int out_cap = 0;
     VoFrameOut* out_host = nullptr;   // pinned
+    int32_t* lo_host = nullptr;       // pinned: VoState::lo after a chunk
     uint8_t* stage_host = nullptr;    // pinned frame staging
     uint16_t* tab_dev = nullptr;
+    double stage_F[9] = {0};          // vo_ransac_F's FundamentalMatrix (persists across calls)
     int timing = 0;                   // 0 off, 1 all kernels, 100+k only kernel k
     std::vector<hipEvent_t> ev_pool;
     std::vector<float> ktime_ms;
-    std::vector<int> kcount;
+    std::vector<int> kcount;          // timed launches per kernel
+    std::vector<int> klaunch;         // launches per kernel in the last call
+    int last_frames = 0;
 };
 
 namespace {
@@ -116,38 +113,48 @@ int dalloc(T** p, size_t n)
     return hip_ok(hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T)));
 }
 
-int sync_ext(vo_ctx* c)
+int sync_all(vo_ctx* c)
 {
-    for (hipStream_t q : c->se)
-        if (q) HIPCHK(hipStreamSynchronize(q));
+    if (c->se) HIPCHK(hipStreamSynchronize(c->se));
+    if (c->s) HIPCHK(hipStreamSynchronize(c->s));
     return VO_OK;
 }
-#define SYNC_EXT(c)                        \
+#define SYNC_ALL(c)                        \
     do {                                   \
-        int _rc = sync_ext(c);             \
+        int _rc = sync_all(c);             \
         if (_rc != VO_OK) return _rc;      \
     } while (0)
 
 int read_state(vo_ctx* c, VoState* h)
 {
-    SYNC_EXT(c);
-    HIPCHK(hipMemcpyAsync(h, c->d.st, sizeof(VoState), hipMemcpyDeviceToHost, c->s));
-    HIPCHK(hipStreamSynchronize(c->s));
-    return VO_OK;
-}
-int write_state(vo_ctx* c, const VoState* h)
-{
-    HIPCHK(hipMemcpyAsync(c->d.st, h, sizeof(VoState), hipMemcpyHostToDevice, c->s));
-    HIPCHK(hipStreamSynchronize(c->s));
+    SYNC_ALL(c);
+    HIPCHK(hipMemcpy(h, c->d.st, sizeof(VoState), hipMemcpyDeviceToHost));
     return VO_OK;
 }
 
-int read_ext(vo_ctx* c, VoExt* h)
+int read_work0(vo_ctx* c, VoWork* w)
 {
-    SYNC_EXT(c);
-    HIPCHK(hipMemcpyAsync(h, c->d.ext, sizeof(VoExt), hipMemcpyDeviceToHost, c->s));
-    HIPCHK(hipStreamSynchronize(c->s));
+    SYNC_ALL(c);
+    HIPCHK(hipMemcpy(w, c->d.work, sizeof(VoWork), hipMemcpyDeviceToHost));
     return VO_OK;
+}
+
+int write_work0(vo_ctx* c, const VoWork* w)
+{
+    SYNC_ALL(c);
+    HIPCHK(hipMemcpy(c->d.work, w, sizeof(VoWork), hipMemcpyHostToDevice));
+    return VO_OK;
+}
+
+// work[0] of a stage call: status OK, counters clear
+void stage_work(VoWork* w)
+{
+    std::memset(w, 0, sizeof(*w));
+    w->status = VO_STATUS_OK;
+    w->frame = -1;
+    w->bestk = -1;
+    w->prev = VO_STAGE_SLOT;
+    w->cur = VO_STAGE_SLOT + 1;
 }
 
 // host frame (any stride) -> frame_in on stream `st`, via the pinned staging buffer
@@ -155,8 +162,7 @@ int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride, hipStream_t st)
 {
     const int W = c->cfg.width, H = c->cfg.height;
     if (stride == 0) stride = (size_t)W;
-    HIPCHK(hipStreamSynchronize(c->s));   // staging buffer / frame_in may still be in use
-    SYNC_EXT(c);
+    SYNC_ALL(c);                          // staging buffer / frame_in may still be in use
     if (stride == (size_t)W) {
         std::memcpy(c->stage_host, gray, (size_t)W * H);
     } else {
@@ -166,36 +172,26 @@ int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride, hipStream_t st)
     return VO_OK;
 }
 
-// stage extract (vo_extract): slot VO_STAGE_SLOT, on the pose stream
-void enqueue_extract(vo_ctx* c, const uint8_t* dframe, int write_response)
+// stage extract (vo_extract / vo_response): frame_in -> slot VO_STAGE_SLOT, scratch 0
+void enqueue_stage_extract(vo_ctx* c)
 {
-    vo::launch_stencil(c->d, dframe, write_response, c->s);
-    vo::launch_select(c->d, -1, c->s);
-    vo::launch_describe(c->d, -1, c->s);
+    vo::launch_stencil(c->d, c->d.frame_in, 0, 1, 0, c->s);
+    vo::launch_select(c->d, 0, 1, VO_STAGE_SLOT, c->s);
+    vo::launch_describe(c->d, 0, 1, VO_STAGE_SLOT, 0u, c->s);
 }
 
-// stage calls borrow the ctx; they restore the trajectory state (and the zeroed
-// histogram / arrival counters the next frame expects) afterwards
-int restore_state(vo_ctx* c, const VoState* saved)
-{
-    HIPCHK(hipMemsetAsync(c->d.hist, 0, sizeof(uint32_t) * VO_HIST_BINS, c->s));   // queue 0's
-    HIPCHK(hipMemsetAsync(c->d.ctr, 0, sizeof(unsigned) * VO_CTR_COUNTERS, c->s));
-    return write_state(c, saved);
-}
-
-// the full trajectory-loop iteration for one frame (VisualOdometry.cpp:68-189).
-// Timing: every timed kernel is bracketed by two events on the stream it runs on (all
+// Timing: every timed launch is bracketed by two events on the stream it runs on (all
 // kernels, or only kernel `only`); vo_last_kernel_times averages end - start.
 struct EvRec {
     std::vector<hipEvent_t>* pool;
     size_t used;
     int only;   // -1: all kernels
-    int frame;  // frame being enqueued; single-kernel mode brackets every VO_TIMING_STRIDE-th frame
+    std::vector<int>* launches;
     std::vector<std::pair<int, size_t>> spans;   // (kernel, index of its start event)
 };
 // An event pair costs ~6 us of queue time per bracketed launch (rocprofv3 kernel trace), so
-// the bench's live single-kernel timing samples one frame in VO_TIMING_STRIDE.
-#define VO_TIMING_STRIDE 8
+// the bench's live single-kernel timing samples one launch in VO_TIMING_STRIDE.
+#define VO_TIMING_STRIDE 4
 
 size_t ev_mark(EvRec* ev, hipStream_t st)
 {
@@ -211,9 +207,10 @@ size_t ev_mark(EvRec* ev, hipStream_t st)
 }
 
 template <typename F>
-void timed(EvRec* ev, int k, hipStream_t st, F&& launch)
+void timed(vo_ctx* c, EvRec* ev, int k, hipStream_t st, F&& launch)
 {
-    const bool on = ev && (ev->only < 0 || (ev->only == k && ev->frame % VO_TIMING_STRIDE == 0));
+    const int nth = c->klaunch[k]++;
+    const bool on = ev && (ev->only < 0 || (ev->only == k && nth % VO_TIMING_STRIDE == 0));
     size_t b = on ? ev_mark(ev, st) : 0;
     launch();
     if (on) {
@@ -222,59 +219,64 @@ void timed(EvRec* ev, int k, hipStream_t st, F&& launch)
     }
 }
 
-// more: the caller enqueues frame f+1 right after this one (the batch path)
-void enqueue_frame(vo_ctx* c, const uint8_t* dframe, VoFrameOut* out, EvRec* ev, bool more)
+// extract of nb frames f0.. (device images img0 + z * frame_bytes) on stream q; publish:
+// the pose queue may wait for frames < f0 + nb
+void enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, int nb, bool publish,
+                     hipStream_t q, EvRec* ev)
 {
-    const int f = c->fidx++;
-    if (ev) ev->frame = f;
-    VoDev d = c->d;
-    d.out = out;
-    // Cross-queue order by frame counters the kernels publish (describe's last workgroup:
-    // frame f extracted; finalize: pose chain done).  An event record + wait costs ~11-18 us
-    // of queue time per hop on MI355X (tools/evtest.hip); a stream-wait-value packet on a
-    // kernel-written counter ~1-6 us (ROCclr runs it as a small wait kernel); a poll inside
-    // the consuming kernel ~1 us.
-    const uint32_t seq = (uint32_t)f + 1u;
-    d.seqno = seq;
-    // extract queue q = f % E with its own scratch; frames on different queues overlap
-    const int q = f % VO_EXT_QUEUES;
-    hipStream_t se = c->serial ? c->s : c->se[q];
-    d.eq = q;
-    if (q > 0) {
-        const vo_ctx::Scratch& x = c->xs[q];
-        d.blurred = x.blurred; d.cand = x.cand; d.tilerows = x.tilerows;
-        d.ckeys = x.ckeys; d.selbits = x.selbits; d.hist = x.hist;
-    }
-    // ring slot f % R is read by the pose chains of frames f - R (cur) and f - R + 1 (prev,
-    // or the carry copy finalize(f - R + 1) makes): frame f - R + 1's chain must be done
-    if (f >= VO_RING_SLOTS - 1 && !c->serial)
-        (void)hipStreamWaitValue32(se, c->d.ctr + VO_SYNC_POSE, seq - (uint32_t)(VO_RING_SLOTS - 1),
-                                   hipStreamWaitValueGte, 0xFFFFFFFFu);
-    if (dframe) {
-        timed(ev, 0, se, [&] { vo::launch_stencil(d, dframe, 0, se); });
-        timed(ev, 1, se, [&] { vo::launch_select(d, f, se); });
-        timed(ev, 2, se, [&] { vo::launch_describe(d, f, se); });
+    timed(c, ev, 0, q, [&] { vo::launch_stencil(c->d, img0, frame_bytes, nb, 0, q); });
+    timed(c, ev, 1, q, [&] { vo::launch_select(c->d, f0, nb, -1, q); });
+    timed(c, ev, 2, q, [&] { vo::launch_describe(c->d, f0, nb, -1, publish ? (unsigned)(f0 + nb) : 0u, q); });
+}
+
+// one pose pass over the window [lo, lo + B) of the frames enqueued so far
+void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev)
+{
+    hipStream_t s = c->s;
+    timed(c, ev, 3, s, [&] { vo::launch_match(c->d, 0, s); });
+    timed(c, ev, 4, s, [&] { vo::launch_ransac(c->d, 0, s); });
+    timed(c, ev, 5, s, [&] { vo::launch_refit(c->d, 1, 0, s); });
+    timed(c, ev, 6, s, [&] { vo::launch_triangulate(c->d, 0, s); });
+    timed(c, ev, 7, s, [&] { vo::launch_finalize(c->d, out, out_base, s); });
+}
+
+// frames [c->fidx, c->fidx + nf) (nf <= VO_CHUNK): set the end, enqueue the extract
+// batches (img != null: device images; null: one missing image) and one pass per window,
+// then repeat passes until every frame is committed (a pass commits at least its first frame)
+int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFrameOut* out, int out_base, EvRec* ev,
+              bool host_frame)
+{
+    const int base = c->fidx, end = base + nf, B = c->B;
+    hipStream_t s = c->s;
+    hipStream_t q = (c->serial || host_frame || !img0) ? s : c->se;
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&c->d.st->end, end, 1, s));
+    const int nb = (nf + B - 1) / B;
+    if (!img0) {
+        vo::launch_ext_missing(c->d, base % VO_RING, s);
     } else {
-        vo::launch_ext_missing(d, f, se);
+        for (int j = 0; j < nb; ++j) {
+            const int cnt = std::min(B, nf - j * B);
+            enqueue_extract(c, img0 + (size_t)j * B * frame_bytes, frame_bytes, base + j * B, cnt, q != s, q, ev);
+        }
     }
-    // The pose queue needs frame f's extract before k_match.  Inside a batch the previous
-    // frame's finalize (one workgroup) waited for it at its end, so k_match starts behind a
-    // kernel boundary with the descriptors in place; otherwise a stream-wait-value packet.
-    // (A poll inside k_match itself can deadlock: 250 spinning workgroups can hold the CUs
-    // the extract's single 1024-thread select workgroup needs.)
-    if (c->ext_ready != seq && !c->serial)
-        (void)hipStreamWaitValue32(c->s, c->d.ctr + VO_SYNC_EXT + (f & (VO_EXT_RING - 1)), seq, hipStreamWaitValueGte,
-                                   0xFFFFFFFFu);
-    d.wait_next = more && !c->serial ? seq + 1u : 0u;
-    c->ext_ready = d.wait_next;
-    if (dframe) {
-        timed(ev, 3, c->s, [&] { vo::launch_match(d, c->s); });
-        timed(ev, 4, c->s, [&] { vo::launch_ransac(d, c->max_hyp, c->s); });
-        timed(ev, 5, c->s, [&] { vo::launch_refit(d, 1, c->s); });
-        timed(ev, 6, c->s, [&] { vo::launch_triangulate(d, c->s); });
-    } else {
-        vo::launch_missing(d, c->s);
+    c->fidx = end;
+    for (int k = 0; k < nb; ++k) {
+        if (q != s)
+            (void)hipStreamWaitValue32(s, c->d.ctr + VO_SYNC_EXT, (uint32_t)std::min(base + (k + 1) * B, end),
+                                       hipStreamWaitValueGte, 0xFFFFFFFFu);
+        enqueue_pass(c, out, out_base, ev);
     }
+    for (;;) {
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(c->lo_host, &c->d.st->lo, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const int lo = *c->lo_host;
+        if (lo >= end) break;
+        if (lo < base) return VO_ERR_STATE;
+        // frames after skipped ones: their windows restart at lo (extracts are complete)
+        for (int k = 0; k < (end - lo + B - 1) / B; ++k) enqueue_pass(c, out, out_base, ev);
+    }
+    return VO_OK;
 }
 
 int ensure_out(vo_ctx* c, int n)
@@ -289,16 +291,31 @@ int ensure_out(vo_ctx* c, int n)
     return VO_OK;
 }
 
-void init_state(vo_ctx* c, VoState* h)
+void init_state(VoState* h)
 {
     std::memset(h, 0, sizeof(*h));
-    h->frame = 0;
-    h->status = VO_STATUS_OK;
-    h->cur = 0; h->prev = 0;
-    h->bestk = -1;
+    h->lo = 0; h->end = 0;
+    h->prev_slot = 0;
+    h->last_valid = 0;
+    h->model_n = 0;
     h->scale_override = std::nan("");
     for (int i = 0; i < 16; ++i) h->Tcurr[i] = (i % 5 == 0) ? 1.0 : 0.0;
-    (void)c;
+}
+
+int finish_timing(vo_ctx* c, EvRec* ev)
+{
+    const int nk = vo::kernel_count();
+    c->ktime_ms.assign(nk, 0.f);
+    c->kcount.assign(nk, 0);
+    if (!ev) return VO_OK;
+    SYNC_ALL(c);
+    for (const auto& sp : ev->spans) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, c->ev_pool[sp.second], c->ev_pool[sp.second + 1]);
+        c->ktime_ms[sp.first] += ms;
+        c->kcount[sp.first] += 1;
+    }
+    return VO_OK;
 }
 
 }  // namespace
@@ -351,6 +368,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     if (!(k.resp_thr >= 0.0f)) return VO_ERR_ARG;
     if (k.match_bits != 32 && k.match_bits != 512) return VO_ERR_ARG;
     if (!(k.ransac_p > 0.0 && k.ransac_p < 1.0) || k.ransac_chunk_threads < 1) return VO_ERR_ARG;
+    if (k.frame_batch < 0 || k.frame_batch > VO_MAX_BATCH) return VO_ERR_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return VO_ERR_NO_DEVICE;
     if (k.device < 0 || k.device >= ndev) return VO_ERR_NO_DEVICE;
@@ -362,6 +380,9 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     VoDev& d = c->d;
     std::memset(&d, 0, sizeof(d));
     const int W = k.width, H = k.height, N = k.max_kpts;
+    const int B = k.frame_batch ? k.frame_batch : VO_DEFAULT_BATCH;
+    c->B = B;
+    d.B = B;
     d.W = W; d.H = H; d.N = N;
     d.nms_k = k.nms_k; d.brow = k.border_row; d.bcol = k.border_col;
     d.resp_thr = k.resp_thr;
@@ -374,73 +395,45 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
         double outlierRatio = 0.5;
         d.maxit_initial = to_int_x86(std::log(1.0 - k.ransac_p) / std::log(1.0 - std::pow(1.0 - outlierRatio, 8.0)));
     }
-    c->max_hyp = std::max(VO_MAX_HYP, std::min(d.maxit_initial, 1 << 20));
+    d.max_hyp = std::max(VO_MAX_HYP, std::min(d.maxit_initial, 1 << 20));
     const int ntiles = ((W + 63) / 64) * ((H + 15) / 16);
     if (ntiles > 2048) { delete c; return VO_ERR_ARG; }      // SEL_MAX_TILES (select kernel LDS)
+    d.ntiles = ntiles;
     d.cand_cap = (uint32_t)ntiles * 256u;
     int rc = VO_OK;
     auto bail = [&](int r) { vo_destroy(c); return r; };
-    // no stream priorities: k_match waits inside the kernel for the extract queue, and a
-    // high-priority queue spinning on low-priority work can starve it (observed: the wait ran
-    // into its timeout when 250 match workgroups were pending at high priority)
     c->serial = getenv("VO_SERIAL") && atoi(getenv("VO_SERIAL")) != 0;
-    const char* cu_env = getenv("VO_CU_POSE");
-    const int cu_pose = cu_env ? atoi(cu_env) : 0;
-    int ncu = 0;
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, k.device);
-    if (cu_pose > 0 && cu_pose < ncu && ncu <= 1024) {
-        // experimental: disjoint CU sets for the two queues (CU ids spread evenly)
-        std::vector<uint32_t> mp((ncu + 31) / 32, 0u), me((ncu + 31) / 32, 0u);
-        for (int i = 0; i < ncu; ++i) {
-            const bool pose = (long)(i + 1) * cu_pose / ncu != (long)i * cu_pose / ncu;
-            (pose ? mp : me)[i >> 5] |= 1u << (i & 31);
-        }
-        if (hip_ok(hipExtStreamCreateWithCUMask(&c->s, (uint32_t)mp.size(), mp.data())) != VO_OK) return bail(VO_ERR_HIP);
-        for (hipStream_t& q : c->se)
-            if (hip_ok(hipExtStreamCreateWithCUMask(&q, (uint32_t)me.size(), me.data())) != VO_OK) return bail(VO_ERR_HIP);
-    } else {
-        if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
-        for (hipStream_t& q : c->se)
-            if (hip_ok(hipStreamCreateWithFlags(&q, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
-    }
+    if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(hipStreamCreateWithFlags(&c->se, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
     d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
     if (d.sel_lds < 0) return bail(VO_ERR_HIP);
-    rc |= dalloc(&d.frame_in, (size_t)W * H);
-    rc |= dalloc(&d.blurred, (size_t)W * H);
-    rc |= dalloc(&d.response, (size_t)W * H);
-    rc |= dalloc(&d.cand, d.cand_cap);
-    rc |= dalloc(&d.tilerows, (size_t)ntiles * 16);
-    rc |= dalloc(&d.ckeys, d.cand_cap);
-    rc |= dalloc(&d.selbits, d.cand_cap / 64 + 1);
-    rc |= dalloc(&d.hist, VO_HIST_BINS);
-    for (int q = 1; q < VO_EXT_QUEUES; ++q) {
-        vo_ctx::Scratch& x = c->xs[q];
-        rc |= dalloc(&x.blurred, (size_t)W * H);
-        rc |= dalloc(&x.cand, d.cand_cap);
-        rc |= dalloc(&x.tilerows, (size_t)ntiles * 16);
-        rc |= dalloc(&x.ckeys, d.cand_cap);
-        rc |= dalloc(&x.selbits, d.cand_cap / 64 + 1);
-        rc |= dalloc(&x.hist, VO_HIST_BINS);
-    }
-    for (int s = 0; s < VO_SLOTS; ++s) {
-        rc |= dalloc(&d.kps[s], N);
-        rc |= dalloc(&d.desc[s], (size_t)N * 8);
-        rc |= dalloc(&d.pre[s], N);
-    }
-    rc |= dalloc(&d.match_j, N);
-    rc |= dalloc(&d.match_pairs, N);
-    rc |= dalloc(&d.pts, (size_t)N * 4);
-    rc |= dalloc(&d.hypF, (size_t)c->max_hyp * 9);
-    rc |= dalloc(&d.counts, c->max_hyp);
-    rc |= dalloc(&d.inl, N);
+    const size_t np = (size_t)W * H;
+    rc |= dalloc(&d.frame_in, np);
+    rc |= dalloc(&d.blurred, np * B);
+    rc |= dalloc(&d.response, np);
+    rc |= dalloc(&d.cand, (size_t)d.cand_cap * B);
+    rc |= dalloc(&d.tilerows, (size_t)ntiles * 16 * B);
+    rc |= dalloc(&d.ckeys, (size_t)d.cand_cap * B);
+    rc |= dalloc(&d.selbits, ((size_t)d.cand_cap / 64 + 1) * B);
+    rc |= dalloc(&d.hist, (size_t)VO_HIST_BINS * B);
+    rc |= dalloc(&d.kps, (size_t)N * VO_SLOTS);
+    rc |= dalloc(&d.desc, (size_t)N * 8 * VO_SLOTS);
+    rc |= dalloc(&d.pre, (size_t)N * VO_SLOTS);
+    rc |= dalloc(&d.match_j, (size_t)N * B);
+    rc |= dalloc(&d.match_pairs, (size_t)N * B);
+    rc |= dalloc(&d.pts, (size_t)N * 4 * B);
+    rc |= dalloc(&d.hypF, (size_t)d.max_hyp * 9 * B);
+    rc |= dalloc(&d.counts, (size_t)d.max_hyp * B);
+    rc |= dalloc(&d.inl, (size_t)N * B);
     d.mask_words = (N + 63) / 64;
-    rc |= dalloc(&d.inlmask, (size_t)c->max_hyp * d.mask_words);
-    rc |= dalloc(&d.model_p, (size_t)N * 4);
+    rc |= dalloc(&d.inlmask, (size_t)d.max_hyp * d.mask_words * B);
+    rc |= dalloc(&d.model_p, (size_t)N * 4 * B);
+    rc |= dalloc(&d.work, B);
     rc |= dalloc(&d.st, 1);
     rc |= dalloc(&d.ext, 1);
     rc |= dalloc(&d.ctr, VO_CTR_WORDS);
 #ifdef VO_STAMPS
-    rc |= dalloc(&d.dbg, (size_t)c->max_hyp * 16);
+    rc |= dalloc(&d.dbg, (size_t)d.max_hyp * 16);
 #endif
     if (rc != VO_OK) return bail(VO_ERR_HIP);
     const std::vector<uint16_t>& tab = maxit_table(N, k.ransac_p);
@@ -448,15 +441,15 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     if (hip_ok(hipMemcpy(c->tab_dev, tab.data(), tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice)) != VO_OK)
         return bail(VO_ERR_HIP);
     d.maxit_tab = c->tab_dev;
-    if (hip_ok(hipHostMalloc((void**)&c->stage_host, (size_t)W * H, hipHostMallocDefault)) != VO_OK) return bail(VO_ERR_HIP);
-    // zero the descriptor / keypoint slots (deterministic contents before first use)
-    for (int s = 0; s < VO_SLOTS; ++s) {
-        (void)hipMemset(d.kps[s], 0, sizeof(int2) * N);
-        (void)hipMemset(d.desc[s], 0, sizeof(uint64_t) * 8 * N);
-        (void)hipMemset(d.pre[s], 0, sizeof(uint32_t) * N);
-    }
+    if (hip_ok(hipHostMalloc((void**)&c->stage_host, np, hipHostMallocDefault)) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(hipHostMalloc((void**)&c->lo_host, sizeof(int32_t), hipHostMallocDefault)) != VO_OK)
+        return bail(VO_ERR_HIP);
+    // deterministic contents before first use
+    (void)hipMemset(d.kps, 0, sizeof(int2) * N * VO_SLOTS);
+    (void)hipMemset(d.desc, 0, sizeof(uint64_t) * 8 * N * VO_SLOTS);
+    (void)hipMemset(d.pre, 0, sizeof(uint32_t) * N * VO_SLOTS);
     if (ensure_out(c, 16) != VO_OK) return bail(VO_ERR_HIP);
-    (void)hipMemset(d.ctr, 0, sizeof(unsigned) * VO_CTR_WORDS);
+    c->klaunch.assign(vo::kernel_count(), 0);
     if (vo_reset(c) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipDeviceSynchronize()) != VO_OK) return bail(VO_ERR_HIP);
     *out = c;
@@ -467,30 +460,19 @@ void vo_destroy(vo_ctx* c)
 {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
-    for (hipStream_t q : c->se)
-        if (q) (void)hipStreamSynchronize(q);
+    if (c->se) (void)hipStreamSynchronize(c->se);
     if (c->s) (void)hipStreamSynchronize(c->s);
     VoDev& d = c->d;
-    for (int s = 0; s < VO_SLOTS; ++s) {
-        void* sp[] = {d.kps[s], d.desc[s], d.pre[s]};
-        for (void* p : sp)
-            if (p) (void)hipFree(p);
-    }
     void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.tilerows, d.ckeys, d.selbits, d.hist, d.ext,
-                    d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.inlmask, d.model_p,
-                    d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr, d.dbg};
+                    d.kps, d.desc, d.pre, d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.inlmask,
+                    d.model_p, d.work, d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr, d.dbg};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    for (const vo_ctx::Scratch& x : c->xs) {
-        void* xp[] = {x.blurred, x.cand, x.tilerows, x.ckeys, x.selbits, x.hist};
-        for (void* p : xp)
-            if (p) (void)hipFree(p);
-    }
     if (c->out_host) (void)hipHostFree(c->out_host);
     if (c->stage_host) (void)hipHostFree(c->stage_host);
+    if (c->lo_host) (void)hipHostFree(c->lo_host);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
-    for (hipStream_t q : c->se)
-        if (q) (void)hipStreamDestroy(q);
+    if (c->se) (void)hipStreamDestroy(c->se);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
 }
@@ -499,24 +481,17 @@ int vo_reset(vo_ctx* c)
 {
     if (!c) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    SYNC_EXT(c);
+    SYNC_ALL(c);
     VoState h;
-    init_state(c, &h);
-    int rc = write_state(c, &h);
-    if (rc) return rc;
-    VoExt e;
-    std::memset(&e, 0, sizeof(e));
-    for (int i = 0; i < VO_EXT_RING; ++i) { e.slot[i] = -1; e.status[i] = VO_STATUS_OK; }
-    HIPCHK(hipMemcpyAsync(c->d.ext, &e, sizeof(e), hipMemcpyHostToDevice, c->s));
-    HIPCHK(hipMemsetAsync(c->d.hist, 0, sizeof(uint32_t) * VO_HIST_BINS, c->s));
-    for (int q = 1; q < VO_EXT_QUEUES; ++q)
-        HIPCHK(hipMemsetAsync(c->xs[q].hist, 0, sizeof(uint32_t) * VO_HIST_BINS, c->s));
+    init_state(&h);
+    HIPCHK(hipMemcpy(c->d.st, &h, sizeof(h), hipMemcpyHostToDevice));
+    std::vector<int32_t> e(2 * VO_SLOTS, 0);          // n_kps = 0, status = VO_STATUS_OK
+    HIPCHK(hipMemcpy(c->d.ext, e.data(), sizeof(VoExt), hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(c->d.hist, 0, sizeof(uint32_t) * VO_HIST_BINS * c->B));
+    HIPCHK(hipMemset(c->d.work, 0, sizeof(VoWork) * c->B));
+    HIPCHK(hipMemset(c->d.ctr, 0, sizeof(unsigned) * VO_CTR_WORDS));
     c->fidx = 0;
-    c->ext_ready = 0;
-    HIPCHK(hipMemsetAsync(c->d.ctr, 0, sizeof(unsigned) * VO_CTR_WORDS, c->s));   // + frame counters
-    vo::launch_frame_begin(c->d, VO_MODE_FRAME, c->s);     // frame 0 set up on the device
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(c->s));
+    HIPCHK(hipDeviceSynchronize());
     return VO_OK;
 }
 
@@ -524,7 +499,7 @@ int vo_set_ground_truth(vo_ctx* c, const double* poses12, int n)
 {
     if (!c || n < 0 || (n > 0 && !poses12)) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    HIPCHK(hipStreamSynchronize(c->s));
+    SYNC_ALL(c);
     if (n > c->gt_cap) {
         if (c->d.gt) (void)hipFree((void*)c->d.gt);
         double* g = nullptr;
@@ -543,17 +518,18 @@ int vo_extract(vo_ctx* c, const uint8_t* gray, size_t stride, vo_kp* kps, uint64
     HIPCHK(hipSetDevice(c->cfg.device));
     int rc = upload_frame(c, gray, stride, c->s);
     if (rc) return rc;
-    enqueue_extract(c, c->d.frame_in, 0);      // slot VO_STAGE_SLOT: the trajectory's slots are untouched
+    enqueue_stage_extract(c);      // slot VO_STAGE_SLOT: the trajectory's slots are untouched
     HIPCHK(hipGetLastError());
-    VoExt e;
-    rc = read_ext(c, &e);
-    if (rc) return rc;
-    if (e.stage_status != VO_STATUS_OK) return VO_ERR_CAPACITY;
-    const int nk = e.n_kps[VO_STAGE_SLOT];
+    SYNC_ALL(c);
+    int32_t nk = 0, status = 0;
+    HIPCHK(hipMemcpy(&nk, &c->d.ext->n_kps[VO_STAGE_SLOT], sizeof(int32_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&status, &c->d.ext->status[VO_STAGE_SLOT], sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (status != VO_STATUS_OK) return VO_ERR_CAPACITY;
     *n = nk;
-    if (kps && nk) HIPCHK(hipMemcpy(kps, c->d.kps[VO_STAGE_SLOT], sizeof(vo_kp) * nk, hipMemcpyDeviceToHost));
+    const size_t N = (size_t)c->cfg.max_kpts;
+    if (kps && nk) HIPCHK(hipMemcpy(kps, c->d.kps + VO_STAGE_SLOT * N, sizeof(vo_kp) * nk, hipMemcpyDeviceToHost));
     if (desc && nk)
-        HIPCHK(hipMemcpy(desc, c->d.desc[VO_STAGE_SLOT], sizeof(uint64_t) * 8 * nk, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(desc, c->d.desc + VO_STAGE_SLOT * N * 8, sizeof(uint64_t) * 8 * nk, hipMemcpyDeviceToHost));
     if (blurred)
         HIPCHK(hipMemcpy(blurred, c->d.blurred, (size_t)c->cfg.width * c->cfg.height, hipMemcpyDeviceToHost));
     return VO_OK;
@@ -567,7 +543,7 @@ int vo_response(vo_ctx* c, const uint8_t* gray, size_t stride, float* R)
     if (rc) return rc;
     const size_t np = (size_t)c->cfg.width * c->cfg.height;
     HIPCHK(hipMemsetAsync(c->d.response, 0, np * sizeof(float), c->s));
-    vo::launch_stencil(c->d, c->d.frame_in, 1, c->s);
+    vo::launch_stencil(c->d, c->d.frame_in, 0, 1, 1, c->s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(R, c->d.response, np * sizeof(float), hipMemcpyDeviceToHost, c->s));
     // the stencil histogram is consumed by select; nothing selects here, so clear it
@@ -585,31 +561,26 @@ int vo_match(vo_ctx* c, const uint64_t* d_prev, int n_prev, const uint64_t* d_cu
     std::vector<uint32_t> p0(n_prev), p1(n_cur);
     for (int i = 0; i < n_prev; ++i) p0[i] = (uint32_t)d_prev[8 * (size_t)i];
     for (int i = 0; i < n_cur; ++i) p1[i] = (uint32_t)d_cur[8 * (size_t)i];
-    SYNC_EXT(c);
-    HIPCHK(hipStreamSynchronize(c->s));
+    SYNC_ALL(c);
+    const size_t N = (size_t)c->cfg.max_kpts;
     const int a = VO_STAGE_SLOT, b = VO_STAGE_SLOT + 1;     // stage slots: the trajectory's stay intact
-    HIPCHK(hipMemcpy(c->d.desc[a], d_prev, sizeof(uint64_t) * 8 * n_prev, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d.desc[b], d_cur, sizeof(uint64_t) * 8 * n_cur, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d.pre[a], p0.data(), sizeof(uint32_t) * n_prev, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d.pre[b], p1.data(), sizeof(uint32_t) * n_cur, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d.desc + a * N * 8, d_prev, sizeof(uint64_t) * 8 * n_prev, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d.desc + b * N * 8, d_cur, sizeof(uint64_t) * 8 * n_cur, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d.pre + a * N, p0.data(), sizeof(uint32_t) * n_prev, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d.pre + b * N, p1.data(), sizeof(uint32_t) * n_cur, hipMemcpyHostToDevice));
     const int nk2[2] = {n_prev, n_cur};
     HIPCHK(hipMemcpy(c->d.ext->n_kps + a, nk2, sizeof(nk2), hipMemcpyHostToDevice));
-    VoState h;
-    int rc = read_state(c, &h);
+    VoWork w;
+    stage_work(&w);
+    int rc = write_work0(c, &w);
     if (rc) return rc;
-    VoState saved = h;
-    h.prev = a; h.cur = b;
-    h.status = VO_STATUS_OK; h.mode = VO_MODE_STAGE;
-    rc = write_state(c, &h);
-    if (rc) return rc;
-    vo::launch_match(c->d, c->s);
+    vo::launch_match(c->d, 1, c->s);
     HIPCHK(hipGetLastError());
-    rc = read_state(c, &h);
+    rc = read_work0(c, &w);
     if (rc) return rc;
-    *m = h.M;
-    if (out && h.M) HIPCHK(hipMemcpy(out, c->d.match_pairs, sizeof(vo_match_t) * h.M, hipMemcpyDeviceToHost));
-    // restore the trajectory bookkeeping (stage calls do not advance the loop)
-    return restore_state(c, &saved);
+    *m = w.M;
+    if (out && w.M) HIPCHK(hipMemcpy(out, c->d.match_pairs, sizeof(vo_match_t) * w.M, hipMemcpyDeviceToHost));
+    return VO_OK;
 }
 
 int vo_ransac_F(vo_ctx* c, const double* pts, int m, uint64_t seed, double F[9], int* fitted, int32_t* inlier_idx,
@@ -617,35 +588,32 @@ int vo_ransac_F(vo_ctx* c, const double* pts, int m, uint64_t seed, double F[9],
 {
     if (!c || !pts || m < 8 || m > c->cfg.max_kpts) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    HIPCHK(hipStreamSynchronize(c->s));
+    SYNC_ALL(c);
     HIPCHK(hipMemcpy(c->d.pts, pts, sizeof(double) * 4 * (size_t)m, hipMemcpyHostToDevice));
-    VoState h;
-    int rc = read_state(c, &h);
+    VoWork w;
+    stage_work(&w);
+    w.M = m;
+    w.scored = (m / c->cfg.ransac_chunk_threads) * c->cfg.ransac_chunk_threads;
+    w.frame_seed = seed;
+    int rc = write_work0(c, &w);
     if (rc) return rc;
-    VoState saved = h;
-    h.status = VO_STATUS_OK; h.mode = VO_MODE_STAGE;
-    h.M = m; h.scored = (m / c->cfg.ransac_chunk_threads) * c->cfg.ransac_chunk_threads;
-    h.frame_seed = seed; h.bestk = -1; h.need_more = 0; h.fitted = 0; h.n_inl = 0;
-    rc = write_state(c, &h);
-    if (rc) return rc;
-    vo::launch_ransac(c->d, c->max_hyp, c->s);
-    vo::launch_refit(c->d, 0, c->s);
+    vo::launch_ransac(c->d, 1, c->s);
+    vo::launch_refit(c->d, 0, 1, c->s);
     HIPCHK(hipGetLastError());
-    rc = read_state(c, &h);
+    rc = read_work0(c, &w);
     if (rc) return rc;
-    if (F) std::memcpy(F, h.model_F, sizeof(h.model_F));
-    if (fitted) *fitted = h.fitted;
-    if (n_inl) *n_inl = h.n_inl;
-    if (best_k) *best_k = h.bestk;
-    if (n_evaluated) *n_evaluated = h.n_eval;
-    if (inlier_idx && h.bestk >= 0 && h.n_inl > 0)
-        HIPCHK(hipMemcpy(inlier_idx, c->d.inl, sizeof(int32_t) * h.n_inl, hipMemcpyDeviceToHost));
-    if (counts && h.n_eval > 0)
-        HIPCHK(hipMemcpy(counts, c->d.counts, sizeof(int32_t) * std::min(h.n_eval, VO_MAX_HYP), hipMemcpyDeviceToHost));
-    // the model (F + inliers) persists like FundamentalMatrix model (VisualOdometry.cpp:49)
-    saved.model_n = h.model_n;
-    std::memcpy(saved.model_F, h.model_F, sizeof(h.model_F));
-    return restore_state(c, &saved);
+    // the model persists across calls like FundamentalMatrix model (VisualOdometry.cpp:49)
+    if (w.fitted) std::memcpy(c->stage_F, w.F, sizeof(c->stage_F));
+    if (F) std::memcpy(F, c->stage_F, sizeof(c->stage_F));
+    if (fitted) *fitted = w.fitted;
+    if (n_inl) *n_inl = w.n_inl;
+    if (best_k) *best_k = w.bestk;
+    if (n_evaluated) *n_evaluated = w.n_eval;
+    if (inlier_idx && w.bestk >= 0 && w.n_inl > 0)
+        HIPCHK(hipMemcpy(inlier_idx, c->d.inl, sizeof(int32_t) * w.n_inl, hipMemcpyDeviceToHost));
+    if (counts && w.n_eval > 0)
+        HIPCHK(hipMemcpy(counts, c->d.counts, sizeof(int32_t) * std::min(w.n_eval, VO_MAX_HYP), hipMemcpyDeviceToHost));
+    return VO_OK;
 }
 
 int vo_pose(vo_ctx* c, const double F[9], const float* p1, const float* p2, int n, double scale, double R[9],
@@ -658,33 +626,34 @@ int vo_pose(vo_ctx* c, const double F[9], const float* p1, const float* p2, int 
         mp[4 * i] = p1[2 * i]; mp[4 * i + 1] = p1[2 * i + 1];
         mp[4 * i + 2] = p2[2 * i]; mp[4 * i + 3] = p2[2 * i + 1];
     }
-    HIPCHK(hipStreamSynchronize(c->s));
+    SYNC_ALL(c);
     HIPCHK(hipMemcpy(c->d.model_p, mp.data(), sizeof(float) * mp.size(), hipMemcpyHostToDevice));
-    VoState h;
-    int rc = read_state(c, &h);
+    HIPCHK(hipMemcpy(&c->d.st->scale_override, &scale, sizeof(double), hipMemcpyHostToDevice));
+    VoWork w;
+    stage_work(&w);
+    w.fitted = 1;
+    w.n_fit = n;
+    std::memcpy(w.F, F, sizeof(w.F));
+    int rc = write_work0(c, &w);
     if (rc) return rc;
-    VoState saved = h;
-    h.status = VO_STATUS_OK; h.mode = VO_MODE_STAGE;
-    h.model_n = n;
-    std::memcpy(h.model_F, F, sizeof(h.model_F));
-    h.scale_override = scale;
-    rc = write_state(c, &h);
-    if (rc) return rc;
-    vo::launch_pose_prep(c->d, c->s);
-    vo::launch_triangulate(c->d, c->s);
+    vo::launch_pose_stage(c->d, 0, c->s);
+    vo::launch_triangulate(c->d, 1, c->s);
+    vo::launch_pose_stage(c->d, 1, c->s);
     HIPCHK(hipGetLastError());
+    VoState h;
     rc = read_state(c, &h);
     if (rc) return rc;
+    rc = read_work0(c, &w);
+    if (rc) return rc;
     int ret = VO_OK;
-    if (h.status == VO_STATUS_DEGENERATE) ret = VO_ERR_DEGENERATE_E;
-    else if (h.status != VO_STATUS_OK) ret = VO_ERR_STATE;
+    if (h.pose_status == VO_STATUS_DEGENERATE) ret = VO_ERR_DEGENERATE_E;
+    else if (h.pose_status != VO_STATUS_OK) ret = VO_ERR_STATE;
     if (ret == VO_OK) {
         if (R) std::memcpy(R, h.pose_R, sizeof(h.pose_R));
         if (t) std::memcpy(t, h.pose_t, sizeof(h.pose_t));
     }
-    if (counts4) std::memcpy(counts4, h.counts4, sizeof(h.counts4));
-    rc = restore_state(c, &saved);
-    return ret != VO_OK ? ret : rc;
+    if (counts4) std::memcpy(counts4, w.counts4, sizeof(w.counts4));
+    return ret;
 }
 
 int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_out[12], int* status, int32_t* info)
@@ -692,13 +661,14 @@ int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_
     if (!c) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
     if (gray) {
-        int rc = upload_frame(c, gray, stride, c->serial ? c->s : c->se[c->fidx % VO_EXT_QUEUES]);
+        int rc = upload_frame(c, gray, stride, c->s);
         if (rc) return rc;
     }
-    enqueue_frame(c, gray ? c->d.frame_in : nullptr, c->out_dev, nullptr, false);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(c->out_host, c->out_dev, sizeof(VoFrameOut), hipMemcpyDeviceToHost, c->s));
-    HIPCHK(hipStreamSynchronize(c->s));
+    const int f = c->fidx;
+    // one frame: extract on the pose queue, a window of one (no speculation)
+    int rc = run_chunk(c, gray ? c->d.frame_in : nullptr, 0, 1, c->out_dev, f, nullptr, true);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(c->out_host, c->out_dev, sizeof(VoFrameOut), hipMemcpyDeviceToHost));
     const VoFrameOut& o = c->out_host[0];
     if (pose_out) std::memcpy(pose_out, o.pose, sizeof(o.pose));
     if (status) *status = o.status;
@@ -717,25 +687,20 @@ int vo_process_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
     HIPCHK(hipSetDevice(c->cfg.device));
     int rc = ensure_out(c, std::max(nframes, 1));
     if (rc) return rc;
-    EvRec rec{&c->ev_pool, 0, c->timing >= 100 ? c->timing - 100 : -1, 0, {}};
+    c->klaunch.assign(vo::kernel_count(), 0);
+    EvRec rec{&c->ev_pool, 0, c->timing >= 100 ? c->timing - 100 : -1, &c->klaunch, {}};
     EvRec* evp = c->timing ? &rec : nullptr;
-    for (int f = 0; f < nframes; ++f)
-        enqueue_frame(c, d_frames + (size_t)f * frame_bytes, c->out_dev + f, evp, f + 1 < nframes);
-    HIPCHK(hipGetLastError());
-    if (nframes)
-        HIPCHK(hipMemcpyAsync(c->out_host, c->out_dev, sizeof(VoFrameOut) * nframes, hipMemcpyDeviceToHost, c->s));
-    HIPCHK(hipStreamSynchronize(c->s));
-    if (evp) {
-        const int nk = vo::kernel_count();
-        c->ktime_ms.assign(nk, 0.f);
-        c->kcount.assign(nk, 0);
-        for (const auto& sp : rec.spans) {
-            float ms = 0.f;
-            (void)hipEventElapsedTime(&ms, c->ev_pool[sp.second], c->ev_pool[sp.second + 1]);
-            c->ktime_ms[sp.first] += ms;
-            c->kcount[sp.first] += 1;
-        }
+    const int base = c->fidx;
+    for (int f0 = 0; f0 < nframes; f0 += VO_CHUNK) {
+        const int nf = std::min(VO_CHUNK, nframes - f0);
+        rc = run_chunk(c, d_frames + (size_t)f0 * frame_bytes, frame_bytes, nf, c->out_dev, base, evp, false);
+        if (rc) return rc;
     }
+    if (nframes)
+        HIPCHK(hipMemcpy(c->out_host, c->out_dev, sizeof(VoFrameOut) * nframes, hipMemcpyDeviceToHost));
+    rc = finish_timing(c, evp);
+    if (rc) return rc;
+    c->last_frames = nframes;
     for (int f = 0; f < nframes; ++f) {
         const VoFrameOut& o = c->out_host[f];
         if (poses_out) std::memcpy(poses_out + 12 * (size_t)f, o.pose, sizeof(o.pose));
@@ -759,11 +724,18 @@ int vo_enable_kernel_timing(vo_ctx* c, int on)
 
 int vo_last_kernel_times(vo_ctx* c, const char** names, float* ms, int cap)
 {
+    return vo_last_kernel_stats(c, names, ms, nullptr, cap);
+}
+
+int vo_last_kernel_stats(vo_ctx* c, const char** names, float* ms_per_launch, float* frames_per_launch, int cap)
+{
     if (!c) return VO_ERR_ARG;
     int nk = std::min<int>((int)c->ktime_ms.size(), cap);
     for (int k = 0; k < nk; ++k) {
         if (names) names[k] = vo::kernel_name(k);
-        if (ms) ms[k] = c->kcount[k] ? c->ktime_ms[k] / (float)c->kcount[k] : -1.f;
+        if (ms_per_launch) ms_per_launch[k] = c->kcount[k] ? c->ktime_ms[k] / (float)c->kcount[k] : -1.f;
+        if (frames_per_launch)
+            frames_per_launch[k] = c->klaunch[k] ? (float)c->last_frames / (float)c->klaunch[k] : 0.f;
     }
     return nk;
 }
@@ -772,7 +744,7 @@ int vo_last_kernel_times(vo_ctx* c, const char** names, float* ms, int cap)
 int vo_debug_stamps(vo_ctx* c, unsigned long long* out, int n)
 {
     if (!c || !c->d.dbg) return 0;
-    int m = std::min(n, c->max_hyp * 16);
+    int m = std::min(n, c->d.max_hyp * 16);
     HIPCHK(hipStreamSynchronize(c->s));
     HIPCHK(hipMemcpy(out, c->d.dbg, sizeof(unsigned long long) * m, hipMemcpyDeviceToHost));
     return m;

@@ -1,100 +1,111 @@
 // vo_internal.h -- device-resident state and buffer layout of one vo_ctx, shared by
 // the HIP kernels (vo_kernels.hip) and the host driver (vo_api.cpp).
 //
+// Execution model: frames are processed in WINDOWS of up to B
+// frames per launch.  Extract (stencil / select / describe) runs B frames per launch on
+// its own queue into a ring of keypoint/descriptor slots; a POSE PASS (match, RANSAC x2,
+// refit, triangulate, finalize) runs the window [lo, lo + B) of uncommitted frames, each
+// frame speculatively matched against frame f-1.  k_finalize walks the window in frame
+// order, applies the trajectory loop's rules (VisualOdometry.cpp:68-189) and commits every
+// frame whose speculation holds; the first frame after a skipped one is re-run by the next
+// pass against the right previous frame.  So results are those of the sequential loop.
+//
 // HBM layout (allocated once per ctx in vo_create; the reference allocates every
 // cl::Buffer per frame, corner_detection_parallel_GPU.cpp:45-49,85 and
-// FREAK_feature_descriptor_parallel_GPU.cpp:53-78):
-//   frame_in    u8  W*H         staging for host-supplied frames
-//   blurred     u8  W*H         7x7 Gaussian output (read back by describe)
-//   response    f32 W*H         optional dense R map (debug / parity only)
-//   cand        u64 256/tile    NMS survivors per 64x16 tile, key = Rbits<<32 | row<<16 | col
-//   tilerows    u8  16/tile     survivors per tile row (select emits raster order from them)
-//   ckeys       u64 256/tile    compact survivors (only when they overflow select's LDS)
-//   selbits     u64 4/tile      selected-survivor bitmap (only when it overflows LDS)
-//   hist        u32 4096        coarse histogram of candidate R (top-N boundary)
-//   kps[2]      int2 N          raster-ordered keypoints, slot ping-pong
-//   desc[2]     u64 8N          packed 512-test descriptors (slot ping-pong)
-//   pre[2]      u32 N           tests 0..31 (the matcher's 32-bit prefix)
-//   match_j     i32 N           best cur index per prev query, -1 if rejected
-//   pts         f64 4N          matched (x1,y1,x2,y2), ascending prev index
-//   hypF        f64 9*2000      per-hypothesis F (kept for the refit)
-//   counts      i32 2000        per-hypothesis inlier counts
-//   inl         i32 N           bestInlierSet indices
-//   model_p     f32 4N          model inliers (x1,y1,x2,y2) as cv::Point2f pairs
-//   maxit_tab   u16 tri(N)      ransac.cpp:179-190 iteration bound per (M, best)
-//   gt          f64 12*gt_cap   ground-truth rows for the GT scale
-//   out         VoFrameOut per frame of a batch
+// FREAK_feature_descriptor_parallel_GPU.cpp:53-78).  x B = one copy per frame of a batch.
+//   frame_in    u8  W*H            staging for host-supplied frames
+//   blurred     u8  W*H      x B   7x7 Gaussian output (read back by describe)
+//   response    f32 W*H            optional dense R map (debug / parity only)
+//   cand        u64 256/tile x B   NMS survivors per 64x16 tile, key = Rbits<<32 | row<<16 | col
+//   tilerows    u8  16/tile  x B   survivors per tile row (select emits raster order from them)
+//   ckeys       u64 256/tile x B   compact survivors (only when they overflow select's LDS)
+//   selbits     u64 4/tile   x B   selected-survivor bitmap (only when it overflows LDS)
+//   hist        u32 4096     x B   coarse histogram of candidate R (top-N boundary)
+//   kps         int2 N  x SLOTS    raster-ordered keypoints: ring slot f % VO_RING, carry, stage
+//   desc        u64 8N  x SLOTS    packed 512-test descriptors
+//   pre         u32 N   x SLOTS    tests 0..31 (the matcher's 32-bit prefix)
+//   match_j     i32 N        x B   best cur index per prev query, -1 if rejected
+//   match_pairs int2 N       x B   (prev, cur) matches, ascending prev index
+//   pts         f64 4N       x B   matched (x1,y1,x2,y2)
+//   hypF        f64 9*H      x B   per-hypothesis F (kept for the refit)
+//   counts      i32 H        x B   per-hypothesis inlier counts
+//   inlmask     u64 H*N/64   x B   per-hypothesis Sampson inlier bits
+//   inl         i32 N        x B   bestInlierSet indices
+//   model_p     f32 4N       x B   refit inliers (x1,y1,x2,y2) as cv::Point2f pairs
+//   work        VoWork       x B   per-frame control state of the window
+//   maxit_tab   u16 tri(N)         ransac.cpp:179-190 iteration bound per (M, best)
+//   gt          f64 12*gt_cap      ground-truth rows for the GT scale
+//   out         VoFrameOut per frame of a call
 #pragma once
 #include <stdint.h>
 
 #define VO_HIST_BINS 4096
-// keypoint/descriptor slots: frame f of the pipeline extracts into ring slot f % VO_RING_SLOTS;
-// a prev that must outlive its ring slot (frames skipped after it) is copied to the carry
-// slot; the stage APIs (vo_extract / vo_match) use their own two slots
-#define VO_RING_SLOTS 8
-#define VO_CARRY_SLOT 8
-#define VO_STAGE_SLOT 9
-#define VO_SLOTS 11
-#define VO_EXT_RING 16         // per-frame extract results, indexed f & (VO_EXT_RING - 1)
-#define VO_EXT_QUEUES 3        // extract queues: frame f on queue f % VO_EXT_QUEUES (+1 pose queue = 4 HW queues)
-// ctr words: in-launch arrival counters [0, VO_CTR_COUNTERS), then the cross-queue frame
-// counters on lines of their own: the pose chain's (monotonic, read by the extract queues'
-// stream-wait-value packets) and one extract-done word per ring entry (polled by k_match)
-#define VO_CTR_COUNTERS 16
-#define VO_CTR_DESCRIBE 4      // + extract queue
-#define VO_SYNC_POSE 48        // frames whose pose chain is complete
-#define VO_SYNC_EXT 64         // + (f & (VO_EXT_RING - 1)): f + 1 once frame f is extracted
-#define VO_CTR_WORDS 96
+// keypoint/descriptor slots: frame f (since vo_reset) is extracted into ring slot
+// f % VO_RING; the last valid frame's copy lives in the carry slot during a skip run; the
+// stage APIs (vo_extract / vo_match) use their own two slots
+#define VO_RING 256
+#define VO_CARRY_SLOT VO_RING
+#define VO_STAGE_SLOT (VO_RING + 1)
+#define VO_SLOTS (VO_RING + 3)
+// frames per host chunk: a chunk never extracts over a slot one of its passes still reads
+// (frame f's slot is rewritten by frame f + VO_RING; passes read frames >= lo - 1)
+#define VO_CHUNK (VO_RING - 1)
+#define VO_MAX_BATCH 64
+#define VO_DEFAULT_BATCH 16
+// ctr words: cross-queue counters on lines of their own
+#define VO_CTR_DESCRIBE 0      // describe's in-launch arrival counter
+#define VO_SYNC_EXT 32         // frames extracted since vo_reset (the pose queue waits on it)
+#define VO_CTR_WORDS 64
 #define VO_MAX_HYP 2000
 #define VO_HYP_CHUNK0 256
-#define VO_RED_THREADS 256
-
-// frame modes for k_frame_begin
-#define VO_MODE_FRAME 0        // full trajectory-loop iteration
-#define VO_MODE_MISSING 1      // image missing: only push T_curr
-#define VO_MODE_EXTRACT 2      // vo_extract: extract into slot 0, no state change
-#define VO_MODE_STAGE 3        // stage APIs (match / ransac / pose): status OK, no trajectory
 
 struct VoFrameOut {
     int32_t status, n_kps, n_matches, n_inl, best_k, n_eval, fitted, frame;
     double pose[12];
 };
 
-// Extract-side state.  The extract kernels of frames f+1, f+2, ... run on their own queues
-// while frame f's match -> pose chain runs; they never touch VoState, and the pose chain only
-// reads the ring entries of its own frame here (the carry copy in finalize reads a slot no
-// extract in flight writes), so the queues never write the same field.
+// Extract-side state, per keypoint/descriptor slot.
 struct VoExt {
-    int32_t slot[VO_EXT_RING];    // slot extracted for frame f (ring f & 15); -1: image missing
-    int32_t status[VO_EXT_RING];  // VO_STATUS_OK, or VO_STATUS_OVERFLOW (select capacity)
     int32_t n_kps[VO_SLOTS];
-    int32_t stage_status;  // status of the last stage extract (vo_extract)
-    int32_t pad[2];
+    int32_t status[VO_SLOTS];   // VO_STATUS_OK, VO_STATUS_OVERFLOW (select capacity), VO_STATUS_MISSING
 };
 
-struct VoState {
-    int32_t frame;        // index of the frame being processed
-    int32_t status;       // VO_STATUS_* of the current frame
-    int32_t mode;
-    int32_t cur, prev;    // keypoint/descriptor slots: prev always; cur only in stage mode
-                          // (frame mode: VoExt::slot[frame & (VO_EXT_RING - 1)])
-    uint32_t cand_count;
+// Per-frame control state of a pose pass (one per window frame).  k_match writes the
+// header, the RANSAC launches their counters and the replay's result, k_refit the model,
+// k_triangulate the cheirality counts; k_finalize reads it all.
+struct VoWork {
+    int32_t status;       // VO_STATUS_* (speculative: assumes frame - 1 was a valid frame)
+    int32_t frame;        // frame index since vo_reset
+    int32_t cur, prev;    // keypoint/descriptor slots
     int32_t M;            // matches
     int32_t scored;       // T * floor(M / T)   (ransac.cpp:152-157)
     int32_t maxit, best, bestk, k_done, need_more, n_eval;
-    int32_t n_inl, fitted;
-    int32_t model_n;
-    int32_t degenerate;
-    int32_t counts4[4];
-    int32_t last_valid;
-    int32_t out_index;    // slot in the batch output array
-    int32_t pad0;
+    int32_t n_inl;        // best hypothesis' inlier count
+    int32_t fitted;       // refit ran (>= 8 inliers); else the model leaks (quirk 9)
+    int32_t n_fit;        // refit inliers (== n_inl when fitted)
+    int32_t degenerate;   // getPose would throw on this frame's F (PoseUpdate.hpp:71-73)
+    int32_t counts4[4];   // positive-depth counts per (R, t) candidate
+    uint32_t ctr[4];      // in-launch arrival counters: [0] match, [1] ransac chunk 1, [2] chunk 2
     uint64_t frame_seed;
-    double model_F[9];
+    double F[9];          // refit F (valid iff fitted)
     double R1[9], R2[9], t[3];
-    double pose_R[9], pose_t[3];   // last getPose result (stage API)
-    double scale_override;         // NaN: GT-derived scale
+};
+
+// Trajectory state (VisualOdometry::run's locals), read and written by k_finalize only.
+struct VoState {
+    int32_t lo;           // frames committed since vo_reset (the next pass starts here)
+    int32_t end;          // end of the frames enqueued so far
+    int32_t prev_slot;    // slot of the last valid frame's keypoints / descriptors (desc1)
+    int32_t last_valid;   // VisualOdometry.cpp:62,164
+    int32_t model_n;      // FundamentalMatrix model (VisualOdometry.cpp:49): inliers of the last fit
+    int32_t model_degenerate;
+    int32_t pose_status;  // stage vo_pose result
+    int32_t pad;
+    double model_F[9];
+    double model_R[9], model_t[3];   // getPose(model) before scaling: det-fixed R, signed unit t
     double Tcurr[16];
+    double pose_R[9], pose_t[3];     // stage vo_pose result
+    double scale_override;           // stage vo_pose scale
 };
 
 // Everything a kernel needs, passed by value.
@@ -108,61 +119,61 @@ struct VoDev {
     double ransac_p, sampson_thr;
     int T;
     int maxit_initial;
+    int max_hyp;
+    int B;                // window / extract batch capacity (frames)
     uint64_t seed;
     double K[9];
-    uint32_t cand_cap;
+    uint32_t cand_cap;    // per frame
+    int ntiles;
     int gt_n;
     uint8_t* frame_in;
-    uint8_t* blurred;
+    uint8_t* blurred;     // x B
     float* response;
-    uint64_t* cand;       // per stencil tile: up to 256 keys in tile-local raster order
-    uint8_t* tilerows;    // per stencil tile: candidate count of each of its 16 rows
-    uint64_t* ckeys;      // select: compact candidate keys when they exceed the LDS capacity
-    uint64_t* selbits;    // select: selected-key bitmap when it exceeds the LDS capacity
+    uint64_t* cand;       // x B: per stencil tile up to 256 keys in tile-local raster order
+    uint8_t* tilerows;    // x B: per stencil tile the candidate count of each of its 16 rows
+    uint64_t* ckeys;      // x B: select's compact keys when they exceed the LDS capacity
+    uint64_t* selbits;    // x B: select's selected-key bitmap when it exceeds the LDS capacity
     int sel_lds;          // select: dynamic LDS bytes
-    uint32_t* hist;
-    int2* kps[VO_SLOTS];
-    uint64_t* desc[VO_SLOTS];
-    uint32_t* pre[VO_SLOTS];
-    int32_t* match_j;
-    int2* match_pairs;
-    double* pts;
-    double* hypF;
-    int32_t* counts;
-    int32_t* inl;
-    uint64_t* inlmask;    // per hypothesis: Sampson inlier bits of the scored matches
+    uint32_t* hist;       // x B
+    int2* kps;            // x SLOTS (N each)
+    uint64_t* desc;       // x SLOTS (8N each)
+    uint32_t* pre;        // x SLOTS (N each)
+    int32_t* match_j;     // x B
+    int2* match_pairs;    // x B
+    double* pts;          // x B
+    double* hypF;         // x B
+    int32_t* counts;      // x B
+    int32_t* inl;         // x B
+    uint64_t* inlmask;    // x B: per hypothesis the Sampson inlier bits of the scored matches
     int mask_words;       // (N + 63) / 64
-    float* model_p;
+    float* model_p;       // x B
+    VoWork* work;         // x B
     const uint16_t* maxit_tab;
     const double* gt;
     VoState* st;
     VoExt* ext;
-    VoFrameOut* out;
-    unsigned* ctr;        // in-launch arrival counters: [0] match, [1] ransac, [2] triangulate,
-                          // [3] ransac chunk 2, [4] describe; cross-queue counters (VO_SYNC_*)
-    uint32_t seqno;       // frame pipeline: 1 + frame index since vo_reset; 0 outside it
-    uint32_t wait_next;   // finalize then waits for this frame's extract (seqno + 1), or 0
-    int eq;               // extract queue of this frame (its scratch: blurred .. hist)
+    unsigned* ctr;
     unsigned long long* dbg;   // diagnostic s_memtime stamps (VO_STAMPS builds only)
 };
 
 // launch wrappers (vo_kernels.hip)
 #include <hip/hip_runtime.h>
 namespace vo {
-void launch_frame_begin(const VoDev& d, int mode, hipStream_t s);
-void launch_stencil(const VoDev& d, const uint8_t* frame, int write_response, hipStream_t s);
-// fidx: frame index since vo_reset (frame pipeline; select picks the slot), or -1 for the
-// stage API (slot VO_STAGE_SLOT)
-void launch_select(const VoDev& d, int fidx, hipStream_t s);
+// extract of nb frames: frame f0 + z reads img0 + z * frame_bytes into slot
+// (slot_override >= 0 ? slot_override : (f0 + z) % VO_RING), scratch z.  publish > 0: the
+// last describe workgroup stores it to ctr[VO_SYNC_EXT] for the pose queue
+void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int nb, int write_response, hipStream_t s);
+void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s);
 int select_lds_bytes(int W, int H, int* key_cap);     // sets the kernel attribute; <0 on failure
-void launch_describe(const VoDev& d, int fidx, hipStream_t s);
-void launch_ext_missing(const VoDev& d, int fidx, hipStream_t s);   // extract side of a missing image
-void launch_match(const VoDev& d, hipStream_t s);          // + ordered compaction (last workgroup)
-void launch_ransac(const VoDev& d, int nhyp, hipStream_t s); // all hypotheses + replay (last workgroup)
-void launch_refit(const VoDev& d, int with_pose, hipStream_t s);
-void launch_pose_prep(const VoDev& d, hipStream_t s);
-void launch_triangulate(const VoDev& d, hipStream_t s);    // + finalize / next-frame setup
-void launch_missing(const VoDev& d, hipStream_t s);
+void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned publish, hipStream_t s);
+void launch_ext_missing(const VoDev& d, int slot, hipStream_t s);   // extract side of a missing image
+// pose pass over the window (stage = 0) or over work[0] prepared by a stage API (stage = 1)
+void launch_match(const VoDev& d, int stage, hipStream_t s);        // + ordered compaction per frame
+void launch_ransac(const VoDev& d, int stage, hipStream_t s);       // all hypotheses + replay per frame
+void launch_refit(const VoDev& d, int with_pose, int stage, hipStream_t s);
+void launch_triangulate(const VoDev& d, int stage, hipStream_t s);
+void launch_finalize(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s);
+void launch_pose_stage(const VoDev& d, int phase, hipStream_t s);   // vo_pose: 0 prepare, 1 choose
 void launch_selftest_arith(const float* fa, const float* fb, float* fo, const double* da,
                            const double* db, double* dout, int n, hipStream_t s);
 int kernel_count();

@@ -344,35 +344,6 @@ __device__ __forceinline__ unsigned long long ballot64(bool p) { return __ballot
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 // ---------------------------------------------------------------------------
-// frame begin: reset per-frame counters (1 block)
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(1024) k_frame_begin(VoDev d, int mode)
-{
-    VoState* st = d.st;
-    for (int i = threadIdx.x; i < VO_HIST_BINS; i += blockDim.x) d.hist[i] = 0;
-    if (threadIdx.x == 0) {
-        st->mode = mode;
-        st->cand_count = 0;
-        st->M = 0;
-        st->n_inl = 0;
-        st->fitted = 0;
-        st->degenerate = 0;
-        st->bestk = -1;
-        st->n_eval = 0;
-        st->need_more = 0;
-        for (int c = 0; c < 4; ++c) st->counts4[c] = 0;
-        if (mode == VO_MODE_FRAME) {
-            st->status = st->frame == 0 ? VO_STATUS_FIRST : VO_STATUS_OK;
-            st->frame_seed = mix64(d.seed + 0x632BE59BD9B4E019ULL * (uint64_t)(st->frame + 1));
-        } else if (mode == VO_MODE_MISSING) {
-            st->status = VO_STATUS_MISSING;
-        } else {
-            st->status = VO_STATUS_OK;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // stencil: blur7x7 -> gradients -> 5x5 response -> strict 3x3 NMS candidates
 // One 256-thread workgroup per 64x16 output tile; every intermediate lives in LDS.
 // kernels/feature_extraction_kernel_functions.c:43-120, corner_detection_parallel_GPU.cpp:146-180
@@ -395,7 +366,8 @@ __device__ __forceinline__ int refl101(int i, int n)
     return i;
 }
 
-__global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restrict__ img, int write_response)
+__global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restrict__ img0, size_t frame_bytes,
+                                                  int write_response)
 {
     __shared__ uint8_t s_src[ST_SH][ST_SW];
     __shared__ uint32_t s_hb[ST_SH][ST_BW];
@@ -407,6 +379,13 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
     const int W = d.W, H = d.H;
     const int x0 = blockIdx.x * ST_TW, y0 = blockIdx.y * ST_TH;
     const int tid = threadIdx.x;
+    // frame z of the batch: its image and its scratch copy
+    const int z = blockIdx.z;
+    const uint8_t* __restrict__ img = img0 + (size_t)z * frame_bytes;
+    uint8_t* blurred = d.blurred + (size_t)z * W * H;
+    uint64_t* cand = d.cand + (size_t)z * d.cand_cap;
+    uint8_t* tilerows = d.tilerows + (size_t)z * d.ntiles * ST_TH;
+    uint32_t* hist = d.hist + (size_t)z * VO_HIST_BINS;
 
     // 1. source tile with BORDER_REFLECT_101 addressing
     for (int e = tid; e < ST_SH * ST_SW; e += 256) {
@@ -432,7 +411,7 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
         s_bl[r][c] = (float)b;
         int y = y0 - 4 + r, x = x0 - 4 + c;
         if (r >= 4 && r < 4 + ST_TH && c >= 4 && c < 4 + ST_TW && y < H && x < W)
-            d.blurred[(size_t)y * W + x] = (uint8_t)b;
+            blurred[(size_t)y * W + x] = (uint8_t)b;
     }
     __syncthreads();
     // 4. gradients (kernel .c:59-76), 0 outside 1<=i<=H-2, 1<=j<=W-2
@@ -510,7 +489,7 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
     }
     __syncthreads();
     const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-    if (tid < ST_TH) d.tilerows[tile * ST_TH + tid] = (uint8_t)__popcll(s_bal[tid]);
+    if (tid < ST_TH) tilerows[tile * ST_TH + tid] = (uint8_t)__popcll(s_bal[tid]);
 #pragma unroll
     for (int kk = 0; kk < ST_TH / 4; ++kk) {
         if (!mxk[kk]) continue;
@@ -520,10 +499,10 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
         off += __popcll(s_bal[r] & ((1ull << lane) - 1ull));
         const int i = y0 + r, j = x0 + c;
         const uint32_t bits = __float_as_uint(cvk[kk]);
-        d.cand[(size_t)tile * (ST_TW * ST_TH / 4) + off] = ((uint64_t)bits << 32) | ((uint64_t)i << 16) | (uint64_t)j;
+        cand[(size_t)tile * (ST_TW * ST_TH / 4) + off] = ((uint64_t)bits << 32) | ((uint64_t)i << 16) | (uint64_t)j;
         uint32_t bin = (bits - d.thr_bits) >> 15;
         if (bin > VO_HIST_BINS - 1) bin = VO_HIST_BINS - 1;
-        atomicAdd(&d.hist[bin], 1u);
+        atomicAdd(&hist[bin], 1u);
     }
 }
 
@@ -592,19 +571,19 @@ __device__ __forceinline__ uint32_t sel_bin(uint64_t key, uint32_t thr_bits)
 //   D  selected-key bitmap (ballots) + per-(row, tile) selected counts (u8, LDS atomics)
 //   E  chunked block scan over the (row, tile) segments in raster order
 //   F  each selected key computes its raster position directly and writes its keypoint
-__device__ __forceinline__ int ext_slot(const VoDev& d, int fidx)
+// slot of frame f0 + z of an extract batch (vo_internal.h: ring slot, or a stage slot)
+__device__ __forceinline__ int ext_slot(int f0, int z, int slot_override)
 {
-    return fidx < 0 ? VO_STAGE_SLOT : fidx % VO_RING_SLOTS;
+    return slot_override >= 0 ? slot_override : (f0 + z) % VO_RING;
 }
 
-// the pose chain's current slot: frame mode reads the extract ring, stage mode st->cur
-__device__ __forceinline__ int cur_slot(const VoDev& d, const VoState* st)
+__global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_override)
 {
-    return st->mode == VO_MODE_FRAME ? d.ext->slot[st->frame & (VO_EXT_RING - 1)] : st->cur;
-}
-
-__global__ void __launch_bounds__(1024) k_select(VoDev d, int fidx)
-{
+    // frame z of the batch: its scratch copy (written by k_stencil's z-slice)
+    const int z = blockIdx.x;
+    const uint8_t* tilerows = d.tilerows + (size_t)z * d.ntiles * ST_TH;
+    const uint64_t* cand = d.cand + (size_t)z * d.cand_cap;
+    uint32_t* hist = d.hist + (size_t)z * VO_HIST_BINS;
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ uint32_t s_hs[16];
     __shared__ int s_wsum[16];
@@ -627,8 +606,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int fidx)
     const size_t TCAP = ST_TW * ST_TH / 4;
     if (tid == 0) {
         s_nbnd = 0; s_b = -1; s_above = 0;
-        const int slot = ext_slot(d, fidx);    // ring slot f % R (vo_api.cpp enqueue_frame)
-        s_slot = slot;
+        s_slot = ext_slot(f0, z, slot_override);
     }
     VO_STAMP(d, 1990, 0);
     // A
@@ -639,7 +617,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int fidx)
     for (int u = 0; u < 2; ++u) {
         const int t = tid * tpt + u;
         if (u < tpt && t < ntiles) {
-            uint4 rc = reinterpret_cast<const uint4*>(d.tilerows)[t];
+            uint4 rc = reinterpret_cast<const uint4*>(tilerows)[t];
             s_rows[t] = rc;
             const uint32_t w4[4] = {rc.x, rc.y, rc.z, rc.w};
             int tot = 0;
@@ -668,12 +646,12 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int fidx)
     }
     if (tid == 0) s_tpre[ntiles] = C;
     const bool bits_lds = C <= SEL_LDS_BITS;
-    uint64_t* bits = bits_lds ? s_bitsl : d.selbits;
+    uint64_t* bits = bits_lds ? s_bitsl : d.selbits + (size_t)z * (d.cand_cap / 64 + 1);
     for (int w = tid; w < (C + 63) / 64; w += 1024) bits[w] = 0ull;
     __syncthreads();
     // B
     const bool staged = C <= L.key_cap;
-    uint64_t* keys = staged ? s_keys : d.ckeys;
+    uint64_t* keys = staged ? s_keys : d.ckeys + (size_t)z * d.cand_cap;
     {
         auto slot_of = [&](int g) -> size_t {
             int lo = 0, hi = ntiles - 1;
@@ -688,7 +666,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int fidx)
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int g = g0 + u * 1024;
-                v[u] = g < C ? d.cand[slot_of(g)] : 0ull;
+                v[u] = g < C ? cand[slot_of(g)] : 0ull;
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u)
@@ -704,7 +682,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int fidx)
     if (C > N) {
         uint32_t h[4], hs = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) { h[q] = d.hist[4 * tid + q]; hs += h[q]; }
+        for (int q = 0; q < 4; ++q) { h[q] = hist[4 * tid + q]; hs += h[q]; }
         uint32_t suf = hs;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
@@ -825,7 +803,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int fidx)
     VO_STAMP(d, 1990, 5);
     // F
     const int slot = s_slot;
-    int2* out = d.kps[slot];
+    int2* out = d.kps + (size_t)slot * N;
     for (int r0 = 0; r0 < nround; r0 += 4) {
         uint64_t v[4];
 #pragma unroll
@@ -863,15 +841,10 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int fidx)
     }
     VO_STAMP(d, 1990, 6);
     // select is the histogram's only reader: leave it zeroed for the next frame's stencil
-    for (int i = tid; i < VO_HIST_BINS; i += 1024) d.hist[i] = 0u;
+    for (int i = tid; i < VO_HIST_BINS; i += 1024) hist[i] = 0u;
     if (tid == 0) {
-        const int status = ovf ? VO_STATUS_OVERFLOW : VO_STATUS_OK;
         d.ext->n_kps[slot] = ovf ? 0 : (C < N ? C : N);
-        if (fidx >= 0) {
-            d.ext->slot[fidx & (VO_EXT_RING - 1)] = slot;
-            d.ext->status[fidx & (VO_EXT_RING - 1)] = status;
-        }
-        else d.ext->stage_status = status;
+        d.ext->status[slot] = ovf ? VO_STATUS_OVERFLOW : VO_STATUS_OK;
     }
 }
 
@@ -919,15 +892,13 @@ __device__ __forceinline__ void publish_seq(unsigned* flag, unsigned v)
     if (threadIdx.x == 0) __hip_atomic_store((gu32*)flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// extract side of a missing image (VisualOdometry.cpp:77-82): the frame owns no slot (-1);
-// its pose chain reads none, so the next frame's choice only has to avoid prev
-__global__ void k_ext_missing(VoDev d, int fidx)
+// extract side of a missing image (VisualOdometry.cpp:77-82): the slot holds no keypoints
+__global__ void k_ext_missing(VoDev d, int slot)
 {
     if (threadIdx.x == 0) {
-        d.ext->slot[fidx & (VO_EXT_RING - 1)] = -1;
-        d.ext->status[fidx & (VO_EXT_RING - 1)] = VO_STATUS_OK;
+        d.ext->n_kps[slot] = 0;
+        d.ext->status[slot] = VO_STATUS_MISSING;
     }
-    if (d.seqno) publish_seq(d.ctr + VO_SYNC_EXT + (fidx & (VO_EXT_RING - 1)), d.seqno);
 }
 
 // ---------------------------------------------------------------------------
@@ -938,7 +909,8 @@ __global__ void k_ext_missing(VoDev d, int fidx)
 #define DS_KPB 8
 #define DS_TSTRIDE 905
 
-__device__ __forceinline__ void describe_block(const VoDev& d, int cur, int n, int base)
+__device__ __forceinline__ void describe_block(const VoDev& d, const uint8_t* __restrict__ img, int cur, int n,
+                                               int base)
 {
     const int nk = min(DS_KPB, n - base);
     __shared__ float s_I0[DS_KPB][VO_FREAK_NPOINTS];
@@ -948,8 +920,7 @@ __device__ __forceinline__ void describe_block(const VoDev& d, int cur, int n, i
     __shared__ uint8_t s_I1[DS_KPB][48];
     const int tid = threadIdx.x;
     const int W = d.W, H = d.H;
-    const uint8_t* img = d.blurred;
-    const int2* kps = d.kps[cur] + base;
+    const int2* kps = d.kps + (size_t)cur * d.N + base;
 
     for (int e = tid; e < nk * VO_FREAK_NPOINTS; e += 256) {
         int k = e / VO_FREAK_NPOINTS, p = e - k * VO_FREAK_NPOINTS;
@@ -1004,41 +975,29 @@ __device__ __forceinline__ void describe_block(const VoDev& d, int cur, int n, i
         bool bit = s_I1[k][c_pair_p[e]] > s_I1[k][c_pair_q[e]];
         unsigned long long word = ballot64(bit);
         if (lane == 0) {
-            d.desc[cur][(size_t)(base + k) * 8 + w] = word;
-            if (w == 0) d.pre[cur][base + k] = (uint32_t)word;
+            d.desc[((size_t)cur * d.N + base + k) * 8 + w] = word;
+            if (w == 0) d.pre[(size_t)cur * d.N + base + k] = (uint32_t)word;
         }
     }
 }
 
-__global__ void __launch_bounds__(256) k_describe(VoDev d, int fidx)
+// grid (N / DS_KPB, nb): frame z = blockIdx.y of the batch.  publish > 0: the last
+// workgroup of the launch tells the pose queue that frames < publish are extracted
+__global__ void __launch_bounds__(256) k_describe(VoDev d, int f0, int slot_override, unsigned publish)
 {
-    const int cur = ext_slot(d, fidx);
+    const int z = blockIdx.y;
+    const int cur = ext_slot(f0, z, slot_override);
     const int n = d.ext->n_kps[cur];
     const int base = blockIdx.x * DS_KPB;
-    if (base < n) describe_block(d, cur, n, base);
-    if (!d.seqno) return;
-    // frame pipeline: the last workgroup tells the pose queue this frame's descriptors are in
+    if (base < n) describe_block(d, d.blurred + (size_t)z * d.W * d.H, cur, n, base);
+    if (!publish) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __shared__ unsigned s_last;
-    if (!arrive_last(d.ctr + VO_CTR_DESCRIBE + d.eq, gridDim.x, &s_last)) return;
-    if (threadIdx.x == 0) d.ctr[VO_CTR_DESCRIBE + d.eq] = 0u;
-    publish_seq(d.ctr + VO_SYNC_EXT + (fidx & (VO_EXT_RING - 1)), d.seqno);
-}
-
-// next frame's bookkeeping (VisualOdometry.cpp:68-100 loop head): status, slot, sampler
-// seed, counters, histogram.  Run by the workgroup that finalizes the current frame.
-__device__ void setup_next_frame(const VoDev& d, VoState* st, int f)
-{
-    if (threadIdx.x == 0) {
-        st->mode = VO_MODE_FRAME;
-        st->status = f == 0 ? VO_STATUS_FIRST : VO_STATUS_OK;
-        st->frame_seed = mix64(d.seed + 0x632BE59BD9B4E019ULL * (uint64_t)(f + 1));
-        st->cand_count = 0; st->M = 0; st->n_inl = 0; st->fitted = 0; st->degenerate = 0;
-        st->bestk = -1; st->n_eval = 0; st->need_more = 0;
-        for (int c = 0; c < 4; ++c) st->counts4[c] = 0;
-    }
+    if (!arrive_last(d.ctr + VO_CTR_DESCRIBE, gridDim.x * gridDim.y, &s_last)) return;
+    if (threadIdx.x == 0) d.ctr[VO_CTR_DESCRIBE] = 0u;
+    publish_seq(d.ctr + VO_SYNC_EXT, publish);
 }
 
 // ---------------------------------------------------------------------------
@@ -1080,48 +1039,57 @@ __host__ __device__ inline int match_blocks(int N, int match_bits)
     return match_bits == 32 ? (N + MT_QPB - 1) / MT_QPB : (N + 3) / 4;
 }
 
-// Frame pipeline: one workgroup waits for the extract queue's counter of the next frame
-// (finalize_frame, at the end of the previous frame's chain), so k_match always starts behind
-// a kernel boundary.  Lane 0 polls, then an agent-scope acquire + barrier.  The extract of
-// frame f+1 waits only for frame f-6's chain, long complete, so the poll ends; the bound
-// (~1 s) only guards against a broken pipeline: the caller then marks the frame STALLED.
-__device__ __forceinline__ bool wait_seq(unsigned* flag, unsigned v)
+// Window of a pose pass: frames [st->lo, st->lo + n), n = min(B, st->end - st->lo); a stage
+// call works on work[0] alone.  st changes only in k_finalize, the pass's last kernel.
+__device__ __forceinline__ int win_count(const VoDev& d, int stage)
 {
-    __shared__ int s_ok;
-    if (threadIdx.x == 0) {
-        int ok = 0;
-        for (unsigned spin = 0; spin < (1u << 24); ++spin) {
-            // an atomic read-modify-write, not a load: a polled line can stay cached in this
-            // XCD's L2 and miss the producer's write-through store from another XCD
-            if (__hip_atomic_fetch_or((gu32*)flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= v) { ok = 1; break; }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        s_ok = ok;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    return s_ok != 0;
+    if (stage) return 1;
+    const int n = d.st->end - d.st->lo;
+    return n < d.B ? n : d.B;
 }
 
-__global__ void __launch_bounds__(256) k_match(VoDev d)
+__device__ __forceinline__ uint64_t frame_seed_of(const VoDev& d, int f)
 {
-    VoState* st = d.st;
-    if (blockIdx.x == 0) VO_STAMP(d, 1993, 0);
-    if (st->mode == VO_MODE_FRAME && d.ext->status[st->frame & (VO_EXT_RING - 1)] != VO_STATUS_OK) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) st->status = VO_STATUS_OVERFLOW;   // select capacity
-        return;
+    return mix64(d.seed + 0x632BE59BD9B4E019ULL * (uint64_t)(f + 1));
+}
+
+// grid (match_blocks, B): frame wf = blockIdx.y of the window.  Speculation: the previous
+// frame of window frame wf > 0 is frame f - 1 (k_finalize re-runs f when that was skipped).
+__global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
+{
+    const int wf = blockIdx.y;
+    if (wf >= win_count(d, stage)) return;
+    VoWork* w = d.work + wf;
+    int f, cur, prev, status = VO_STATUS_OK;
+    if (stage) {
+        f = -1; prev = VO_STAGE_SLOT; cur = VO_STAGE_SLOT + 1;
+    } else {
+        f = d.st->lo + wf;
+        cur = f % VO_RING;
+        prev = wf == 0 ? d.st->prev_slot : (f - 1) % VO_RING;
+        const int es = d.ext->status[cur];
+        if (f == 0) status = VO_STATUS_FIRST;                 // VisualOdometry.cpp:58,64-66
+        else if (es != VO_STATUS_OK) status = es;              // MISSING / OVERFLOW
     }
-    if (st->status != VO_STATUS_OK) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        w->frame = f; w->cur = cur; w->prev = prev;
+        w->bestk = -1; w->n_eval = 0; w->n_inl = 0; w->fitted = 0; w->n_fit = 0; w->degenerate = 0;
+        w->need_more = 0;
+        for (int c = 0; c < 4; ++c) w->counts4[c] = 0;
+        if (!stage) w->frame_seed = frame_seed_of(d, f);
+        if (status != VO_STATUS_OK) { w->status = status; w->M = 0; w->scored = 0; }
+    }
+    if (status != VO_STATUS_OK) return;
     __shared__ unsigned s_last;
     __shared__ int s_wsum[4];
     __shared__ uint32_t s_cand[4096];
-    const int prev = st->prev, cur = cur_slot(d, st);
+    const int N = d.N;
     const int n1 = d.ext->n_kps[prev], n2 = d.ext->n_kps[cur];
+    int32_t* match_j = d.match_j + (size_t)wf * N;
     const int lane = threadIdx.x & 63;
     if (d.match_bits == 32) {
         if (blockIdx.x * MT_QPB < n1) {
-            const uint32_t* cand = d.pre[cur];
+            const uint32_t* cand = d.pre + (size_t)cur * N;
             for (int j0 = threadIdx.x; j0 < n2; j0 += 4 * 256) {
                 uint32_t v[4];
 #pragma unroll
@@ -1134,7 +1102,7 @@ __global__ void __launch_bounds__(256) k_match(VoDev d)
             uint32_t qv[MT_QPW], m1[MT_QPW], m2[MT_QPW];
 #pragma unroll
             for (int u = 0; u < MT_QPW; ++u) {
-                qv[u] = q0 + u < n1 ? d.pre[prev][q0 + u] : 0u;
+                qv[u] = q0 + u < n1 ? d.pre[(size_t)prev * N + q0 + u] : 0u;
                 m1[u] = 0xFFFFFFFFu;
                 m2[u] = 0xFFFFFFFFu;
             }
@@ -1149,18 +1117,18 @@ __global__ void __launch_bounds__(256) k_match(VoDev d)
 #pragma unroll
             for (int u = 0; u < MT_QPW; ++u) {
                 top2_wave(m1[u], m2[u]);
-                if (lane == 0 && q0 + u < n1) st_sc1(d.match_j + q0 + u, ratio_accept(m1[u], m2[u], d.ratio));
+                if (lane == 0 && q0 + u < n1) st_sc1(match_j + q0 + u, ratio_accept(m1[u], m2[u], d.ratio));
             }
         }
     } else {
         const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
         if (q < n1) {
             uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
-            const uint64_t* qd = d.desc[prev] + (size_t)q * 8;
+            const uint64_t* qd = d.desc + ((size_t)prev * N + q) * 8;
             uint64_t qw[8];
 #pragma unroll
             for (int w = 0; w < 8; ++w) qw[w] = qd[w];
-            const uint64_t* cd = d.desc[cur];
+            const uint64_t* cd = d.desc + (size_t)cur * N * 8;
             for (int j = lane; j < n2; j += 64) {
                 int dist = 0;
 #pragma unroll
@@ -1168,15 +1136,17 @@ __global__ void __launch_bounds__(256) k_match(VoDev d)
                 top2_insert(((uint32_t)dist << 16) | (uint32_t)j, m1, m2);
             }
             top2_wave(m1, m2);
-            if (lane == 0) st_sc1(d.match_j + q, ratio_accept(m1, m2, d.ratio));
+            if (lane == 0) st_sc1(match_j + q, ratio_accept(m1, m2, d.ratio));
         }
     }
     if (blockIdx.x == 0) VO_STAMP(d, 1993, 1);
-    if (!arrive_last(d.ctr + 0, gridDim.x, &s_last)) return;
+    if (!arrive_last(&w->ctr[0], gridDim.x, &s_last)) return;
     // ---- last workgroup: ordered compaction, thread t owns queries [t*per, (t+1)*per) ----
     const int tid = threadIdx.x, wave = tid >> 6;
-    const int2* kp1 = d.kps[prev];
-    const int2* kp2 = d.kps[cur];
+    const int2* kp1 = d.kps + (size_t)prev * N;
+    const int2* kp2 = d.kps + (size_t)cur * N;
+    int2* match_pairs = d.match_pairs + (size_t)wf * N;
+    double* pts = d.pts + (size_t)wf * 4 * N;
     const int per = (n1 + 255) / 256;            // <= 16 (N <= 4096)
     const int q0 = tid * per;
     VO_STAMP(d, 1993, 2);
@@ -1186,7 +1156,7 @@ __global__ void __launch_bounds__(256) k_match(VoDev d)
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
         int i = q0 + u;
-        js[u] = (u < per && i < n1) ? ld_sc1(d.match_j + i) : -1;
+        js[u] = (u < per && i < n1) ? ld_sc1(match_j + i) : -1;
         cnt += js[u] >= 0;
     }
     // all keypoint gathers in flight before the scan (no load-use chain per match)
@@ -1210,9 +1180,9 @@ __global__ void __launch_bounds__(256) k_match(VoDev d)
     for (int u = 0; u < 16; ++u) {
         if (js[u] >= 0) {
             int i = q0 + u, j = js[u];
-            d.match_pairs[pos] = make_int2(i, j);
+            match_pairs[pos] = make_int2(i, j);
             const int2 a = ka[u], b = kb[u];
-            double2* p = reinterpret_cast<double2*>(d.pts + 4 * (size_t)pos);
+            double2* p = reinterpret_cast<double2*>(pts + 4 * (size_t)pos);
             p[0] = make_double2((double)a.x, (double)a.y);
             p[1] = make_double2((double)b.x, (double)b.y);
             ++pos;
@@ -1220,10 +1190,10 @@ __global__ void __launch_bounds__(256) k_match(VoDev d)
     }
     if (tid == 0) {
         int M = ((s_wsum[0] + s_wsum[1]) + s_wsum[2]) + s_wsum[3];
-        st->M = M;
-        st->scored = (M / d.T) * d.T;
-        if (M < 8) st->status = VO_STATUS_FEW_MATCHES;
-        d.ctr[0] = 0u;
+        w->M = M;
+        w->scored = (M / d.T) * d.T;
+        w->status = M < 8 ? VO_STATUS_FEW_MATCHES : VO_STATUS_OK;   // VisualOdometry.cpp:108-115
+        w->ctr[0] = 0u;
     }
     VO_STAMP(d, 1993, 3);
 }
@@ -1535,35 +1505,40 @@ __device__ void inv4(const double* M, double* Inv)
 // path); second chunk: four single-wave hypotheses per workgroup, since it usually exits at
 // once (fewer workgroups to dispatch).
 template <int WPH, int HPB>
-__global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, int k1, int nhyp)
+__global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, int k1, int nhyp, int stage)
 {
-    VoState* st = d.st;
-    if (st->status != VO_STATUS_OK) return;
-    if (k0 > 0 && !st->need_more) return;          // the replay of [0, k0) already stopped
+    const int wf = blockIdx.y;                     // window frame
+    if (wf >= win_count(d, stage)) return;
+    VoWork* w = d.work + wf;
+    if (w->status != VO_STATUS_OK) return;
+    if (k0 > 0 && !w->need_more) return;           // the replay of [0, k0) already stopped
     __shared__ unsigned s_last;
     __shared__ int s_cnt[HPB][WPH];
     const int wave = threadIdx.x >> 6, h = wave / WPH, sw = wave - h * WPH;
     const int k = k0 + blockIdx.x * HPB + h;
     const int lane = threadIdx.x & 63;
-    const int M = st->M, scored = st->scored;
+    const int M = w->M, scored = w->scored;
+    const double* pts = d.pts + (size_t)wf * 4 * d.N;
+    int32_t* counts = d.counts + (size_t)wf * d.max_hyp;
     if (k < k1) {
         VO_STAMP(d, k, 0);
         int s8[8];
-        sample8(st->frame_seed, k, M, s8);
+        sample8(w->frame_seed, k, M, s8);
         VO_STAMP(d, k, 1);
         double F[9];
-        fit_F8_wave(d, d.pts, s8, lane, F, k);
+        fit_F8_wave(d, pts, s8, lane, F, k);
         VO_STAMP(d, k, 5);
         if (sw == 0 && lane < 9) {
             double v = 0.0;
 #pragma unroll
             for (int c = 0; c < 9; ++c) if (c == lane) v = F[c];
-            d.hypF[(size_t)k * 9 + lane] = v;
+            d.hypF[((size_t)wf * d.max_hyp + k) * 9 + lane] = v;
         }
         const int cnt =
-            count_inliers<WPH>(d.pts, scored, F, d.sampson_thr, lane, sw, d.inlmask + (size_t)k * d.mask_words);
+            count_inliers<WPH>(pts, scored, F, d.sampson_thr, lane, sw,
+                               d.inlmask + ((size_t)wf * d.max_hyp + k) * d.mask_words);
         if (WPH == 1) {
-            if (lane == 0) st_sc1(d.counts + k, cnt);
+            if (lane == 0) st_sc1(counts + k, cnt);
         } else if (lane == 0) {
             s_cnt[h][sw] = cnt;
         }
@@ -1575,10 +1550,10 @@ __global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, 
             int t = 0;
 #pragma unroll
             for (int w = 0; w < WPH; ++w) t += s_cnt[h][w];
-            st_sc1(d.counts + k, t);
+            st_sc1(counts + k, t);
         }
     }
-    unsigned* ctr = d.ctr + (k0 == 0 ? 1 : 3);
+    unsigned* ctr = &w->ctr[k0 == 0 ? 1 : 2];
     if (!arrive_last(ctr, gridDim.x, &s_last)) return;
     if (threadIdx.x >= 64) return;                 // the replay is one wave's
     VO_STAMP(d, 1997 + (k0 > 0), 0);
@@ -1588,12 +1563,12 @@ __global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, 
     const uint16_t* tab = d.maxit_tab + (size_t)M * (M + 1) / 2;
     int kk, maxit, best, bestk;
     if (k0 == 0) { kk = 0; maxit = d.maxit_initial; best = 0; bestk = -1; }
-    else { kk = st->k_done; maxit = st->maxit; best = st->best; bestk = st->bestk; }
+    else { kk = w->k_done; maxit = w->maxit; best = w->best; bestk = w->bestk; }
     if (maxit > nhyp) maxit = nhyp;
     const int lim = k1;
     while (kk < maxit && kk < lim) {
         const int base = kk, idx = base + lane;
-        const int c = idx < lim ? ld_sc1(d.counts + idx) : -1;
+        const int c = idx < lim ? ld_sc1(counts + idx) : -1;
         const int u = c >= 0 ? (int)tab[c] : 0xFFFF;
         for (;;) {
             const unsigned long long bal = ballot64(idx >= kk && idx < maxit && idx < lim && c > best);
@@ -1612,9 +1587,9 @@ __global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, 
     }
     VO_STAMP(d, 1997 + (k0 > 0), 1);
     if (lane == 0) {
-        st->k_done = kk; st->maxit = maxit; st->best = best; st->bestk = bestk;
-        st->need_more = kk < maxit ? 1 : 0;
-        st->n_eval = kk;
+        w->k_done = kk; w->maxit = maxit; w->best = best; w->bestk = bestk;
+        w->need_more = kk < maxit ? 1 : 0;
+        w->n_eval = kk;
         *ctr = 0u;
     }
 }
@@ -1624,12 +1599,12 @@ __global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, 
 // getPose prologue (PoseUpdate.hpp:61-96).  One wavefront; sums in the oracle's order.
 // ---------------------------------------------------------------------------
 
-// E = K^T F K, SVD, the 4 (R, t) candidates; sets FEW_INLIERS / DEGENERATE (1 thread)
-__device__ void pose_prep(const VoDev& d, VoState* st)
+// getPose prologue on w->F (PoseUpdate.hpp:64-99): E = K^T F K / |E|_F, SVD, the 4 (R, t)
+// candidates; sets w->degenerate where the reference throws (PoseUpdate.hpp:71-73).  1 thread.
+__device__ void pose_prep(const VoDev& d, VoWork* w)
 {
-    if (st->model_n < 8) { st->status = VO_STATUS_FEW_INLIERS; return; }
     double E[9], G[9];
-    mtm3(d.K, st->model_F, G);
+    mtm3(d.K, w->F, G);
     mm3(G, d.K, E);
     double nn = 0.0;
     for (int i = 0; i < 9; ++i) nn = nn + E[i] * E[i];
@@ -1637,7 +1612,7 @@ __device__ void pose_prep(const VoDev& d, VoState* st)
     double inv = 1.0 / nn;
     int nz = 0;
     for (int i = 0; i < 9; ++i) { E[i] = E[i] * inv; nz += (E[i] != 0.0); }
-    if (nz < 5) { st->status = VO_STATUS_DEGENERATE; st->degenerate = 1; return; }
+    if (nz < 5) { w->degenerate = 1; return; }
     double U[9], S[3], Vt[9];
     svd3(E, U, S, Vt);
     if (det3(U) < 0) for (int i = 0; i < 9; ++i) U[i] = -U[i];
@@ -1649,9 +1624,34 @@ __device__ void pose_prep(const VoDev& d, VoState* st)
     mm3(U, Wt, T); mm3(T, Vt, R2);
     if (det3(R1) < 0) for (int i = 0; i < 9; ++i) R1[i] = -R1[i];
     if (det3(R2) < 0) for (int i = 0; i < 9; ++i) R2[i] = -R2[i];
-    for (int i = 0; i < 9; ++i) { st->R1[i] = R1[i]; st->R2[i] = R2[i]; }
-    st->t[0] = U[2]; st->t[1] = U[5]; st->t[2] = U[8];
-    for (int c = 0; c < 4; ++c) st->counts4[c] = 0;
+    for (int i = 0; i < 9; ++i) { w->R1[i] = R1[i]; w->R2[i] = R2[i]; }
+    w->t[0] = U[2]; w->t[1] = U[5]; w->t[2] = U[8];
+    w->degenerate = 0;
+}
+
+// candidate choice (PoseUpdate.hpp:142-178, first max wins) and det fix; t is the signed unit
+// column before scaling
+__device__ void choose_pose(const int* counts4, const double* R1, const double* R2, const double* t0, double* Rf,
+                            double* tf)
+{
+    int maxPos = -1, bestc = 0;
+    for (int c = 0; c < 4; ++c)
+        if (counts4[c] > maxPos) { maxPos = counts4[c]; bestc = c; }
+    const double* R = bestc < 2 ? R1 : R2;
+    const double sg = (bestc & 1) ? -1.0 : 1.0;
+    for (int i = 0; i < 9; ++i) Rf[i] = R[i];
+    if (det3(Rf) < 0) for (int i = 0; i < 9; ++i) Rf[i] = -Rf[i];
+    tf[0] = t0[0] * sg; tf[1] = t0[1] * sg; tf[2] = t0[2] * sg;
+}
+
+// t *= scale / |t| (PoseUpdate.hpp:174-177)
+__device__ __forceinline__ void scale_t(double* tf, double scale)
+{
+    const double tn = sqrt((tf[0] * tf[0] + tf[1] * tf[1]) + tf[2] * tf[2]);
+    if (tn > 1e-6) {
+        const double f = scale / tn;
+        tf[0] = tf[0] * f; tf[1] = tf[1] * f; tf[2] = tf[2] * f;
+    }
 }
 
 // least-squares null vector (mirror of oracle ls_nullvec9): Cholesky with a pivot floor,
@@ -1835,21 +1835,26 @@ __device__ __forceinline__ void refit_sums(const double (&part)[NS], double (*s_
 }
 
 // inlier point i of the refit: LDS for i < RF_PCAP, HBM beyond
-__device__ __forceinline__ void refit_pt(const double2* s_p, const VoDev& d, int i, double* p)
+__device__ __forceinline__ void refit_pt(const double2* s_p, const double* pts, const int32_t* inl, int i, double* p)
 {
     double2 a, b;
     if (i < RF_PCAP) { a = s_p[2 * i]; b = s_p[2 * i + 1]; }
     else {
-        const double2* g = reinterpret_cast<const double2*>(d.pts + 4 * (size_t)d.inl[i]);
+        const double2* g = reinterpret_cast<const double2*>(pts + 4 * (size_t)inl[i]);
         a = g[0]; b = g[1];
     }
     p[0] = a.x; p[1] = a.y; p[2] = b.x; p[3] = b.y;
 }
 
-__global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
+__global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose, int stage)
 {
-    VoState* st = d.st;
-    if (st->status != VO_STATUS_OK) return;
+    const int wf = blockIdx.x;                     // window frame
+    if (wf >= win_count(d, stage)) return;
+    VoWork* w = d.work + wf;
+    if (w->status != VO_STATUS_OK) return;
+    const double* pts = d.pts + (size_t)wf * 4 * d.N;
+    int32_t* inl = d.inl + (size_t)wf * d.N;
+    float* model_p = d.model_p + (size_t)wf * 4 * d.N;
     __shared__ double s_part[45][RF_T + 1];
     __shared__ double s_sum[45];
     __shared__ double s_A[81];
@@ -1858,38 +1863,38 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
     __shared__ uint64_t s_w[64];
     __shared__ int s_woff[64];
     const int tid = threadIdx.x, lane = tid & 63;
-    const int bestk = st->bestk;
-    const int scored = st->scored;
+    const int bestk = w->bestk;
+    const int scored = w->scored;
     VO_STAMP(d, 1995, 0);
     // ordered compaction of the best hypothesis' inliers from its Sampson mask (written by
     // k_ransac_hyp with the same F and test): word offsets by a wave scan, then every thread
     // places its bits; the points are staged in LDS for the three passes below
     const int nw = bestk >= 0 ? (scored + 63) >> 6 : 0;
     if (tid < 64) {
-        const uint64_t w = lane < nw ? d.inlmask[(size_t)bestk * d.mask_words + lane] : 0ull;
-        const int c = __popcll(w);
+        const uint64_t mw = lane < nw ? d.inlmask[((size_t)wf * d.max_hyp + bestk) * d.mask_words + lane] : 0ull;
+        const int c = __popcll(mw);
         int x = c;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
             const int y = __shfl_up(x, off);
             if (lane >= off) x += y;
         }
-        s_w[lane] = w;
+        s_w[lane] = mw;
         s_woff[lane] = x - c;
-        if (lane == 63) { s_n = x; st->n_inl = x; }
+        if (lane == 63) { s_n = x; w->n_inl = x; }
     }
     __syncthreads();
     VO_STAMP(d, 1995, 1);
     const int n = s_n;
     for (int i = tid; i < nw * 64; i += RF_T) {
-        const uint64_t w = s_w[i >> 6];
-        if ((w >> (i & 63)) & 1ull) {
-            const int pos = s_woff[i >> 6] + __popcll(w & ((1ull << (i & 63)) - 1ull));
-            const double2* g = reinterpret_cast<const double2*>(d.pts + 4 * (size_t)i);
+        const uint64_t mw = s_w[i >> 6];
+        if ((mw >> (i & 63)) & 1ull) {
+            const int pos = s_woff[i >> 6] + __popcll(mw & ((1ull << (i & 63)) - 1ull));
+            const double2* g = reinterpret_cast<const double2*>(pts + 4 * (size_t)i);
             const double2 a = g[0], b = g[1];
             if (pos < RF_PCAP) { s_p[2 * pos] = a; s_p[2 * pos + 1] = b; }
-            d.inl[pos] = i;
-            reinterpret_cast<float4*>(d.model_p)[pos] = make_float4((float)a.x, (float)a.y, (float)b.x, (float)b.y);
+            inl[pos] = i;
+            reinterpret_cast<float4*>(model_p)[pos] = make_float4((float)a.x, (float)a.y, (float)b.x, (float)b.y);
         }
     }
     __syncthreads();
@@ -1897,7 +1902,7 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
         double pm[4] = {0.0, 0.0, 0.0, 0.0};
         for (int i = tid; i < n; i += RF_T) {
             double p[4];
-            refit_pt(s_p, d, i, p);
+            refit_pt(s_p, pts, inl, i, p);
 #pragma unroll
             for (int c = 0; c < 4; ++c) pm[c] = pm[c] + p[c];
         }
@@ -1909,7 +1914,7 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
         double ps[2] = {0.0, 0.0};
         for (int i = tid; i < n; i += RF_T) {
             double p[4];
-            refit_pt(s_p, d, i, p);
+            refit_pt(s_p, pts, inl, i, p);
 #pragma unroll
             for (int g = 0; g < 2; ++g) {
                 double a = p[2 * g] - mean[2 * g], b = p[2 * g + 1] - mean[2 * g + 1];
@@ -1926,7 +1931,7 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
         for (int e = 0; e < 45; ++e) acc[e] = 0.0;
         for (int i = tid; i < n; i += RF_T) {
             double p[4];
-            refit_pt(s_p, d, i, p);
+            refit_pt(s_p, pts, inl, i, p);
             double a[9];
             design_row(sc1 * p[0] + o1x, sc1 * p[1] + o1y, sc2 * p[2] + o2x, sc2 * p[3] + o2y, a);
             int e = 0;
@@ -1946,7 +1951,7 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
         }
         __syncthreads();
         double Fb[9], f0[9], f[9];
-        for (int i = 0; i < 9; ++i) Fb[i] = d.hypF[(size_t)bestk * 9 + i];
+        for (int i = 0; i < 9; ++i) Fb[i] = d.hypF[((size_t)wf * d.max_hyp + bestk) * 9 + i];
         VO_STAMP(d, 1995, 5);
         warm_start(Fb, sc1, mean[0], mean[1], sc2, mean[2], mean[3], f0);
         const int its = ls_nullvec9_par(d, s_A, f0, f, &s_part[0][0], &s_part[9][0], &s_part[18][0]);
@@ -1961,163 +1966,15 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose)
             denormalize(f, sc1, mean[0], mean[1], sc2, mean[2], mean[3], Fn);
             rank2(Fn);
             VO_STAMP(d, 1995, 7);
-            for (int i = 0; i < 9; ++i) st->model_F[i] = Fn[i];
-            st->fitted = 1;
-            st->model_n = n;
+            for (int i = 0; i < 9; ++i) w->F[i] = Fn[i];
+            w->fitted = 1;
+            w->n_fit = n;
+            if (with_pose) pose_prep(d, w);
         }
     } else if (tid == 0) {
-        st->fitted = 0;            // fit() returns early: the previous model stays (quirk 9)
+        w->fitted = 0;             // fit() returns early: the previous model stays (quirk 9)
     }
-    if (with_pose && tid == 0) pose_prep(d, st);
     if (tid == 0) VO_STAMP(d, 1995, 8);
-}
-
-__global__ void k_pose_prep(VoDev d)
-{
-    VoState* st = d.st;
-    if (threadIdx.x != 0 || st->status != VO_STATUS_OK) return;
-    pose_prep(d, st);
-}
-
-// finalize (PoseUpdate.hpp:142-178, VisualOdometry.cpp:106-186): pick the candidate, scale
-// t, compose T_curr, emit the pose row, then set up the next frame.  Thread 0 works; the
-// whole workgroup zeroes the next frame's histogram.
-__device__ void finalize_frame(const VoDev& d, VoState* st)
-{
-    __shared__ int s_mode, s_copy;
-    __shared__ VoState sv;                 // snapshot: one round of parallel loads, not a chain
-    __shared__ double s_gt[24];
-    __shared__ int s_cur, s_ncur, s_next;
-    {
-        // agent-scope loads: counts4 arrived by atomics from the other workgroups
-        const int nwd = (int)(sizeof(VoState) / 8);
-        for (int i = threadIdx.x; i < nwd; i += blockDim.x)
-            reinterpret_cast<unsigned long long*>(&sv)[i] = __hip_atomic_load(
-                reinterpret_cast<unsigned long long*>(st) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (threadIdx.x == 0) s_copy = -1;
-    }
-    __syncthreads();
-    {
-        const int fi = sv.frame, last = sv.last_valid;
-        const bool want_gt = sv.mode == VO_MODE_FRAME && sv.status == VO_STATUS_OK && d.gt_n > 0 && fi < d.gt_n &&
-                             last < d.gt_n;
-        const int t = threadIdx.x;
-        if (want_gt && t < 24) s_gt[t] = d.gt[12 * (size_t)(t < 12 ? fi : last) + (t < 12 ? t : t - 12)];
-        if (t == 32) {
-            const int cur = sv.mode == VO_MODE_FRAME ? d.ext->slot[fi & (VO_EXT_RING - 1)] : sv.cur;
-            s_cur = cur;
-            s_ncur = cur >= 0 ? d.ext->n_kps[cur] : 0;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int status = sv.status;
-        const int mode = sv.mode;
-        s_mode = mode;
-        double Tc[16];
-        for (int i = 0; i < 16; ++i) Tc[i] = sv.Tcurr[i];
-        double Rf[9], tf[3];
-        bool have_pose = false;
-        if (status == VO_STATUS_OK) {
-            int maxPos = -1, bestc = 0;
-            for (int c = 0; c < 4; ++c) {
-                const int v = sv.counts4[c];
-                if (v > maxPos) { maxPos = v; bestc = c; }
-            }
-            const double* R = bestc < 2 ? sv.R1 : sv.R2;
-            double sg = (bestc & 1) ? -1.0 : 1.0;
-            for (int i = 0; i < 9; ++i) Rf[i] = R[i];
-            if (det3(Rf) < 0) for (int i = 0; i < 9; ++i) Rf[i] = -Rf[i];
-            tf[0] = sv.t[0] * sg; tf[1] = sv.t[1] * sg; tf[2] = sv.t[2] * sg;
-            double scale = sv.scale_override;
-            if (mode == VO_MODE_FRAME) {
-                scale = 1.0;
-                const int fi = sv.frame, last = sv.last_valid;
-                if (d.gt_n > 0 && fi < d.gt_n && last < d.gt_n) {
-                    double Gi[16], Gl[16], Ii[16], Tr[16];
-                    for (int r = 0; r < 16; ++r) {
-                        Gi[r] = r < 12 ? s_gt[r] : (r == 15 ? 1.0 : 0.0);
-                        Gl[r] = r < 12 ? s_gt[12 + r] : (r == 15 ? 1.0 : 0.0);
-                    }
-                    inv4(Gi, Ii);
-                    mm4(Ii, Gl, Tr);
-                    scale = sqrt((Tr[3] * Tr[3] + Tr[7] * Tr[7]) + Tr[11] * Tr[11]);
-                }
-            }
-            double tn = sqrt((tf[0] * tf[0] + tf[1] * tf[1]) + tf[2] * tf[2]);
-            if (tn > 1e-6) {
-                double f = scale / tn;
-                tf[0] = tf[0] * f; tf[1] = tf[1] * f; tf[2] = tf[2] * f;
-            }
-            for (int i = 0; i < 9; ++i) st->pose_R[i] = Rf[i];
-            for (int i = 0; i < 3; ++i) st->pose_t[i] = tf[i];
-            have_pose = true;
-        }
-        if (mode == VO_MODE_FRAME || mode == VO_MODE_MISSING) {
-            VoFrameOut* o = d.out;
-            int flip = 1;
-            if (status == VO_STATUS_FIRST || status == VO_STATUS_MISSING) flip = 0;
-            const int cur = s_cur;
-            int prev = sv.prev;
-            if (status == VO_STATUS_OK || status == VO_STATUS_DEGENERATE) {
-                st->last_valid = sv.frame;      // VisualOdometry.cpp:161-166 precede getPose
-                prev = cur;
-            }
-            if (status == VO_STATUS_FIRST) { prev = cur; st->last_valid = 0; }
-            // a skipped frame keeps prev (quirk 10); its ring slot is rewritten R frames on, so
-            // the descriptors move to the carry slot now (rare: one copy per skip run)
-            if (prev >= 0 && prev < VO_RING_SLOTS && status != VO_STATUS_OK && status != VO_STATUS_DEGENERATE &&
-                status != VO_STATUS_FIRST) {
-                s_copy = prev;
-                prev = VO_CARRY_SLOT;
-            }
-            st->prev = prev;
-            if (have_pose) {
-                double Trel[16] = {Rf[0], Rf[1], Rf[2], tf[0], Rf[3], Rf[4], Rf[5], tf[1],
-                                   Rf[6], Rf[7], Rf[8], tf[2], 0, 0, 0, 1};
-                mm4(Tc, Trel, Tc);
-                for (int i = 0; i < 16; ++i) st->Tcurr[i] = Tc[i];
-            }
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 4; ++c) o->pose[r * 4 + c] = (flip && r == 2) ? -Tc[r * 4 + c] : Tc[r * 4 + c];
-            o->status = status;
-            o->n_kps = status == VO_STATUS_MISSING ? 0 : s_ncur;
-            o->n_matches = sv.M;
-            o->n_inl = sv.n_inl;
-            o->best_k = sv.bestk;
-            o->n_eval = sv.n_eval;
-            o->fitted = sv.fitted;
-            o->frame = sv.frame;
-            st->frame = sv.frame + 1;
-            s_next = sv.frame + 1;
-        }
-    }
-    __syncthreads();
-    if (s_mode == VO_MODE_FRAME || s_mode == VO_MODE_MISSING) setup_next_frame(d, st, s_next);
-    if (s_copy >= 0) {
-        const int src = s_copy, n = d.ext->n_kps[src];
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            d.kps[VO_CARRY_SLOT][i] = d.kps[src][i];
-            d.pre[VO_CARRY_SLOT][i] = d.pre[src][i];
-        }
-        for (int i = threadIdx.x; i < 8 * n; i += blockDim.x) d.desc[VO_CARRY_SLOT][i] = d.desc[src][i];
-        if (threadIdx.x == 0) d.ext->n_kps[VO_CARRY_SLOT] = n;
-    }
-    // the extract queues may now rewrite the ring slots this chain read.  They read nothing
-    // the chain wrote, so the counter needs no release of data (no L2 write-back on the
-    // critical path): every load of this workgroup (the carry copy) has returned, then one
-    // write-through store the command processor reads from memory
-    if (d.seqno) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0)
-            __hip_atomic_store((gu32*)(d.ctr + VO_SYNC_POSE), d.seqno, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    // the next frame's k_match follows this kernel: hold it until that frame's descriptors
-    // are published (one workgroup spinning cannot starve the extract queues)
-    if (d.wait_next && !wait_seq(d.ctr + VO_SYNC_EXT + ((d.wait_next - 1u) & (VO_EXT_RING - 1)), d.wait_next)) {
-        if (threadIdx.x == 0 && st->status == VO_STATUS_OK) st->status = VO_STATUS_STALLED;
-    }
 }
 
 // smallest right singular vector of the 4x4 triangulation matrix (mirror of oracle nullvec4):
@@ -2219,24 +2076,21 @@ __device__ __forceinline__ void nullvec4(const double* A, double* x)
     }
 }
 
-// cheirality test of the 4 (R, t) candidates, one thread per (model inlier, candidate)
-// (cv::undistortPoints + cv::triangulatePoints + depth test, PoseUpdate.hpp:101-147);
-// the last workgroup finalizes the frame.  On a skipped frame workgroup 0 finalizes.
+// cheirality test of the 4 (R, t) candidates, one thread per (refit inlier, candidate)
+// (cv::undistortPoints + cv::triangulatePoints + depth test, PoseUpdate.hpp:101-147).
+// grid (4N / TRI_BLOCK, B): frame wf = blockIdx.y; only frames whose own refit ran (a frame
+// whose model leaked reuses the pose of the model's frame, k_finalize).
 #define TRI_BLOCK 128
-__global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d)
+__global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d, int stage)
 {
-    VoState* st = d.st;
-    __shared__ int s_cnt[4];
-    __shared__ unsigned s_last;
-    const int status = st->status;
-    if (status != VO_STATUS_OK) {
-        if (blockIdx.x == 0) finalize_frame(d, st);
-        return;
-    }
-    const int n = st->model_n;
+    const int wf = blockIdx.y;
+    if (wf >= win_count(d, stage)) return;
+    VoWork* w = d.work + wf;
+    if (w->status != VO_STATUS_OK || !w->fitted || w->degenerate) return;
+    const int n = w->n_fit;
     const unsigned active = (unsigned)((4 * n + TRI_BLOCK - 1) / TRI_BLOCK);
     if (blockIdx.x >= active) return;
-    if (blockIdx.x == 0) VO_STAMP(d, 1996, 0);
+    __shared__ int s_cnt[4];
     if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
     __syncthreads();
     const int g = blockIdx.x * TRI_BLOCK + threadIdx.x;   // (point, candidate) = (g >> 2, g & 3)
@@ -2245,13 +2099,13 @@ __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d)
     if (i < n) {
         const double fx = d.K[0], fy = d.K[4], cx = d.K[2], cy = d.K[5];
         const double ifx = 1.0 / fx, ify = 1.0 / fy;
-        const float4 p = reinterpret_cast<const float4*>(d.model_p)[i];
+        const float4 p = reinterpret_cast<const float4*>(d.model_p + (size_t)wf * 4 * d.N)[i];
         float x1 = (float)(((double)p.x - cx) * ifx), y1 = (float)(((double)p.y - cy) * ify);
         float x2 = (float)(((double)p.z - cx) * ifx), y2 = (float)(((double)p.w - cy) * ify);
         double X1 = x1, Y1 = y1, X2 = x2, Y2 = y2;
-        const double* R = cnd < 2 ? st->R1 : st->R2;
+        const double* R = cnd < 2 ? w->R1 : w->R2;
         double sg = (cnd & 1) ? -1.0 : 1.0;
-        double tc0 = st->t[0] * sg, tc1 = st->t[1] * sg, tc2 = st->t[2] * sg;
+        double tc0 = w->t[0] * sg, tc1 = w->t[1] * sg, tc2 = w->t[2] * sg;
         double P2[12] = {R[0], R[1], R[2], tc0, R[3], R[4], R[5], tc1, R[6], R[7], R[8], tc2};
         const double P1[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
         double A[16];
@@ -2265,16 +2119,15 @@ __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d)
         double X[4];
         nullvec4(A, X);
         double h0 = (double)(float)X[0], h1 = (double)(float)X[1], h2 = (double)(float)X[2], h3 = (double)(float)X[3];
-        double w = h3;
-        if (!(fabs(w) < 1e-6)) {
-            double iw = 1.0 / w;
+        double wv = h3;
+        if (!(fabs(wv) < 1e-6)) {
+            double iw = 1.0 / wv;
             double Xh0 = h0 * iw, Xh1 = h1 * iw, Xh2 = h2 * iw;
             double z1 = Xh2;
             double z2 = ((R[6] * Xh0 + R[7] * Xh1) + R[8] * Xh2) + tc2;
             pos = (z1 > 0 && z2 > 0);
         }
     }
-    if (blockIdx.x == 0) VO_STAMP(d, 1996, 1);
     unsigned long long bal = ballot64(pos);
     const int lane = threadIdx.x & 63;
     if (lane < 4) {
@@ -2284,22 +2137,203 @@ __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d)
     }
     __syncthreads();
     if (threadIdx.x < 4 && s_cnt[threadIdx.x])
-        __hip_atomic_fetch_add((gi32*)&st->counts4[threadIdx.x], s_cnt[threadIdx.x], __ATOMIC_RELAXED,
+        __hip_atomic_fetch_add((gi32*)&w->counts4[threadIdx.x], s_cnt[threadIdx.x], __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
-    if (!arrive_last(d.ctr + 2, active, &s_last)) return;
-    VO_STAMP(d, 1996, 2);
-    if (threadIdx.x == 0) d.ctr[2] = 0u;
-    finalize_frame(d, st);
-    VO_STAMP(d, 1996, 3);
 }
 
-// a missing image (VisualOdometry.cpp:77-82): push T_curr, advance the frame counter
-__global__ void __launch_bounds__(128) k_missing(VoDev d)
+// ---------------------------------------------------------------------------
+// finalize: the trajectory loop's bookkeeping over the window, in frame order
+// (VisualOdometry.cpp:68-189, PoseUpdate.hpp:142-178).  One workgroup:
+//   0  per frame (thread wf): its status, slots, and the pose of its own refit
+//   1  thread 0: the sequential rules -- skips, missing images, the model leak (quirk 9),
+//      desc1 / last_valid advance (quirk 10) -- and the commit point: the first frame after
+//      a frame that did not advance desc1 was matched against the wrong previous frame, so
+//      it and everything after it go to the next pass
+//   2  per committed frame: GT scale (VisualOdometry.cpp:161-162) and T_rel
+//   3  wave 0, lane = entry: T_curr = T_curr * T_rel in frame order (mm4's operation order)
+//   4  per committed frame: the output row; thread 0: the trajectory state; all: the carry
+//      copy of desc1 when the window ends in a skip (its ring slot will be rewritten)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int out_base)
 {
+    __shared__ int s_n, s_ncommit, s_lo, s_copy, s_model_wf, s_newlv, s_newprev;
+    __shared__ int s_status[VO_MAX_BATCH], s_kind[VO_MAX_BATCH], s_src[VO_MAX_BATCH], s_lvb[VO_MAX_BATCH];
+    __shared__ int s_flip[VO_MAX_BATCH], s_fitted[VO_MAX_BATCH], s_degen[VO_MAX_BATCH], s_cur[VO_MAX_BATCH];
+    __shared__ double s_R[VO_MAX_BATCH + 1][9], s_t[VO_MAX_BATCH + 1][3];   // [B]: the model before the window
+    __shared__ double s_Trel[VO_MAX_BATCH][16];
+    __shared__ double s_row[VO_MAX_BATCH][12];
+    __shared__ double s_T[16];
+    const int tid = threadIdx.x;
     VoState* st = d.st;
-    if (threadIdx.x == 0) { st->status = VO_STATUS_MISSING; st->mode = VO_MODE_MISSING; }
+    if (tid == 0) {
+        const int lo = st->lo;
+        const int n = min(st->end - lo, d.B);
+        s_lo = lo;
+        s_n = n;
+        s_copy = -1;
+        s_model_wf = -1;
+    }
     __syncthreads();
-    finalize_frame(d, st);
+    const int n = s_n, lo = s_lo;
+    if (n <= 0) return;
+    const int MB = VO_MAX_BATCH;
+    // 0
+    if (tid < n) {
+        const VoWork* w = d.work + tid;
+        s_status[tid] = w->status;
+        s_cur[tid] = w->cur;
+        const int fit = w->status == VO_STATUS_OK && w->fitted;
+        s_fitted[tid] = fit;
+        s_degen[tid] = w->degenerate;
+        if (fit && !w->degenerate) {
+            int c4[4];
+            for (int c = 0; c < 4; ++c) c4[c] = w->counts4[c];
+            choose_pose(c4, w->R1, w->R2, w->t, s_R[tid], s_t[tid]);
+        }
+    } else if (tid == 64) {
+        for (int i = 0; i < 9; ++i) s_R[MB][i] = st->model_R[i];
+        for (int i = 0; i < 3; ++i) s_t[MB][i] = st->model_t[i];
+    } else if (tid == 96) {
+        for (int i = 0; i < 16; ++i) s_T[i] = st->Tcurr[i];
+    }
+    __syncthreads();
+    // 1
+    if (tid == 0) {
+        int lv = st->last_valid, prev = st->prev_slot;
+        int msrc = st->model_n >= 8 ? MB : -1;          // MB: the model fitted before this window
+        const int mdeg = st->model_degenerate;
+        int wf = 0, adv = 1;
+        for (; wf < n; ++wf) {
+            if (wf > 0 && !adv) break;                  // matched against frame f-1, which was not desc1
+            const int f = lo + wf;
+            int s = s_status[wf], kind = 0, flip = 1;
+            adv = 0;
+            if (s == VO_STATUS_FIRST) {                 // :58 identity, desc1 = frame 0
+                flip = 0; adv = 1; lv = 0; prev = s_cur[wf];
+            } else if (s == VO_STATUS_MISSING) {        // :77-82 T_curr pushed unflipped
+                flip = 0;
+            } else if (s == VO_STATUS_OK) {
+                if (s_fitted[wf]) msrc = wf;            // fit() ran: the model is this frame's
+                if (msrc < 0) {
+                    s = VO_STATUS_FEW_INLIERS;          // :147-153 (no model was ever fitted)
+                } else {
+                    s_lvb[wf] = lv;                     // :161-166 precede getPose
+                    lv = f; prev = s_cur[wf]; adv = 1;
+                    s_src[wf] = msrc;
+                    const int dg = msrc == MB ? mdeg : s_degen[msrc];
+                    if (dg) s = VO_STATUS_DEGENERATE; else kind = 1;
+                }
+            }                                           // FEW_MATCHES / OVERFLOW: :108-115
+            s_status[wf] = s; s_kind[wf] = kind; s_flip[wf] = flip;
+        }
+        s_ncommit = wf;
+        if (msrc >= 0 && msrc < MB) s_model_wf = msrc;
+        if (!adv && prev < VO_RING) { s_copy = prev; prev = VO_CARRY_SLOT; }
+        s_newlv = lv; s_newprev = prev;
+    }
+    __syncthreads();
+    const int nc = s_ncommit;
+    // 2
+    if (tid < nc && s_kind[tid] == 1) {
+        const int f = lo + tid, lvb = s_lvb[tid], src = s_src[tid];
+        double scale = 1.0;
+        if (d.gt_n > 0 && f < d.gt_n && lvb < d.gt_n) {
+            double Gi[16], Gl[16], Ii[16], Tr[16];
+            for (int r = 0; r < 16; ++r) {
+                Gi[r] = r < 12 ? d.gt[12 * (size_t)f + r] : (r == 15 ? 1.0 : 0.0);
+                Gl[r] = r < 12 ? d.gt[12 * (size_t)lvb + r] : (r == 15 ? 1.0 : 0.0);
+            }
+            inv4(Gi, Ii);
+            mm4(Ii, Gl, Tr);
+            scale = sqrt((Tr[3] * Tr[3] + Tr[7] * Tr[7]) + Tr[11] * Tr[11]);
+        }
+        const double* R = s_R[src];
+        double tf[3] = {s_t[src][0], s_t[src][1], s_t[src][2]};
+        scale_t(tf, scale);
+        double* T = s_Trel[tid];
+        T[0] = R[0]; T[1] = R[1]; T[2] = R[2]; T[3] = tf[0];
+        T[4] = R[3]; T[5] = R[4]; T[6] = R[5]; T[7] = tf[1];
+        T[8] = R[6]; T[9] = R[7]; T[10] = R[8]; T[11] = tf[2];
+        T[12] = 0.0; T[13] = 0.0; T[14] = 0.0; T[15] = 1.0;
+    }
+    __syncthreads();
+    // 3
+    if (tid < 64) {
+        const int e = tid & 15, i = e >> 2, j = e & 3;
+        double Tv = s_T[e];
+        for (int wf = 0; wf < nc; ++wf) {
+            if (s_kind[wf] == 1) {
+                const double a0 = __shfl(Tv, i * 4 + 0), a1 = __shfl(Tv, i * 4 + 1);
+                const double a2 = __shfl(Tv, i * 4 + 2), a3 = __shfl(Tv, i * 4 + 3);
+                const double* B = s_Trel[wf];
+                Tv = ((a0 * B[0 * 4 + j] + a1 * B[1 * 4 + j]) + a2 * B[2 * 4 + j]) + a3 * B[3 * 4 + j];
+            }
+            if (tid < 12) s_row[wf][tid] = (s_flip[wf] && i == 2) ? -Tv : Tv;
+        }
+        if (tid < 16) s_T[tid] = Tv;
+    }
+    __syncthreads();
+    // 4
+    if (tid < nc) {
+        const VoWork* w = d.work + tid;
+        const int s = s_status[tid];
+        VoFrameOut* o = out + (lo + tid - out_base);
+        for (int r = 0; r < 12; ++r) o->pose[r] = s_row[tid][r];
+        o->status = s;
+        o->n_kps = s == VO_STATUS_MISSING ? 0 : d.ext->n_kps[s_cur[tid]];
+        o->n_matches = w->M;
+        o->n_inl = w->n_inl;
+        o->best_k = w->bestk;
+        o->n_eval = w->n_eval;
+        o->fitted = s_fitted[tid];
+        o->frame = lo + tid;
+    } else if (tid == 64) {
+        st->lo = lo + nc;
+        st->last_valid = s_newlv;
+        st->prev_slot = s_newprev;
+        for (int i = 0; i < 16; ++i) st->Tcurr[i] = s_T[i];
+        const int m = s_model_wf;
+        if (m >= 0) {
+            const VoWork* w = d.work + m;
+            st->model_n = w->n_fit;
+            st->model_degenerate = s_degen[m];
+            for (int i = 0; i < 9; ++i) st->model_F[i] = w->F[i];
+            for (int i = 0; i < 9; ++i) st->model_R[i] = s_R[m][i];
+            for (int i = 0; i < 3; ++i) st->model_t[i] = s_t[m][i];
+        }
+    }
+    if (s_copy >= 0) {
+        const int src = s_copy, nk = d.ext->n_kps[src];
+        const size_t N = (size_t)d.N;
+        for (int i = tid; i < nk; i += blockDim.x) {
+            d.kps[VO_CARRY_SLOT * N + i] = d.kps[src * N + i];
+            d.pre[VO_CARRY_SLOT * N + i] = d.pre[src * N + i];
+        }
+        for (int i = tid; i < 8 * nk; i += blockDim.x) d.desc[VO_CARRY_SLOT * N * 8 + i] = d.desc[src * N * 8 + i];
+        if (tid == 0) {
+            d.ext->n_kps[VO_CARRY_SLOT] = nk;
+            d.ext->status[VO_CARRY_SLOT] = VO_STATUS_OK;
+        }
+    }
+}
+
+// vo_pose (PoseUpdate::getPose on caller data in work[0]): phase 0 the prologue, phase 1
+// (after k_triangulate) the candidate choice and the caller's scale
+__global__ void k_pose_stage(VoDev d, int phase)
+{
+    if (threadIdx.x != 0) return;
+    VoWork* w = d.work;
+    VoState* st = d.st;
+    if (phase == 0) { pose_prep(d, w); return; }
+    if (w->degenerate) { st->pose_status = VO_STATUS_DEGENERATE; return; }
+    int c4[4];
+    for (int c = 0; c < 4; ++c) c4[c] = w->counts4[c];
+    double Rf[9], tf[3];
+    choose_pose(c4, w->R1, w->R2, w->t, Rf, tf);
+    scale_t(tf, st->scale_override);
+    for (int i = 0; i < 9; ++i) st->pose_R[i] = Rf[i];
+    for (int i = 0; i < 3; ++i) st->pose_t[i] = tf[i];
+    st->pose_status = VO_STATUS_OK;
 }
 
 // arithmetic self-test: the ops whose rounding the parity contract depends on
@@ -2323,28 +2357,24 @@ __global__ void k_selftest_arith(const float* fa, const float* fb, float* fo, co
 // ---------------------------------------------------------------------------
 // launch wrappers
 // ---------------------------------------------------------------------------
-static const char* g_names[] = {"stencil", "select", "describe", "match", "ransac", "refit", "triangulate"};
+static const char* g_names[] = {"stencil", "select", "describe", "match", "ransac", "refit", "triangulate",
+                                "finalize"};
 int kernel_count() { return (int)(sizeof(g_names) / sizeof(g_names[0])); }
 const char* kernel_name(int i) { return g_names[i]; }
 
-void launch_frame_begin(const VoDev& d, int mode, hipStream_t s)
+void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int nb, int write_response, hipStream_t s)
 {
     ensure_tables();
-    hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(1024), 0, s, d, mode);
+    dim3 g((d.W + ST_TW - 1) / ST_TW, (d.H + ST_TH - 1) / ST_TH, nb);
+    hipLaunchKernelGGL(k_stencil, g, dim3(256), 0, s, d, img0, frame_bytes, write_response);
 }
-void launch_stencil(const VoDev& d, const uint8_t* frame, int write_response, hipStream_t s)
+void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s)
 {
-    ensure_tables();
-    dim3 g((d.W + ST_TW - 1) / ST_TW, (d.H + ST_TH - 1) / ST_TH);
-    hipLaunchKernelGGL(k_stencil, g, dim3(256), 0, s, d, frame, write_response);
+    hipLaunchKernelGGL(k_select, dim3(nb), dim3(1024), (size_t)d.sel_lds, s, d, f0, slot_override);
 }
-void launch_select(const VoDev& d, int fidx, hipStream_t s)
+void launch_ext_missing(const VoDev& d, int slot, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(1024), (size_t)d.sel_lds, s, d, fidx);
-}
-void launch_ext_missing(const VoDev& d, int fidx, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_ext_missing, dim3(1), dim3(64), 0, s, d, fidx);
+    hipLaunchKernelGGL(k_ext_missing, dim3(1), dim3(64), 0, s, d, slot);
 }
 int select_lds_bytes(int W, int H, int* key_cap)
 {
@@ -2357,31 +2387,42 @@ int select_lds_bytes(int W, int H, int* key_cap)
     if (key_cap) *key_cap = L.key_cap;
     return bytes;
 }
-void launch_describe(const VoDev& d, int fidx, hipStream_t s)
+void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned publish, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_describe, dim3((d.N + DS_KPB - 1) / DS_KPB), dim3(256), 0, s, d, fidx);
+    ensure_tables();
+    hipLaunchKernelGGL(k_describe, dim3((d.N + DS_KPB - 1) / DS_KPB, nb), dim3(256), 0, s, d, f0, slot_override,
+                       publish);
 }
-void launch_match(const VoDev& d, hipStream_t s)
+void launch_match(const VoDev& d, int stage, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_match, dim3(match_blocks(d.N, d.match_bits)), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_match, dim3(match_blocks(d.N, d.match_bits), stage ? 1 : d.B), dim3(256), 0, s, d, stage);
 }
-void launch_ransac(const VoDev& d, int nhyp, hipStream_t s)
+void launch_ransac(const VoDev& d, int stage, hipStream_t s)
 {
+    const int nhyp = d.max_hyp, nb = stage ? 1 : d.B;
     const int k0 = nhyp < VO_HYP_CHUNK0 ? nhyp : VO_HYP_CHUNK0;
-    hipLaunchKernelGGL((k_ransac_hyp<4, 1>), dim3(k0), dim3(256), 0, s, d, 0, k0, nhyp);
+    hipLaunchKernelGGL((k_ransac_hyp<4, 1>), dim3(k0, nb), dim3(256), 0, s, d, 0, k0, nhyp, stage);
     if (nhyp > k0)
-        hipLaunchKernelGGL((k_ransac_hyp<1, 4>), dim3((nhyp - k0 + 3) / 4), dim3(256), 0, s, d, k0, nhyp, nhyp);
+        hipLaunchKernelGGL((k_ransac_hyp<1, 4>), dim3((nhyp - k0 + 3) / 4, nb), dim3(256), 0, s, d, k0, nhyp, nhyp,
+                           stage);
 }
-void launch_refit(const VoDev& d, int with_pose, hipStream_t s)
+void launch_refit(const VoDev& d, int with_pose, int stage, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_refit, dim3(1), dim3(RF_T), 0, s, d, with_pose);
+    hipLaunchKernelGGL(k_refit, dim3(stage ? 1 : d.B), dim3(RF_T), 0, s, d, with_pose, stage);
 }
-void launch_pose_prep(const VoDev& d, hipStream_t s) { hipLaunchKernelGGL(k_pose_prep, dim3(1), dim3(64), 0, s, d); }
-void launch_triangulate(const VoDev& d, hipStream_t s)
+void launch_triangulate(const VoDev& d, int stage, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_triangulate, dim3((4 * d.N + TRI_BLOCK - 1) / TRI_BLOCK), dim3(TRI_BLOCK), 0, s, d);
+    hipLaunchKernelGGL(k_triangulate, dim3((4 * d.N + TRI_BLOCK - 1) / TRI_BLOCK, stage ? 1 : d.B), dim3(TRI_BLOCK), 0,
+                       s, d, stage);
 }
-void launch_missing(const VoDev& d, hipStream_t s) { hipLaunchKernelGGL(k_missing, dim3(1), dim3(128), 0, s, d); }
+void launch_finalize(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, d, out, out_base);
+}
+void launch_pose_stage(const VoDev& d, int phase, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_pose_stage, dim3(1), dim3(64), 0, s, d, phase);
+}
 void launch_selftest_arith(const float* fa, const float* fb, float* fo, const double* da, const double* db,
                            double* dout, int n, hipStream_t s)
 {

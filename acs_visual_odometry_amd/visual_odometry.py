@@ -137,10 +137,16 @@ class Context:
         return poses.reshape(n, 3, 4), st, info
 
     def kernel_times(self):
+        """Average ms per timed launch of each kernel in the last process_frames_device call."""
+        return {k: v[0] for k, v in self.kernel_stats().items()}
+
+    def kernel_stats(self):
+        """{kernel: (ms per timed launch, frames per launch)} of the last process_frames_device call."""
         names = (C.c_char_p * 32)()
         ms = (C.c_float * 32)()
-        k = self.lib.vo_last_kernel_times(self.h, names, ms, 32)
-        return {names[i].decode(): ms[i] for i in range(k) if ms[i] >= 0}
+        fpl = (C.c_float * 32)()
+        k = self.lib.vo_last_kernel_stats(self.h, names, ms, fpl, 32)
+        return {names[i].decode(): (ms[i], fpl[i]) for i in range(k) if ms[i] >= 0}
 
 
 class DeviceFrames:

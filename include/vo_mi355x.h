@@ -68,6 +68,8 @@ typedef struct {
     uint64_t seed;            /* RANSAC sampler seed (replaces std::random_device)     */
     double K[9];              /* PoseUpdate.hpp:36-39                                  */
     int device;               /* HIP device ordinal                                    */
+    int frame_batch;          /* frames per extract batch / pose-pass window (1..64);
+                                 0 = default 16.  Results do not depend on it.         */
 } vo_config;
 
 /* Fill the reference defaults for a width x height stream. */
@@ -122,9 +124,12 @@ int  vo_process_frame(vo_ctx* ctx, const uint8_t* gray, size_t stride, double po
                       int* status, int32_t* info);
 
 /* Batched, device-resident variant: nframes frames already in HBM at
- * d_frames + f * frame_bytes (dense W x H u8).  Enqueues every frame on the ctx stream
- * with no host synchronisation between frames, then waits once.  poses_out: nframes*12,
- * status_out: nframes (both host, optional). */
+ * d_frames + f * frame_bytes (dense W x H u8).  Frames are extracted frame_batch at a time
+ * on one queue and posed in windows of frame_batch frames on another (each frame matched
+ * speculatively against its predecessor; a frame after a skipped one is re-run), with one
+ * host synchronisation per VO_CHUNK = 255 frames (more only after skipped frames).  Results
+ * are those of nframes vo_process_frame calls.  poses_out: nframes*12, status_out: nframes,
+ * info_out: nframes*8 (all host, optional). */
 int  vo_process_frames_device(vo_ctx* ctx, const uint8_t* d_frames, size_t frame_bytes, int nframes,
                               double* poses_out, int* status_out, int32_t* info_out);
 
@@ -137,10 +142,13 @@ int  vo_device_upload(vo_ctx* ctx, void* dptr, const void* src, size_t bytes);
 int  vo_reset(vo_ctx* ctx);
 
 /* Per-kernel timing of vo_process_frames_device (HIP events on the stream each kernel runs on).
- * on: 0 off, 1 every kernel of every frame, 100+k only kernel k, on every 8th frame (an event
- * pair costs ~6 us of queue time, so the live timing samples).  times: average ms per timed
- * launch over the last call (-1 if not timed).  Returns the number written. */
+ * on: 0 off, 1 every launch of every kernel, 100+k only kernel k, on every 4th launch (an
+ * event pair costs ~6 us of queue time, so the live timing samples).  times: average ms per
+ * timed launch over the last call (-1 if not timed).  Returns the number written.
+ * vo_last_kernel_stats also gives the frames per launch (frames of the call / launches). */
 int  vo_last_kernel_times(vo_ctx* ctx, const char** names, float* ms, int cap);
+int  vo_last_kernel_stats(vo_ctx* ctx, const char** names, float* ms_per_launch, float* frames_per_launch,
+                          int cap);
 int  vo_enable_kernel_timing(vo_ctx* ctx, int on);
 
 /* desc512 (8 words) -> 512 bytes in {0,1}: the reference's byte-per-test layout

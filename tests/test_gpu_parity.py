@@ -274,21 +274,12 @@ def test_skip_few_matches_keeps_previous_descriptors():
     ctx.close()
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("blank", [(), tuple(range(10, 21)), (3, 4, 9, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26)])
-def test_pipelined_batch_matches_oracle_across_ring_wraps(blank):
-    """The device batch path runs extract on VO_EXT_QUEUES queues, up to R-1 = 7 frames ahead
-    of the pose chain, over a ring of 8 keypoint/descriptor slots.  40 frames wrap the ring
-    five times; a skip run longer than the ring (blank frames -> < 8 matches) must keep the
-    last good frame's descriptors (quirk 10) through the carry slot."""
-    seq = SceneSequence(nframes=40, step=0.05)
-    frames = seq.frames()
-    for b in blank:
-        frames[b] = 128
-    cfg = O.config(seq.W, seq.H, K=seq.K.reshape(9))
+def _device_vs_oracle(seq, frames, **ctx_kw):
+    cfg = O.config(seq.W, seq.H, K=seq.K.reshape(9), max_kpts=ctx_kw.get("max_kpts", 2000))
     vo = O.VO(cfg, gt=seq.gt())
     ref = [vo.process(frames[f]) for f in range(seq.n)]
-    ctx = Context(seq.W, seq.H, K=seq.K)
+    vo.close()
+    ctx = Context(seq.W, seq.H, K=seq.K, **ctx_kw)
     ctx.set_ground_truth(seq.gt())
     df = ctx.device_frames(frames)
     poses, st, info = ctx.process_frames_device(df)
@@ -297,5 +288,31 @@ def test_pipelined_batch_matches_oracle_across_ring_wraps(blank):
         assert st[f] == sr, (f, st[f], sr)
         assert np.array_equal(info[f, :6], ir[:6]), (f, info[f], ir)
         assert np.array_equal(poses[f], pr), f
+        assert info[f, 6] == f
     df.free()
     ctx.close()
+
+
+@pytest.mark.parametrize("batch", [1, 3, 16])
+@pytest.mark.parametrize("blank", [(), tuple(range(10, 21)), (3, 4, 9, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26)])
+def test_windowed_batch_matches_oracle(blank, batch):
+    """vo_process_frames_device extracts `batch` frames per launch and poses windows of
+    `batch` frames, each frame matched speculatively against its predecessor.  Blank frames
+    (< 8 matches) do not advance desc1 (quirk 10): the frame after a skip is re-run by the
+    next pass against the last valid frame, whose descriptors move to the carry slot while
+    the skip run lasts.  The trajectory must equal the sequential oracle row for row."""
+    seq = SceneSequence(nframes=40, step=0.05)
+    frames = seq.frames()
+    for b in blank:
+        frames[b] = 128
+    _device_vs_oracle(seq, frames, frame_batch=batch)
+
+
+def test_windowed_batch_across_chunks_and_ring_wrap():
+    """300 frames: two host chunks (VO_CHUNK = 255) and a wrap of the 256-slot ring, with a
+    skip run that straddles the chunk boundary (the carry slot outlives the chunk)."""
+    seq = SceneSequence(400, 240, nframes=300, step=0.05)
+    frames = seq.frames()
+    for b in range(250, 262):
+        frames[b] = 128
+    _device_vs_oracle(seq, frames, max_kpts=300, frame_batch=16)
