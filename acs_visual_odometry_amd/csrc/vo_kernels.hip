@@ -23,10 +23,10 @@ __constant__ int8_t c_pt_y[VO_FREAK_NPOINTS];
 __constant__ uint8_t c_pair_p[VO_FREAK_NPAIRS];
 __constant__ uint8_t c_pair_q[VO_FREAK_NPAIRS];
 __constant__ int16_t c_patch[VO_FREAK_NTESTS];
-// per pair: dx, dy (f32) and 1/|d| (f64).  (ic*d)/|d| in f32 == (float)((double)(ic*d) * (1/|d|))
-// for every ic in [-255,255] and every pair (tests/test_describe_division.py, exhaustive)
-__constant__ float c_pdx[VO_FREAK_NPAIRS];
-__constant__ float c_pdy[VO_FREAK_NPAIRS];
+// per pair: p | q << 8 | (int8)dx << 16 | (int8)dy << 24, and 1/|d| (f64).  (ic*d)/|d| in f32 ==
+// (float)((double)(ic*d) * (1/|d|)) for every ic in [-255,255] and every pair
+// (tests/test_describe_division.py, exhaustive)
+__constant__ uint32_t c_pairpk[VO_FREAK_NPAIRS];
 __constant__ double c_prn[VO_FREAK_NPAIRS];
 
 static bool g_tables_ready = false;
@@ -44,15 +44,17 @@ static void ensure_tables()
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pair_p), pp, sizeof(pp));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pair_q), pq, sizeof(pq));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_patch), vo_freak_patch, sizeof(vo_freak_patch));
-    float pdx[VO_FREAK_NPAIRS], pdy[VO_FREAK_NPAIRS];
+    uint32_t pk[VO_FREAK_NPAIRS];
     double prn[VO_FREAK_NPAIRS];
     for (int t = 0; t < VO_FREAK_NPAIRS; ++t) {
-        float dx = (float)(px[pp[t]] - px[pq[t]]), dy = (float)(py[pp[t]] - py[pq[t]]);
+        const int ix = px[pp[t]] - px[pq[t]], iy = py[pp[t]] - py[pq[t]];     // |.| <= 70: int8
+        float dx = (float)ix, dy = (float)iy;
         float nrm = sqrtf(dx * dx + dy * dy);          // host sqrtf: correctly rounded
-        pdx[t] = dx; pdy[t] = dy; prn[t] = 1.0 / (double)nrm;
+        pk[t] = (uint32_t)pp[t] | ((uint32_t)pq[t] << 8) | ((uint32_t)(uint8_t)(int8_t)ix << 16) |
+                ((uint32_t)(uint8_t)(int8_t)iy << 24);
+        prn[t] = 1.0 / (double)nrm;
     }
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pdx), pdx, sizeof(pdx));
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pdy), pdy, sizeof(pdy));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pairpk), pk, sizeof(pk));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_prn), prn, sizeof(prn));
     g_tables_ready = true;
 }
@@ -369,12 +371,23 @@ __device__ __forceinline__ int refl101(int i, int n)
 __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restrict__ img0, size_t frame_bytes,
                                                   int write_response)
 {
-    __shared__ uint8_t s_src[ST_SH][ST_SW];
-    __shared__ uint32_t s_hb[ST_SH][ST_BW];
-    __shared__ float s_bl[ST_BH][ST_BW];
-    __shared__ float s_jx[ST_GH][ST_GW], s_jy[ST_GH][ST_GW], s_jxy[ST_GH][ST_GW];
-    __shared__ float s_r[ST_RH][ST_RW];
+    // LDS, aliased by lifetime (25 KB: 6 workgroups per CU): region X holds the source tile
+    // (phases 1-2), then the blurred tile (3-4), then the response (5-6); region Y the
+    // horizontal blur sums (2-3), then the three gradient planes (4-5)
+    constexpr int X_BYTES = ST_BH * ST_BW * 4;                 // the largest of the three
+    constexpr int Y_BYTES = 3 * ST_GH * ST_GW * 4;
+    static_assert(ST_SH * ST_SW <= X_BYTES && ST_RH * ST_RW * 4 <= X_BYTES, "stencil LDS region X");
+    static_assert(ST_SH * ST_BW * 4 <= Y_BYTES, "stencil LDS region Y");
+    __shared__ __align__(16) unsigned char s_x[X_BYTES];
+    __shared__ __align__(16) unsigned char s_y[Y_BYTES];
     __shared__ unsigned long long s_bal[ST_TH];
+    uint8_t (*s_src)[ST_SW] = reinterpret_cast<uint8_t (*)[ST_SW]>(s_x);
+    float (*s_bl)[ST_BW] = reinterpret_cast<float (*)[ST_BW]>(s_x);
+    float (*s_r)[ST_RW] = reinterpret_cast<float (*)[ST_RW]>(s_x);
+    uint32_t (*s_hb)[ST_BW] = reinterpret_cast<uint32_t (*)[ST_BW]>(s_y);
+    float (*s_jx)[ST_GW] = reinterpret_cast<float (*)[ST_GW]>(s_y);
+    float (*s_jy)[ST_GW] = reinterpret_cast<float (*)[ST_GW]>(s_y + ST_GH * ST_GW * 4);
+    float (*s_jxy)[ST_GW] = reinterpret_cast<float (*)[ST_GW]>(s_y + 2 * ST_GH * ST_GW * 4);
 
     const int W = d.W, H = d.H;
     const int x0 = blockIdx.x * ST_TW, y0 = blockIdx.y * ST_TH;
@@ -387,11 +400,26 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
     uint8_t* tilerows = d.tilerows + (size_t)z * d.ntiles * ST_TH;
     uint32_t* hist = d.hist + (size_t)z * VO_HIST_BINS;
 
-    // 1. source tile with BORDER_REFLECT_101 addressing
-    for (int e = tid; e < ST_SH * ST_SW; e += 256) {
-        int r = e / ST_SW, c = e - r * ST_SW;
-        int y = refl101(y0 - 7 + r, H), x = refl101(x0 - 7 + c, W);
-        s_src[r][c] = img[(size_t)y * W + x];
+    // 1. source tile with BORDER_REFLECT_101 addressing: every load of the thread in flight
+    //    before the first LDS store (no load-use chain per element)
+    {
+        constexpr int NE = ST_SH * ST_SW, NIT = (NE + 255) / 256;
+        uint8_t v[NIT];
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int e = tid + it * 256;
+            v[it] = 0;
+            if (e < NE) {
+                const int r = e / ST_SW, c = e - r * ST_SW;
+                const int y = refl101(y0 - 7 + r, H), x = refl101(x0 - 7 + c, W);
+                v[it] = img[(size_t)y * W + x];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int e = tid + it * 256;
+            if (e < NE) s_x[e] = v[it];
+        }
     }
     __syncthreads();
     // 2. horizontal 7-tap (exact u32)
@@ -434,31 +462,57 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
         s_jx[r][c] = jx; s_jy[r][c] = jy; s_jxy[r][c] = jxy;
     }
     __syncthreads();
-    // 5. response (kernel .c:97-114), m-outer n-inner f32 accumulation; 0 outside 2<=i<=H-3
-    const float thr = d.resp_thr;
-    for (int e = tid; e < ST_RH * ST_RW; e += 256) {
-        int r = e / ST_RW, c = e - r * ST_RW;
-        int y = y0 - 1 + r, x = x0 - 1 + c;
-        float out = 0.0f;
-        if (y >= 2 && y <= H - 3 && x >= 2 && x <= W - 3) {
-            float jx2 = 0.0f, jy2 = 0.0f, s = 0.0f;
+    // 5. response (kernel .c:97-114), m-outer n-inner f32 accumulation; 0 outside 2<=i<=H-3.
+    //    Thread (strip, column) computes RS vertically adjacent outputs and walks the source
+    //    rows once; each output's three sums still run in its own m-outer n-inner order.
+    {
+        constexpr int RS = ST_RH / 3;                               // 3 strips x ST_RW columns
+        static_assert(RS * 3 == ST_RH && 3 * ST_RW <= 256, "response strips");
+        const float thr = d.resp_thr;
+        const bool act = tid < 3 * ST_RW;
+        const int strip = act ? tid / ST_RW : 0, c = act ? tid - strip * ST_RW : 0, r0 = strip * RS;
+        float ax[RS], ay[RS], as[RS];
 #pragma unroll
-            for (int m = 0; m < 5; ++m)
+        for (int o = 0; o < RS; ++o) { ax[o] = 0.0f; ay[o] = 0.0f; as[o] = 0.0f; }
+        if (act) {
+#pragma unroll
+            for (int mr = 0; mr < RS + 4; ++mr) {
+                float jx[5], jy[5], jxy[5];
 #pragma unroll
                 for (int n = 0; n < 5; ++n) {
-                    float jx = s_jx[r + m][c + n], jy = s_jy[r + m][c + n], jxy = s_jxy[r + m][c + n];
-                    s = s + jxy;
-                    jx2 = jx2 + jx * jx;
-                    jy2 = jy2 + jy * jy;
+                    jx[n] = s_jx[r0 + mr][c + n]; jy[n] = s_jy[r0 + mr][c + n]; jxy[n] = s_jxy[r0 + mr][c + n];
                 }
-            float det = (jx2 * jy2) - (s * s);
-            float tr = jx2 + jy2;
-            float rv = (tr / 2.0f) - (0.5f * sqrtf(tr * tr - 4.0f * det));
-            out = rv > thr ? rv : 0.0f;
+#pragma unroll
+                for (int o = 0; o < RS; ++o) {
+                    const int m = mr - o;
+                    if (m < 0 || m > 4) continue;
+#pragma unroll
+                    for (int n = 0; n < 5; ++n) {
+                        as[o] = as[o] + jxy[n];
+                        ax[o] = ax[o] + jx[n] * jx[n];
+                        ay[o] = ay[o] + jy[n] * jy[n];
+                    }
+                }
+            }
         }
-        s_r[r][c] = out;
-        if (write_response && r >= 1 && r <= ST_TH && c >= 1 && c <= ST_TW && y < H && x < W)
-            d.response[(size_t)y * W + x] = out;
+        __syncthreads();                                           // s_r aliases s_bl's region
+        if (act) {
+#pragma unroll
+            for (int o = 0; o < RS; ++o) {
+                const int r = r0 + o;
+                const int y = y0 - 1 + r, x = x0 - 1 + c;
+                float out = 0.0f;
+                if (y >= 2 && y <= H - 3 && x >= 2 && x <= W - 3) {
+                    float det = (ax[o] * ay[o]) - (as[o] * as[o]);
+                    float tr = ax[o] + ay[o];
+                    float rv = (tr / 2.0f) - (0.5f * sqrtf(tr * tr - 4.0f * det));
+                    out = rv > thr ? rv : 0.0f;
+                }
+                s_r[r][c] = out;
+                if (write_response && r >= 1 && r <= ST_TH && c >= 1 && c <= ST_TW && y < H && x < W)
+                    d.response[(size_t)y * W + x] = out;
+            }
+        }
     }
     __syncthreads();
     // 6. strict 3x3 NMS inside the retinal margin (corner_detection_parallel_GPU.cpp:152-180).
@@ -902,82 +956,107 @@ __global__ void k_ext_missing(VoDev d, int slot)
 }
 
 // ---------------------------------------------------------------------------
-// describe: orientation (903-term sequential f32 sums) + rotation + 512 tests
-// 8 keypoints per 256-thread workgroup.  FREAK_feature_descriptor_parallel_GPU.cpp:10-210,
-// kernels .c:124-225, orientation order FREAK_feature_descriptor_parallel.cpp:16-44.
+// describe: orientation (903-term sequential f32 sums) + rotation + 512 tests.
+// FREAK_feature_descriptor_parallel_GPU.cpp:10-210, kernels .c:124-225, orientation order
+// FREAK_feature_descriptor_parallel.cpp:16-44.
+// One wave per DS_KPW = 32 keypoints: lane = keypoint k + 32 * component (0: O_x, 1: O_y),
+// so each lane runs one 903-term sum itself, in order, with the pair table read by scalar
+// loads (the pair index is wave-uniform) and the samples from LDS.  No cross-lane reduction,
+// ~7 KB of LDS per wave.
 // ---------------------------------------------------------------------------
-#define DS_KPB 8
-#define DS_TSTRIDE 905
+#define DS_KPW 32
+#define DS_WAVES 4
+#define DS_KPB (DS_KPW * DS_WAVES)
+#define DS_I1W 44                 // s_I1 row bytes: 11 dwords, odd, so 32 rows hit 32 banks
 
-__device__ __forceinline__ void describe_block(const VoDev& d, const uint8_t* __restrict__ img, int cur, int n,
-                                               int base)
+__device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __restrict__ img, int cur, int n,
+                                              int base, float (*s_I0)[VO_FREAK_NPOINTS],
+                                              uint8_t (*s_I1)[DS_I1W])
 {
-    const int nk = min(DS_KPB, n - base);
-    __shared__ float s_I0[DS_KPB][VO_FREAK_NPOINTS];
-    __shared__ float s_term[DS_KPB * 2][DS_TSTRIDE];
-    __shared__ float s_O[DS_KPB][2];
-    __shared__ float s_cs[DS_KPB][2];
-    __shared__ uint8_t s_I1[DS_KPB][48];
-    const int tid = threadIdx.x;
+    constexpr int NP = VO_FREAK_NPOINTS, HALF = (NP + 1) / 2;     // points per component lane
+    const int lane = threadIdx.x & 63, k = lane & 31, comp = lane >> 5;
     const int W = d.W, H = d.H;
-    const int2* kps = d.kps + (size_t)cur * d.N + base;
-
-    for (int e = tid; e < nk * VO_FREAK_NPOINTS; e += 256) {
-        int k = e / VO_FREAK_NPOINTS, p = e - k * VO_FREAK_NPOINTS;
-        int2 kp = kps[k];
-        s_I0[k][p] = (float)img[(size_t)(kp.y + c_pt_y[p]) * W + (kp.x + c_pt_x[p])];
-    }
-    __syncthreads();
-    for (int e = tid; e < nk * VO_FREAK_NPAIRS; e += 256) {
-        int k = e / VO_FREAK_NPAIRS, t = e - k * VO_FREAK_NPAIRS;
-        int p = c_pair_p[t], q = c_pair_q[t];
-        float ic = s_I0[k][p] - s_I0[k][q];
-        const double rn = c_prn[t];
-        s_term[2 * k][t] = (float)((double)(ic * c_pdx[t]) * rn);
-        s_term[2 * k + 1][t] = (float)((double)(ic * c_pdy[t]) * rn);
-    }
-    __syncthreads();
-    if (tid < 2 * nk) {
-        const float* row = s_term[tid];
-        float acc = 0.0f;
-        for (int t = 0; t < VO_FREAK_NPAIRS; ++t) acc = acc + row[t];
-        s_O[tid >> 1][tid & 1] = acc;
-    }
-    __syncthreads();
-    if (tid < nk) {
-        float Ox = s_O[tid][0], Oy = s_O[tid][1];
-        float angle = 0.0f;
-        if (!(isnan(Ox) || isnan(Oy))) angle = (float)det_atan2((double)Oy, (double)Ox);
-        double sd, cd;
-        det_sincos((double)angle, &sd, &cd);
-        s_cs[tid][0] = (float)cd;
-        s_cs[tid][1] = (float)sd;
-    }
-    __syncthreads();
-    for (int e = tid; e < nk * VO_FREAK_NPOINTS; e += 256) {
-        int k = e / VO_FREAK_NPOINTS, p = e - k * VO_FREAK_NPOINTS;
-        int2 kp = kps[k];
-        float c = s_cs[k][0], s = s_cs[k][1];
-        float ms = -1.0f * s;
-        int px = c_pt_x[p], py = c_pt_y[p];
-        int x = (int)(((float)kp.x + (float)px * c) + (float)py * s);
-        int y = (int)(((float)kp.y + (float)(-1 * px) * ms) + (float)py * c);
-        x = min(max(x, 0), W - 1);   // in range for every keypoint inside the margin
-        y = min(max(y, 0), H - 1);
-        s_I1[k][p] = img[(size_t)y * W + x];
-    }
-    __syncthreads();
-    const int wave = tid >> 6, lane = tid & 63;
-    for (int it = wave; it < nk * 8; it += 4) {
-        int k = it >> 3, w = it & 7;
-        int t = w * 64 + lane;
-        int e = c_patch[t];
-        bool bit = s_I1[k][c_pair_p[e]] > s_I1[k][c_pair_q[e]];
-        unsigned long long word = ballot64(bit);
-        if (lane == 0) {
-            d.desc[((size_t)cur * d.N + base + k) * 8 + w] = word;
-            if (w == 0) d.pre[(size_t)cur * d.N + base + k] = (uint32_t)word;
+    const bool valid = base + k < n;
+    const int2 kp = valid ? d.kps[(size_t)cur * d.N + base + k] : make_int2(0, 0);
+    // 1. pattern samples of keypoint k: component 0 lanes points [0, HALF), 1 the rest; all
+    //    loads in flight before the LDS stores
+    {
+        uint8_t v[HALF];
+#pragma unroll
+        for (int u = 0; u < HALF; ++u) {
+            const int p = comp ? HALF + u : u;
+            const int px = comp ? (HALF + u < NP ? c_pt_x[HALF + u] : 0) : c_pt_x[u];
+            const int py = comp ? (HALF + u < NP ? c_pt_y[HALF + u] : 0) : c_pt_y[u];
+            v[u] = (valid && p < NP) ? img[(size_t)(kp.y + py) * W + (kp.x + px)] : (uint8_t)0;
         }
+#pragma unroll
+        for (int u = 0; u < HALF; ++u) {
+            const int p = comp ? HALF + u : u;
+            if (p < NP) s_I0[k][p] = (float)v[u];
+        }
+    }
+    __syncthreads();
+    // 2. O_comp = sum over pairs t = 0..902 of (ic * d_comp) / |d|, sequential f32
+    float acc = 0.0f;
+    {
+        const float* I0k = s_I0[k];
+#pragma unroll 8
+        for (int t = 0; t < VO_FREAK_NPAIRS; ++t) {
+            const uint32_t pk = c_pairpk[t];
+            const int p = (int)(pk & 0xFF), q = (int)((pk >> 8) & 0xFF);
+            const float dx = (float)(int8_t)(pk >> 16), dy = (float)(int8_t)(pk >> 24);
+            const float ic = I0k[p] - I0k[q];
+            acc = acc + (float)((double)(ic * (comp ? dy : dx)) * c_prn[t]);
+        }
+    }
+    // 3. angle and rotation (both lanes of keypoint k)
+    const float Ox = __shfl(acc, k), Oy = __shfl(acc, k + 32);
+    float angle = 0.0f;
+    if (!(isnan(Ox) || isnan(Oy))) angle = (float)det_atan2((double)Oy, (double)Ox);
+    double sd, cd;
+    det_sincos((double)angle, &sd, &cd);
+    const float c = (float)cd, s = (float)sd, ms = -1.0f * s;
+    // 4. rotated samples (quirk 4: A = [[c, s], [s, c]], (int) truncation)
+    {
+        uint8_t v[HALF];
+#pragma unroll
+        for (int u = 0; u < HALF; ++u) {
+            const int p = comp ? HALF + u : u;
+            const int px = comp ? (HALF + u < NP ? c_pt_x[HALF + u] : 0) : c_pt_x[u];
+            const int py = comp ? (HALF + u < NP ? c_pt_y[HALF + u] : 0) : c_pt_y[u];
+            int x = (int)(((float)kp.x + (float)px * c) + (float)py * s);
+            int y = (int)(((float)kp.y + (float)(-1 * px) * ms) + (float)py * c);
+            x = min(max(x, 0), W - 1);   // in range for every keypoint inside the margin
+            y = min(max(y, 0), H - 1);
+            v[u] = (valid && p < NP) ? img[(size_t)y * W + x] : (uint8_t)0;
+        }
+#pragma unroll
+        for (int u = 0; u < HALF; ++u) {
+            const int p = comp ? HALF + u : u;
+            if (p < NP) s_I1[k][p] = v[u];
+        }
+    }
+    __syncthreads();
+    // 5. the 512 tests: lane l owns test w * 64 + l of word w; one ballot per (keypoint, word)
+    uint32_t tpq[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        const int e = c_patch[w * 64 + lane];
+        tpq[w] = (uint32_t)c_pair_p[e] | ((uint32_t)c_pair_q[e] << 8);
+    }
+    const int nk = min(DS_KPW, n - base);
+    uint64_t* desc = d.desc + ((size_t)cur * d.N + base) * 8;
+    uint32_t* pre = d.pre + (size_t)cur * d.N + base;
+    for (int kk = 0; kk < nk; ++kk) {
+        unsigned long long mine = 0ull;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            const bool bit = s_I1[kk][tpq[w] & 0xFF] > s_I1[kk][tpq[w] >> 8];
+            const unsigned long long word = ballot64(bit);
+            mine = lane == w ? word : mine;
+        }
+        if (lane < 8) desc[(size_t)kk * 8 + lane] = mine;
+        if (lane == 0) pre[kk] = (uint32_t)mine;
     }
 }
 
@@ -985,11 +1064,15 @@ __device__ __forceinline__ void describe_block(const VoDev& d, const uint8_t* __
 // workgroup of the launch tells the pose queue that frames < publish are extracted
 __global__ void __launch_bounds__(256) k_describe(VoDev d, int f0, int slot_override, unsigned publish)
 {
+    __shared__ float s_I0[DS_WAVES][DS_KPW][VO_FREAK_NPOINTS];
+    __shared__ uint8_t s_I1[DS_WAVES][DS_KPW][DS_I1W];
     const int z = blockIdx.y;
     const int cur = ext_slot(f0, z, slot_override);
     const int n = d.ext->n_kps[cur];
-    const int base = blockIdx.x * DS_KPB;
-    if (base < n) describe_block(d, d.blurred + (size_t)z * d.W * d.H, cur, n, base);
+    const int wave = threadIdx.x >> 6;
+    const int base = blockIdx.x * DS_KPB + wave * DS_KPW;
+    if (blockIdx.x * DS_KPB < n)             // workgroup-uniform: the barriers inside are met by all
+        describe_wave(d, d.blurred + (size_t)z * d.W * d.H, cur, n, base, s_I0[wave], s_I1[wave]);
     if (!publish) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1032,7 +1115,7 @@ __device__ __forceinline__ int ratio_accept(uint32_t m1, uint32_t m2, float rati
 
 // 32-bit prefix mode: the cur frame's prefixes are staged once per workgroup in LDS
 // (16 KB at N = 4096), and each wave scores MT_QPW queries per candidate read.
-#define MT_QPW 2
+#define MT_QPW 8
 #define MT_QPB (4 * MT_QPW)
 __host__ __device__ inline int match_blocks(int N, int match_bits)
 {
