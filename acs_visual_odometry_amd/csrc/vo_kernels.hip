@@ -371,23 +371,23 @@ __device__ __forceinline__ int refl101(int i, int n)
 __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restrict__ img0, size_t frame_bytes,
                                                   int write_response)
 {
-    // LDS, aliased by lifetime (25 KB: 6 workgroups per CU): region X holds the source tile
-    // (phases 1-2), then the blurred tile (3-4), then the response (5-6); region Y the
-    // horizontal blur sums (2-3), then the three gradient planes (4-5)
-    constexpr int X_BYTES = ST_BH * ST_BW * 4;                 // the largest of the three
+    // LDS, aliased by lifetime (23 KB): region X holds the source tile (phases 1-2), then the
+    // blurred tile (3-4), then the response (5-6); region Y the horizontal blur sums (2-3),
+    // then the gradient planes Jx^2, Jy^2, Jxy (4-5)
+    constexpr int X_BYTES = ST_RH * ST_RW * 4;                 // the largest of the three
     constexpr int Y_BYTES = 3 * ST_GH * ST_GW * 4;
-    static_assert(ST_SH * ST_SW <= X_BYTES && ST_RH * ST_RW * 4 <= X_BYTES, "stencil LDS region X");
+    static_assert(ST_SH * ST_SW <= X_BYTES && ST_BH * ST_BW <= X_BYTES, "stencil LDS region X");
     static_assert(ST_SH * ST_BW * 4 <= Y_BYTES, "stencil LDS region Y");
     __shared__ __align__(16) unsigned char s_x[X_BYTES];
     __shared__ __align__(16) unsigned char s_y[Y_BYTES];
     __shared__ unsigned long long s_bal[ST_TH];
     uint8_t (*s_src)[ST_SW] = reinterpret_cast<uint8_t (*)[ST_SW]>(s_x);
-    float (*s_bl)[ST_BW] = reinterpret_cast<float (*)[ST_BW]>(s_x);
+    uint8_t (*s_bl)[ST_BW] = reinterpret_cast<uint8_t (*)[ST_BW]>(s_x);
     float (*s_r)[ST_RW] = reinterpret_cast<float (*)[ST_RW]>(s_x);
     uint32_t (*s_hb)[ST_BW] = reinterpret_cast<uint32_t (*)[ST_BW]>(s_y);
-    float (*s_jx)[ST_GW] = reinterpret_cast<float (*)[ST_GW]>(s_y);
-    float (*s_jy)[ST_GW] = reinterpret_cast<float (*)[ST_GW]>(s_y + ST_GH * ST_GW * 4);
-    float (*s_jxy)[ST_GW] = reinterpret_cast<float (*)[ST_GW]>(s_y + 2 * ST_GH * ST_GW * 4);
+    uint32_t (*s_qx)[ST_GW] = reinterpret_cast<uint32_t (*)[ST_GW]>(s_y);
+    uint32_t (*s_qy)[ST_GW] = reinterpret_cast<uint32_t (*)[ST_GW]>(s_y + ST_GH * ST_GW * 4);
+    int32_t (*s_qxy)[ST_GW] = reinterpret_cast<int32_t (*)[ST_GW]>(s_y + 2 * ST_GH * ST_GW * 4);
 
     const int W = d.W, H = d.H;
     const int x0 = blockIdx.x * ST_TW, y0 = blockIdx.y * ST_TH;
@@ -436,64 +436,91 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
         uint32_t v = 8u * s_hb[r][c] + 28u * s_hb[r + 1][c] + 56u * s_hb[r + 2][c] + 72u * s_hb[r + 3][c] +
                      56u * s_hb[r + 4][c] + 28u * s_hb[r + 5][c] + 8u * s_hb[r + 6][c];
         uint32_t b = (v + 32768u) >> 16;
-        s_bl[r][c] = (float)b;
+        s_bl[r][c] = (uint8_t)b;
         int y = y0 - 4 + r, x = x0 - 4 + c;
         if (r >= 4 && r < 4 + ST_TH && c >= 4 && c < 4 + ST_TW && y < H && x < W)
             blurred[(size_t)y * W + x] = (uint8_t)b;
     }
     __syncthreads();
-    // 4. gradients (kernel .c:59-76), 0 outside 1<=i<=H-2, 1<=j<=W-2
+    // 4. gradients (kernel .c:59-76), 0 outside 1<=i<=H-2, 1<=j<=W-2.  The reference computes
+    //    them in f32 on u8 values: every intermediate is an integer below 2^11, so integer
+    //    arithmetic gives the same values; Jx*Jx and Jy*Jy (< 2^21) are exact in f32 as well.
     for (int e = tid; e < ST_GH * ST_GW; e += 256) {
         int r = e / ST_GW, c = e - r * ST_GW;
         int y = y0 - 3 + r, x = x0 - 3 + c;
-        float jx = 0.f, jy = 0.f, jxy = 0.f;
+        int jx = 0, jy = 0, jxy = 0;
         if (y >= 1 && y <= H - 2 && x >= 1 && x <= W - 2) {
-            float sx[3], sy[3];
+            int sx[3], sy[3];
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                float a = s_bl[r][c + k], m = s_bl[r + 1][c + k], cc = s_bl[r + 2][c + k];
+                int a = s_bl[r][c + k], m = s_bl[r + 1][c + k], cc = s_bl[r + 2][c + k];
                 sx[k] = a - cc;
-                sy[k] = (a + 2.0f * m) + cc;
+                sy[k] = (a + 2 * m) + cc;
             }
-            jx = (sx[0] + 2.0f * sx[1]) + sx[2];
+            jx = (sx[0] + 2 * sx[1]) + sx[2];
             jy = sy[0] - sy[2];
             jxy = sx[0] - sx[2];
         }
-        s_jx[r][c] = jx; s_jy[r][c] = jy; s_jxy[r][c] = jxy;
+        s_qx[r][c] = (uint32_t)(jx * jx); s_qy[r][c] = (uint32_t)(jy * jy); s_qxy[r][c] = jxy;
     }
     __syncthreads();
-    // 5. response (kernel .c:97-114), m-outer n-inner f32 accumulation; 0 outside 2<=i<=H-3.
-    //    Thread (strip, column) computes RS vertically adjacent outputs and walks the source
-    //    rows once; each output's three sums still run in its own m-outer n-inner order.
+    // 5. response (kernel .c:97-114): 5x5 sums of Jx^2, Jy^2, Jxy accumulated in f32, m-outer
+    //    n-inner.  Every term is a non-negative integer (Jxy: |sum| < 2^14), so while the exact
+    //    total is <= 2^24 every f32 partial sum is exact and the in-order f32 sum equals the
+    //    integer sum: computed here as integer box sums, with the in-order f32 loop only for a
+    //    total above 2^24 (strong corners).  Thread (strip, column): RS outputs down a column.
     {
         constexpr int RS = ST_RH / 3;                               // 3 strips x ST_RW columns
         static_assert(RS * 3 == ST_RH && 3 * ST_RW <= 256, "response strips");
         const float thr = d.resp_thr;
         const bool act = tid < 3 * ST_RW;
         const int strip = act ? tid / ST_RW : 0, c = act ? tid - strip * ST_RW : 0, r0 = strip * RS;
-        float ax[RS], ay[RS], as[RS];
+        uint32_t ax[RS], ay[RS];
+        int as[RS];
 #pragma unroll
-        for (int o = 0; o < RS; ++o) { ax[o] = 0.0f; ay[o] = 0.0f; as[o] = 0.0f; }
+        for (int o = 0; o < RS; ++o) { ax[o] = 0u; ay[o] = 0u; as[o] = 0; }
         if (act) {
 #pragma unroll
             for (int mr = 0; mr < RS + 4; ++mr) {
-                float jx[5], jy[5], jxy[5];
+                uint32_t hx = 0u, hy = 0u;
+                int hs = 0;
 #pragma unroll
                 for (int n = 0; n < 5; ++n) {
-                    jx[n] = s_jx[r0 + mr][c + n]; jy[n] = s_jy[r0 + mr][c + n]; jxy[n] = s_jxy[r0 + mr][c + n];
+                    hx += s_qx[r0 + mr][c + n]; hy += s_qy[r0 + mr][c + n]; hs += s_qxy[r0 + mr][c + n];
                 }
 #pragma unroll
                 for (int o = 0; o < RS; ++o) {
                     const int m = mr - o;
                     if (m < 0 || m > 4) continue;
-#pragma unroll
-                    for (int n = 0; n < 5; ++n) {
-                        as[o] = as[o] + jxy[n];
-                        ax[o] = ax[o] + jx[n] * jx[n];
-                        ay[o] = ay[o] + jy[n] * jy[n];
-                    }
+                    ax[o] += hx; ay[o] += hy; as[o] += hs;
                 }
             }
+        }
+        float rv_out[RS];
+#pragma unroll
+        for (int o = 0; o < RS; ++o) {
+            const int r = r0 + o;
+            const int y = y0 - 1 + r, x = x0 - 1 + c;
+            float out = 0.0f;
+            if (act && y >= 2 && y <= H - 3 && x >= 2 && x <= W - 3) {
+                float jx2 = (float)ax[o], jy2 = (float)ay[o];
+                const float sxy = (float)as[o];
+                if (ax[o] > (1u << 24)) {                           // rare: the in-order f32 sum
+                    jx2 = 0.0f;
+                    for (int m = 0; m < 5; ++m)
+                        for (int n = 0; n < 5; ++n) jx2 = jx2 + (float)s_qx[r + m][c + n];
+                }
+                if (ay[o] > (1u << 24)) {
+                    jy2 = 0.0f;
+                    for (int m = 0; m < 5; ++m)
+                        for (int n = 0; n < 5; ++n) jy2 = jy2 + (float)s_qy[r + m][c + n];
+                }
+                float det = (jx2 * jy2) - (sxy * sxy);
+                float tr = jx2 + jy2;
+                float rv = (tr / 2.0f) - (0.5f * sqrtf(tr * tr - 4.0f * det));
+                out = rv > thr ? rv : 0.0f;
+            }
+            rv_out[o] = out;
         }
         __syncthreads();                                           // s_r aliases s_bl's region
         if (act) {
@@ -501,16 +528,9 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
             for (int o = 0; o < RS; ++o) {
                 const int r = r0 + o;
                 const int y = y0 - 1 + r, x = x0 - 1 + c;
-                float out = 0.0f;
-                if (y >= 2 && y <= H - 3 && x >= 2 && x <= W - 3) {
-                    float det = (ax[o] * ay[o]) - (as[o] * as[o]);
-                    float tr = ax[o] + ay[o];
-                    float rv = (tr / 2.0f) - (0.5f * sqrtf(tr * tr - 4.0f * det));
-                    out = rv > thr ? rv : 0.0f;
-                }
-                s_r[r][c] = out;
+                s_r[r][c] = rv_out[o];
                 if (write_response && r >= 1 && r <= ST_TH && c >= 1 && c <= ST_TW && y < H && x < W)
-                    d.response[(size_t)y * W + x] = out;
+                    d.response[(size_t)y * W + x] = rv_out[o];
             }
         }
     }
@@ -644,6 +664,8 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     __shared__ int s_nbnd, s_b, s_above;
     __shared__ uint64_t s_tb;
     __shared__ int s_slot;
+    __shared__ uint32_t s_dh[256];
+    __shared__ int s_dsel, s_rem;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int N = d.N;
     const int ntx = (d.W + ST_TW - 1) / ST_TW, nty = (d.H + ST_TH - 1) / ST_TH, ntiles = ntx * nty;
@@ -770,13 +792,41 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
         __syncthreads();
         VO_STAMP(d, 1990, 3);
         const int nb = s_nbnd;
-        if (nb > BND_CAP) {            // boundary bin too large for LDS (never observed)
-            ovf = true;
-        }
         // the need-th largest boundary key: the one with exactly need-1 larger keys
         const int need = N - s_above;
         Tb = ~0ull;
-        if (need > 0 && !ovf) {
+        if (nb > BND_CAP && need > 0) {
+            // boundary bin too large to rank in LDS (periodic patterns: many equal responses):
+            // radix select over the bin's full 64-bit keys, 8 bits per pass from the top
+            uint64_t prefix = 0ull, pmask = 0ull;
+            int rem = need;
+            for (int shift = 56; shift >= 0; shift -= 8) {
+                if (tid < 256) s_dh[tid] = 0u;
+                __syncthreads();
+                for (int g = tid; g < C; g += 1024) {
+                    const uint64_t v = keys[g];
+                    if ((int)sel_bin(v, d.thr_bits) == b && (v & pmask) == prefix)
+                        atomicAdd(&s_dh[(v >> shift) & 0xFF], 1u);
+                }
+                __syncthreads();
+                if (tid == 0) {
+                    int run = 0, dsel = 0;
+                    for (int dd = 255; dd >= 0; --dd) {
+                        const int h = (int)s_dh[dd];
+                        if (run + h >= rem) { dsel = dd; break; }
+                        run += h;
+                    }
+                    s_dsel = dsel;
+                    s_rem = rem - run;
+                }
+                __syncthreads();
+                prefix |= (uint64_t)s_dsel << shift;
+                pmask |= 0xFFull << shift;
+                rem = s_rem;
+                __syncthreads();
+            }
+            Tb = prefix;                               // keys are unique: one key matches all 64 bits
+        } else if (need > 0) {
             for (int e = tid; e < nb; e += 1024) {
                 const uint64_t ke = s_bnd[e];
                 int rank = 0;
@@ -2462,7 +2512,7 @@ void launch_ext_missing(const VoDev& d, int slot, hipStream_t s)
 int select_lds_bytes(int W, int H, int* key_cap)
 {
     const int ntiles = ((W + ST_TW - 1) / ST_TW) * ((H + ST_TH - 1) / ST_TH);
-    const int bytes = 160 * 1024 - 512;                // static __shared__ of k_select < 512 B
+    const int bytes = 160 * 1024 - 2048;               // static __shared__ of k_select < 2 KB
     if (hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
         return -1;
     const SelLayout L = sel_layout(ntiles, bytes);

@@ -85,6 +85,27 @@ def test_response_map_bit_exact(ctx_kitti, scene, factory):
     c2.close()
 
 
+def test_response_map_strong_edges_bit_exact(ctx_kitti):
+    """0/255 blocks: the strongest gradients a blurred u8 image can have.  The stencil sums
+    Jx^2, Jy^2 as integers, which equals the reference's in-order f32 sums while the totals
+    stay <= 2^24.  After the 7-tap blur a 2-pixel difference is at most 127.5, so |J| <= 510
+    and a 5x5 sum of squares <= 6.5e6: the bound always holds (the kernel keeps an in-order
+    f32 fallback regardless)."""
+    H, W = 376, 1241
+    yy, xx = np.mgrid[0:H, 0:W]
+    img = np.where(((yy // 9) + (xx // 11)) % 2 == 0, 0, 255).astype(np.uint8)
+    img[100:140, 300:700] = 255
+    img[200:260, 500:540] = 0
+    G = O.gradients(O.blur7(img))
+    assert max(np.abs(G[0]).max(), np.abs(G[1]).max()) <= 510
+    R = ctx_kitti.response(img)
+    Rr = O.response(O.blur7(img))
+    assert np.array_equal(R.view(np.uint32), Rr.view(np.uint32))
+    k_gpu, d_gpu = ctx_kitti.extract(img)
+    k_ref, d_ref, _ = O.extract(img, O.config(W, H))
+    assert np.array_equal(k_gpu, k_ref) and np.array_equal(d_gpu, d_ref)
+
+
 @pytest.mark.parametrize("which", ["scene0", "scene3", "noise", "factory1", "factory2"])
 def test_extract_bit_exact(which, ctx_kitti, scene, factory):
     seq, frames = scene
