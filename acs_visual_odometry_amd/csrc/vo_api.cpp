@@ -45,6 +45,8 @@ struct vo_ctx {
     int out_cap = 0;
     VoFrameOut* out_host = nullptr;   // pinned
     int32_t* lo_host = nullptr;       // pinned: VoState::lo after a chunk
+    hipEvent_t ev_reset = nullptr;    // recorded on s by vo_reset; the extract queue waits on it
+    bool reset_pending = false;
     uint8_t* stage_host = nullptr;    // pinned frame staging
     uint16_t* tab_dev = nullptr;
     double stage_F[9] = {0};          // vo_ransac_F's FundamentalMatrix (persists across calls)
@@ -249,6 +251,10 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     const int base = c->fidx, end = base + nf, B = c->B;
     hipStream_t s = c->s;
     hipStream_t q = (c->serial || host_frame || !img0) ? s : c->se;
+    if (q != s && c->reset_pending) {
+        HIPCHK(hipStreamWaitEvent(q, c->ev_reset, 0));
+        c->reset_pending = false;
+    }
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&c->d.st->end, end, 1, s));
     const int nb = (nf + B - 1) / B;
     if (!img0) {
@@ -268,6 +274,9 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     }
     for (;;) {
         HIPCHK(hipGetLastError());
+        // the chunk's output rows and the commit point in one round trip
+        HIPCHK(hipMemcpyAsync(c->out_host + (base - out_base), out + (base - out_base), sizeof(VoFrameOut) * nf,
+                              hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(c->lo_host, &c->d.st->lo, sizeof(int32_t), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         const int lo = *c->lo_host;
@@ -289,17 +298,6 @@ int ensure_out(vo_ctx* c, int n)
     HIPCHK(hipHostMalloc((void**)&c->out_host, sizeof(VoFrameOut) * (size_t)n, hipHostMallocDefault));
     c->out_cap = n;
     return VO_OK;
-}
-
-void init_state(VoState* h)
-{
-    std::memset(h, 0, sizeof(*h));
-    h->lo = 0; h->end = 0;
-    h->prev_slot = 0;
-    h->last_valid = 0;
-    h->model_n = 0;
-    h->scale_override = std::nan("");
-    for (int i = 0; i < 16; ++i) h->Tcurr[i] = (i % 5 == 0) ? 1.0 : 0.0;
 }
 
 int finish_timing(vo_ctx* c, EvRec* ev)
@@ -405,6 +403,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     c->serial = getenv("VO_SERIAL") && atoi(getenv("VO_SERIAL")) != 0;
     if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipStreamCreateWithFlags(&c->se, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming)) != VO_OK) return bail(VO_ERR_HIP);
     d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
     if (d.sel_lds < 0) return bail(VO_ERR_HIP);
     const size_t np = (size_t)W * H;
@@ -472,26 +471,23 @@ void vo_destroy(vo_ctx* c)
     if (c->stage_host) (void)hipHostFree(c->stage_host);
     if (c->lo_host) (void)hipHostFree(c->lo_host);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->ev_reset) (void)hipEventDestroy(c->ev_reset);
     if (c->se) (void)hipStreamDestroy(c->se);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
 }
 
+// Asynchronous: one kernel on the pose queue (every API call ends synchronised, so nothing
+// is in flight); the extract queue's next batch waits for it through ev_reset.
 int vo_reset(vo_ctx* c)
 {
     if (!c) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    SYNC_ALL(c);
-    VoState h;
-    init_state(&h);
-    HIPCHK(hipMemcpy(c->d.st, &h, sizeof(h), hipMemcpyHostToDevice));
-    std::vector<int32_t> e(2 * VO_SLOTS, 0);          // n_kps = 0, status = VO_STATUS_OK
-    HIPCHK(hipMemcpy(c->d.ext, e.data(), sizeof(VoExt), hipMemcpyHostToDevice));
-    HIPCHK(hipMemset(c->d.hist, 0, sizeof(uint32_t) * VO_HIST_BINS * c->B));
-    HIPCHK(hipMemset(c->d.work, 0, sizeof(VoWork) * c->B));
-    HIPCHK(hipMemset(c->d.ctr, 0, sizeof(unsigned) * VO_CTR_WORDS));
+    vo::launch_reset(c->d, c->s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev_reset, c->s));
+    c->reset_pending = true;
     c->fidx = 0;
-    HIPCHK(hipDeviceSynchronize());
     return VO_OK;
 }
 
@@ -668,7 +664,6 @@ int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_
     // one frame: extract on the pose queue, a window of one (no speculation)
     int rc = run_chunk(c, gray ? c->d.frame_in : nullptr, 0, 1, c->out_dev, f, nullptr, true);
     if (rc) return rc;
-    HIPCHK(hipMemcpy(c->out_host, c->out_dev, sizeof(VoFrameOut), hipMemcpyDeviceToHost));
     const VoFrameOut& o = c->out_host[0];
     if (pose_out) std::memcpy(pose_out, o.pose, sizeof(o.pose));
     if (status) *status = o.status;
@@ -696,8 +691,6 @@ int vo_process_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
         rc = run_chunk(c, d_frames + (size_t)f0 * frame_bytes, frame_bytes, nf, c->out_dev, base, evp, false);
         if (rc) return rc;
     }
-    if (nframes)
-        HIPCHK(hipMemcpy(c->out_host, c->out_dev, sizeof(VoFrameOut) * nframes, hipMemcpyDeviceToHost));
     rc = finish_timing(c, evp);
     if (rc) return rc;
     c->last_frames = nframes;

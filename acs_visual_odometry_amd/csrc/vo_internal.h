@@ -174,6 +174,7 @@ void launch_refit(const VoDev& d, int with_pose, int stage, hipStream_t s);
 void launch_triangulate(const VoDev& d, int stage, hipStream_t s);
 void launch_finalize(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s);
 void launch_pose_stage(const VoDev& d, int phase, hipStream_t s);   // vo_pose: 0 prepare, 1 choose
+void launch_reset(const VoDev& d, hipStream_t s);                   // vo_reset's device state
 void launch_selftest_arith(const float* fa, const float* fb, float* fo, const double* da,
                            const double* db, double* dout, int n, hipStream_t s);
 int kernel_count();

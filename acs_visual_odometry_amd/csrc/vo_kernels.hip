@@ -2450,6 +2450,28 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
     }
 }
 
+// vo_reset on the device (VisualOdometry.cpp:50-62 initial state): trajectory state, slot
+// statuses, histograms, window records and cross-queue counters; no host round trip
+__global__ void __launch_bounds__(256) k_reset(VoDev d)
+{
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+    if (tid == 0) {
+        VoState* st = d.st;
+        st->lo = 0; st->end = 0; st->prev_slot = 0; st->last_valid = 0;
+        st->model_n = 0; st->model_degenerate = 0; st->pose_status = 0;
+        for (int i = 0; i < 9; ++i) { st->model_F[i] = 0.0; st->model_R[i] = 0.0; st->pose_R[i] = 0.0; }
+        for (int i = 0; i < 3; ++i) { st->model_t[i] = 0.0; st->pose_t[i] = 0.0; }
+        for (int i = 0; i < 16; ++i) st->Tcurr[i] = (i % 5 == 0) ? 1.0 : 0.0;
+        st->scale_override = __longlong_as_double(0x7FF8000000000000ll);
+    }
+    int32_t* ext = reinterpret_cast<int32_t*>(d.ext);
+    for (int i = tid; i < (int)(sizeof(VoExt) / 4); i += nth) ext[i] = 0;   // n_kps 0, status OK
+    for (int i = tid; i < VO_HIST_BINS * d.B; i += nth) d.hist[i] = 0u;
+    uint32_t* w = reinterpret_cast<uint32_t*>(d.work);
+    for (int i = tid; i < (int)(sizeof(VoWork) / 4) * d.B; i += nth) w[i] = 0u;
+    for (int i = tid; i < VO_CTR_WORDS; i += nth) d.ctr[i] = 0u;
+}
+
 // vo_pose (PoseUpdate::getPose on caller data in work[0]): phase 0 the prologue, phase 1
 // (after k_triangulate) the candidate choice and the caller's scale
 __global__ void k_pose_stage(VoDev d, int phase)
@@ -2551,6 +2573,10 @@ void launch_triangulate(const VoDev& d, int stage, hipStream_t s)
 void launch_finalize(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s)
 {
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, d, out, out_base);
+}
+void launch_reset(const VoDev& d, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_reset, dim3(16), dim3(256), 0, s, d);
 }
 void launch_pose_stage(const VoDev& d, int phase, hipStream_t s)
 {
