@@ -43,7 +43,7 @@
 // keypoint/descriptor slots: frame f (since vo_reset) is extracted into ring slot
 // f % VO_RING; the last valid frame's copy lives in the carry slot during a skip run; the
 // stage APIs (vo_extract / vo_match) use their own two slots
-#define VO_RING 256
+#define VO_RING 1024
 #define VO_CARRY_SLOT VO_RING
 #define VO_STAGE_SLOT (VO_RING + 1)
 #define VO_SLOTS (VO_RING + 3)

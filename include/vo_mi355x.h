@@ -127,7 +127,7 @@ int  vo_process_frame(vo_ctx* ctx, const uint8_t* gray, size_t stride, double po
  * d_frames + f * frame_bytes (dense W x H u8).  Frames are extracted frame_batch at a time
  * on one queue and posed in windows of frame_batch frames on another (each frame matched
  * speculatively against its predecessor; a frame after a skipped one is re-run), with one
- * host synchronisation per VO_CHUNK = 255 frames (more only after skipped frames).  Results
+ * host synchronisation per VO_CHUNK = 1023 frames (more only after skipped frames).  Results
  * are those of nframes vo_process_frame calls.  poses_out: nframes*12, status_out: nframes,
  * info_out: nframes*8 (all host, optional). */
 int  vo_process_frames_device(vo_ctx* ctx, const uint8_t* d_frames, size_t frame_bytes, int nframes,

@@ -330,10 +330,10 @@ def test_windowed_batch_matches_oracle(blank, batch):
 
 
 def test_windowed_batch_across_chunks_and_ring_wrap():
-    """300 frames: two host chunks (VO_CHUNK = 255) and a wrap of the 256-slot ring, with a
+    """1100 frames: two host chunks (VO_CHUNK = 1023) and a wrap of the 1024-slot ring, with a
     skip run that straddles the chunk boundary (the carry slot outlives the chunk)."""
-    seq = SceneSequence(400, 240, nframes=300, step=0.05)
+    seq = SceneSequence(320, 192, nframes=1100, step=0.05)
     frames = seq.frames()
-    for b in range(250, 262):
+    for b in range(1015, 1030):
         frames[b] = 128
-    _device_vs_oracle(seq, frames, max_kpts=300, frame_batch=16)
+    _device_vs_oracle(seq, frames, max_kpts=200, frame_batch=16)
