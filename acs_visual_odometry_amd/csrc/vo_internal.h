@@ -57,7 +57,8 @@
 #define VO_SYNC_EXT 32         // frames extracted since vo_reset (the pose queue waits on it)
 #define VO_CTR_WORDS 64
 #define VO_MAX_HYP 2000
-#define VO_HYP_CHUNK0 256
+#define VO_HYP_CHUNK0 128     // RANSAC launch chunks (vo_kernels.hip launch_ransac)
+#define VO_HYP_CHUNK1 512
 
 struct VoFrameOut {
     int32_t status, n_kps, n_matches, n_inl, best_k, n_eval, fitted, frame;

@@ -361,6 +361,15 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #define ST_RW (ST_TW + 2)    // response tile
 #define ST_RH (ST_TH + 2)
 
+// (r, c) of element e -> of element e + 256 in a row-major array of COLS columns
+template <int COLS>
+__device__ __forceinline__ void rc_step(int& r, int& c)
+{
+    r += 256 / COLS;
+    c += 256 % COLS;
+    if (c >= COLS) { c -= COLS; ++r; }
+}
+
 __device__ __forceinline__ int refl101(int i, int n)
 {
     if (n == 1) return 0;
@@ -405,14 +414,25 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
     {
         constexpr int NE = ST_SH * ST_SW, NIT = (NE + 255) / 256;
         uint8_t v[NIT];
+        int r = tid / ST_SW, c = tid - r * ST_SW;               // element tid + 256 * it, stepped
+        // workgroup-uniform: tiles whose source window is inside the image need no reflection
+        const bool interior = x0 >= 7 && y0 >= 7 && x0 - 7 + ST_SW <= W && y0 - 7 + ST_SH <= H;
+        if (interior) {
+            const uint8_t* __restrict__ org = img + (size_t)(y0 - 7) * W + (x0 - 7);
 #pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            const int e = tid + it * 256;
-            v[it] = 0;
-            if (e < NE) {
-                const int r = e / ST_SW, c = e - r * ST_SW;
-                const int y = refl101(y0 - 7 + r, H), x = refl101(x0 - 7 + c, W);
-                v[it] = img[(size_t)y * W + x];
+            for (int it = 0; it < NIT; ++it) {
+                v[it] = r < ST_SH ? org[(size_t)r * W + c] : (uint8_t)0;
+                rc_step<ST_SW>(r, c);
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < NIT; ++it) {
+                v[it] = 0;
+                if (r < ST_SH) {
+                    const int y = refl101(y0 - 7 + r, H), x = refl101(x0 - 7 + c, W);
+                    v[it] = img[(size_t)y * W + x];
+                }
+                rc_step<ST_SW>(r, c);
             }
         }
 #pragma unroll
@@ -422,19 +442,19 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
         }
     }
     __syncthreads();
-    // 2. horizontal 7-tap (exact u32)
-    for (int e = tid; e < ST_SH * ST_BW; e += 256) {
-        int r = e / ST_BW, c = e - r * ST_BW;
-        const uint8_t* s = &s_src[r][c];
-        uint32_t h = 8u * s[0] + 28u * s[1] + 56u * s[2] + 72u * s[3] + 56u * s[4] + 28u * s[5] + 8u * s[6];
+    // 2. horizontal 7-tap (exact; 24-bit multiplies: every product < 2^24)
+    for (int r = tid / ST_BW, c = tid - (tid / ST_BW) * ST_BW; r < ST_SH; rc_step<ST_BW>(r, c)) {
+        const uint8_t* sp = &s_src[r][c];
+        // symmetric taps: 8(s0+s6) + 28(s1+s5) + 56(s2+s4) + 72 s3, exact in u32
+        uint32_t h = __umul24(8u, (uint32_t)sp[0] + sp[6]) + __umul24(28u, (uint32_t)sp[1] + sp[5]) +
+                     __umul24(56u, (uint32_t)sp[2] + sp[4]) + __umul24(72u, (uint32_t)sp[3]);
         s_hb[r][c] = h;
     }
     __syncthreads();
     // 3. vertical 7-tap, round, u8 (cv::GaussianBlur 8U fixed point); blurred -> HBM
-    for (int e = tid; e < ST_BH * ST_BW; e += 256) {
-        int r = e / ST_BW, c = e - r * ST_BW;
-        uint32_t v = 8u * s_hb[r][c] + 28u * s_hb[r + 1][c] + 56u * s_hb[r + 2][c] + 72u * s_hb[r + 3][c] +
-                     56u * s_hb[r + 4][c] + 28u * s_hb[r + 5][c] + 8u * s_hb[r + 6][c];
+    for (int r = tid / ST_BW, c = tid - (tid / ST_BW) * ST_BW; r < ST_BH; rc_step<ST_BW>(r, c)) {
+        uint32_t v = __umul24(8u, s_hb[r][c] + s_hb[r + 6][c]) + __umul24(28u, s_hb[r + 1][c] + s_hb[r + 5][c]) +
+                     __umul24(56u, s_hb[r + 2][c] + s_hb[r + 4][c]) + __umul24(72u, s_hb[r + 3][c]);
         uint32_t b = (v + 32768u) >> 16;
         s_bl[r][c] = (uint8_t)b;
         int y = y0 - 4 + r, x = x0 - 4 + c;
@@ -445,8 +465,7 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
     // 4. gradients (kernel .c:59-76), 0 outside 1<=i<=H-2, 1<=j<=W-2.  The reference computes
     //    them in f32 on u8 values: every intermediate is an integer below 2^11, so integer
     //    arithmetic gives the same values; Jx*Jx and Jy*Jy (< 2^21) are exact in f32 as well.
-    for (int e = tid; e < ST_GH * ST_GW; e += 256) {
-        int r = e / ST_GW, c = e - r * ST_GW;
+    for (int r = tid / ST_GW, c = tid - (tid / ST_GW) * ST_GW; r < ST_GH; rc_step<ST_GW>(r, c)) {
         int y = y0 - 3 + r, x = x0 - 3 + c;
         int jx = 0, jy = 0, jxy = 0;
         if (y >= 1 && y <= H - 2 && x >= 1 && x <= W - 2) {
@@ -461,7 +480,7 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
             jy = sy[0] - sy[2];
             jxy = sx[0] - sx[2];
         }
-        s_qx[r][c] = (uint32_t)(jx * jx); s_qy[r][c] = (uint32_t)(jy * jy); s_qxy[r][c] = jxy;
+        s_qx[r][c] = (uint32_t)__mul24(jx, jx); s_qy[r][c] = (uint32_t)__mul24(jy, jy); s_qxy[r][c] = jxy;
     }
     __syncthreads();
     // 5. response (kernel .c:97-114): 5x5 sums of Jx^2, Jy^2, Jxy accumulated in f32, m-outer
@@ -517,7 +536,8 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
                 }
                 float det = (jx2 * jy2) - (sxy * sxy);
                 float tr = jx2 + jy2;
-                float rv = (tr / 2.0f) - (0.5f * sqrtf(tr * tr - 4.0f * det));
+                // tr / 2 == tr * 0.5 exactly (both the correctly rounded halving)
+                float rv = (tr * 0.5f) - (0.5f * sqrtf(tr * tr - 4.0f * det));
                 out = rv > thr ? rv : 0.0f;
             }
             rv_out[o] = out;
@@ -1027,36 +1047,55 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
     const int lane = threadIdx.x & 63, k = lane & 31, comp = lane >> 5;
     const int W = d.W, H = d.H;
     const bool valid = base + k < n;
-    const int2 kp = valid ? d.kps[(size_t)cur * d.N + base + k] : make_int2(0, 0);
+    // lanes past n sample around a keypoint inside the margin: every address stays in bounds
+    // and the gathers need no branches (their values are never used)
+    const int2 kp = valid ? d.kps[(size_t)cur * d.N + base + k] : make_int2(d.bcol, d.brow);
+    // point u of this lane's half (the second half's last slot repeats point NP - 1)
+    auto pt = [&](int u, int& px, int& py) {
+        const int pa = u, pb = HALF + u < NP ? HALF + u : NP - 1;   // both wave-uniform
+        px = comp ? c_pt_x[pb] : c_pt_x[pa];
+        py = comp ? c_pt_y[pb] : c_pt_y[pa];
+    };
     // 1. pattern samples of keypoint k: component 0 lanes points [0, HALF), 1 the rest; all
     //    loads in flight before the LDS stores
     {
         uint8_t v[HALF];
 #pragma unroll
         for (int u = 0; u < HALF; ++u) {
-            const int p = comp ? HALF + u : u;
-            const int px = comp ? (HALF + u < NP ? c_pt_x[HALF + u] : 0) : c_pt_x[u];
-            const int py = comp ? (HALF + u < NP ? c_pt_y[HALF + u] : 0) : c_pt_y[u];
-            v[u] = (valid && p < NP) ? img[(size_t)(kp.y + py) * W + (kp.x + px)] : (uint8_t)0;
+            int px, py;
+            pt(u, px, py);
+            v[u] = img[(size_t)(kp.y + py) * W + (kp.x + px)];
         }
 #pragma unroll
-        for (int u = 0; u < HALF; ++u) {
-            const int p = comp ? HALF + u : u;
-            if (p < NP) s_I0[k][p] = (float)v[u];
-        }
+        for (int u = 0; u < HALF; ++u)
+            if (!comp || HALF + u < NP) s_I0[k][comp ? HALF + u : u] = (float)v[u];
     }
     __syncthreads();
-    // 2. O_comp = sum over pairs t = 0..902 of (ic * d_comp) / |d|, sequential f32
+    // 2. O_comp = sum over pairs t = 0..902 of (ic * d_comp) / |d|, in order in f32.  The
+    //    terms of DS_U consecutive pairs are independent: computed first (their conversions
+    //    and f64 products overlap), then added in order.
     float acc = 0.0f;
     {
+        constexpr int DS_U = 8;
         const float* I0k = s_I0[k];
-#pragma unroll 8
-        for (int t = 0; t < VO_FREAK_NPAIRS; ++t) {
+        const int shift = comp ? 24 : 16;
+        int t = 0;
+        for (; t + DS_U <= VO_FREAK_NPAIRS; t += DS_U) {
+            float tm[DS_U];
+#pragma unroll
+            for (int u = 0; u < DS_U; ++u) {
+                const uint32_t pk = c_pairpk[t + u];
+                const float ic = I0k[pk & 0xFF] - I0k[(pk >> 8) & 0xFF];
+                const float dd = (float)(int8_t)(pk >> shift);
+                tm[u] = (float)((double)(ic * dd) * c_prn[t + u]);
+            }
+#pragma unroll
+            for (int u = 0; u < DS_U; ++u) acc = acc + tm[u];
+        }
+        for (; t < VO_FREAK_NPAIRS; ++t) {
             const uint32_t pk = c_pairpk[t];
-            const int p = (int)(pk & 0xFF), q = (int)((pk >> 8) & 0xFF);
-            const float dx = (float)(int8_t)(pk >> 16), dy = (float)(int8_t)(pk >> 24);
-            const float ic = I0k[p] - I0k[q];
-            acc = acc + (float)((double)(ic * (comp ? dy : dx)) * c_prn[t]);
+            const float ic = I0k[pk & 0xFF] - I0k[(pk >> 8) & 0xFF];
+            acc = acc + (float)((double)(ic * (float)(int8_t)(pk >> shift)) * c_prn[t]);
         }
     }
     // 3. angle and rotation (both lanes of keypoint k)
@@ -1071,20 +1110,17 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
         uint8_t v[HALF];
 #pragma unroll
         for (int u = 0; u < HALF; ++u) {
-            const int p = comp ? HALF + u : u;
-            const int px = comp ? (HALF + u < NP ? c_pt_x[HALF + u] : 0) : c_pt_x[u];
-            const int py = comp ? (HALF + u < NP ? c_pt_y[HALF + u] : 0) : c_pt_y[u];
+            int px, py;
+            pt(u, px, py);
             int x = (int)(((float)kp.x + (float)px * c) + (float)py * s);
             int y = (int)(((float)kp.y + (float)(-1 * px) * ms) + (float)py * c);
             x = min(max(x, 0), W - 1);   // in range for every keypoint inside the margin
             y = min(max(y, 0), H - 1);
-            v[u] = (valid && p < NP) ? img[(size_t)y * W + x] : (uint8_t)0;
+            v[u] = img[(size_t)y * W + x];
         }
 #pragma unroll
-        for (int u = 0; u < HALF; ++u) {
-            const int p = comp ? HALF + u : u;
-            if (p < NP) s_I1[k][p] = v[u];
-        }
+        for (int u = 0; u < HALF; ++u)
+            if (!comp || HALF + u < NP) s_I1[k][comp ? HALF + u : u] = v[u];
     }
     __syncthreads();
     // 5. the 512 tests: lane l owns test w * 64 + l of word w; one ballot per (keypoint, word)
@@ -1686,7 +1722,7 @@ __global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, 
             st_sc1(counts + k, t);
         }
     }
-    unsigned* ctr = &w->ctr[k0 == 0 ? 1 : 2];
+    unsigned* ctr = &w->ctr[k0 == 0 ? 1 : (k0 < VO_HYP_CHUNK1 ? 2 : 3)];   // one arrival counter per chunk
     if (!arrive_last(ctr, gridDim.x, &s_last)) return;
     if (threadIdx.x >= 64) return;                 // the replay is one wave's
     VO_STAMP(d, 1997 + (k0 > 0), 0);
@@ -2552,14 +2588,21 @@ void launch_match(const VoDev& d, int stage, hipStream_t s)
 {
     hipLaunchKernelGGL(k_match, dim3(match_blocks(d.N, d.match_bits), stage ? 1 : d.B), dim3(256), 0, s, d, stage);
 }
+// hypotheses in three chunks, [0, C0), [C0, C1), [C1, max_hyp): a frame's later chunks exit at
+// once when its replay has already stopped (ransac.cpp:139 adaptive bound; 100 hypotheses for
+// most frames).  One wave per hypothesis, four per workgroup: with B frames per launch there
+// are enough hypotheses to fill the chip, so no wave repeats another's 8-point fit.
 void launch_ransac(const VoDev& d, int stage, hipStream_t s)
 {
     const int nhyp = d.max_hyp, nb = stage ? 1 : d.B;
-    const int k0 = nhyp < VO_HYP_CHUNK0 ? nhyp : VO_HYP_CHUNK0;
-    hipLaunchKernelGGL((k_ransac_hyp<4, 1>), dim3(k0, nb), dim3(256), 0, s, d, 0, k0, nhyp, stage);
-    if (nhyp > k0)
-        hipLaunchKernelGGL((k_ransac_hyp<1, 4>), dim3((nhyp - k0 + 3) / 4, nb), dim3(256), 0, s, d, k0, nhyp, nhyp,
-                           stage);
+    const int cut[3] = {std::min(nhyp, VO_HYP_CHUNK0), std::min(nhyp, VO_HYP_CHUNK1), nhyp};
+    int k0 = 0;
+    for (int c = 0; c < 3; ++c) {
+        const int k1 = cut[c];
+        if (k1 <= k0) continue;
+        hipLaunchKernelGGL((k_ransac_hyp<1, 4>), dim3((k1 - k0 + 3) / 4, nb), dim3(256), 0, s, d, k0, k1, nhyp, stage);
+        k0 = k1;
+    }
 }
 void launch_refit(const VoDev& d, int with_pose, int stage, hipStream_t s)
 {
