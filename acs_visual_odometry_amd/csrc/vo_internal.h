@@ -51,7 +51,7 @@
 // (frame f's slot is rewritten by frame f + VO_RING; passes read frames >= lo - 1)
 #define VO_CHUNK (VO_RING - 1)
 #define VO_MAX_BATCH 64
-#define VO_DEFAULT_BATCH 16
+#define VO_DEFAULT_BATCH 32
 // ctr words: cross-queue counters on lines of their own
 #define VO_CTR_DESCRIBE 0      // describe's in-launch arrival counter
 #define VO_SYNC_EXT 32         // frames extracted since vo_reset (the pose queue waits on it)

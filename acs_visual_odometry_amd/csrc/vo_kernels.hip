@@ -380,11 +380,11 @@ __device__ __forceinline__ int refl101(int i, int n)
 __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restrict__ img0, size_t frame_bytes,
                                                   int write_response)
 {
-    // LDS, aliased by lifetime (23 KB): region X holds the source tile (phases 1-2), then the
+    // LDS, aliased by lifetime (29 KB): region X holds the source tile (phases 1-2), then the
     // blurred tile (3-4), then the response (5-6); region Y the horizontal blur sums (2-3),
     // then the gradient planes Jx^2, Jy^2, Jxy (4-5)
     constexpr int X_BYTES = ST_RH * ST_RW * 4;                 // the largest of the three
-    constexpr int Y_BYTES = 3 * ST_GH * ST_GW * 4;
+    constexpr int Y_BYTES = ST_GH * ST_GW * 16;
     static_assert(ST_SH * ST_SW <= X_BYTES && ST_BH * ST_BW <= X_BYTES, "stencil LDS region X");
     static_assert(ST_SH * ST_BW * 4 <= Y_BYTES, "stencil LDS region Y");
     __shared__ __align__(16) unsigned char s_x[X_BYTES];
@@ -394,9 +394,8 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
     uint8_t (*s_bl)[ST_BW] = reinterpret_cast<uint8_t (*)[ST_BW]>(s_x);
     float (*s_r)[ST_RW] = reinterpret_cast<float (*)[ST_RW]>(s_x);
     uint32_t (*s_hb)[ST_BW] = reinterpret_cast<uint32_t (*)[ST_BW]>(s_y);
-    uint32_t (*s_qx)[ST_GW] = reinterpret_cast<uint32_t (*)[ST_GW]>(s_y);
-    uint32_t (*s_qy)[ST_GW] = reinterpret_cast<uint32_t (*)[ST_GW]>(s_y + ST_GH * ST_GW * 4);
-    int32_t (*s_qxy)[ST_GW] = reinterpret_cast<int32_t (*)[ST_GW]>(s_y + 2 * ST_GH * ST_GW * 4);
+    // gradient planes interleaved per pixel {Jx^2, Jy^2, Jxy, 0}: one 16-byte LDS access each
+    uint4 (*s_q)[ST_GW] = reinterpret_cast<uint4 (*)[ST_GW]>(s_y);
 
     const int W = d.W, H = d.H;
     const int x0 = blockIdx.x * ST_TW, y0 = blockIdx.y * ST_TH;
@@ -480,7 +479,7 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
             jy = sy[0] - sy[2];
             jxy = sx[0] - sx[2];
         }
-        s_qx[r][c] = (uint32_t)__mul24(jx, jx); s_qy[r][c] = (uint32_t)__mul24(jy, jy); s_qxy[r][c] = jxy;
+        s_q[r][c] = make_uint4((uint32_t)__mul24(jx, jx), (uint32_t)__mul24(jy, jy), (uint32_t)jxy, 0u);
     }
     __syncthreads();
     // 5. response (kernel .c:97-114): 5x5 sums of Jx^2, Jy^2, Jxy accumulated in f32, m-outer
@@ -505,7 +504,8 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
                 int hs = 0;
 #pragma unroll
                 for (int n = 0; n < 5; ++n) {
-                    hx += s_qx[r0 + mr][c + n]; hy += s_qy[r0 + mr][c + n]; hs += s_qxy[r0 + mr][c + n];
+                    const uint4 q = s_q[r0 + mr][c + n];
+                    hx += q.x; hy += q.y; hs += (int)q.z;
                 }
 #pragma unroll
                 for (int o = 0; o < RS; ++o) {
@@ -527,12 +527,12 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
                 if (ax[o] > (1u << 24)) {                           // rare: the in-order f32 sum
                     jx2 = 0.0f;
                     for (int m = 0; m < 5; ++m)
-                        for (int n = 0; n < 5; ++n) jx2 = jx2 + (float)s_qx[r + m][c + n];
+                        for (int n = 0; n < 5; ++n) jx2 = jx2 + (float)s_q[r + m][c + n].x;
                 }
                 if (ay[o] > (1u << 24)) {
                     jy2 = 0.0f;
                     for (int m = 0; m < 5; ++m)
-                        for (int n = 0; n < 5; ++n) jy2 = jy2 + (float)s_qy[r + m][c + n];
+                        for (int n = 0; n < 5; ++n) jy2 = jy2 + (float)s_q[r + m][c + n].y;
                 }
                 float det = (jx2 * jy2) - (sxy * sxy);
                 float tr = jx2 + jy2;
