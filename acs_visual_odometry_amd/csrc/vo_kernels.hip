@@ -1979,16 +1979,19 @@ __device__ __forceinline__ void warm_start(const double* Fb, double s1, double m
 }
 
 #define RF_T 128
-#define RF_PCAP 2048     // inlier points staged in LDS as f64 (beyond: read from HBM)
+#define RF_PCAP 512      // inlier points staged in LDS as f64 (beyond: read from L2 / HBM)
+#define RF_ROWS 23       // partial-sum rows in LDS: the 45 moment sums go in two rounds
 // one sum over the refit threads in the oracle's order (red_finish): per-thread partials
 // -> LDS -> thread e sums the RF_T partials of quantity e as 8 sequential chains of 16,
-// combined pairwise
-template <int NS>
-__device__ __forceinline__ void refit_sums(const double (&part)[NS], double (*s_part)[RF_T + 1], double* s_out)
+// combined pairwise.  Quantities [E0, E0 + NS) of part, RF_ROWS at a time (42 KB of LDS in
+// all: a refit workgroup fits beside the extract queue's stencil workgroups on one CU).
+template <int NS, int E0 = 0, int NT = NS>
+__device__ __forceinline__ void refit_sums(const double (&part)[NT], double (*s_part)[RF_T + 1], double* s_out)
 {
+    static_assert(NS <= RF_ROWS && E0 + NS <= NT, "refit_sums rows");
     const int tid = threadIdx.x;
 #pragma unroll
-    for (int e = 0; e < NS; ++e) s_part[e][tid] = part[e];
+    for (int e = 0; e < NS; ++e) s_part[e][tid] = part[E0 + e];
     __syncthreads();
     if (tid < NS) {
         double c[8];
@@ -1998,7 +2001,7 @@ __device__ __forceinline__ void refit_sums(const double (&part)[NS], double (*s_
         for (int t = 0; t < 16; ++t)
 #pragma unroll
             for (int j = 0; j < 8; ++j) c[j] = c[j] + s_part[tid][16 * j + t];
-        s_out[tid] = ((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7]));
+        s_out[E0 + tid] = ((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7]));
     }
     __syncthreads();
 }
@@ -2024,7 +2027,7 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose, int stag
     const double* pts = d.pts + (size_t)wf * 4 * d.N;
     int32_t* inl = d.inl + (size_t)wf * d.N;
     float* model_p = d.model_p + (size_t)wf * 4 * d.N;
-    __shared__ double s_part[45][RF_T + 1];
+    __shared__ double s_part[RF_ROWS][RF_T + 1];
     __shared__ double s_sum[45];
     __shared__ double s_A[81];
     __shared__ int s_n;
@@ -2109,7 +2112,8 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose, int stag
 #pragma unroll
                 for (int v = u; v < 9; ++v) { acc[e] = acc[e] + a[u] * a[v]; ++e; }
         }
-        refit_sums<45>(acc, s_part, s_sum);
+        refit_sums<23, 0>(acc, s_part, s_sum);
+        refit_sums<22, 23>(acc, s_part, s_sum);
         VO_STAMP(d, 1995, 4);
         if (tid < 45) {
             int u = 0, e = tid;
