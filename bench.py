@@ -33,9 +33,9 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 METRIC = "VO frames/sec (extract+match+pose), 1241×376 mono, 2000 kpts/frame"
-# committed rocprofv3 FETCH_SIZE / WRITE_SIZE summary of this workload (tools/profile.sh ->
-# tools/rocprof_summary.py --fetch-x2 --json): source of roofline.traffic
-PMC_PROFILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1_pipeline_kernels.json")
+# committed rocprofv3 FETCH_SIZE / WRITE_SIZE summaries of the two bench configs (tools/profile.sh
+# -> tools/rocprof_summary.py --fetch-x2 --json): the source of roofline.traffic
+PMC_PROFILES = {(1241, 376): "r1_batched_kitti_kernels.json", (1920, 1080): "r1_batched_1080_kernels.json"}
 ROCPROF_NAME = {"stencil": "k_stencil", "select": "k_select", "describe": "k_describe", "match": "k_match",
                 "ransac": "k_ransac_hyp", "refit": "k_refit", "triangulate": "k_triangulate",
                 "finalize": "k_finalize"}
@@ -69,9 +69,12 @@ def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray, N: int) -> 
     return float(W * H + 80 * n + 24 * M + 96)       # whole path
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed PMC profile (None if absent); the
-    RANSAC launch pair counts as one launch, as in the live timing."""
+def pmc_traffic(kernel: str, W: int, H: int):
+    """HBM bytes per launch of `kernel` from the committed PMC profile of this frame size (None
+    if absent); the RANSAC launches of a pass count as one launch, as in the live timing."""
+    if (W, H) not in PMC_PROFILES:
+        return None, None
+    PMC_PROFILE = os.path.join(ROOT, "profiles", PMC_PROFILES[(W, H)])
     try:
         prof = json.load(open(PMC_PROFILE))["kernels"]
         rows = [r for k, r in prof.items() if k.split("<")[0] == ROCPROF_NAME[kernel]]   # template instances
@@ -196,7 +199,7 @@ def main():
     if rank == 0:
         abytes = algorithmic_bytes(dominant, seq.W, seq.H, info, args.max_kpts) * dom_fpl   # per launch
         achieved = abytes / (dom_ms * 1e-3) / 1e9
-        traffic, tsrc = pmc_traffic(dominant)
+        traffic, tsrc = pmc_traffic(dominant, seq.W, seq.H)
         roof = {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
                 "avg_launch_ms": dom_ms, "frames_per_launch": dom_fpl, "algorithmic_bytes_per_launch": abytes}
