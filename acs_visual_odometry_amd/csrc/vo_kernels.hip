@@ -441,45 +441,81 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
         }
     }
     __syncthreads();
-    // 2. horizontal 7-tap (exact; 24-bit multiplies: every product < 2^24)
-    for (int r = tid / ST_BW, c = tid - (tid / ST_BW) * ST_BW; r < ST_SH; rc_step<ST_BW>(r, c)) {
-        const uint8_t* sp = &s_src[r][c];
-        // symmetric taps: 8(s0+s6) + 28(s1+s5) + 56(s2+s4) + 72 s3, exact in u32
-        uint32_t h = __umul24(8u, (uint32_t)sp[0] + sp[6]) + __umul24(28u, (uint32_t)sp[1] + sp[5]) +
-                     __umul24(56u, (uint32_t)sp[2] + sp[4]) + __umul24(72u, (uint32_t)sp[3]);
-        s_hb[r][c] = h;
+    // 2. horizontal 7-tap (exact; 24-bit multiplies: every product < 2^24).  Thread (row, run
+    //    of 9 columns): the 15 source bytes of the run are read once and slide through registers.
+    {
+        constexpr int RUN = 9, NRUN = ST_BW / RUN;                  // 8 runs x 30 rows = 240 threads
+        static_assert(RUN * NRUN == ST_BW && NRUN * ST_SH <= 256, "h-blur runs");
+        if (tid < NRUN * ST_SH) {
+            const int r = tid / NRUN, c0 = (tid - r * NRUN) * RUN;
+            uint32_t sv[RUN + 6];
+#pragma unroll
+            for (int j = 0; j < RUN + 6; ++j) sv[j] = s_src[r][c0 + j];
+#pragma unroll
+            for (int j = 0; j < RUN; ++j)
+                // symmetric taps: 8(s0+s6) + 28(s1+s5) + 56(s2+s4) + 72 s3
+                s_hb[r][c0 + j] = __umul24(8u, sv[j] + sv[j + 6]) + __umul24(28u, sv[j + 1] + sv[j + 5]) +
+                                  __umul24(56u, sv[j + 2] + sv[j + 4]) + __umul24(72u, sv[j + 3]);
+        }
     }
     __syncthreads();
-    // 3. vertical 7-tap, round, u8 (cv::GaussianBlur 8U fixed point); blurred -> HBM
-    for (int r = tid / ST_BW, c = tid - (tid / ST_BW) * ST_BW; r < ST_BH; rc_step<ST_BW>(r, c)) {
-        uint32_t v = __umul24(8u, s_hb[r][c] + s_hb[r + 6][c]) + __umul24(28u, s_hb[r + 1][c] + s_hb[r + 5][c]) +
-                     __umul24(56u, s_hb[r + 2][c] + s_hb[r + 4][c]) + __umul24(72u, s_hb[r + 3][c]);
-        uint32_t b = (v + 32768u) >> 16;
-        s_bl[r][c] = (uint8_t)b;
-        int y = y0 - 4 + r, x = x0 - 4 + c;
-        if (r >= 4 && r < 4 + ST_TH && c >= 4 && c < 4 + ST_TW && y < H && x < W)
-            blurred[(size_t)y * W + x] = (uint8_t)b;
+    // 3. vertical 7-tap, round, u8 (cv::GaussianBlur 8U fixed point); blurred -> HBM.  Thread
+    //    (column, run of 8 rows): 14 horizontal sums read once.
+    {
+        constexpr int RUN = 8, NRUN = ST_BH / RUN;                  // 3 runs x 72 columns = 216 threads
+        static_assert(RUN * NRUN == ST_BH && NRUN * ST_BW <= 256, "v-blur runs");
+        if (tid < NRUN * ST_BW) {
+            const int k = tid / ST_BW, c = tid - k * ST_BW, r0 = k * RUN;
+            uint32_t hv[RUN + 6];
+#pragma unroll
+            for (int j = 0; j < RUN + 6; ++j) hv[j] = s_hb[r0 + j][c];
+            const int x = x0 - 4 + c;
+            const bool xin = c >= 4 && c < 4 + ST_TW && x < W;
+#pragma unroll
+            for (int j = 0; j < RUN; ++j) {
+                const uint32_t v = __umul24(8u, hv[j] + hv[j + 6]) + __umul24(28u, hv[j + 1] + hv[j + 5]) +
+                                   __umul24(56u, hv[j + 2] + hv[j + 4]) + __umul24(72u, hv[j + 3]);
+                const uint32_t bb = (v + 32768u) >> 16;
+                const int r = r0 + j, y = y0 - 4 + r;
+                s_bl[r][c] = (uint8_t)bb;
+                if (xin && r >= 4 && r < 4 + ST_TH && y < H) blurred[(size_t)y * W + x] = (uint8_t)bb;
+            }
+        }
     }
     __syncthreads();
     // 4. gradients (kernel .c:59-76), 0 outside 1<=i<=H-2, 1<=j<=W-2.  The reference computes
     //    them in f32 on u8 values: every intermediate is an integer below 2^11, so integer
     //    arithmetic gives the same values; Jx*Jx and Jy*Jy (< 2^21) are exact in f32 as well.
-    for (int r = tid / ST_GW, c = tid - (tid / ST_GW) * ST_GW; r < ST_GH; rc_step<ST_GW>(r, c)) {
-        int y = y0 - 3 + r, x = x0 - 3 + c;
-        int jx = 0, jy = 0, jxy = 0;
-        if (y >= 1 && y <= H - 2 && x >= 1 && x <= W - 2) {
-            int sx[3], sy[3];
+    //    Thread (column, run of rows): the 3x3 window slides down, one new row of 3 per output.
+    {
+        constexpr int NRUN = 3, RUN = (ST_GH + NRUN - 1) / NRUN;    // 3 runs (8, 7, 7) x 70 columns
+        static_assert(NRUN * ST_GW <= 256 && RUN == 8, "gradient runs");
+        if (tid < NRUN * ST_GW) {
+            const int k = tid / ST_GW, c = tid - k * ST_GW;
+            const int r0 = k == 0 ? 0 : (k == 1 ? 8 : 15), len = k == 0 ? 8 : 7;
+            const int x = x0 - 3 + c;
+            const bool xin = x >= 1 && x <= W - 2;
+            int a0 = s_bl[r0][c], a1 = s_bl[r0][c + 1], a2 = s_bl[r0][c + 2];
+            int m0 = s_bl[r0 + 1][c], m1 = s_bl[r0 + 1][c + 1], m2 = s_bl[r0 + 1][c + 2];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                int a = s_bl[r][c + k], m = s_bl[r + 1][c + k], cc = s_bl[r + 2][c + k];
-                sx[k] = a - cc;
-                sy[k] = (a + 2 * m) + cc;
+            for (int j = 0; j < RUN; ++j) {
+                if (j < len) {
+                    const int r = r0 + j, y = y0 - 3 + r;
+                    const int e0 = s_bl[r + 2][c], e1 = s_bl[r + 2][c + 1], e2 = s_bl[r + 2][c + 2];
+                    int jx = 0, jy = 0, jxy = 0;
+                    if (xin && y >= 1 && y <= H - 2) {
+                        const int sx0 = a0 - e0, sx1 = a1 - e1, sx2 = a2 - e2;
+                        const int sy0 = (a0 + 2 * m0) + e0, sy2 = (a2 + 2 * m2) + e2;
+                        jx = (sx0 + 2 * sx1) + sx2;
+                        jy = sy0 - sy2;
+                        jxy = sx0 - sx2;
+                    }
+                    s_q[r][c] = make_uint4((uint32_t)__mul24(jx, jx), (uint32_t)__mul24(jy, jy), (uint32_t)jxy, 0u);
+                    a0 = m0; a1 = m1; a2 = m2;
+                    m0 = e0; m1 = e1; m2 = e2;
+                }
             }
-            jx = (sx[0] + 2 * sx[1]) + sx[2];
-            jy = sy[0] - sy[2];
-            jxy = sx[0] - sx[2];
         }
-        s_q[r][c] = make_uint4((uint32_t)__mul24(jx, jx), (uint32_t)__mul24(jy, jy), (uint32_t)jxy, 0u);
     }
     __syncthreads();
     // 5. response (kernel .c:97-114): 5x5 sums of Jx^2, Jy^2, Jxy accumulated in f32, m-outer
