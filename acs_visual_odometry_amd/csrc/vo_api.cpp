@@ -232,14 +232,28 @@ void enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0,
 }
 
 // one pose pass over the window [lo, lo + B) of the frames enqueued so far
-void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev)
+// cap: the window size of this pass (<= B); every kernel of the pass sees the same VoDev
+void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int cap)
 {
     hipStream_t s = c->s;
-    timed(c, ev, 3, s, [&] { vo::launch_match(c->d, 0, s); });
-    timed(c, ev, 4, s, [&] { vo::launch_ransac(c->d, 0, s); });
-    timed(c, ev, 5, s, [&] { vo::launch_refit(c->d, 1, 0, s); });
-    timed(c, ev, 6, s, [&] { vo::launch_triangulate(c->d, 0, s); });
-    timed(c, ev, 7, s, [&] { vo::launch_finalize(c->d, out, out_base, s); });
+    VoDev d = c->d;
+    d.B = cap;
+    timed(c, ev, 3, s, [&] { vo::launch_match(d, 0, s); });
+    timed(c, ev, 4, s, [&] { vo::launch_ransac(d, 0, s); });
+    timed(c, ev, 5, s, [&] { vo::launch_refit(d, 1, 0, s); });
+    timed(c, ev, 6, s, [&] { vo::launch_triangulate(d, 0, s); });
+    timed(c, ev, 7, s, [&] { vo::launch_finalize(d, out, out_base, s); });
+}
+
+// Batch sizes of a chunk: B frames per extract batch and per pass window (the last one
+// shorter).  Pass k's window starts at or before batch k's first frame, so its frames are
+// extracted once batch k is.  (Smaller first batches to start the pose queue earlier were
+// measured slower: more passes, each with a fixed latency.)
+std::vector<int> batch_schedule(int nf, int B)
+{
+    std::vector<int> v;
+    for (int done = 0; done < nf; done += B) v.push_back(std::min(B, nf - done));
+    return v;
 }
 
 // frames [c->fidx, c->fidx + nf) (nf <= VO_CHUNK): set the end, enqueue the extract
@@ -256,21 +270,26 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         c->reset_pending = false;
     }
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&c->d.st->end, end, 1, s));
-    const int nb = (nf + B - 1) / B;
+    const std::vector<int> sched = batch_schedule(nf, B);
     if (!img0) {
         vo::launch_ext_missing(c->d, base % VO_RING, s);
     } else {
-        for (int j = 0; j < nb; ++j) {
-            const int cnt = std::min(B, nf - j * B);
-            enqueue_extract(c, img0 + (size_t)j * B * frame_bytes, frame_bytes, base + j * B, cnt, q != s, q, ev);
+        int f0 = 0;
+        for (int cnt : sched) {
+            enqueue_extract(c, img0 + (size_t)f0 * frame_bytes, frame_bytes, base + f0, cnt, q != s, q, ev);
+            f0 += cnt;
         }
     }
     c->fidx = end;
-    for (int k = 0; k < nb; ++k) {
-        if (q != s)
-            (void)hipStreamWaitValue32(s, c->d.ctr + VO_SYNC_EXT, (uint32_t)std::min(base + (k + 1) * B, end),
-                                       hipStreamWaitValueGte, 0xFFFFFFFFu);
-        enqueue_pass(c, out, out_base, ev);
+    {
+        int f1 = 0;
+        for (int cnt : sched) {
+            f1 += cnt;
+            if (q != s)
+                (void)hipStreamWaitValue32(s, c->d.ctr + VO_SYNC_EXT, (uint32_t)(base + f1), hipStreamWaitValueGte,
+                                           0xFFFFFFFFu);
+            enqueue_pass(c, out, out_base, ev, cnt);
+        }
     }
     for (;;) {
         HIPCHK(hipGetLastError());
@@ -283,7 +302,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         if (lo >= end) break;
         if (lo < base) return VO_ERR_STATE;
         // frames after skipped ones: their windows restart at lo (extracts are complete)
-        for (int k = 0; k < (end - lo + B - 1) / B; ++k) enqueue_pass(c, out, out_base, ev);
+        for (int k = 0; k < (end - lo + B - 1) / B; ++k) enqueue_pass(c, out, out_base, ev, B);
     }
     return VO_OK;
 }

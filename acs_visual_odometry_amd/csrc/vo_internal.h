@@ -51,13 +51,13 @@
 // (frame f's slot is rewritten by frame f + VO_RING; passes read frames >= lo - 1)
 #define VO_CHUNK (VO_RING - 1)
 #define VO_MAX_BATCH 64
-#define VO_DEFAULT_BATCH 32
+#define VO_DEFAULT_BATCH 64
 // ctr words: cross-queue counters on lines of their own
 #define VO_CTR_DESCRIBE 0      // describe's in-launch arrival counter
 #define VO_SYNC_EXT 32         // frames extracted since vo_reset (the pose queue waits on it)
 #define VO_CTR_WORDS 64
 #define VO_MAX_HYP 2000
-#define VO_HYP_CHUNK0 128     // RANSAC launch chunks (vo_kernels.hip launch_ransac)
+#define VO_HYP_CHUNK0 100     // RANSAC launch chunks (vo_kernels.hip launch_ransac); 100 = the clamp
 #define VO_HYP_CHUNK1 512
 
 struct VoFrameOut {

@@ -592,30 +592,36 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
     }
     __syncthreads();
     // 6. strict 3x3 NMS inside the retinal margin (corner_detection_parallel_GPU.cpp:152-180).
-    //    Survivors are compacted in tile-local raster order: wave w owns tile rows w, w+4, ...
+    //    Survivors are compacted in tile-local raster order: wave w owns tile rows 4w..4w+3
     //    (lane = column), so ballots give the order; per-row counts go to tilerows[] so the
-    //    select kernel can emit the global raster order without sorting.
+    //    select kernel can emit the global raster order without sorting.  The 3x3 window
+    //    slides down the wave's rows: three new response values per row.
     const int hk = d.nms_k / 2;
     const int lane = tid & 63, wave = tid >> 6;
     float cvk[ST_TH / 4];
     bool mxk[ST_TH / 4];
+    {
+        const int c = lane, rb = 4 * wave;
+        float up0 = s_r[rb][c], up1 = s_r[rb][c + 1], up2 = s_r[rb][c + 2];
+        float md0 = s_r[rb + 1][c], md1 = s_r[rb + 1][c + 1], md2 = s_r[rb + 1][c + 2];
 #pragma unroll
-    for (int kk = 0; kk < ST_TH / 4; ++kk) {
-        const int r = 4 * kk + wave, c = lane;
-        const int i = y0 + r, j = x0 + c;
-        bool ok = i < H && j < W && i >= hk && i < H - hk && j >= hk && j < W - hk &&
-                  (j >= d.bcol) && (j <= W - d.bcol) && (i >= d.brow) && (i <= H - d.brow);
-        float cv = s_r[r + 1][c + 1];
-        bool mx = ok;
-#pragma unroll
-        for (int a2 = -1; a2 <= 1; ++a2)
-#pragma unroll
-            for (int b2 = -1; b2 <= 1; ++b2)
-                if ((a2 | b2) != 0 && s_r[r + 1 + a2][c + 1 + b2] >= cv) mx = false;
-        unsigned long long bal = ballot64(mx);
-        if (lane == 0) s_bal[r] = bal;
-        cvk[kk] = cv;
-        mxk[kk] = mx;
+        for (int kk = 0; kk < ST_TH / 4; ++kk) {
+            const int r = rb + kk;
+            const int i = y0 + r, j = x0 + c;
+            const float dn0 = s_r[r + 2][c], dn1 = s_r[r + 2][c + 1], dn2 = s_r[r + 2][c + 2];
+            const bool ok = i < H && j < W && i >= hk && i < H - hk && j >= hk && j < W - hk &&
+                            (j >= d.bcol) && (j <= W - d.bcol) && (i >= d.brow) && (i <= H - d.brow);
+            const float cv = md1;
+            // strict maximum: any neighbour >= the centre rejects it
+            const bool mx = ok && !(up0 >= cv || up1 >= cv || up2 >= cv || md0 >= cv || md2 >= cv ||
+                                    dn0 >= cv || dn1 >= cv || dn2 >= cv);
+            unsigned long long bal = ballot64(mx);
+            if (lane == 0) s_bal[r] = bal;
+            cvk[kk] = cv;
+            mxk[kk] = mx;
+            up0 = md0; up1 = md1; up2 = md2;
+            md0 = dn0; md1 = dn1; md2 = dn2;
+        }
     }
     __syncthreads();
     const int tile = blockIdx.y * gridDim.x + blockIdx.x;
@@ -623,7 +629,7 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
 #pragma unroll
     for (int kk = 0; kk < ST_TH / 4; ++kk) {
         if (!mxk[kk]) continue;
-        const int r = 4 * kk + wave, c = lane;
+        const int r = 4 * wave + kk, c = lane;
         int off = 0;
         for (int rr = 0; rr < r; ++rr) off += __popcll(s_bal[rr]);
         off += __popcll(s_bal[r] & ((1ull << lane) - 1ull));

@@ -217,7 +217,7 @@ def main():
                        "frames_per_step": args.frames, "width": seq.W, "height": seq.H,
                        "max_kpts": args.max_kpts, "sequence": f"scene seq=rank, {args.motion} m/frame",
                        "parallelism": f"replicas: 1 sequence per GPU x {world}",
-                       "frame_batch": ctx.cfg.frame_batch or 32,
+                       "frame_batch": ctx.cfg.frame_batch or 64,
                        "mean_kpts": float(info[:, 0].mean()), "mean_matches": float(info[:, 1].mean()),
                        "mean_inliers": float(info[:, 2].mean()), "mean_hypotheses": float(info[:, 4].mean()),
                        "frames_ok": ok},

@@ -69,7 +69,7 @@ typedef struct {
     double K[9];              /* PoseUpdate.hpp:36-39                                  */
     int device;               /* HIP device ordinal                                    */
     int frame_batch;          /* frames per extract batch / pose-pass window (1..64);
-                                 0 = default 32.  Results do not depend on it.         */
+                                 0 = default 64.  Results do not depend on it.         */
 } vo_config;
 
 /* Fill the reference defaults for a width x height stream. */
