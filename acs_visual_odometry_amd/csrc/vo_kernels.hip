@@ -534,21 +534,30 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
 #pragma unroll
         for (int o = 0; o < RS; ++o) { ax[o] = 0u; ay[o] = 0u; as[o] = 0; }
         if (act) {
+            // horizontal 5-sums of the RS + 4 source rows, then vertical sums as a running
+            // window (exact integers: any order gives the same sum)
+            uint32_t hx[RS + 4], hy[RS + 4];
+            int hs[RS + 4];
 #pragma unroll
             for (int mr = 0; mr < RS + 4; ++mr) {
-                uint32_t hx = 0u, hy = 0u;
-                int hs = 0;
+                hx[mr] = 0u; hy[mr] = 0u; hs[mr] = 0;
 #pragma unroll
                 for (int n = 0; n < 5; ++n) {
                     const uint4 q = s_q[r0 + mr][c + n];
-                    hx += q.x; hy += q.y; hs += (int)q.z;
+                    hx[mr] += q.x; hy[mr] += q.y; hs[mr] += (int)q.z;
                 }
+            }
+            uint32_t sx = 0u, sy = 0u;
+            int ss = 0;
 #pragma unroll
-                for (int o = 0; o < RS; ++o) {
-                    const int m = mr - o;
-                    if (m < 0 || m > 4) continue;
-                    ax[o] += hx; ay[o] += hy; as[o] += hs;
-                }
+            for (int m = 0; m < 5; ++m) { sx += hx[m]; sy += hy[m]; ss += hs[m]; }
+            ax[0] = sx; ay[0] = sy; as[0] = ss;
+#pragma unroll
+            for (int o = 1; o < RS; ++o) {
+                sx = (sx + hx[o + 4]) - hx[o - 1];
+                sy = (sy + hy[o + 4]) - hy[o - 1];
+                ss = (ss + hs[o + 4]) - hs[o - 1];
+                ax[o] = sx; ay[o] = sy; as[o] = ss;
             }
         }
         float rv_out[RS];
