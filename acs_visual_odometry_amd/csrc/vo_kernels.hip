@@ -1227,9 +1227,14 @@ __global__ void __launch_bounds__(256) k_describe(VoDev d, int f0, int slot_over
 // key = dist<<16 | j, so the min key is (min dist, first j) and the 2nd key gives `second`
 // ---------------------------------------------------------------------------
 // branch-free top-2 update (keys are unique: the low 16 bits carry the candidate index)
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
+{
+    return max(min(a, b), min(max(a, b), c));     // selected as v_med3_u32
+}
+// (m1 <= m2 always: the new second smallest is the median of key, m1, m2 -- one v_med3_u32)
 __device__ __forceinline__ void top2_insert(uint32_t key, uint32_t& m1, uint32_t& m2)
 {
-    m2 = min(m2, max(key, m1));
+    m2 = med3_u32(key, m1, m2);
     m1 = min(m1, key);
 }
 __device__ __forceinline__ void top2_wave(uint32_t& m1, uint32_t& m2)
