@@ -393,9 +393,9 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
     uint8_t (*s_src)[ST_SW] = reinterpret_cast<uint8_t (*)[ST_SW]>(s_x);
     uint8_t (*s_bl)[ST_BW] = reinterpret_cast<uint8_t (*)[ST_BW]>(s_x);
     float (*s_r)[ST_RW] = reinterpret_cast<float (*)[ST_RW]>(s_x);
-    uint32_t (*s_hb)[ST_BW] = reinterpret_cast<uint32_t (*)[ST_BW]>(s_y);
+    uint16_t (*s_hb)[ST_BW] = reinterpret_cast<uint16_t (*)[ST_BW]>(s_y);   // <= 65280: u16
     // gradient planes interleaved per pixel {Jx^2, Jy^2, Jxy, 0}: one 16-byte LDS access each
-    uint4 (*s_q)[ST_GW] = reinterpret_cast<uint4 (*)[ST_GW]>(s_y);
+    float4 (*s_q)[ST_GW] = reinterpret_cast<float4 (*)[ST_GW]>(s_y);
 
     const int W = d.W, H = d.H;
     const int x0 = blockIdx.x * ST_TW, y0 = blockIdx.y * ST_TH;
@@ -420,7 +420,7 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
             const uint8_t* __restrict__ org = img + (size_t)(y0 - 7) * W + (x0 - 7);
 #pragma unroll
             for (int it = 0; it < NIT; ++it) {
-                v[it] = r < ST_SH ? org[(size_t)r * W + c] : (uint8_t)0;
+                v[it] = r < ST_SH ? org[(uint32_t)(r * W + c)] : (uint8_t)0;     // frames < 2^31 px
                 rc_step<ST_SW>(r, c);
             }
         } else {
@@ -429,7 +429,7 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
                 v[it] = 0;
                 if (r < ST_SH) {
                     const int y = refl101(y0 - 7 + r, H), x = refl101(x0 - 7 + c, W);
-                    v[it] = img[(size_t)y * W + x];
+                    v[it] = img[(uint32_t)(y * W + x)];
                 }
                 rc_step<ST_SW>(r, c);
             }
@@ -454,8 +454,8 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
 #pragma unroll
             for (int j = 0; j < RUN; ++j)
                 // symmetric taps: 8(s0+s6) + 28(s1+s5) + 56(s2+s4) + 72 s3
-                s_hb[r][c0 + j] = __umul24(8u, sv[j] + sv[j + 6]) + __umul24(28u, sv[j + 1] + sv[j + 5]) +
-                                  __umul24(56u, sv[j + 2] + sv[j + 4]) + __umul24(72u, sv[j + 3]);
+                s_hb[r][c0 + j] = (uint16_t)(8u * (sv[j] + sv[j + 6]) + 28u * (sv[j + 1] + sv[j + 5]) +
+                                             56u * (sv[j + 2] + sv[j + 4]) + 72u * sv[j + 3]);
         }
     }
     __syncthreads();
@@ -473,12 +473,13 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
             const bool xin = c >= 4 && c < 4 + ST_TW && x < W;
 #pragma unroll
             for (int j = 0; j < RUN; ++j) {
-                const uint32_t v = __umul24(8u, hv[j] + hv[j + 6]) + __umul24(28u, hv[j + 1] + hv[j + 5]) +
-                                   __umul24(56u, hv[j + 2] + hv[j + 4]) + __umul24(72u, hv[j + 3]);
+                // operands < 2^17 (u16 loads): selected as 24-bit multiply-adds
+                const uint32_t v = 8u * (hv[j] + hv[j + 6]) + 28u * (hv[j + 1] + hv[j + 5]) +
+                                   56u * (hv[j + 2] + hv[j + 4]) + 72u * hv[j + 3];
                 const uint32_t bb = (v + 32768u) >> 16;
                 const int r = r0 + j, y = y0 - 4 + r;
                 s_bl[r][c] = (uint8_t)bb;
-                if (xin && r >= 4 && r < 4 + ST_TH && y < H) blurred[(size_t)y * W + x] = (uint8_t)bb;
+                if (xin && r >= 4 && r < 4 + ST_TH && y < H) blurred[(uint32_t)(y * W + x)] = (uint8_t)bb;
             }
         }
     }
@@ -510,7 +511,8 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
                         jy = sy0 - sy2;
                         jxy = sx0 - sx2;
                     }
-                    s_q[r][c] = make_uint4((uint32_t)__mul24(jx, jx), (uint32_t)__mul24(jy, jy), (uint32_t)jxy, 0u);
+                        const float fx = (float)jx, fy = (float)jy;     // squares < 2^21: exact in f32
+                    s_q[r][c] = make_float4(fx * fx, fy * fy, (float)jxy, 0.0f);
                     a0 = m0; a1 = m1; a2 = m2;
                     m0 = e0; m1 = e1; m2 = e2;
                 }
@@ -519,36 +521,34 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
     }
     __syncthreads();
     // 5. response (kernel .c:97-114): 5x5 sums of Jx^2, Jy^2, Jxy accumulated in f32, m-outer
-    //    n-inner.  Every term is a non-negative integer (Jxy: |sum| < 2^14), so while the exact
-    //    total is <= 2^24 every f32 partial sum is exact and the in-order f32 sum equals the
-    //    integer sum: computed here as integer box sums, with the in-order f32 loop only for a
-    //    total above 2^24 (strong corners).  Thread (strip, column): RS outputs down a column.
+    //    n-inner.  Every term is an integer and, after the 7-tap blur, |J| <= 510: a sum of 25
+    //    squares stays below 2^24, so every f32 partial sum in any order is exact and equals the
+    //    in-order sum.  Computed here as f32 box sums (horizontal 5-sums per row, then a running
+    //    vertical window), with the in-order loop kept for a total above 2^24 (unreachable for
+    //    u8 input).  Thread (strip, column): RS outputs down a column.
     {
         constexpr int RS = ST_RH / 3;                               // 3 strips x ST_RW columns
         static_assert(RS * 3 == ST_RH && 3 * ST_RW <= 256, "response strips");
         const float thr = d.resp_thr;
         const bool act = tid < 3 * ST_RW;
         const int strip = act ? tid / ST_RW : 0, c = act ? tid - strip * ST_RW : 0, r0 = strip * RS;
-        uint32_t ax[RS], ay[RS];
-        int as[RS];
+        float ax[RS], ay[RS], as[RS];
 #pragma unroll
-        for (int o = 0; o < RS; ++o) { ax[o] = 0u; ay[o] = 0u; as[o] = 0; }
+        for (int o = 0; o < RS; ++o) { ax[o] = 0.0f; ay[o] = 0.0f; as[o] = 0.0f; }
         if (act) {
             // horizontal 5-sums of the RS + 4 source rows, then vertical sums as a running
             // window (exact integers: any order gives the same sum)
-            uint32_t hx[RS + 4], hy[RS + 4];
-            int hs[RS + 4];
+            float hx[RS + 4], hy[RS + 4], hs[RS + 4];
 #pragma unroll
             for (int mr = 0; mr < RS + 4; ++mr) {
-                hx[mr] = 0u; hy[mr] = 0u; hs[mr] = 0;
+                hx[mr] = 0.0f; hy[mr] = 0.0f; hs[mr] = 0.0f;
 #pragma unroll
                 for (int n = 0; n < 5; ++n) {
-                    const uint4 q = s_q[r0 + mr][c + n];
-                    hx[mr] += q.x; hy[mr] += q.y; hs[mr] += (int)q.z;
+                    const float4 q = s_q[r0 + mr][c + n];
+                    hx[mr] += q.x; hy[mr] += q.y; hs[mr] += q.z;
                 }
             }
-            uint32_t sx = 0u, sy = 0u;
-            int ss = 0;
+            float sx = 0.0f, sy = 0.0f, ss = 0.0f;
 #pragma unroll
             for (int m = 0; m < 5; ++m) { sx += hx[m]; sy += hy[m]; ss += hs[m]; }
             ax[0] = sx; ay[0] = sy; as[0] = ss;
@@ -567,17 +567,17 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
             const int y = y0 - 1 + r, x = x0 - 1 + c;
             float out = 0.0f;
             if (act && y >= 2 && y <= H - 3 && x >= 2 && x <= W - 3) {
-                float jx2 = (float)ax[o], jy2 = (float)ay[o];
-                const float sxy = (float)as[o];
-                if (ax[o] > (1u << 24)) {                           // rare: the in-order f32 sum
+                float jx2 = ax[o], jy2 = ay[o];
+                const float sxy = as[o];
+                if (ax[o] > 16777216.0f) {                          // never for u8 input: in-order f32
                     jx2 = 0.0f;
                     for (int m = 0; m < 5; ++m)
-                        for (int n = 0; n < 5; ++n) jx2 = jx2 + (float)s_q[r + m][c + n].x;
+                        for (int n = 0; n < 5; ++n) jx2 = jx2 + s_q[r + m][c + n].x;
                 }
-                if (ay[o] > (1u << 24)) {
+                if (ay[o] > 16777216.0f) {
                     jy2 = 0.0f;
                     for (int m = 0; m < 5; ++m)
-                        for (int n = 0; n < 5; ++n) jy2 = jy2 + (float)s_q[r + m][c + n].y;
+                        for (int n = 0; n < 5; ++n) jy2 = jy2 + s_q[r + m][c + n].y;
                 }
                 float det = (jx2 * jy2) - (sxy * sxy);
                 float tr = jx2 + jy2;
