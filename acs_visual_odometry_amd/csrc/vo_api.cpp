@@ -35,7 +35,7 @@ struct vo_ctx {
     vo_config cfg;
     VoDev d;
     hipStream_t s = nullptr;          // pose passes, stage APIs, the single-frame path
-    hipStream_t se = nullptr;         // extract batches of the device path
+    hipStream_t se[VO_EXT_QUEUES] = {};   // extract batches of the device path (batch j on j % n)
     int B = VO_DEFAULT_BATCH;         // frames per extract batch / pose-pass window
     int fidx = 0;                     // frames enqueued since vo_reset
     bool serial = false;              // VO_SERIAL=1: every kernel on one queue, no cross-queue
@@ -117,7 +117,8 @@ int dalloc(T** p, size_t n)
 
 int sync_all(vo_ctx* c)
 {
-    if (c->se) HIPCHK(hipStreamSynchronize(c->se));
+    for (hipStream_t q : c->se)
+        if (q) HIPCHK(hipStreamSynchronize(q));
     if (c->s) HIPCHK(hipStreamSynchronize(c->s));
     return VO_OK;
 }
@@ -223,12 +224,22 @@ void timed(vo_ctx* c, EvRec* ev, int k, hipStream_t st, F&& launch)
 
 // extract of nb frames f0.. (device images img0 + z * frame_bytes) on stream q; publish:
 // the pose queue may wait for frames < f0 + nb
+// eq: extract queue index (its scratch copy and counters)
 void enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, int nb, bool publish,
-                     hipStream_t q, EvRec* ev)
+                     hipStream_t q, EvRec* ev, int eq)
 {
-    timed(c, ev, 0, q, [&] { vo::launch_stencil(c->d, img0, frame_bytes, nb, 0, q); });
-    timed(c, ev, 1, q, [&] { vo::launch_select(c->d, f0, nb, -1, q); });
-    timed(c, ev, 2, q, [&] { vo::launch_describe(c->d, f0, nb, -1, publish ? (unsigned)(f0 + nb) : 0u, q); });
+    VoDev d = c->d;
+    const size_t B = (size_t)c->B, np = (size_t)d.W * d.H;
+    d.eq = eq;
+    d.blurred += np * B * eq;
+    d.cand += (size_t)d.cand_cap * B * eq;
+    d.tilerows += (size_t)d.ntiles * 16 * B * eq;
+    d.ckeys += (size_t)d.cand_cap * B * eq;
+    d.selbits += ((size_t)d.cand_cap / 64 + 1) * B * eq;
+    d.hist += (size_t)VO_HIST_BINS * B * eq;
+    timed(c, ev, 0, q, [&] { vo::launch_stencil(d, img0, frame_bytes, nb, 0, q); });
+    timed(c, ev, 1, q, [&] { vo::launch_select(d, f0, nb, -1, q); });
+    timed(c, ev, 2, q, [&] { vo::launch_describe(d, f0, nb, -1, publish ? (unsigned)(f0 + nb) : 0u, q); });
 }
 
 // one pose pass over the window [lo, lo + B) of the frames enqueued so far
@@ -264,9 +275,10 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
 {
     const int base = c->fidx, end = base + nf, B = c->B;
     hipStream_t s = c->s;
-    hipStream_t q = (c->serial || host_frame || !img0) ? s : c->se;
-    if (q != s && c->reset_pending) {
-        HIPCHK(hipStreamWaitEvent(q, c->ev_reset, 0));
+    const bool multi = !(c->serial || host_frame || !img0);   // extract on its own queues
+    static const int nq = getenv("VO_EXTQ") ? std::max(1, std::min(VO_EXT_QUEUES, atoi(getenv("VO_EXTQ")))) : VO_EXT_QUEUES;
+    if (multi && c->reset_pending) {
+        for (hipStream_t q : c->se) HIPCHK(hipStreamWaitEvent(q, c->ev_reset, 0));
         c->reset_pending = false;
     }
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&c->d.st->end, end, 1, s));
@@ -274,21 +286,27 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     if (!img0) {
         vo::launch_ext_missing(c->d, base % VO_RING, s);
     } else {
-        int f0 = 0;
+        int f0 = 0, j = 0;
         for (int cnt : sched) {
-            enqueue_extract(c, img0 + (size_t)f0 * frame_bytes, frame_bytes, base + f0, cnt, q != s, q, ev);
+            const int eq = multi ? j % nq : 0;
+            enqueue_extract(c, img0 + (size_t)f0 * frame_bytes, frame_bytes, base + f0, cnt, multi,
+                            multi ? c->se[eq] : s, ev, eq);
             f0 += cnt;
+            ++j;
         }
     }
     c->fidx = end;
     {
-        int f1 = 0;
+        // pass k waits for batch k on its queue; batch k-1 (the other queue) was waited for
+        // by pass k-1, which precedes pass k on the pose queue
+        int f1 = 0, k = 0;
         for (int cnt : sched) {
             f1 += cnt;
-            if (q != s)
-                (void)hipStreamWaitValue32(s, c->d.ctr + VO_SYNC_EXT, (uint32_t)(base + f1), hipStreamWaitValueGte,
-                                           0xFFFFFFFFu);
+            if (multi)
+                (void)hipStreamWaitValue32(s, c->d.ctr + VO_SYNC_EXT + 16 * (k % nq), (uint32_t)(base + f1),
+                                           hipStreamWaitValueGte, 0xFFFFFFFFu);
             enqueue_pass(c, out, out_base, ev, cnt);
+            ++k;
         }
     }
     for (;;) {
@@ -421,19 +439,20 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     auto bail = [&](int r) { vo_destroy(c); return r; };
     c->serial = getenv("VO_SERIAL") && atoi(getenv("VO_SERIAL")) != 0;
     if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
-    if (hip_ok(hipStreamCreateWithFlags(&c->se, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
+    for (hipStream_t& q : c->se)
+        if (hip_ok(hipStreamCreateWithFlags(&q, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming)) != VO_OK) return bail(VO_ERR_HIP);
     d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
     if (d.sel_lds < 0) return bail(VO_ERR_HIP);
     const size_t np = (size_t)W * H;
     rc |= dalloc(&d.frame_in, np);
-    rc |= dalloc(&d.blurred, np * B);
+    rc |= dalloc(&d.blurred, np * B * VO_EXT_QUEUES);
     rc |= dalloc(&d.response, np);
-    rc |= dalloc(&d.cand, (size_t)d.cand_cap * B);
-    rc |= dalloc(&d.tilerows, (size_t)ntiles * 16 * B);
-    rc |= dalloc(&d.ckeys, (size_t)d.cand_cap * B);
-    rc |= dalloc(&d.selbits, ((size_t)d.cand_cap / 64 + 1) * B);
-    rc |= dalloc(&d.hist, (size_t)VO_HIST_BINS * B);
+    rc |= dalloc(&d.cand, (size_t)d.cand_cap * B * VO_EXT_QUEUES);
+    rc |= dalloc(&d.tilerows, (size_t)ntiles * 16 * B * VO_EXT_QUEUES);
+    rc |= dalloc(&d.ckeys, (size_t)d.cand_cap * B * VO_EXT_QUEUES);
+    rc |= dalloc(&d.selbits, ((size_t)d.cand_cap / 64 + 1) * B * VO_EXT_QUEUES);
+    rc |= dalloc(&d.hist, (size_t)VO_HIST_BINS * B * VO_EXT_QUEUES);
     rc |= dalloc(&d.kps, (size_t)N * VO_SLOTS);
     rc |= dalloc(&d.desc, (size_t)N * 8 * VO_SLOTS);
     rc |= dalloc(&d.pre, (size_t)N * VO_SLOTS);
@@ -478,7 +497,8 @@ void vo_destroy(vo_ctx* c)
 {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
-    if (c->se) (void)hipStreamSynchronize(c->se);
+    for (hipStream_t q : c->se)
+        if (q) (void)hipStreamSynchronize(q);
     if (c->s) (void)hipStreamSynchronize(c->s);
     VoDev& d = c->d;
     void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.tilerows, d.ckeys, d.selbits, d.hist, d.ext,
@@ -491,7 +511,8 @@ void vo_destroy(vo_ctx* c)
     if (c->lo_host) (void)hipHostFree(c->lo_host);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->ev_reset) (void)hipEventDestroy(c->ev_reset);
-    if (c->se) (void)hipStreamDestroy(c->se);
+    for (hipStream_t q : c->se)
+        if (q) (void)hipStreamDestroy(q);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
 }

@@ -53,8 +53,10 @@
 #define VO_MAX_BATCH 64
 #define VO_DEFAULT_BATCH 64
 // ctr words: cross-queue counters on lines of their own
-#define VO_CTR_DESCRIBE 0      // describe's in-launch arrival counter
-#define VO_SYNC_EXT 32         // frames extracted since vo_reset (the pose queue waits on it)
+#define VO_EXT_QUEUES 1        // extract queues (batch j on queue j % n, own scratch); 2 measured no faster
+#define VO_CTR_DESCRIBE 0      // + 16 * queue: describe's in-launch arrival counter
+#define VO_SYNC_EXT 32         // + 16 * queue: frames extracted since vo_reset by that queue
+                               // (its batches complete in order; the pose queue waits on it)
 #define VO_CTR_WORDS 64
 #define VO_MAX_HYP 2000
 #define VO_HYP_CHUNK0 100     // RANSAC launch chunks (vo_kernels.hip launch_ransac); 100 = the clamp
@@ -122,6 +124,7 @@ struct VoDev {
     int maxit_initial;
     int max_hyp;
     int B;                // window / extract batch capacity (frames)
+    int eq;               // extract queue of this launch (its scratch copy and counters)
     uint64_t seed;
     double K[9];
     uint32_t cand_cap;    // per frame
@@ -135,7 +138,7 @@ struct VoDev {
     uint64_t* ckeys;      // x B: select's compact keys when they exceed the LDS capacity
     uint64_t* selbits;    // x B: select's selected-key bitmap when it exceeds the LDS capacity
     int sel_lds;          // select: dynamic LDS bytes
-    uint32_t* hist;       // x B
+    uint32_t* hist;       // x B (scratch of extract queue eq; x VO_EXT_QUEUES allocated)
     int2* kps;            // x SLOTS (N each)
     uint64_t* desc;       // x SLOTS (8N each)
     uint32_t* pre;        // x SLOTS (N each)

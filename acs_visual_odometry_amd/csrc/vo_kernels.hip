@@ -1215,9 +1215,9 @@ __global__ void __launch_bounds__(256) k_describe(VoDev d, int f0, int slot_over
     __syncthreads();
     if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __shared__ unsigned s_last;
-    if (!arrive_last(d.ctr + VO_CTR_DESCRIBE, gridDim.x * gridDim.y, &s_last)) return;
-    if (threadIdx.x == 0) d.ctr[VO_CTR_DESCRIBE] = 0u;
-    publish_seq(d.ctr + VO_SYNC_EXT, publish);
+    if (!arrive_last(d.ctr + VO_CTR_DESCRIBE + 16 * d.eq, gridDim.x * gridDim.y, &s_last)) return;
+    if (threadIdx.x == 0) d.ctr[VO_CTR_DESCRIBE + 16 * d.eq] = 0u;
+    publish_seq(d.ctr + VO_SYNC_EXT + 16 * d.eq, publish);
 }
 
 // ---------------------------------------------------------------------------
@@ -2562,7 +2562,7 @@ __global__ void __launch_bounds__(256) k_reset(VoDev d)
     }
     int32_t* ext = reinterpret_cast<int32_t*>(d.ext);
     for (int i = tid; i < (int)(sizeof(VoExt) / 4); i += nth) ext[i] = 0;   // n_kps 0, status OK
-    for (int i = tid; i < VO_HIST_BINS * d.B; i += nth) d.hist[i] = 0u;
+    for (int i = tid; i < VO_HIST_BINS * d.B * VO_EXT_QUEUES; i += nth) d.hist[i] = 0u;
     uint32_t* w = reinterpret_cast<uint32_t*>(d.work);
     for (int i = tid; i < (int)(sizeof(VoWork) / 4) * d.B; i += nth) w[i] = 0u;
     for (int i = tid; i < VO_CTR_WORDS; i += nth) d.ctr[i] = 0u;
