@@ -431,10 +431,11 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
         d.maxit_initial = to_int_x86(std::log(1.0 - k.ransac_p) / std::log(1.0 - std::pow(1.0 - outlierRatio, 8.0)));
     }
     d.max_hyp = std::max(VO_MAX_HYP, std::min(d.maxit_initial, 1 << 20));
-    const int ntiles = ((W + 63) / 64) * ((H + 15) / 16);
-    if (ntiles > 2048) { delete c; return VO_ERR_ARG; }      // SEL_MAX_TILES (select kernel LDS)
+    // stencil tiles of VO_TILE_W x VO_TILE_H, at most 1/4 of a tile's pixels are strict maxima
+    const int ntiles = ((W + VO_TILE_W - 1) / VO_TILE_W) * ((H + VO_TILE_H - 1) / VO_TILE_H);
+    if (ntiles > 3072) { delete c; return VO_ERR_ARG; }      // SEL_MAX_TILES (select kernel LDS)
     d.ntiles = ntiles;
-    d.cand_cap = (uint32_t)ntiles * 256u;
+    d.cand_cap = (uint32_t)ntiles * (VO_TILE_W * VO_TILE_H / 4);
     int rc = VO_OK;
     auto bail = [&](int r) { vo_destroy(c); return r; };
     c->serial = getenv("VO_SERIAL") && atoi(getenv("VO_SERIAL")) != 0;
@@ -579,7 +580,7 @@ int vo_response(vo_ctx* c, const uint8_t* gray, size_t stride, float* R)
     if (rc) return rc;
     const size_t np = (size_t)c->cfg.width * c->cfg.height;
     HIPCHK(hipMemsetAsync(c->d.response, 0, np * sizeof(float), c->s));
-    vo::launch_stencil(c->d, c->d.frame_in, 0, 1, 1, c->s);
+    vo::launch_stencil(c->d, c->d.frame_in, 0, 1, getenv("VO_DBG") ? atoi(getenv("VO_DBG")) : 1, c->s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(R, c->d.response, np * sizeof(float), hipMemcpyDeviceToHost, c->s));
     // the stencil histogram is consumed by select; nothing selects here, so clear it

@@ -16,7 +16,7 @@
 //   frame_in    u8  W*H            staging for host-supplied frames
 //   blurred     u8  W*H      x B   7x7 Gaussian output (read back by describe)
 //   response    f32 W*H            optional dense R map (debug / parity only)
-//   cand        u64 256/tile x B   NMS survivors per 64x16 tile, key = Rbits<<32 | row<<16 | col
+//   cand        u64 192/tile x B   NMS survivors per 48x16 tile, key = Rbits<<32 | row<<16 | col
 //   tilerows    u8  16/tile  x B   survivors per tile row (select emits raster order from them)
 //   ckeys       u64 256/tile x B   compact survivors (only when they overflow select's LDS)
 //   selbits     u64 4/tile   x B   selected-survivor bitmap (only when it overflows LDS)
@@ -40,6 +40,8 @@
 #include <stdint.h>
 
 #define VO_HIST_BINS 4096
+#define VO_TILE_W 48       // stencil tile = one wave's strip width x 16 rows (k_stencil ST_TW, ST_TH)
+#define VO_TILE_H 16
 // keypoint/descriptor slots: frame f (since vo_reset) is extracted into ring slot
 // f % VO_RING; the last valid frame's copy lives in the carry slot during a skip run; the
 // stage APIs (vo_extract / vo_match) use their own two slots

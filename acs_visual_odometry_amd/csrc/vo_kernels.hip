@@ -347,28 +347,26 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 // ---------------------------------------------------------------------------
 // stencil: blur7x7 -> gradients -> 5x5 response -> strict 3x3 NMS candidates
-// One 256-thread workgroup per 64x16 output tile; every intermediate lives in LDS.
 // kernels/feature_extraction_kernel_functions.c:43-120, corner_detection_parallel_GPU.cpp:146-180
+//
+// Column-streaming form: one wave owns a strip of ST_TW = 48 output columns and walks down a
+// segment of ST_SEG = 64 output rows.  Lane L holds column x = xs - 7 + L in every stage, so
+// the 7 halo columns on each side cost 16 of the 64 lanes.  Vertical neighbours are register
+// histories (one new source row per step), horizontal neighbours are DPP wave shifts; there
+// is no LDS and no barrier.  Source row k of the segment (y = ys - 7 + k) completes blurred
+// row ys - 10 + k, gradient row ys - 11 + k, response row ys - 13 + k and NMS row ys - 14 + k;
+// 78 source rows give the 64 output rows.  Every stage but the response is exact integer
+// arithmetic, so the order of its sums is free.
 // ---------------------------------------------------------------------------
-#define ST_TW 64
-#define ST_TH 16
-#define ST_SW (ST_TW + 14)   // source tile (blur radius 3 + gradient 1 + window 2 + nms 1)
-#define ST_SH (ST_TH + 14)
-#define ST_BW (ST_TW + 8)    // blurred tile
-#define ST_BH (ST_TH + 8)
-#define ST_GW (ST_TW + 6)    // gradient tile
-#define ST_GH (ST_TH + 6)
-#define ST_RW (ST_TW + 2)    // response tile
-#define ST_RH (ST_TH + 2)
-
-// (r, c) of element e -> of element e + 256 in a row-major array of COLS columns
-template <int COLS>
-__device__ __forceinline__ void rc_step(int& r, int& c)
-{
-    r += 256 / COLS;
-    c += 256 % COLS;
-    if (c >= COLS) { c -= COLS; ++r; }
-}
+#define ST_TW VO_TILE_W                // tile / strip width (output columns per wave): 48
+#define ST_TH VO_TILE_H                // tile height (select reads 16 row counts per tile)
+#define ST_SEGT 4                      // tiles per wave segment
+#define ST_SEG (ST_TH * ST_SEGT)       // output rows per wave
+#define ST_HALO 7                      // blur 3 + gradient 1 + window 2 + nms 1
+#define ST_ROWS (ST_SEG + 2 * ST_HALO) // source rows streamed per wave
+#define ST_U 26                        // rows per unrolled block (ST_ROWS = 3 blocks)
+static_assert(ST_ROWS % ST_U == 0, "stencil row blocks");
+static_assert(ST_TW + 2 * ST_HALO <= 64, "strip + halo within one wave");
 
 __device__ __forceinline__ int refl101(int i, int n)
 {
@@ -376,278 +374,158 @@ __device__ __forceinline__ int refl101(int i, int n)
     while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
     return i;
 }
+// DPP wave shifts (gfx9 wave_shr:1 / wave_shl:1): the value of lane L - 1 / lane L + 1.  A DPP
+// read of a lane that is off in EXEC returns 0, so the shift must run with the whole wave on:
+// the empty volatile asm pins it where it is written (the compiler otherwise sank a shift into
+// the masked arm of a select, and border lanes read 0 from their masked neighbours).
+__device__ __forceinline__ int from_left(int v)
+{
+    int r = __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
+    asm volatile("" : "+v"(r));
+    return r;
+}
+__device__ __forceinline__ int from_right(int v)
+{
+    int r = __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false);
+    asm volatile("" : "+v"(r));
+    return r;
+}
 
 __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restrict__ img0, size_t frame_bytes,
                                                   int write_response)
 {
-    // LDS, aliased by lifetime (29 KB): region X holds the source tile (phases 1-2), then the
-    // blurred tile (3-4), then the response (5-6); region Y the horizontal blur sums (2-3),
-    // then the gradient planes Jx^2, Jy^2, Jxy (4-5)
-    constexpr int X_BYTES = ST_RH * ST_RW * 4;                 // the largest of the three
-    constexpr int Y_BYTES = ST_GH * ST_GW * 16;
-    static_assert(ST_SH * ST_SW <= X_BYTES && ST_BH * ST_BW <= X_BYTES, "stencil LDS region X");
-    static_assert(ST_SH * ST_BW * 4 <= Y_BYTES, "stencil LDS region Y");
-    __shared__ __align__(16) unsigned char s_x[X_BYTES];
-    __shared__ __align__(16) unsigned char s_y[Y_BYTES];
-    __shared__ unsigned long long s_bal[ST_TH];
-    uint8_t (*s_src)[ST_SW] = reinterpret_cast<uint8_t (*)[ST_SW]>(s_x);
-    uint8_t (*s_bl)[ST_BW] = reinterpret_cast<uint8_t (*)[ST_BW]>(s_x);
-    float (*s_r)[ST_RW] = reinterpret_cast<float (*)[ST_RW]>(s_x);
-    uint16_t (*s_hb)[ST_BW] = reinterpret_cast<uint16_t (*)[ST_BW]>(s_y);   // <= 65280: u16
-    // gradient planes interleaved per pixel {Jx^2, Jy^2, Jxy, 0}: one 16-byte LDS access each
-    float4 (*s_q)[ST_GW] = reinterpret_cast<float4 (*)[ST_GW]>(s_y);
-
     const int W = d.W, H = d.H;
-    const int x0 = blockIdx.x * ST_TW, y0 = blockIdx.y * ST_TH;
-    const int tid = threadIdx.x;
+    const int ntx = (W + ST_TW - 1) / ST_TW, nty = (H + ST_TH - 1) / ST_TH;
+    const int nseg = (nty + ST_SEGT - 1) / ST_SEGT;
+    const int g = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
+    if (g >= ntx * nseg) return;
+    const int strip = g % ntx, seg = g / ntx;
+    const int lane = threadIdx.x & 63;
     // frame z of the batch: its image and its scratch copy
-    const int z = blockIdx.z;
+    const int z = blockIdx.y;
     const uint8_t* __restrict__ img = img0 + (size_t)z * frame_bytes;
-    uint8_t* blurred = d.blurred + (size_t)z * W * H;
-    uint64_t* cand = d.cand + (size_t)z * d.cand_cap;
-    uint8_t* tilerows = d.tilerows + (size_t)z * d.ntiles * ST_TH;
-    uint32_t* hist = d.hist + (size_t)z * VO_HIST_BINS;
+    uint8_t* __restrict__ blurred = d.blurred + (size_t)z * W * H;
+    uint64_t* __restrict__ cand = d.cand + (size_t)z * d.cand_cap;
+    uint8_t* __restrict__ tilerows = d.tilerows + (size_t)z * d.ntiles * ST_TH;
+    uint32_t* __restrict__ hist = d.hist + (size_t)z * VO_HIST_BINS;
+    float* __restrict__ response = d.response;
 
-    // 1. source tile with BORDER_REFLECT_101 addressing: every load of the thread in flight
-    //    before the first LDS store (no load-use chain per element)
-    {
-        constexpr int NE = ST_SH * ST_SW, NIT = (NE + 255) / 256;
-        uint8_t v[NIT];
-        int r = tid / ST_SW, c = tid - r * ST_SW;               // element tid + 256 * it, stepped
-        // workgroup-uniform: tiles whose source window is inside the image need no reflection
-        const bool interior = x0 >= 7 && y0 >= 7 && x0 - 7 + ST_SW <= W && y0 - 7 + ST_SH <= H;
-        if (interior) {
-            const uint8_t* __restrict__ org = img + (size_t)(y0 - 7) * W + (x0 - 7);
-#pragma unroll
-            for (int it = 0; it < NIT; ++it) {
-                v[it] = r < ST_SH ? org[(uint32_t)(r * W + c)] : (uint8_t)0;     // frames < 2^31 px
-                rc_step<ST_SW>(r, c);
-            }
-        } else {
-#pragma unroll
-            for (int it = 0; it < NIT; ++it) {
-                v[it] = 0;
-                if (r < ST_SH) {
-                    const int y = refl101(y0 - 7 + r, H), x = refl101(x0 - 7 + c, W);
-                    v[it] = img[(uint32_t)(y * W + x)];
-                }
-                rc_step<ST_SW>(r, c);
-            }
-        }
-#pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            const int e = tid + it * 256;
-            if (e < NE) s_x[e] = v[it];
-        }
-    }
-    __syncthreads();
-    // 2. horizontal 7-tap (exact; 24-bit multiplies: every product < 2^24).  Thread (row, run
-    //    of 9 columns): the 15 source bytes of the run are read once and slide through registers.
-    {
-        constexpr int RUN = 9, NRUN = ST_BW / RUN;                  // 8 runs x 30 rows = 240 threads
-        static_assert(RUN * NRUN == ST_BW && NRUN * ST_SH <= 256, "h-blur runs");
-        if (tid < NRUN * ST_SH) {
-            const int r = tid / NRUN, c0 = (tid - r * NRUN) * RUN;
-            uint32_t sv[RUN + 6];
-#pragma unroll
-            for (int j = 0; j < RUN + 6; ++j) sv[j] = s_src[r][c0 + j];
-#pragma unroll
-            for (int j = 0; j < RUN; ++j)
-                // symmetric taps: 8(s0+s6) + 28(s1+s5) + 56(s2+s4) + 72 s3
-                s_hb[r][c0 + j] = (uint16_t)(8u * (sv[j] + sv[j + 6]) + 28u * (sv[j + 1] + sv[j + 5]) +
-                                             56u * (sv[j + 2] + sv[j + 4]) + 72u * sv[j + 3]);
-        }
-    }
-    __syncthreads();
-    // 3. vertical 7-tap, round, u8 (cv::GaussianBlur 8U fixed point); blurred -> HBM.  Thread
-    //    (column, run of 8 rows): 14 horizontal sums read once.
-    {
-        constexpr int RUN = 8, NRUN = ST_BH / RUN;                  // 3 runs x 72 columns = 216 threads
-        static_assert(RUN * NRUN == ST_BH && NRUN * ST_BW <= 256, "v-blur runs");
-        if (tid < NRUN * ST_BW) {
-            const int k = tid / ST_BW, c = tid - k * ST_BW, r0 = k * RUN;
-            uint32_t hv[RUN + 6];
-#pragma unroll
-            for (int j = 0; j < RUN + 6; ++j) hv[j] = s_hb[r0 + j][c];
-            const int x = x0 - 4 + c;
-            const bool xin = c >= 4 && c < 4 + ST_TW && x < W;
-#pragma unroll
-            for (int j = 0; j < RUN; ++j) {
-                // operands < 2^17 (u16 loads): selected as 24-bit multiply-adds
-                const uint32_t v = 8u * (hv[j] + hv[j + 6]) + 28u * (hv[j + 1] + hv[j + 5]) +
-                                   56u * (hv[j + 2] + hv[j + 4]) + 72u * hv[j + 3];
-                const uint32_t bb = (v + 32768u) >> 16;
-                const int r = r0 + j, y = y0 - 4 + r;
-                s_bl[r][c] = (uint8_t)bb;
-                if (xin && r >= 4 && r < 4 + ST_TH && y < H) blurred[(uint32_t)(y * W + x)] = (uint8_t)bb;
-            }
-        }
-    }
-    __syncthreads();
-    // 4. gradients (kernel .c:59-76), 0 outside 1<=i<=H-2, 1<=j<=W-2.  The reference computes
-    //    them in f32 on u8 values: every intermediate is an integer below 2^11, so integer
-    //    arithmetic gives the same values; Jx*Jx and Jy*Jy (< 2^21) are exact in f32 as well.
-    //    Thread (column, run of rows): the 3x3 window slides down, one new row of 3 per output.
-    {
-        constexpr int NRUN = 3, RUN = (ST_GH + NRUN - 1) / NRUN;    // 3 runs (8, 7, 7) x 70 columns
-        static_assert(NRUN * ST_GW <= 256 && RUN == 8, "gradient runs");
-        if (tid < NRUN * ST_GW) {
-            const int k = tid / ST_GW, c = tid - k * ST_GW;
-            const int r0 = k == 0 ? 0 : (k == 1 ? 8 : 15), len = k == 0 ? 8 : 7;
-            const int x = x0 - 3 + c;
-            const bool xin = x >= 1 && x <= W - 2;
-            int a0 = s_bl[r0][c], a1 = s_bl[r0][c + 1], a2 = s_bl[r0][c + 2];
-            int m0 = s_bl[r0 + 1][c], m1 = s_bl[r0 + 1][c + 1], m2 = s_bl[r0 + 1][c + 2];
-#pragma unroll
-            for (int j = 0; j < RUN; ++j) {
-                if (j < len) {
-                    const int r = r0 + j, y = y0 - 3 + r;
-                    const int e0 = s_bl[r + 2][c], e1 = s_bl[r + 2][c + 1], e2 = s_bl[r + 2][c + 2];
-                    int jx = 0, jy = 0, jxy = 0;
-                    if (xin && y >= 1 && y <= H - 2) {
-                        const int sx0 = a0 - e0, sx1 = a1 - e1, sx2 = a2 - e2;
-                        const int sy0 = (a0 + 2 * m0) + e0, sy2 = (a2 + 2 * m2) + e2;
-                        jx = (sx0 + 2 * sx1) + sx2;
-                        jy = sy0 - sy2;
-                        jxy = sx0 - sx2;
-                    }
-                        const float fx = (float)jx, fy = (float)jy;     // squares < 2^21: exact in f32
-                    s_q[r][c] = make_float4(fx * fx, fy * fy, (float)jxy, 0.0f);
-                    a0 = m0; a1 = m1; a2 = m2;
-                    m0 = e0; m1 = e1; m2 = e2;
-                }
-            }
-        }
-    }
-    __syncthreads();
-    // 5. response (kernel .c:97-114): 5x5 sums of Jx^2, Jy^2, Jxy accumulated in f32, m-outer
-    //    n-inner.  Every term is an integer and, after the 7-tap blur, |J| <= 510: a sum of 25
-    //    squares stays below 2^24, so every f32 partial sum in any order is exact and equals the
-    //    in-order sum.  Computed here as f32 box sums (horizontal 5-sums per row, then a running
-    //    vertical window), with the in-order loop kept for a total above 2^24 (unreachable for
-    //    u8 input).  Thread (strip, column): RS outputs down a column.
-    {
-        constexpr int RS = ST_RH / 3;                               // 3 strips x ST_RW columns
-        static_assert(RS * 3 == ST_RH && 3 * ST_RW <= 256, "response strips");
-        const float thr = d.resp_thr;
-        const bool act = tid < 3 * ST_RW;
-        const int strip = act ? tid / ST_RW : 0, c = act ? tid - strip * ST_RW : 0, r0 = strip * RS;
-        float ax[RS], ay[RS], as[RS];
-#pragma unroll
-        for (int o = 0; o < RS; ++o) { ax[o] = 0.0f; ay[o] = 0.0f; as[o] = 0.0f; }
-        if (act) {
-            // horizontal 5-sums of the RS + 4 source rows, then vertical sums as a running
-            // window (exact integers: any order gives the same sum)
-            float hx[RS + 4], hy[RS + 4], hs[RS + 4];
-#pragma unroll
-            for (int mr = 0; mr < RS + 4; ++mr) {
-                hx[mr] = 0.0f; hy[mr] = 0.0f; hs[mr] = 0.0f;
-#pragma unroll
-                for (int n = 0; n < 5; ++n) {
-                    const float4 q = s_q[r0 + mr][c + n];
-                    hx[mr] += q.x; hy[mr] += q.y; hs[mr] += q.z;
-                }
-            }
-            float sx = 0.0f, sy = 0.0f, ss = 0.0f;
-#pragma unroll
-            for (int m = 0; m < 5; ++m) { sx += hx[m]; sy += hy[m]; ss += hs[m]; }
-            ax[0] = sx; ay[0] = sy; as[0] = ss;
-#pragma unroll
-            for (int o = 1; o < RS; ++o) {
-                sx = (sx + hx[o + 4]) - hx[o - 1];
-                sy = (sy + hy[o + 4]) - hy[o - 1];
-                ss = (ss + hs[o + 4]) - hs[o - 1];
-                ax[o] = sx; ay[o] = sy; as[o] = ss;
-            }
-        }
-        float rv_out[RS];
-#pragma unroll
-        for (int o = 0; o < RS; ++o) {
-            const int r = r0 + o;
-            const int y = y0 - 1 + r, x = x0 - 1 + c;
-            float out = 0.0f;
-            if (act && y >= 2 && y <= H - 3 && x >= 2 && x <= W - 3) {
-                float jx2 = ax[o], jy2 = ay[o];
-                const float sxy = as[o];
-                if (ax[o] > 16777216.0f) {                          // never for u8 input: in-order f32
-                    jx2 = 0.0f;
-                    for (int m = 0; m < 5; ++m)
-                        for (int n = 0; n < 5; ++n) jx2 = jx2 + s_q[r + m][c + n].x;
-                }
-                if (ay[o] > 16777216.0f) {
-                    jy2 = 0.0f;
-                    for (int m = 0; m < 5; ++m)
-                        for (int n = 0; n < 5; ++n) jy2 = jy2 + s_q[r + m][c + n].y;
-                }
-                float det = (jx2 * jy2) - (sxy * sxy);
-                float tr = jx2 + jy2;
-                // tr / 2 == tr * 0.5 exactly (both the correctly rounded halving)
-                float rv = (tr * 0.5f) - (0.5f * sqrtf(tr * tr - 4.0f * det));
-                out = rv > thr ? rv : 0.0f;
-            }
-            rv_out[o] = out;
-        }
-        __syncthreads();                                           // s_r aliases s_bl's region
-        if (act) {
-#pragma unroll
-            for (int o = 0; o < RS; ++o) {
-                const int r = r0 + o;
-                const int y = y0 - 1 + r, x = x0 - 1 + c;
-                s_r[r][c] = rv_out[o];
-                if (write_response && r >= 1 && r <= ST_TH && c >= 1 && c <= ST_TW && y < H && x < W)
-                    d.response[(size_t)y * W + x] = rv_out[o];
-            }
-        }
-    }
-    __syncthreads();
-    // 6. strict 3x3 NMS inside the retinal margin (corner_detection_parallel_GPU.cpp:152-180).
-    //    Survivors are compacted in tile-local raster order: wave w owns tile rows 4w..4w+3
-    //    (lane = column), so ballots give the order; per-row counts go to tilerows[] so the
-    //    select kernel can emit the global raster order without sorting.  The 3x3 window
-    //    slides down the wave's rows: three new response values per row.
+    const int xs = strip * ST_TW, ys = seg * ST_SEG;
+    const int x = xs - ST_HALO + lane;
+    const uint32_t xl = (uint32_t)refl101(x, W);              // BORDER_REFLECT_101 column
+    const int yend = min(ys + ST_SEG, H);                     // image rows of this segment
+    const int tend = min(ys + ST_SEG, nty * ST_TH);           // tile rows of this segment
+    const bool out_lane = lane >= ST_HALO && lane < ST_HALO + ST_TW && x < W;
+    const bool gx_ok = x >= 1 && x <= W - 2;                  // kernel .c:59-76
+    const bool rx_ok = x >= 2 && x <= W - 3;                  // kernel .c:97-114
     const int hk = d.nms_k / 2;
-    const int lane = tid & 63, wave = tid >> 6;
-    float cvk[ST_TH / 4];
-    bool mxk[ST_TH / 4];
-    {
-        const int c = lane, rb = 4 * wave;
-        float up0 = s_r[rb][c], up1 = s_r[rb][c + 1], up2 = s_r[rb][c + 2];
-        float md0 = s_r[rb + 1][c], md1 = s_r[rb + 1][c + 1], md2 = s_r[rb + 1][c + 2];
+    const bool nx_ok = out_lane && x >= hk && x < W - hk && x >= d.bcol && x <= W - d.bcol;
+    const float thr = d.resp_thr;
+    const uint32_t thr_bits = d.thr_bits;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+
+    // register histories (index 0 oldest)
+    int s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0;          // source rows
+    int ba = 0, bm = 0, be = 0;                                          // blurred rows
+    int qx0 = 0, qx1 = 0, qx2 = 0, qx3 = 0, qx4 = 0, vx = 0;             // Jx^2 rows + vertical sum
+    int qy0 = 0, qy1 = 0, qy2 = 0, qy3 = 0, qy4 = 0, vy = 0;             // Jy^2
+    int qs0 = 0, qs1 = 0, qs2 = 0, qs3 = 0, qs4 = 0, vs = 0;             // Jxy
+    float ru = 0.0f, rm = 0.0f, rd = 0.0f;                               // response rows
+    int toff = 0;                                                        // candidates so far in the tile
+
+    for (int k0 = 0; k0 < ST_ROWS; k0 += ST_U) {
+        // every load of the block in flight before the first use
+        uint32_t src[ST_U];
 #pragma unroll
-        for (int kk = 0; kk < ST_TH / 4; ++kk) {
-            const int r = rb + kk;
-            const int i = y0 + r, j = x0 + c;
-            const float dn0 = s_r[r + 2][c], dn1 = s_r[r + 2][c + 1], dn2 = s_r[r + 2][c + 2];
-            const bool ok = i < H && j < W && i >= hk && i < H - hk && j >= hk && j < W - hk &&
-                            (j >= d.bcol) && (j <= W - d.bcol) && (i >= d.brow) && (i <= H - d.brow);
-            const float cv = md1;
-            // strict maximum: any neighbour >= the centre rejects it
-            const bool mx = ok && !(up0 >= cv || up1 >= cv || up2 >= cv || md0 >= cv || md2 >= cv ||
-                                    dn0 >= cv || dn1 >= cv || dn2 >= cv);
-            unsigned long long bal = ballot64(mx);
-            if (lane == 0) s_bal[r] = bal;
-            cvk[kk] = cv;
-            mxk[kk] = mx;
-            up0 = md0; up1 = md1; up2 = md2;
-            md0 = dn0; md1 = dn1; md2 = dn2;
+        for (int u = 0; u < ST_U; ++u) {
+            const int yr = refl101(ys - ST_HALO + k0 + u, H);
+            src[u] = img[(uint32_t)yr * (uint32_t)W + xl];                 // frames < 2^32 px
         }
-    }
-    __syncthreads();
-    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-    if (tid < ST_TH) tilerows[tile * ST_TH + tid] = (uint8_t)__popcll(s_bal[tid]);
 #pragma unroll
-    for (int kk = 0; kk < ST_TH / 4; ++kk) {
-        if (!mxk[kk]) continue;
-        const int r = 4 * wave + kk, c = lane;
-        int off = 0;
-        for (int rr = 0; rr < r; ++rr) off += __popcll(s_bal[rr]);
-        off += __popcll(s_bal[r] & ((1ull << lane) - 1ull));
-        const int i = y0 + r, j = x0 + c;
-        const uint32_t bits = __float_as_uint(cvk[kk]);
-        cand[(size_t)tile * (ST_TW * ST_TH / 4) + off] = ((uint64_t)bits << 32) | ((uint64_t)i << 16) | (uint64_t)j;
-        uint32_t bin = (bits - d.thr_bits) >> 15;
-        if (bin > VO_HIST_BINS - 1) bin = VO_HIST_BINS - 1;
-        atomicAdd(&hist[bin], 1u);
+        for (int u = 0; u < ST_U; ++u) {
+            const int k = k0 + u;
+            s0 = s1; s1 = s2; s2 = s3; s3 = s4; s4 = s5; s5 = s6; s6 = (int)src[u];
+            // 1. 7x7 blur (cv::GaussianBlur 8U fixed point, A.1): vertical taps in registers,
+            //    horizontal taps by wave shifts, one rounding: (sum k_i k_j I + 2^15) >> 16
+            const int vb = (int)(__umul24(8u, s0 + s6) + __umul24(28u, s1 + s5) + __umul24(56u, s2 + s4) + __umul24(72u, s3));     // <= 65280
+            const int l1 = from_left(vb), l2 = from_left(l1), l3 = from_left(l2);
+            const int r1 = from_right(vb), r2 = from_right(r1), r3 = from_right(r2);
+            const int hb = (int)(__umul24(8u, l3 + r3) + __umul24(28u, l2 + r2) + __umul24(56u, l1 + r1) + __umul24(72u, vb));   // < 2^24
+            const int b = (hb + 32768) >> 16;
+            const int yb = ys - 10 + k;
+            if (yb >= ys && yb < yend && out_lane) blurred[(uint32_t)yb * (uint32_t)W + (uint32_t)x] = (uint8_t)b;
+            ba = bm; bm = be; be = b;
+            // 2. gradients of row yb - 1 (kernel .c:59-76), 0 outside 1<=i<=H-2, 1<=j<=W-2; the
+            //    reference's f32 values are these integers (all below 2^11)
+            const int yg = yb - 1;
+            const int dv = ba - be, sv = (ba + 2 * bm) + be;
+            const int dl = from_left(dv), dr = from_right(dv), sl = from_left(sv), sr = from_right(sv);
+            const bool gm = gx_ok && yg >= 1 && yg <= H - 2;
+            const int jx = gm ? (dl + 2 * dv) + dr : 0;
+            const int jy = gm ? sl - sr : 0;
+            const int jxy = gm ? dl - dr : 0;
+            // 3. 5x5 window sums (kernel .c:97-107): |J| <= 512 after the blur, so a sum of 25
+            //    squares is below 2^24 and the in-order f32 sum is this integer sum
+            const int qx = __mul24(jx, jx), qy = __mul24(jy, jy);
+            vx += qx - qx0; qx0 = qx1; qx1 = qx2; qx2 = qx3; qx3 = qx4; qx4 = qx;
+            vy += qy - qy0; qy0 = qy1; qy1 = qy2; qy2 = qy3; qy3 = qy4; qy4 = qy;
+            vs += jxy - qs0; qs0 = qs1; qs1 = qs2; qs2 = qs3; qs3 = qs4; qs4 = jxy;
+            int sx, sy, ss;
+            {
+                const int a1 = from_left(vx), c1 = from_right(vx);
+                sx = ((vx + a1) + c1) + (from_left(a1) + from_right(c1));
+                const int a2 = from_left(vy), c2 = from_right(vy);
+                sy = ((vy + a2) + c2) + (from_left(a2) + from_right(c2));
+                const int a3 = from_left(vs), c3 = from_right(vs);
+                ss = ((vs + a3) + c3) + (from_left(a3) + from_right(c3));
+            }
+            // 4. response of row yg - 2 (kernel .c:108-114), threshold (corner_detection_parallel_GPU.h:25)
+            const int yr = yg - 2;
+            float out = 0.0f;
+            if (yr >= 2 && yr <= H - 3) {
+                const float jx2 = (float)sx, jy2 = (float)sy, sxy = (float)ss;
+                const float det = (jx2 * jy2) - (sxy * sxy);
+                const float tr = jx2 + jy2;
+                // tr / 2 == tr * 0.5 exactly (both the correctly rounded halving)
+                const float rv = (tr * 0.5f) - (0.5f * sqrtf(tr * tr - 4.0f * det));
+                out = (rx_ok && rv > thr) ? rv : 0.0f;
+            }
+            if (write_response == 1 && yr >= ys && yr < yend && out_lane)
+                response[(size_t)yr * W + x] = out;
+            if (write_response > 1 && yr >= ys && yr < yend && out_lane)
+                response[(size_t)yr * W + x] = write_response == 2 ? (float)sx : write_response == 3 ? (float)sy : write_response == 4 ? (float)ss : write_response == 5 ? (float)vx : (float)qx4;
+            ru = rm; rm = rd; rd = out;
+            // 5. strict 3x3 NMS of row yr - 1 inside the retinal margin
+            //    (corner_detection_parallel_GPU.cpp:152-180): any neighbour >= the centre rejects
+            //    it (responses are never NaN: 0 or above the threshold)
+            const int yn = yr - 1;
+            if (yn >= ys && yn < tend) {
+                // responses are +0 or above resp_thr >= 0 (vo_create): their bit patterns order
+                // as the values do, so the window maximum is an integer max3
+                const int iu = __float_as_int(ru), im = __float_as_int(rm), id = __float_as_int(rd);
+                const int cm = max(max(iu, im), id);
+                const int cl = from_left(cm), cr = from_right(cm);
+                const int nb = max(max(cl, cr), max(iu, id));
+                const bool row_ok = yn < H && yn >= hk && yn < H - hk && yn >= d.brow && yn <= H - d.brow;
+                const bool mx = nx_ok && row_ok && nb < im;
+                const unsigned long long bal = ballot64(mx);
+                const int r = yn & (ST_TH - 1);
+                const int tile = (yn / ST_TH) * ntx + strip;
+                if (r == 0) toff = 0;
+                if (lane == 0) tilerows[tile * ST_TH + r] = (uint8_t)__popcll(bal);
+                if (mx) {
+                    // tile-local raster order: rows before this one, then lanes (= columns) before
+                    const int off = toff + __popcll(bal & lt_mask);
+                    const uint32_t bits = __float_as_uint(rm);
+                    cand[(size_t)tile * (ST_TW * ST_TH / 4) + off] =
+                        ((uint64_t)bits << 32) | ((uint64_t)yn << 16) | (uint64_t)x;
+                    uint32_t bin = (bits - thr_bits) >> 15;
+                    if (bin > VO_HIST_BINS - 1) bin = VO_HIST_BINS - 1;
+                    atomicAdd(&hist[bin], 1u);
+                }
+                toff += __popcll(bal);
+            }
+        }
     }
 }
 
@@ -659,7 +537,7 @@ __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restr
 // ---------------------------------------------------------------------------
 #define SEL_MAX 4096
 #define BND_CAP 2048
-#define SEL_MAX_TILES 2048
+#define SEL_MAX_TILES 3072
 #define SEL_LDS_BITS 65536
 
 template <typename T, bool ASC>
@@ -757,11 +635,11 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     }
     VO_STAMP(d, 1990, 0);
     // A
-    const int tpt = (ntiles + 1023) / 1024;            // tiles per thread (<= 2)
-    int tt[2] = {0, 0};
+    const int tpt = (ntiles + 1023) / 1024;            // tiles per thread (<= 3)
+    int tt[3] = {0, 0, 0};
     int myC = 0;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < 3; ++u) {
         const int t = tid * tpt + u;
         if (u < tpt && t < ntiles) {
             uint4 rc = reinterpret_cast<const uint4*>(tilerows)[t];
@@ -787,7 +665,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     int C = 0;
     for (int w = 0; w < 16; ++w) { if (w < wave) base += s_wsum[w]; C += s_wsum[w]; }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < 3; ++u) {
         const int t = tid * tpt + u;
         if (u < tpt && t < ntiles) { s_tpre[t] = base; base += tt[u]; }
     }
@@ -936,7 +814,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
             if (lane == 0 && ((r0 + u) * 1024 + wave * 64) < C) bits[((r0 + u) * 1024 + wave * 64) >> 6] = bal;
             if (sel) {
                 const int row = (int)((v[u] >> 16) & 0xFFFF), col = (int)(v[u] & 0xFFFF);
-                const int seg = row * ntx + (col >> 6);
+                const int seg = row * ntx + col / ST_TW;
                 atomicAdd(&s_segw[seg >> 2], 1u << (8 * (seg & 3)));
             }
         }
@@ -991,7 +869,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
             const int g = (r0 + u) * 1024 + tid;
             if (g >= C || !((bits[g >> 6] >> (g & 63)) & 1ull)) continue;
             const int row = (int)((v[u] >> 16) & 0xFFFF), col = (int)(v[u] & 0xFFFF);
-            const int x = col >> 6, r = row & (ST_TH - 1), t = (row / ST_TH) * ntx + x;
+            const int x = col / ST_TW, r = row & (ST_TH - 1), t = (row / ST_TH) * ntx + x;
             const int seg = row * ntx + x;
             // first compact index of this (row, tile) segment
             const uint4 rc = s_rows[t];
@@ -2616,7 +2494,9 @@ const char* kernel_name(int i) { return g_names[i]; }
 void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int nb, int write_response, hipStream_t s)
 {
     ensure_tables();
-    dim3 g((d.W + ST_TW - 1) / ST_TW, (d.H + ST_TH - 1) / ST_TH, nb);
+    const int ntx = (d.W + ST_TW - 1) / ST_TW, nty = (d.H + ST_TH - 1) / ST_TH;
+    const int waves = ntx * ((nty + ST_SEGT - 1) / ST_SEGT);      // one (strip, segment) per wave
+    dim3 g((waves + 3) / 4, nb);
     hipLaunchKernelGGL(k_stencil, g, dim3(256), 0, s, d, img0, frame_bytes, write_response);
 }
 void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s)
