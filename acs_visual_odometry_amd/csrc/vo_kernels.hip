@@ -360,12 +360,10 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // ---------------------------------------------------------------------------
 #define ST_TW VO_TILE_W                // tile / strip width (output columns per wave): 48
 #define ST_TH VO_TILE_H                // tile height (select reads 16 row counts per tile)
-#define ST_SEGT 4                      // tiles per wave segment
-#define ST_SEG (ST_TH * ST_SEGT)       // output rows per wave
 #define ST_HALO 7                      // blur 3 + gradient 1 + window 2 + nms 1
-#define ST_ROWS (ST_SEG + 2 * ST_HALO) // source rows streamed per wave
-#define ST_U 26                        // rows per unrolled block (ST_ROWS = 3 blocks)
-static_assert(ST_ROWS % ST_U == 0, "stencil row blocks");
+#ifndef ST_SEGT_DEFAULT
+#define ST_SEGT_DEFAULT 4              // tiles per wave segment (VO_STSEG picks 4 / 6 / 8)
+#endif
 static_assert(ST_TW + 2 * ST_HALO <= 64, "strip + halo within one wave");
 
 __device__ __forceinline__ int refl101(int i, int n)
@@ -380,20 +378,24 @@ __device__ __forceinline__ int refl101(int i, int n)
 // the masked arm of a select, and border lanes read 0 from their masked neighbours).
 __device__ __forceinline__ int from_left(int v)
 {
-    int r = __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
+    int r = __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true);   // bound_ctrl: edge lanes read 0, no old operand
     asm volatile("" : "+v"(r));
     return r;
 }
 __device__ __forceinline__ int from_right(int v)
 {
-    int r = __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false);
+    int r = __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true);   // bound_ctrl: edge lanes read 0, no old operand
     asm volatile("" : "+v"(r));
     return r;
 }
 
+// SEGT tiles (16 SEGT output rows) per wave, source rows in unrolled blocks of U; rows past
+// the segment's 16 SEGT + 14 in the last block only feed masked outputs
+template <int SEGT, int U>
 __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restrict__ img0, size_t frame_bytes,
                                                   int write_response)
 {
+    constexpr int ST_SEGT = SEGT, ST_SEG = ST_TH * SEGT, ST_ROWS = ST_SEG + 2 * ST_HALO, ST_U = U;
     const int W = d.W, H = d.H;
     const int ntx = (W + ST_TW - 1) / ST_TW, nty = (H + ST_TH - 1) / ST_TH;
     const int nseg = (nty + ST_SEGT - 1) / ST_SEGT;
@@ -2495,9 +2497,16 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
 {
     ensure_tables();
     const int ntx = (d.W + ST_TW - 1) / ST_TW, nty = (d.H + ST_TH - 1) / ST_TH;
-    const int waves = ntx * ((nty + ST_SEGT - 1) / ST_SEGT);      // one (strip, segment) per wave
+    static const int segt = getenv("VO_STSEG") ? atoi(getenv("VO_STSEG")) : ST_SEGT_DEFAULT;
+    const int st = segt == 6 || segt == 8 ? segt : 4;
+    const int waves = ntx * ((nty + st - 1) / st);                 // one (strip, segment) per wave
     dim3 g((waves + 3) / 4, nb);
-    hipLaunchKernelGGL(k_stencil, g, dim3(256), 0, s, d, img0, frame_bytes, write_response);
+    if (st == 8)
+        hipLaunchKernelGGL((k_stencil<8, 24>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response);
+    else if (st == 6)
+        hipLaunchKernelGGL((k_stencil<6, 22>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response);
+    else
+        hipLaunchKernelGGL((k_stencil<4, 26>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response);
 }
 void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s)
 {
