@@ -262,8 +262,14 @@ void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int cap)
 // measured slower: more passes, each with a fixed latency.)
 std::vector<int> batch_schedule(int nf, int B)
 {
+    // experiment knob: VO_FIRST = size of the first batch (pipeline fill), default B
+    static const int first = getenv("VO_FIRST") ? atoi(getenv("VO_FIRST")) : 0;
     std::vector<int> v;
-    for (int done = 0; done < nf; done += B) v.push_back(std::min(B, nf - done));
+    for (int done = 0; done < nf;) {
+        const int want = (done == 0 && first > 0 && first < B) ? first : B;
+        v.push_back(std::min(want, nf - done));
+        done += v.back();
+    }
     return v;
 }
 

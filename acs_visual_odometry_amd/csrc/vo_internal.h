@@ -63,6 +63,7 @@
 #define VO_MAX_HYP 2000
 #define VO_HYP_CHUNK0 100     // RANSAC launch chunks (vo_kernels.hip launch_ransac); 100 = the clamp
 #define VO_HYP_CHUNK1 512
+#define VO_HYP_REPS 1        // hypotheses per wave in the last chunk (VO_RREPS; 4 and 8 measured 1-6 % slower)
 
 struct VoFrameOut {
     int32_t status, n_kps, n_matches, n_inl, best_k, n_eval, fitted, frame;

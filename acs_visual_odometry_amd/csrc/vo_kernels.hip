@@ -1610,7 +1610,9 @@ __device__ void inv4(const double* M, double* Inv)
 // path); second chunk: four single-wave hypotheses per workgroup, since it usually exits at
 // once (fewer workgroups to dispatch).
 template <int WPH, int HPB>
-__global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, int k1, int nhyp, int stage)
+// reps: hypotheses per wave (strided by the grid), so a later chunk, which usually exits at
+// once, dispatches reps times fewer workgroups
+__global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, int k1, int nhyp, int stage, int reps)
 {
     const int wf = blockIdx.y;                     // window frame
     if (wf >= win_count(d, stage)) return;
@@ -1620,11 +1622,12 @@ __global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, 
     __shared__ unsigned s_last;
     __shared__ int s_cnt[HPB][WPH];
     const int wave = threadIdx.x >> 6, h = wave / WPH, sw = wave - h * WPH;
-    const int k = k0 + blockIdx.x * HPB + h;
     const int lane = threadIdx.x & 63;
     const int M = w->M, scored = w->scored;
     const double* pts = d.pts + (size_t)wf * 4 * d.N;
     int32_t* counts = d.counts + (size_t)wf * d.max_hyp;
+    int k = k0 + blockIdx.x * HPB + h;                 // (WPH > 1 only with reps == 1: s_cnt below)
+    for (int rep = 0; rep < reps; ++rep, k += gridDim.x * HPB) {
     if (k < k1) {
         VO_STAMP(d, k, 0);
         int s8[8];
@@ -1648,6 +1651,7 @@ __global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, 
             s_cnt[h][sw] = cnt;
         }
         VO_STAMP(d, k, 6);
+    }
     }
     if (WPH > 1) {
         __syncthreads();
@@ -2551,7 +2555,10 @@ void launch_ransac(const VoDev& d, int stage, hipStream_t s)
     for (int c = 0; c < 3; ++c) {
         const int k1 = cut[c];
         if (k1 <= k0) continue;
-        hipLaunchKernelGGL((k_ransac_hyp<1, 4>), dim3((k1 - k0 + 3) / 4, nb), dim3(256), 0, s, d, k0, k1, nhyp, stage);
+        static const int r2 = getenv("VO_RREPS") ? std::max(1, atoi(getenv("VO_RREPS"))) : VO_HYP_REPS;
+        const int reps = c == 0 ? 1 : (c == 1 ? std::max(1, r2 / 2) : r2);
+        const int blocks = ((k1 - k0 + 3) / 4 + reps - 1) / reps;
+        hipLaunchKernelGGL((k_ransac_hyp<1, 4>), dim3(blocks, nb), dim3(256), 0, s, d, k0, k1, nhyp, stage, reps);
         k0 = k1;
     }
 }
