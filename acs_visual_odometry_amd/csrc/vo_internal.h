@@ -18,7 +18,7 @@
 //   response    f32 W*H            optional dense R map (debug / parity only)
 //   cand        u64 192/tile x B   NMS survivors per 48x16 tile, key = Rbits<<32 | row<<16 | col
 //   tilerows    u8  16/tile  x B   survivors per tile row (select emits raster order from them)
-//   ckeys       u64 256/tile x B   compact survivors (only when they overflow select's LDS)
+//   ckeys       u64 192/tile x B   compact survivors (only when they overflow select's LDS)
 //   selbits     u64 4/tile   x B   selected-survivor bitmap (only when it overflows LDS)
 //   hist        u32 4096     x B   coarse histogram of candidate R (top-N boundary)
 //   kps         int2 N  x SLOTS    raster-ordered keypoints: ring slot f % VO_RING, carry, stage
@@ -136,7 +136,7 @@ struct VoDev {
     uint8_t* frame_in;
     uint8_t* blurred;     // x B
     float* response;
-    uint64_t* cand;       // x B: per stencil tile up to 256 keys in tile-local raster order
+    uint64_t* cand;       // x B: per stencil tile up to 192 keys in tile-local raster order
     uint8_t* tilerows;    // x B: per stencil tile the candidate count of each of its 16 rows
     uint64_t* ckeys;      // x B: select's compact keys when they exceed the LDS capacity
     uint64_t* selbits;    // x B: select's selected-key bitmap when it exceeds the LDS capacity
