@@ -966,7 +966,9 @@ __global__ void k_ext_missing(VoDev d, int slot)
 // ~7 KB of LDS per wave.
 // ---------------------------------------------------------------------------
 #define DS_KPW 32
+#ifndef DS_WAVES
 #define DS_WAVES 4
+#endif
 #define DS_KPB (DS_KPW * DS_WAVES)
 #define DS_I1W 44                 // s_I1 row bytes: 11 dwords, odd, so 32 rows hit 32 banks
 
@@ -1079,7 +1081,7 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
 
 // grid (N / DS_KPB, nb): frame z = blockIdx.y of the batch.  publish > 0: the last
 // workgroup of the launch tells the pose queue that frames < publish are extracted
-__global__ void __launch_bounds__(256) k_describe(VoDev d, int f0, int slot_override, unsigned publish)
+__global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int slot_override, unsigned publish)
 {
     __shared__ float s_I0[DS_WAVES][DS_KPW][VO_FREAK_NPOINTS];
     __shared__ uint8_t s_I1[DS_WAVES][DS_KPW][DS_I1W];
@@ -2536,7 +2538,7 @@ int select_lds_bytes(int W, int H, int* key_cap)
 void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned publish, hipStream_t s)
 {
     ensure_tables();
-    hipLaunchKernelGGL(k_describe, dim3((d.N + DS_KPB - 1) / DS_KPB, nb), dim3(256), 0, s, d, f0, slot_override,
+    hipLaunchKernelGGL(k_describe, dim3((d.N + DS_KPB - 1) / DS_KPB, nb), dim3(64 * DS_WAVES), 0, s, d, f0, slot_override,
                        publish);
 }
 void launch_match(const VoDev& d, int stage, hipStream_t s)
