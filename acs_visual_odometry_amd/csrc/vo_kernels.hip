@@ -1139,7 +1139,9 @@ __device__ __forceinline__ int ratio_accept(uint32_t m1, uint32_t m2, float rati
 
 // 32-bit prefix mode: the cur frame's prefixes are staged once per workgroup in LDS
 // (16 KB at N = 4096), and each wave scores MT_QPW queries per candidate read.
-#define MT_QPW 8
+#ifndef MT_QPW
+#define MT_QPW 16
+#endif
 #define MT_QPB (4 * MT_QPW)
 __host__ __device__ inline int match_blocks(int N, int match_bits)
 {
