@@ -1139,6 +1139,9 @@ __device__ __forceinline__ int ratio_accept(uint32_t m1, uint32_t m2, float rati
 
 // 32-bit prefix mode: the cur frame's prefixes are staged once per workgroup in LDS
 // (16 KB at N = 4096), and each wave scores MT_QPW queries per candidate read.
+#ifndef MT_UNROLL
+#define MT_UNROLL 4    // candidate loop unroll
+#endif
 #ifndef MT_QPW
 #define MT_QPW 16
 #endif
@@ -1216,7 +1219,7 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
                 m2[u] = 0xFFFFFFFFu;
             }
             __syncthreads();
-#pragma unroll 4
+#pragma unroll MT_UNROLL
             for (int j = lane; j < n2; j += 64) {
                 const uint32_t c = s_cand[j];
 #pragma unroll
