@@ -11,6 +11,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VO_LIB_PATH") or os.path.join(_HERE, "libvo_mi355x.so")   # override: diagnostic builds
 
 VO_OK = 0
+VO_ERR_IO = -6
 VO_ERR_DEGENERATE_E = -10
 STATUS = {0: "OK", 1: "FIRST", 2: "MISSING", 3: "FEW_MATCHES", 4: "FEW_INLIERS", 5: "DEGENERATE",
           6: "OVERFLOW", 7: "STALLED"}
@@ -19,7 +20,7 @@ STATUS = {0: "OK", 1: "FIRST", 2: "MISSING", 3: "FEW_MATCHES", 4: "FEW_INLIERS",
 EXPORTS = [
     "vo_config_default", "vo_create", "vo_destroy", "vo_strerror", "vo_abi_version", "vo_extract",
     "vo_response", "vo_match", "vo_ransac_F", "vo_pose", "vo_set_ground_truth", "vo_process_frame",
-    "vo_process_frames_device", "vo_device_alloc", "vo_device_free", "vo_device_upload", "vo_reset",
+    "vo_process_frames_device", "vo_process_frames_host", "vo_extract_frames_device", "vo_host_alloc", "vo_host_free", "vo_imread_gray", "vo_device_alloc", "vo_device_free", "vo_device_upload", "vo_reset",
     "vo_last_kernel_times", "vo_last_kernel_stats", "vo_enable_kernel_timing", "vo_unpack_descriptor",
 ]
 
@@ -63,6 +64,11 @@ def load():
     L.vo_set_ground_truth.argtypes = [P, P, I]
     L.vo_process_frame.argtypes = [P, P, C.c_size_t, P, C.POINTER(I), P]
     L.vo_process_frames_device.argtypes = [P, P, C.c_size_t, I, P, P, P]
+    L.vo_extract_frames_device.argtypes = [P, P, C.c_size_t, I, P, P, P]
+    L.vo_process_frames_host.argtypes = [P, P, C.c_size_t, I, P, P, P]
+    L.vo_imread_gray.argtypes = [C.c_char_p, P, C.c_size_t, C.POINTER(I), C.POINTER(I)]
+    L.vo_host_alloc.argtypes = [P, C.c_size_t, C.POINTER(P)]
+    L.vo_host_free.argtypes = [P, P]
     L.vo_device_alloc.argtypes = [P, C.c_size_t, C.POINTER(P)]
     L.vo_device_free.argtypes = [P, P]
     L.vo_device_upload.argtypes = [P, P, P, C.c_size_t]

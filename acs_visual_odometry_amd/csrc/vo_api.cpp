@@ -40,6 +40,15 @@ struct vo_ctx {
     int fidx = 0;                     // frames enqueued since vo_reset
     bool serial = false;              // VO_SERIAL=1: every kernel on one queue, no cross-queue
                                       // waits (for profilers that serialize dispatches: PMC passes)
+    bool event_wait = false;          // pose queue waits for extract batches on events instead of
+                                      // the stream-wait-value packet (VO_EVENT_WAIT=1, or after the
+                                      // runtime refused a wait-value packet)
+    // per-batch event pools of a chunk: [VO_EV_WAIT] extract done (event_wait mode),
+    // [VO_EV_COPY] H2D copy done, [VO_EV_STENCIL] stencil done (host streaming)
+    std::vector<hipEvent_t> ev_batch[3];
+    hipStream_t sc = nullptr;         // host streaming: H2D copies of frame batches
+    uint8_t* dring = nullptr;         // host streaming: VO_HRING device slots of B frames
+    uint8_t* hstage = nullptr;        // host streaming: pinned staging ring for pageable sources
     int gt_cap = 0;
     VoFrameOut* out_dev = nullptr;
     int out_cap = 0;
@@ -191,6 +200,7 @@ struct EvRec {
     int only;   // -1: all kernels
     std::vector<int>* launches;
     std::vector<std::pair<int, size_t>> spans;   // (kernel, index of its start event)
+    int err = VO_OK;                             // first failed event create / record
 };
 // An event pair costs ~6 us of queue time per bracketed launch (rocprofv3 kernel trace), so
 // the bench's live single-kernel timing samples one launch in VO_TIMING_STRIDE.
@@ -199,34 +209,51 @@ struct EvRec {
 size_t ev_mark(EvRec* ev, hipStream_t st)
 {
     if (ev->used >= ev->pool->size()) {
-        hipEvent_t e;
+        hipEvent_t e = nullptr;
         // device-scope release: a system-scope fence (the default) writes back and invalidates
         // the L2s at every record, which is most of an event's queue cost here
-        (void)hipEventCreateWithFlags(&e, hipEventReleaseToDevice);
+        if (hip_ok(hipEventCreateWithFlags(&e, hipEventReleaseToDevice)) != VO_OK) {
+            ev->err = VO_ERR_HIP;
+            return SIZE_MAX;
+        }
         ev->pool->push_back(e);
     }
-    (void)hipEventRecord((*ev->pool)[ev->used], st);
+    if (hip_ok(hipEventRecord((*ev->pool)[ev->used], st)) != VO_OK) {
+        ev->err = VO_ERR_HIP;
+        return SIZE_MAX;
+    }
     return ev->used++;
+}
+
+// event k of the per-batch pool (created on demand)
+int batch_event(vo_ctx* c, int pool, size_t k, hipEvent_t* e)
+{
+    std::vector<hipEvent_t>& v = c->ev_batch[pool];
+    while (v.size() <= k) {
+        hipEvent_t x = nullptr;
+        HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming | hipEventReleaseToDevice));
+        v.push_back(x);
+    }
+    *e = v[k];
+    return VO_OK;
 }
 
 template <typename F>
 void timed(vo_ctx* c, EvRec* ev, int k, hipStream_t st, F&& launch)
 {
     const int nth = c->klaunch[k]++;
-    const bool on = ev && (ev->only < 0 || (ev->only == k && nth % VO_TIMING_STRIDE == 0));
+    const bool on = ev && ev->err == VO_OK && (ev->only < 0 || (ev->only == k && nth % VO_TIMING_STRIDE == 0));
     size_t b = on ? ev_mark(ev, st) : 0;
     launch();
-    if (on) {
-        ev_mark(ev, st);
-        ev->spans.emplace_back(k, b);
-    }
+    if (on && b != SIZE_MAX && ev_mark(ev, st) != SIZE_MAX) ev->spans.emplace_back(k, b);
 }
 
 // extract of nb frames f0.. (device images img0 + z * frame_bytes) on stream q; publish:
 // the pose queue may wait for frames < f0 + nb
 // eq: extract queue index (its scratch copy and counters)
-void enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, int nb, bool publish,
-                     hipStream_t q, EvRec* ev, int eq)
+// ev_stencil (optional): recorded on q once the stencil (the only reader of the images) is enqueued
+int enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, int nb, bool publish,
+                    hipStream_t q, EvRec* ev, int eq, hipEvent_t ev_stencil = nullptr)
 {
     VoDev d = c->d;
     const size_t B = (size_t)c->B, np = (size_t)d.W * d.H;
@@ -238,8 +265,56 @@ void enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0,
     d.selbits += ((size_t)d.cand_cap / 64 + 1) * B * eq;
     d.hist += (size_t)VO_HIST_BINS * B * eq;
     timed(c, ev, 0, q, [&] { vo::launch_stencil(d, img0, frame_bytes, nb, 0, q); });
+    if (ev_stencil) HIPCHK(hipEventRecord(ev_stencil, q));
     timed(c, ev, 1, q, [&] { vo::launch_select(d, f0, nb, -1, q); });
     timed(c, ev, 2, q, [&] { vo::launch_describe(d, f0, nb, -1, publish ? (unsigned)(f0 + nb) : 0u, q); });
+    return VO_OK;
+}
+
+// Host-frame streaming (vo_process_frames_host): batch j of a chunk is copied from host memory
+// into device ring slot j % VO_HRING on the copy queue `sc` while earlier batches are extracted
+// and posed.  The copy of batch j waits for the stencil of batch j - VO_HRING (the last reader
+// of that slot); the stencil of batch j waits for its copy.  Pinned sources are DMA'd directly;
+// pageable ones go through the pinned staging ring (the host waits for the copy that last
+// used a staging slot before refilling it).
+struct HostSrc {
+    const uint8_t* frames;    // frame f of the chunk at frames + f * frame_bytes (dense W x H rows)
+    size_t frame_bytes;
+    bool pinned;              // DMA from the source; else staged through c->hstage
+};
+
+int enqueue_h2d(vo_ctx* c, const HostSrc& hs, int f0, int nb, int j, uint8_t** dimg)
+{
+    const size_t np = (size_t)c->cfg.width * c->cfg.height, slot = (size_t)(j % VO_HRING);
+    uint8_t* dst = c->dring + slot * (size_t)c->B * np;
+    hipEvent_t e_cp, e_st;
+    int rc = batch_event(c, VO_EV_COPY, (size_t)j, &e_cp);
+    if (rc) return rc;
+    if (j >= VO_HRING) {
+        rc = batch_event(c, VO_EV_STENCIL, (size_t)(j - VO_HRING), &e_st);
+        if (rc) return rc;
+        HIPCHK(hipStreamWaitEvent(c->sc, e_st, 0));
+    }
+    const uint8_t* src = hs.frames + (size_t)f0 * hs.frame_bytes;
+    if (!hs.pinned) {
+        // refill staging slot `slot` once its previous copy (batch j - VO_HRING) has run
+        if (j >= VO_HRING) {
+            hipEvent_t e_prev;
+            rc = batch_event(c, VO_EV_COPY, (size_t)(j - VO_HRING), &e_prev);
+            if (rc) return rc;
+            HIPCHK(hipEventSynchronize(e_prev));
+        }
+        uint8_t* stg = c->hstage + slot * (size_t)c->B * np;
+        for (int z = 0; z < nb; ++z) std::memcpy(stg + (size_t)z * np, src + (size_t)z * hs.frame_bytes, np);
+        HIPCHK(hipMemcpyAsync(dst, stg, np * nb, hipMemcpyHostToDevice, c->sc));
+    } else if (hs.frame_bytes == np) {
+        HIPCHK(hipMemcpyAsync(dst, src, np * nb, hipMemcpyHostToDevice, c->sc));
+    } else {
+        HIPCHK(hipMemcpy2DAsync(dst, np, src, hs.frame_bytes, np, nb, hipMemcpyHostToDevice, c->sc));
+    }
+    HIPCHK(hipEventRecord(e_cp, c->sc));
+    *dimg = dst;
+    return VO_OK;
 }
 
 // one pose pass over the window [lo, lo + B) of the frames enqueued so far
@@ -276,12 +351,13 @@ std::vector<int> batch_schedule(int nf, int B)
 // frames [c->fidx, c->fidx + nf) (nf <= VO_CHUNK): set the end, enqueue the extract
 // batches (img != null: device images; null: one missing image) and one pass per window,
 // then repeat passes until every frame is committed (a pass commits at least its first frame)
+// hs (optional): host frames streamed through the device ring (img0 unused)
 int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFrameOut* out, int out_base, EvRec* ev,
-              bool host_frame)
+              bool host_frame, const HostSrc* hs = nullptr)
 {
     const int base = c->fidx, end = base + nf, B = c->B;
     hipStream_t s = c->s;
-    const bool multi = !(c->serial || host_frame || !img0);   // extract on its own queues
+    const bool multi = hs || !(c->serial || host_frame || !img0);   // extract on its own queues
     static const int nq = getenv("VO_EXTQ") ? std::max(1, std::min(VO_EXT_QUEUES, atoi(getenv("VO_EXTQ")))) : VO_EXT_QUEUES;
     if (multi && c->reset_pending) {
         for (hipStream_t q : c->se) HIPCHK(hipStreamWaitEvent(q, c->ev_reset, 0));
@@ -289,14 +365,35 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     }
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&c->d.st->end, end, 1, s));
     const std::vector<int> sched = batch_schedule(nf, B);
-    if (!img0) {
+    if (!img0 && !hs) {
         vo::launch_ext_missing(c->d, base % VO_RING, s);
     } else {
         int f0 = 0, j = 0;
         for (int cnt : sched) {
             const int eq = multi ? j % nq : 0;
-            enqueue_extract(c, img0 + (size_t)f0 * frame_bytes, frame_bytes, base + f0, cnt, multi,
-                            multi ? c->se[eq] : s, ev, eq);
+            hipStream_t q = multi ? c->se[eq] : s;
+            if (hs) {
+                uint8_t* dimg = nullptr;
+                hipEvent_t e_cp, e_st;
+                int rc = enqueue_h2d(c, *hs, f0, cnt, j, &dimg);
+                if (rc == VO_OK) rc = batch_event(c, VO_EV_COPY, (size_t)j, &e_cp);
+                if (rc == VO_OK) rc = batch_event(c, VO_EV_STENCIL, (size_t)j, &e_st);
+                if (rc) return rc;
+                HIPCHK(hipStreamWaitEvent(q, e_cp, 0));
+                rc = enqueue_extract(c, dimg, (size_t)c->cfg.width * c->cfg.height, base + f0, cnt, multi, q, ev, eq,
+                                     e_st);
+                if (rc) return rc;
+            } else {
+                int rc = enqueue_extract(c, img0 + (size_t)f0 * frame_bytes, frame_bytes, base + f0, cnt, multi, q,
+                                         ev, eq);
+                if (rc) return rc;
+            }
+            if (multi && c->event_wait) {
+                hipEvent_t e;
+                int rc = batch_event(c, VO_EV_WAIT, (size_t)j, &e);
+                if (rc) return rc;
+                HIPCHK(hipEventRecord(e, c->se[eq]));
+            }
             f0 += cnt;
             ++j;
         }
@@ -308,14 +405,39 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         int f1 = 0, k = 0;
         for (int cnt : sched) {
             f1 += cnt;
-            if (multi)
-                (void)hipStreamWaitValue32(s, c->d.ctr + VO_SYNC_EXT + 16 * (k % nq), (uint32_t)(base + f1),
-                                           hipStreamWaitValueGte, 0xFFFFFFFFu);
+            if (multi) {
+                const int eq = k % nq;
+                hipEvent_t e;
+                if (!c->event_wait) {
+                    const hipError_t we = hipStreamWaitValue32(s, c->d.ctr + VO_SYNC_EXT + 16 * eq,
+                                                               (uint32_t)(base + f1), hipStreamWaitValueGte,
+                                                               0xFFFFFFFFu);
+                    if (we != hipSuccess) {
+                        // the packet was refused: events from now on.  This chunk's batches are
+                        // all enqueued, so the fallback event (recorded now) covers every batch
+                        // of queue eq -- later passes of the chunk wait for them all (correct,
+                        // less overlap); later chunks record one event per batch
+                        fprintf(stderr, "[vo_mi355x] hipStreamWaitValue32 failed (%s): event waits\n",
+                                hipGetErrorString(we));
+                        (void)hipGetLastError();
+                        c->event_wait = true;
+                        int rc = batch_event(c, VO_EV_WAIT, 0, &e);
+                        if (rc) return rc;
+                        HIPCHK(hipEventRecord(e, c->se[eq]));
+                        HIPCHK(hipStreamWaitEvent(s, e, 0));
+                    }
+                } else {
+                    int rc = batch_event(c, VO_EV_WAIT, (size_t)k, &e);
+                    if (rc) return rc;
+                    HIPCHK(hipStreamWaitEvent(s, e, 0));
+                }
+            }
             enqueue_pass(c, out, out_base, ev, cnt);
             ++k;
         }
     }
-    for (;;) {
+    // every pass commits at least its first frame, so nf re-pass rounds bound the loop
+    for (int round = 0, prev_lo = base;; ++round) {
         HIPCHK(hipGetLastError());
         // the chunk's output rows and the commit point in one round trip
         HIPCHK(hipMemcpyAsync(c->out_host + (base - out_base), out + (base - out_base), sizeof(VoFrameOut) * nf,
@@ -324,11 +446,16 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         HIPCHK(hipStreamSynchronize(s));
         const int lo = *c->lo_host;
         if (lo >= end) break;
-        if (lo < base) return VO_ERR_STATE;
+        if (lo < base || lo > end || round > nf || (round > 0 && lo <= prev_lo)) {
+            fprintf(stderr, "[vo_mi355x] pose passes made no progress (committed %d of [%d, %d), round %d)\n", lo,
+                    base, end, round);
+            return VO_ERR_STATE;
+        }
+        prev_lo = lo;
         // frames after skipped ones: their windows restart at lo (extracts are complete)
         for (int k = 0; k < (end - lo + B - 1) / B; ++k) enqueue_pass(c, out, out_base, ev, B);
     }
-    return VO_OK;
+    return ev && ev->err ? ev->err : VO_OK;
 }
 
 int ensure_out(vo_ctx* c, int n)
@@ -350,6 +477,7 @@ int finish_timing(vo_ctx* c, EvRec* ev)
     c->kcount.assign(nk, 0);
     if (!ev) return VO_OK;
     SYNC_ALL(c);
+    if (ev->err) return ev->err;
     for (const auto& sp : ev->spans) {
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, c->ev_pool[sp.second], c->ev_pool[sp.second + 1]);
@@ -374,6 +502,7 @@ const char* vo_strerror(int code)
     case VO_ERR_NO_DEVICE: return "no HIP device";
     case VO_ERR_CAPACITY: return "capacity exceeded";
     case VO_ERR_STATE: return "invalid state";
+    case VO_ERR_IO: return "image could not be read";
     case VO_ERR_DEGENERATE_E: return "Degenerate essential matrix";
     default: return "unknown error";
     }
@@ -445,6 +574,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     int rc = VO_OK;
     auto bail = [&](int r) { vo_destroy(c); return r; };
     c->serial = getenv("VO_SERIAL") && atoi(getenv("VO_SERIAL")) != 0;
+    c->event_wait = getenv("VO_EVENT_WAIT") && atoi(getenv("VO_EVENT_WAIT")) != 0;
     if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
     for (hipStream_t& q : c->se)
         if (hip_ok(hipStreamCreateWithFlags(&q, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
@@ -517,6 +647,11 @@ void vo_destroy(vo_ctx* c)
     if (c->stage_host) (void)hipHostFree(c->stage_host);
     if (c->lo_host) (void)hipHostFree(c->lo_host);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    for (auto& v : c->ev_batch)
+        for (hipEvent_t e : v) (void)hipEventDestroy(e);
+    if (c->dring) (void)hipFree(c->dring);
+    if (c->hstage) (void)hipHostFree(c->hstage);
+    if (c->sc) (void)hipStreamDestroy(c->sc);
     if (c->ev_reset) (void)hipEventDestroy(c->ev_reset);
     for (hipStream_t q : c->se)
         if (q) (void)hipStreamDestroy(q);
@@ -721,26 +856,12 @@ int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_
     return o.status == VO_STATUS_DEGENERATE ? VO_ERR_DEGENERATE_E : VO_OK;
 }
 
-int vo_process_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_bytes, int nframes, double* poses_out,
-                             int* status_out, int32_t* info_out)
+}  // extern "C"
+
+namespace {
+// the host-side results of the last nframes frames of a batched call
+void copy_results(vo_ctx* c, int nframes, double* poses_out, int* status_out, int32_t* info_out)
 {
-    if (!c || !d_frames || nframes < 0) return VO_ERR_ARG;
-    if (frame_bytes < (size_t)c->cfg.width * c->cfg.height) return VO_ERR_ARG;
-    HIPCHK(hipSetDevice(c->cfg.device));
-    int rc = ensure_out(c, std::max(nframes, 1));
-    if (rc) return rc;
-    c->klaunch.assign(vo::kernel_count(), 0);
-    EvRec rec{&c->ev_pool, 0, c->timing >= 100 ? c->timing - 100 : -1, &c->klaunch, {}};
-    EvRec* evp = c->timing ? &rec : nullptr;
-    const int base = c->fidx;
-    for (int f0 = 0; f0 < nframes; f0 += VO_CHUNK) {
-        const int nf = std::min(VO_CHUNK, nframes - f0);
-        rc = run_chunk(c, d_frames + (size_t)f0 * frame_bytes, frame_bytes, nf, c->out_dev, base, evp, false);
-        if (rc) return rc;
-    }
-    rc = finish_timing(c, evp);
-    if (rc) return rc;
-    c->last_frames = nframes;
     for (int f = 0; f < nframes; ++f) {
         const VoFrameOut& o = c->out_host[f];
         if (poses_out) std::memcpy(poses_out + 12 * (size_t)f, o.pose, sizeof(o.pose));
@@ -751,6 +872,158 @@ int vo_process_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
             p[4] = o.n_eval; p[5] = o.fitted; p[6] = o.frame; p[7] = 0;
         }
     }
+}
+
+// frames of one batched call: device frames (dev) or host frames (host, streamed)
+int run_frames(vo_ctx* c, const uint8_t* dev, const uint8_t* host, bool pinned, size_t frame_bytes, int nframes,
+               double* poses_out, int* status_out, int32_t* info_out)
+{
+    int rc = ensure_out(c, std::max(nframes, 1));
+    if (rc) return rc;
+    c->klaunch.assign(vo::kernel_count(), 0);
+    EvRec rec{&c->ev_pool, 0, c->timing >= 100 ? c->timing - 100 : -1, &c->klaunch, {}};
+    EvRec* evp = c->timing ? &rec : nullptr;
+    const int base = c->fidx;
+    for (int f0 = 0; f0 < nframes; f0 += VO_CHUNK) {
+        const int nf = std::min(VO_CHUNK, nframes - f0);
+        if (host) {
+            const HostSrc hs{host + (size_t)f0 * frame_bytes, frame_bytes, pinned};
+            rc = run_chunk(c, nullptr, frame_bytes, nf, c->out_dev, base, evp, false, &hs);
+        } else {
+            rc = run_chunk(c, dev + (size_t)f0 * frame_bytes, frame_bytes, nf, c->out_dev, base, evp, false);
+        }
+        if (rc) return rc;
+    }
+    rc = finish_timing(c, evp);
+    if (rc) return rc;
+    c->last_frames = nframes;
+    copy_results(c, nframes, poses_out, status_out, info_out);
+    return VO_OK;
+}
+
+// host streaming resources, allocated on first use
+int ensure_streaming(vo_ctx* c, bool staging)
+{
+    const size_t ring = (size_t)VO_HRING * c->B * c->cfg.width * c->cfg.height;
+    if (!c->sc) HIPCHK(hipStreamCreateWithFlags(&c->sc, hipStreamNonBlocking));
+    if (!c->dring) HIPCHK(hipMalloc((void**)&c->dring, ring));
+    if (staging && !c->hstage) HIPCHK(hipHostMalloc((void**)&c->hstage, ring, hipHostMallocDefault));
+    return VO_OK;
+}
+
+bool is_pinned(const void* p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+}  // namespace
+
+extern "C" {
+
+int vo_process_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_bytes, int nframes, double* poses_out,
+                             int* status_out, int32_t* info_out)
+{
+    if (!c || !d_frames || nframes < 0) return VO_ERR_ARG;
+    if (frame_bytes < (size_t)c->cfg.width * c->cfg.height) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    return run_frames(c, d_frames, nullptr, false, frame_bytes, nframes, poses_out, status_out, info_out);
+}
+
+int vo_process_frames_host(vo_ctx* c, const uint8_t* frames, size_t frame_bytes, int nframes, double* poses_out,
+                           int* status_out, int32_t* info_out)
+{
+    if (!c || nframes < 0 || (nframes > 0 && !frames)) return VO_ERR_ARG;
+    const size_t np = (size_t)c->cfg.width * c->cfg.height;
+    if (frame_bytes < np) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    if (nframes == 0) return VO_OK;
+    bool pinned = is_pinned(frames), registered = false;
+    // VO_HOST_STAGING=1: never register pageable sources (tests the staging ring)
+    const bool staging_only = getenv("VO_HOST_STAGING") && atoi(getenv("VO_HOST_STAGING")) != 0;
+    if (!pinned && !staging_only) {
+        // pageable: pin the call's frames for DMA (one registration per call), else stage them
+        void* p = const_cast<uint8_t*>(frames);
+        if (hipHostRegister(p, (size_t)(nframes - 1) * frame_bytes + np, hipHostRegisterDefault) == hipSuccess) {
+            pinned = registered = true;
+        } else {
+            (void)hipGetLastError();
+        }
+    }
+    int rc = ensure_streaming(c, !pinned);
+    if (rc == VO_OK) rc = run_frames(c, nullptr, frames, pinned, frame_bytes, nframes, poses_out, status_out, info_out);
+    if (registered) {
+        if (rc == VO_OK) rc = sync_all(c);
+        if (c->sc) (void)hipStreamSynchronize(c->sc);
+        if (hipHostUnregister(const_cast<uint8_t*>(frames)) != hipSuccess && rc == VO_OK) rc = VO_ERR_HIP;
+    }
+    return rc;
+}
+
+int vo_extract_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_bytes, int nframes, vo_kp* kps,
+                             uint64_t* desc, int32_t* n_kps)
+{
+    if (!c || !d_frames || nframes < 0) return VO_ERR_ARG;
+    if (frame_bytes < (size_t)c->cfg.width * c->cfg.height) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    // the extract batches run on the pose queue, after the reset kernel (the ring is reused)
+    int rc = vo_reset(c);
+    if (rc) return rc;
+    c->reset_pending = false;
+    c->klaunch.assign(vo::kernel_count(), 0);
+    EvRec rec{&c->ev_pool, 0, c->timing >= 100 ? c->timing - 100 : -1, &c->klaunch, {}};
+    EvRec* evp = c->timing ? &rec : nullptr;
+    const size_t N = (size_t)c->cfg.max_kpts;
+    for (int f0 = 0; f0 < nframes; f0 += VO_RING) {
+        const int nf = std::min(VO_RING, nframes - f0);
+        int off = 0;
+        for (int cnt : batch_schedule(nf, c->B)) {
+            rc = enqueue_extract(c, d_frames + (size_t)(f0 + off) * frame_bytes, frame_bytes, off, cnt, false, c->s,
+                                 evp, 0);
+            if (rc) return rc;
+            off += cnt;
+        }
+        HIPCHK(hipGetLastError());
+        if (n_kps || kps || desc) {
+            HIPCHK(hipStreamSynchronize(c->s));
+            std::vector<int32_t> nk(nf), stt(nf);
+            HIPCHK(hipMemcpy(nk.data(), c->d.ext->n_kps, sizeof(int32_t) * nf, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(stt.data(), c->d.ext->status, sizeof(int32_t) * nf, hipMemcpyDeviceToHost));
+            for (int z = 0; z < nf; ++z) {
+                const size_t f = (size_t)(f0 + z);
+                if (stt[z] != VO_STATUS_OK) return VO_ERR_CAPACITY;      // top-N boundary overflow
+                if (n_kps) n_kps[f] = nk[z];
+                if (kps && nk[z])
+                    HIPCHK(hipMemcpyAsync(kps + f * N, c->d.kps + (size_t)z * N, sizeof(vo_kp) * nk[z],
+                                          hipMemcpyDeviceToHost, c->s));
+                if (desc && nk[z])
+                    HIPCHK(hipMemcpyAsync(desc + f * N * 8, c->d.desc + (size_t)z * N * 8, sizeof(uint64_t) * 8 * nk[z],
+                                          hipMemcpyDeviceToHost, c->s));
+            }
+        }
+    }
+    HIPCHK(hipStreamSynchronize(c->s));
+    rc = finish_timing(c, evp);
+    if (rc) return rc;
+    c->last_frames = nframes;
+    return vo_reset(c);              // the ring no longer holds the trajectory's descriptors
+}
+
+int vo_host_alloc(vo_ctx* c, size_t bytes, void** hptr)
+{
+    if (!c || !hptr) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipHostMalloc(hptr, std::max<size_t>(bytes, 1), hipHostMallocDefault));
+    return VO_OK;
+}
+
+int vo_host_free(vo_ctx* c, void* hptr)
+{
+    if (!c) return VO_ERR_ARG;
+    if (hptr) HIPCHK(hipHostFree(hptr));
     return VO_OK;
 }
 

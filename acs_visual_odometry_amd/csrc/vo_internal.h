@@ -60,6 +60,11 @@
 #define VO_SYNC_EXT 32         // + 16 * queue: frames extracted since vo_reset by that queue
                                // (its batches complete in order; the pose queue waits on it)
 #define VO_CTR_WORDS 64
+// host-frame streaming (vo_process_frames_host): device ring of VO_HRING slots of B frames
+#define VO_HRING 3
+#define VO_EV_WAIT 0           // per-batch event pools of a chunk (vo_api.cpp)
+#define VO_EV_COPY 1
+#define VO_EV_STENCIL 2
 #define VO_MAX_HYP 2000
 #define VO_HYP_CHUNK0 100     // RANSAC launch chunks (vo_kernels.hip launch_ransac); 100 = the clamp
 #define VO_HYP_CHUNK1 512

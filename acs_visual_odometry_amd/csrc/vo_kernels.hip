@@ -1146,9 +1146,10 @@ __device__ __forceinline__ int ratio_accept(uint32_t m1, uint32_t m2, float rati
 #define MT_QPW 16
 #endif
 #define MT_QPB (4 * MT_QPW)
+#define MT512_QPB 256                 // 512-test matcher: queries per workgroup (one per thread)
 __host__ __device__ inline int match_blocks(int N, int match_bits)
 {
-    return match_bits == 32 ? (N + MT_QPB - 1) / MT_QPB : (N + 3) / 4;
+    return match_bits == 32 ? (N + MT_QPB - 1) / MT_QPB : (N + MT512_QPB - 1) / MT512_QPB;
 }
 
 // Window of a pose pass: frames [st->lo, st->lo + n), n = min(B, st->end - st->lo); a stage
@@ -1165,12 +1166,16 @@ __device__ __forceinline__ uint64_t frame_seed_of(const VoDev& d, int f)
     return mix64(d.seed + 0x632BE59BD9B4E019ULL * (uint64_t)(f + 1));
 }
 
-// grid (match_blocks, B): frame wf = blockIdx.y of the window.  Speculation: the previous
-// frame of window frame wf > 0 is frame f - 1 (k_finalize re-runs f when that was skipped).
-__global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
+// Header of a window frame's match: slots and status (speculation: the previous frame of
+// window frame wf > 0 is frame f - 1; k_finalize re-runs f when that was skipped).  Block 0
+// initialises the frame's VoWork.  Returns false if the frame has nothing to match.
+struct MatchFrame {
+    VoWork* w;
+    int f, cur, prev, n1, n2;
+    int32_t* match_j;
+};
+__device__ __forceinline__ bool match_header(const VoDev& d, int stage, int wf, MatchFrame& m)
 {
-    const int wf = blockIdx.y;
-    if (wf >= win_count(d, stage)) return;
     VoWork* w = d.work + wf;
     int f, cur, prev, status = VO_STATUS_OK;
     if (stage) {
@@ -1191,72 +1196,22 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
         if (!stage) w->frame_seed = frame_seed_of(d, f);
         if (status != VO_STATUS_OK) { w->status = status; w->M = 0; w->scored = 0; }
     }
-    if (status != VO_STATUS_OK) return;
-    __shared__ unsigned s_last;
-    __shared__ int s_wsum[4];
-    __shared__ uint32_t s_cand[4096];
-    const int N = d.N;
-    const int n1 = d.ext->n_kps[prev], n2 = d.ext->n_kps[cur];
-    int32_t* match_j = d.match_j + (size_t)wf * N;
-    const int lane = threadIdx.x & 63;
-    if (d.match_bits == 32) {
-        if (blockIdx.x * MT_QPB < n1) {
-            const uint32_t* cand = d.pre + (size_t)cur * N;
-            for (int j0 = threadIdx.x; j0 < n2; j0 += 4 * 256) {
-                uint32_t v[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) v[u] = j0 + u * 256 < n2 ? cand[j0 + u * 256] : 0u;
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (j0 + u * 256 < n2) s_cand[j0 + u * 256] = v[u];
-            }
-            const int q0 = blockIdx.x * MT_QPB + (threadIdx.x >> 6) * MT_QPW;
-            uint32_t qv[MT_QPW], m1[MT_QPW], m2[MT_QPW];
-#pragma unroll
-            for (int u = 0; u < MT_QPW; ++u) {
-                qv[u] = q0 + u < n1 ? d.pre[(size_t)prev * N + q0 + u] : 0u;
-                m1[u] = 0xFFFFFFFFu;
-                m2[u] = 0xFFFFFFFFu;
-            }
-            __syncthreads();
-#pragma unroll MT_UNROLL
-            for (int j = lane; j < n2; j += 64) {
-                const uint32_t c = s_cand[j];
-#pragma unroll
-                for (int u = 0; u < MT_QPW; ++u)
-                    top2_insert(((uint32_t)__popc(qv[u] ^ c) << 16) | (uint32_t)j, m1[u], m2[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < MT_QPW; ++u) {
-                top2_wave(m1[u], m2[u]);
-                if (lane == 0 && q0 + u < n1) st_sc1(match_j + q0 + u, ratio_accept(m1[u], m2[u], d.ratio));
-            }
-        }
-    } else {
-        const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
-        if (q < n1) {
-            uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
-            const uint64_t* qd = d.desc + ((size_t)prev * N + q) * 8;
-            uint64_t qw[8];
-#pragma unroll
-            for (int w = 0; w < 8; ++w) qw[w] = qd[w];
-            const uint64_t* cd = d.desc + (size_t)cur * N * 8;
-            for (int j = lane; j < n2; j += 64) {
-                int dist = 0;
-#pragma unroll
-                for (int w = 0; w < 8; ++w) dist += __popcll(qw[w] ^ cd[(size_t)j * 8 + w]);
-                top2_insert(((uint32_t)dist << 16) | (uint32_t)j, m1, m2);
-            }
-            top2_wave(m1, m2);
-            if (lane == 0) st_sc1(match_j + q, ratio_accept(m1, m2, d.ratio));
-        }
-    }
-    if (blockIdx.x == 0) VO_STAMP(d, 1993, 1);
-    if (!arrive_last(&w->ctr[0], gridDim.x, &s_last)) return;
-    // ---- last workgroup: ordered compaction, thread t owns queries [t*per, (t+1)*per) ----
+    m.w = w; m.f = f; m.cur = cur; m.prev = prev;
+    m.n1 = d.ext->n_kps[prev];
+    m.n2 = d.ext->n_kps[cur];
+    m.match_j = d.match_j + (size_t)wf * d.N;
+    return status == VO_STATUS_OK;
+}
+
+// The frame's last workgroup (256 threads): ordered compaction of the accepted queries into
+// (prev, cur) pairs and f64 points, thread t owning queries [t*per, (t+1)*per); M, scored and
+// the < 8 matches status (VisualOdometry.cpp:108-123).
+__device__ void match_compact(const VoDev& d, int wf, const MatchFrame& m, int* s_wsum)
+{
+    const int N = d.N, n1 = m.n1, lane = threadIdx.x & 63;
     const int tid = threadIdx.x, wave = tid >> 6;
-    const int2* kp1 = d.kps + (size_t)prev * N;
-    const int2* kp2 = d.kps + (size_t)cur * N;
+    const int2* kp1 = d.kps + (size_t)m.prev * N;
+    const int2* kp2 = d.kps + (size_t)m.cur * N;
     int2* match_pairs = d.match_pairs + (size_t)wf * N;
     double* pts = d.pts + (size_t)wf * 4 * N;
     const int per = (n1 + 255) / 256;            // <= 16 (N <= 4096)
@@ -1268,7 +1223,7 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
         int i = q0 + u;
-        js[u] = (u < per && i < n1) ? ld_sc1(match_j + i) : -1;
+        js[u] = (u < per && i < n1) ? ld_sc1(m.match_j + i) : -1;
         cnt += js[u] >= 0;
     }
     // all keypoint gathers in flight before the scan (no load-use chain per match)
@@ -1301,6 +1256,7 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
         }
     }
     if (tid == 0) {
+        VoWork* w = m.w;
         int M = ((s_wsum[0] + s_wsum[1]) + s_wsum[2]) + s_wsum[3];
         w->M = M;
         w->scored = (M / d.T) * d.T;
@@ -1308,6 +1264,139 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
         w->ctr[0] = 0u;
     }
     VO_STAMP(d, 1993, 3);
+}
+
+// 32-test matcher (the reference's quirk 1, feature_matching_parallel.cpp:39-47).
+// grid (match_blocks, B): frame wf = blockIdx.y of the window.
+__global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
+{
+    const int wf = blockIdx.y;
+    if (wf >= win_count(d, stage)) return;
+    MatchFrame m;
+    if (!match_header(d, stage, wf, m)) return;
+    __shared__ unsigned s_last;
+    __shared__ int s_wsum[4];
+    __shared__ uint32_t s_cand[4096];
+    const int N = d.N, n1 = m.n1, n2 = m.n2;
+    const int lane = threadIdx.x & 63;
+    if (blockIdx.x * MT_QPB < n1) {
+        const uint32_t* cand = d.pre + (size_t)m.cur * N;
+        for (int j0 = threadIdx.x; j0 < n2; j0 += 4 * 256) {
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = j0 + u * 256 < n2 ? cand[j0 + u * 256] : 0u;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (j0 + u * 256 < n2) s_cand[j0 + u * 256] = v[u];
+        }
+        const int q0 = blockIdx.x * MT_QPB + (threadIdx.x >> 6) * MT_QPW;
+        uint32_t qv[MT_QPW], m1[MT_QPW], m2[MT_QPW];
+#pragma unroll
+        for (int u = 0; u < MT_QPW; ++u) {
+            qv[u] = q0 + u < n1 ? d.pre[(size_t)m.prev * N + q0 + u] : 0u;
+            m1[u] = 0xFFFFFFFFu;
+            m2[u] = 0xFFFFFFFFu;
+        }
+        __syncthreads();
+#pragma unroll MT_UNROLL
+        for (int j = lane; j < n2; j += 64) {
+            const uint32_t c = s_cand[j];
+#pragma unroll
+            for (int u = 0; u < MT_QPW; ++u)
+                top2_insert(((uint32_t)__popc(qv[u] ^ c) << 16) | (uint32_t)j, m1[u], m2[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < MT_QPW; ++u) {
+            top2_wave(m1[u], m2[u]);
+            if (lane == 0 && q0 + u < n1) st_sc1(m.match_j + q0 + u, ratio_accept(m1[u], m2[u], d.ratio));
+        }
+    }
+    if (blockIdx.x == 0) VO_STAMP(d, 1993, 1);
+    if (!arrive_last(&m.w->ctr[0], gridDim.x, &s_last)) return;
+    match_compact(d, wf, m, s_wsum);
+}
+
+// Full-length 512-test matcher (matching_serial.cpp:24-40,58; config 4's LDS descriptor-tile
+// stress).  Lane = query: each thread holds its query's 512 bits in 16 VGPRs and keeps its own
+// top-2 keys, so no cross-lane merge is needed.  The cur frame's descriptors stream through an
+// LDS tile of MT512_TILE candidates (64 KB: 4096 x 64 B does not fit the CU's 160 KB); every
+// wave walks the tile in candidate order with wave-uniform (broadcast) ds_read_b128s, so the
+// top-2 update sees j ascending and the min key (dist << 16 | j) is the first-index minimum.
+#define MT512_TILE 1024
+// popcount-accumulate as one v_bcnt_u32_b32 (left to itself the compiler splits the chain into
+// bcnt-with-0 plus v_add3: 43 instead of 35 VALU per (query, candidate) pair)
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc)
+{
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
+// Hamming distance of a query (16 words) to one staged candidate (four 16-byte LDS words)
+__device__ __forceinline__ uint32_t dist512(const uint32_t (&qw)[16], const uint4* c)
+{
+    const uint4 c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
+    uint32_t dist = __popc(qw[0] ^ c0.x);
+    dist = bcnt_acc(qw[1] ^ c0.y, dist);
+    dist = bcnt_acc(qw[2] ^ c0.z, dist);
+    dist = bcnt_acc(qw[3] ^ c0.w, dist);
+    dist = bcnt_acc(qw[4] ^ c1.x, dist);
+    dist = bcnt_acc(qw[5] ^ c1.y, dist);
+    dist = bcnt_acc(qw[6] ^ c1.z, dist);
+    dist = bcnt_acc(qw[7] ^ c1.w, dist);
+    dist = bcnt_acc(qw[8] ^ c2.x, dist);
+    dist = bcnt_acc(qw[9] ^ c2.y, dist);
+    dist = bcnt_acc(qw[10] ^ c2.z, dist);
+    dist = bcnt_acc(qw[11] ^ c2.w, dist);
+    dist = bcnt_acc(qw[12] ^ c3.x, dist);
+    dist = bcnt_acc(qw[13] ^ c3.y, dist);
+    dist = bcnt_acc(qw[14] ^ c3.z, dist);
+    return bcnt_acc(qw[15] ^ c3.w, dist);
+}
+
+__global__ void __launch_bounds__(256) k_match512(VoDev d, int stage)
+{
+    const int wf = blockIdx.y;
+    if (wf >= win_count(d, stage)) return;
+    MatchFrame m;
+    if (!match_header(d, stage, wf, m)) return;
+    __shared__ unsigned s_last;
+    __shared__ int s_wsum[4];
+    extern __shared__ uint4 s_tile[];        // MT512_TILE x 64 B
+    const int N = d.N, n1 = m.n1, n2 = m.n2;
+    const int q = blockIdx.x * MT512_QPB + threadIdx.x;
+    const bool wave_live = __builtin_amdgcn_readfirstlane(blockIdx.x * MT512_QPB + (threadIdx.x & ~63)) < n1;
+    if (blockIdx.x * MT512_QPB < n1) {
+        uint32_t qw[16];
+        {
+            const uint4* qd = reinterpret_cast<const uint4*>(d.desc + ((size_t)m.prev * N + (q < n1 ? q : 0)) * 8);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const uint4 v = qd[g];
+                qw[4 * g] = v.x; qw[4 * g + 1] = v.y; qw[4 * g + 2] = v.z; qw[4 * g + 3] = v.w;
+            }
+        }
+        uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
+        const uint4* cd = reinterpret_cast<const uint4*>(d.desc + (size_t)m.cur * N * 8);
+        for (int t0 = 0; t0 < n2; t0 += MT512_TILE) {
+            const int nt = min(MT512_TILE, n2 - t0);
+            __syncthreads();                                  // the previous tile is consumed
+            for (int c = threadIdx.x; c < nt * 4; c += 256) s_tile[c] = cd[(size_t)t0 * 4 + c];
+            __syncthreads();
+            if (wave_live) {
+                // two candidates per iteration: their LDS reads are in flight together
+                int j = 0;
+                for (; j + 1 < nt; j += 2) {
+                    const uint32_t da = dist512(qw, s_tile + 4 * j), db = dist512(qw, s_tile + 4 * j + 4);
+                    top2_insert((da << 16) | (uint32_t)(t0 + j), m1, m2);
+                    top2_insert((db << 16) | (uint32_t)(t0 + j + 1), m1, m2);
+                }
+                if (j < nt) top2_insert((dist512(qw, s_tile + 4 * j) << 16) | (uint32_t)(t0 + j), m1, m2);
+            }
+        }
+        if (q < n1) st_sc1(m.match_j + q, ratio_accept(m1, m2, d.ratio));
+    }
+    if (!arrive_last(&m.w->ctr[0], gridDim.x, &s_last)) return;
+    match_compact(d, wf, m, s_wsum);
 }
 
 // ---------------------------------------------------------------------------
@@ -2548,7 +2637,17 @@ void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned
 }
 void launch_match(const VoDev& d, int stage, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_match, dim3(match_blocks(d.N, d.match_bits), stage ? 1 : d.B), dim3(256), 0, s, d, stage);
+    if (d.match_bits == 32)
+        hipLaunchKernelGGL(k_match, dim3(match_blocks(d.N, 32), stage ? 1 : d.B), dim3(256), 0, s, d, stage);
+    else {
+        // 64 KB of dynamic LDS plus the static hand-off words: above the default 64 KB cap
+        static const bool lds_ok = hipFuncSetAttribute((const void*)k_match512,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       MT512_TILE * 64) == hipSuccess;
+        (void)lds_ok;
+        hipLaunchKernelGGL(k_match512, dim3(match_blocks(d.N, 512), stage ? 1 : d.B), dim3(256),
+                           (size_t)MT512_TILE * 64, s, d, stage);
+    }
 }
 // hypotheses in three chunks, [0, C0), [C0, C1), [C1, max_hyp): a frame's later chunks exit at
 // once when its replay has already stopped (ransac.cpp:139 adaptive bound; 100 hypotheses for

@@ -6,37 +6,26 @@ cv::imread(..., IMREAD_GRAYSCALE) (VisualOdometry.cpp:76).
 from __future__ import annotations
 
 import os
+import re
 from typing import Optional, Sequence
 
 import numpy as np
 
 
 def read_gray(path: str) -> Optional[np.ndarray]:
-    """8-bit gray image (PNG via PIL, binary PGM natively); None if it cannot be read."""
-    if not os.path.exists(path):
+    """cv::imread(path, cv::IMREAD_GRAYSCALE) (VisualOdometry.cpp:65,76) through the library's
+    PNG / PGM decoder (vo_imread_gray, csrc/vo_io.cpp); None where imread returns an empty Mat."""
+    import ctypes as C
+    from ._lib import load
+    L = load()
+    w, h = C.c_int(), C.c_int()
+    bp = os.fsencode(path)
+    if L.vo_imread_gray(bp, None, 0, C.byref(w), C.byref(h)) != 0:
         return None
-    try:
-        if path.endswith(".pgm"):
-            with open(path, "rb") as f:
-                data = f.read()
-            parts = data.split(maxsplit=4)
-            if parts[0] != b"P5":
-                return None
-            w, h, mx = int(parts[1]), int(parts[2]), int(parts[3])
-            if mx > 255:
-                return None
-            return np.frombuffer(parts[4][:w * h], np.uint8).reshape(h, w).copy()
-        from PIL import Image
-        with Image.open(path) as im:
-            if im.mode not in ("L", "I;16", "I"):
-                # cv::IMREAD_GRAYSCALE uses ITU-R 601 luma like PIL's "L" conversion
-                im = im.convert("L")
-            a = np.asarray(im)
-            if a.dtype != np.uint8:
-                a = (a >> 8).astype(np.uint8) if a.max() > 255 else a.astype(np.uint8)
-            return np.ascontiguousarray(a)
-    except Exception:
+    img = np.empty((h.value, w.value), np.uint8)
+    if L.vo_imread_gray(bp, img.ctypes.data_as(C.c_void_p), img.nbytes, C.byref(w), C.byref(h)) != 0:
         return None
+    return img
 
 
 def write_pgm(path: str, img: np.ndarray) -> None:
@@ -46,17 +35,37 @@ def write_pgm(path: str, img: np.ndarray) -> None:
         f.write(img.tobytes())
 
 
+# what libstdc++'s num_get accepts for a double (istream >> double)
+_NUM = re.compile(r"[+-]?(?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?")
+_EYE34 = (1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0)
+
+
+def read_gt_line(line: str) -> np.ndarray:
+    """readGTLine (PoseUpdate.cpp:43-50): T starts as eye(4) and `ss >> T(i/4, i%4)` fills the
+    12 entries in order.  As with std::istream: at end of line the extraction leaves the entry
+    (and every later one) untouched; a token that is not a number writes 0 there and stops."""
+    T = list(_EYE34)
+    pos, n = 0, len(line)
+    for i in range(12):
+        while pos < n and line[pos] in " \t\n\r\v\f":
+            pos += 1
+        if pos >= n:
+            break
+        m = _NUM.match(line, pos)
+        if not m:
+            T[i] = 0.0
+            break
+        T[i] = float(m.group(0))
+        pos = m.end()
+    return np.array(T, dtype=np.float64)
+
+
 def read_kitti_poses(path: str) -> np.ndarray:
-    """One 3x4 row-major pose per line (readGTLine reads 12 doubles)."""
-    rows = []
-    with open(path) as f:
-        for line in f:
-            vals = line.split()
-            if not vals:
-                continue
-            r = [float(v) for v in vals[:12]]
-            r += [0.0] * (12 - len(r))
-            rows.append(r)
+    """One 3x4 row-major pose per getline, blank or short lines included, exactly as
+    VisualOdometry.cpp:50-52 pushes readGTLine(line) for every line (so the GT index of frame i
+    stays line i)."""
+    with open(path, newline=None) as f:
+        rows = [read_gt_line(line.rstrip("\n")) for line in f]
     return np.array(rows, dtype=np.float64).reshape(-1, 12)
 
 

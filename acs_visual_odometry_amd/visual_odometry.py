@@ -136,6 +136,39 @@ class Context:
                                                 _p(info)), "vo_process_frames_device")
         return poses.reshape(n, 3, 4), st, info
 
+    def extract_frames_device(self, dframes: "DeviceFrames", timing: int = 0, outputs: bool = False):
+        """Batched extract only (vo_extract_frames_device).  outputs=True returns the keypoints
+        and descriptors of every frame (lists of arrays); otherwise only the counts.  Resets the
+        trajectory state."""
+        n = dframes.n
+        nk = np.zeros(n, np.int32)
+        kps = np.zeros((n, self.N, 2), np.int32) if outputs else None
+        desc = np.zeros((n, self.N, 8), np.uint64) if outputs else None
+        check(self.lib.vo_enable_kernel_timing(self.h, int(timing)))
+        check(self.lib.vo_extract_frames_device(self.h, dframes.ptr, dframes.frame_bytes, n, _p(kps), _p(desc), _p(nk)),
+              "vo_extract_frames_device")
+        if not outputs:
+            return nk
+        return nk, [kps[f, :nk[f]] for f in range(n)], [desc[f, :nk[f]] for f in range(n)]
+
+    def process_frames_host(self, frames, timing: int = 0):
+        """Host-frame streaming (vo_process_frames_host): frames is an (n, H, W) u8 array in host
+        memory -- a HostFrames buffer (pinned) or any numpy array (pageable: registered for the
+        call).  Batch k+1's H2D copy overlaps the extract/pose work of earlier batches."""
+        arr = frames.array if isinstance(frames, HostFrames) else np.ascontiguousarray(frames, dtype=np.uint8)
+        assert arr.ndim == 3 and arr.shape[1:] == (self.H, self.W)
+        n = arr.shape[0]
+        poses = np.zeros((n, 12))
+        st = np.zeros(n, np.int32)
+        info = np.zeros((n, 8), np.int32)
+        check(self.lib.vo_enable_kernel_timing(self.h, int(timing)))
+        check(self.lib.vo_process_frames_host(self.h, _p(arr), self.W * self.H, n, _p(poses), _p(st), _p(info)),
+              "vo_process_frames_host")
+        return poses.reshape(n, 3, 4), st, info
+
+    def host_frames(self, frames: np.ndarray) -> "HostFrames":
+        return HostFrames(self, frames)
+
     def kernel_times(self):
         """Average ms per timed launch of each kernel in the last process_frames_device call."""
         return {k: v[0] for k, v in self.kernel_stats().items()}
@@ -174,6 +207,34 @@ class DeviceFrames:
             pass
 
 
+class HostFrames:
+    """A batch of frames in pinned host memory (vo_host_alloc): the DMA source of
+    process_frames_host.  ``array`` is an (n, H, W) u8 numpy view of the pinned buffer."""
+
+    def __init__(self, ctx: Context, frames: np.ndarray):
+        f = np.ascontiguousarray(frames, dtype=np.uint8)
+        assert f.ndim == 3 and f.shape[1:] == (ctx.H, ctx.W)
+        self.ctx, self.n = ctx, f.shape[0]
+        p = C.c_void_p()
+        check(ctx.lib.vo_host_alloc(ctx.h, f.nbytes, C.byref(p)), "vo_host_alloc")
+        self.ptr = p
+        buf = (C.c_uint8 * f.nbytes).from_address(p.value)
+        self.array = np.frombuffer(buf, np.uint8).reshape(f.shape)
+        self.array[...] = f
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            self.ctx.lib.vo_host_free(self.ctx.h, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 def unpack_descriptor(words: np.ndarray) -> np.ndarray:
     """8 x u64 words -> 512 bytes in {0,1} (the reference's byte-per-test descriptor)."""
     w = np.ascontiguousarray(words, dtype=np.uint64).reshape(-1, 8)
@@ -199,7 +260,8 @@ class VisualOdometry:
                  **cfg):
         self.kernel_filename = kernel_filename
         self.number_of_threads = int(num_threads)
-        cfg.setdefault("ransac_chunk_threads", self.number_of_threads)
+        cfg.setdefault("ransac_chunk_threads", max(self.number_of_threads, 1))
+        self._cfg = cfg
         self.ctx = Context(width, height, **cfg)
 
     def compute_descriptor_with_key_points(self, image: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
@@ -216,23 +278,53 @@ class VisualOdometry:
         w2 = pack_descriptor(d2) if d2.shape[-1] == 512 else d2
         return [tuple(map(int, r)) for r in self.ctx.match(w1, w2)]
 
+    RUN_BATCH = 256   # frames decoded and streamed per host batch
+
     def run(self, image_dir: str, num_images: int, pose_file: str, output_csv: str) -> None:
-        """VisualOdometry::run (VisualOdometry.cpp:38-193): KITTI sequence -> pose CSV."""
+        """VisualOdometry::run (VisualOdometry.cpp:38-193): image_dir + "%06d.png" for frames
+        0 .. num_images-1 (frame 0 always, as the reference reads it before its loop), GT from
+        pose_file (one readGTLine per line), pose rows to output_csv.  Present frames go to the
+        GPU in batches through process_frames_host; a missing image is one process_frame(None)
+        (VisualOdometry.cpp:77-82).  The context takes frame 0's size."""
+        import sys
         from .io import read_gray, read_kitti_poses, write_pose_csv
         try:
             gt = read_kitti_poses(pose_file)
         except OSError:
-            import sys
             print("Failed to open pose file.", file=sys.stderr)
             return
+        total = max(int(num_images), 1)
+
+        def path(i):
+            return image_dir + f"{i:06d}.png"
+
+        img0 = read_gray(path(0))
+        if img0 is not None and img0.shape != (self.ctx.H, self.ctx.W):
+            self.ctx.close()
+            self.ctx = Context(img0.shape[1], img0.shape[0], **self._cfg)
         self.ctx.reset()
         self.ctx.set_ground_truth(gt)
-        poses = []
-        for i in range(int(num_images)):
-            img = read_gray(os.path.join(image_dir, f"{i:06d}.png"))
-            pose, status, _ = self.ctx.process_frame(img)
-            if status == 5:
-                raise RuntimeError("Degenerate essential matrix")
-            poses.append(pose)
-        write_pose_csv(output_csv, poses)
+        rows = []
+        for i0 in range(0, total, self.RUN_BATCH):
+            imgs = [read_gray(path(i)) for i in range(i0, min(total, i0 + self.RUN_BATCH))]
+            z = 0
+            while z < len(imgs):
+                if imgs[z] is None:
+                    if i0 + z > 0:
+                        print(f"Failed to load image: {path(i0 + z)}", file=sys.stderr)
+                    pose, _, _ = self.ctx.process_frame(None)
+                    rows.append(pose)
+                    z += 1
+                    continue
+                e = z
+                while e < len(imgs) and imgs[e] is not None:
+                    if imgs[e].shape != (self.ctx.H, self.ctx.W):
+                        raise RuntimeError(f"image size differs from frame 0: {path(i0 + e)}")
+                    e += 1
+                poses, st, _ = self.ctx.process_frames_host(np.stack(imgs[z:e]))
+                if (st == 5).any():
+                    raise RuntimeError("Degenerate essential matrix")
+                rows.extend(poses)
+                z = e
+        write_pose_csv(output_csv, rows)
         print(f"Wrote estimated poses to: {output_csv}")

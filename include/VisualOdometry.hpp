@@ -7,10 +7,16 @@
 // INTEGRATION.md shows the cv::Mat adapters a reference build would add.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
+#include <sstream>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -43,12 +49,11 @@ public:
                    int height = 376, int device = 0)
         : kernel_filename_(kernel_filename), number_of_threads_(num_threads)
     {
-        vo_config cfg;
-        vo_config_default(&cfg, width, height);
-        cfg.ransac_chunk_threads = (int)num_threads;
-        cfg.device = device;
-        check(vo_create(&cfg, &ctx_), "vo_create");
-        max_kpts_ = cfg.max_kpts;
+        vo_config_default(&cfg_, width, height);
+        cfg_.ransac_chunk_threads = (int)std::max<std::size_t>(num_threads, 1);
+        cfg_.device = device;
+        check(vo_create(&cfg_, &ctx_), "vo_create");
+        max_kpts_ = cfg_.max_kpts;
     }
     ~VisualOdometry() { vo_destroy(ctx_); }
     VisualOdometry(const VisualOdometry&) = delete;
@@ -101,6 +106,134 @@ public:
         check(vo_set_ground_truth(ctx_, rows12.data(), (int)(rows12.size() / 12)), "vo_set_ground_truth");
     }
 
+    // run (VisualOdometry.h:30, VisualOdometry.cpp:38-193): image_dir + "%06d.png" for frames
+    // 0 .. num_images-1 (frame 0 is always read, as the reference reads it before its loop), GT
+    // poses from pose_file (one readGTLine per line), the pose rows to output_csv.
+    // Present frames are decoded on number_of_threads host threads and streamed to the GPU in
+    // batches (vo_process_frames_host: H2D of batch k+1 overlaps the work of batch k); a missing
+    // image is one vo_process_frame(NULL) (T_curr pushed, VisualOdometry.cpp:77-82).  The context
+    // takes frame 0's size; a later frame of another size throws.
+    void run(const std::string image_dir, std::size_t num_images, const std::string pose_file,
+             const std::string output_csv)
+    {
+        std::ifstream infile(pose_file);
+        if (!infile.is_open()) {
+            std::cerr << "Failed to open pose file.\n";
+            return;
+        }
+        std::vector<double> gt;
+        for (std::string line; std::getline(infile, line);) {
+            const std::vector<double> T = readGTLine(line);
+            gt.insert(gt.end(), T.begin(), T.end());
+        }
+        infile.close();
+
+        const std::size_t total = std::max<std::size_t>(num_images, 1);
+        auto path_of = [&](std::size_t i) {
+            std::stringstream ss;
+            ss << std::setw(6) << std::setfill('0') << i;
+            return image_dir + ss.str() + ".png";
+        };
+        {   // the context takes frame 0's size
+            int w = 0, h = 0;
+            if (vo_imread_gray(path_of(0).c_str(), nullptr, 0, &w, &h) == VO_OK &&
+                (w != cfg_.width || h != cfg_.height)) {
+                vo_config c = cfg_;
+                c.width = w;
+                c.height = h;
+                vo_ctx* nc = nullptr;
+                check(vo_create(&c, &nc), "vo_create");
+                vo_destroy(ctx_);
+                ctx_ = nc;
+                cfg_ = c;
+            }
+        }
+        check(vo_reset(ctx_), "vo_reset");
+        set_ground_truth(gt);
+
+        const std::size_t np = (std::size_t)cfg_.width * cfg_.height;
+        const std::size_t batch = kRunBatch;
+        void* pinned = nullptr;
+        check(vo_host_alloc(ctx_, batch * np, &pinned), "vo_host_alloc");
+        uint8_t* buf = static_cast<uint8_t*>(pinned);
+        std::vector<double> rows;
+        rows.reserve(total * 12);
+        std::vector<int> ok(batch);
+        std::vector<int> status(batch);
+        const unsigned nthreads = (unsigned)std::max<std::size_t>(1, std::min<std::size_t>(number_of_threads_, 64));
+        try {
+            for (std::size_t i0 = 0; i0 < total;) {
+                const std::size_t nb = std::min(batch, total - i0);
+                // decode frames i0 .. i0+nb-1 (thread t takes every nthreads-th frame)
+                std::vector<std::thread> pool;
+                for (unsigned t = 0; t < nthreads && t < nb; ++t)
+                    pool.emplace_back([&, t] {
+                        for (std::size_t z = t; z < nb; z += nthreads) {
+                            int w = 0, h = 0;
+                            const int rc = vo_imread_gray(path_of(i0 + z).c_str(), buf + z * np, np, &w, &h);
+                            const bool same = w == cfg_.width && h == cfg_.height;
+                            ok[z] = (rc == VO_OK && same) ? 1 : ((rc == VO_OK || rc == VO_ERR_CAPACITY) ? -1 : 0);
+                        }
+                    });
+                for (std::thread& th : pool) th.join();
+                for (std::size_t z = 0; z < nb;) {
+                    if (ok[z] < 0) throw std::runtime_error("image size differs from frame 0: " + path_of(i0 + z));
+                    if (ok[z] == 0) {   // cv::imread returned an empty Mat
+                        if (i0 + z > 0) std::cerr << "Failed to load image: " << path_of(i0 + z) << "\n";
+                        double row[12];
+                        process_frame(nullptr, row);
+                        rows.insert(rows.end(), row, row + 12);
+                        ++z;
+                        continue;
+                    }
+                    std::size_t e = z;
+                    while (e < nb && ok[e] == 1) ++e;
+                    std::vector<double> poses((e - z) * 12);
+                    check(vo_process_frames_host(ctx_, buf + z * np, np, (int)(e - z), poses.data(), status.data(),
+                                                 nullptr),
+                          "vo_process_frames_host");
+                    for (std::size_t k = 0; k < e - z; ++k)
+                        if (status[k] == VO_STATUS_DEGENERATE) throw std::runtime_error("Degenerate essential matrix");
+                    rows.insert(rows.end(), poses.begin(), poses.end());
+                    z = e;
+                }
+                i0 += nb;
+            }
+        } catch (...) {
+            vo_host_free(ctx_, pinned);
+            throw;
+        }
+        vo_host_free(ctx_, pinned);
+        writePoseCSV(output_csv, rows);
+        std::cout << "Wrote estimated poses to: " << output_csv << "\n";
+    }
+
+    // readGTLine (PoseUpdate.cpp:43-50): eye(4), then 12 extractions in row-major order
+    static std::vector<double> readGTLine(const std::string& line)
+    {
+        std::stringstream ss(line);
+        std::vector<double> T = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+        for (int i = 0; i < 12; ++i) ss >> T[i];
+        return T;
+    }
+
+    // writePoseCSV (PoseUpdate.cpp:52-69): 12 values per row at setprecision(9)
+    static void writePoseCSV(const std::string& filename, const std::vector<double>& rows12)
+    {
+        std::ofstream file(filename);
+        if (!file.is_open()) {
+            std::cerr << "Failed to open output CSV file.\n";
+            return;
+        }
+        for (std::size_t r = 0; r + 12 <= rows12.size(); r += 12) {
+            for (int k = 0; k < 12; ++k) {
+                file << std::setprecision(9) << rows12[r + k];
+                if (k != 11) file << ",";
+            }
+            file << "\n";
+        }
+    }
+
     vo_ctx* handle() { return ctx_; }
 
 private:
@@ -112,8 +245,10 @@ private:
                 if (d[i][t]) w[i * 8 + (t >> 6)] |= 1ull << (t & 63);
         return w;
     }
+    static constexpr std::size_t kRunBatch = 256;   // frames decoded and streamed per host batch
     std::string kernel_filename_;
     std::size_t number_of_threads_;
+    vo_config cfg_;
     vo_ctx* ctx_ = nullptr;
     int max_kpts_ = 2000;
 };

@@ -36,6 +36,7 @@ extern "C" {
 #define VO_ERR_NO_DEVICE     (-3)   /* VisualOdometry.cpp:17-19 throws "No OpenCL devices" */
 #define VO_ERR_CAPACITY      (-4)
 #define VO_ERR_STATE         (-5)
+#define VO_ERR_IO            (-6)   /* image file missing or not decodable (cv::imread -> empty) */
 #define VO_ERR_DEGENERATE_E  (-10)  /* PoseUpdate.hpp:71-73 throws "Degenerate essential matrix" */
 
 /* per-frame status (VisualOdometry.cpp:68-189) */
@@ -133,6 +134,33 @@ int  vo_process_frame(vo_ctx* ctx, const uint8_t* gray, size_t stride, double po
 int  vo_process_frames_device(vo_ctx* ctx, const uint8_t* d_frames, size_t frame_bytes, int nframes,
                               double* poses_out, int* status_out, int32_t* info_out);
 
+/* Batched extract only (SURVEY config 2; feature_extraction_manager_with_points over many
+ * frames): nframes device-resident frames, frame_batch per launch.  Optional host outputs:
+ * kps (nframes * max_kpts), desc (nframes * max_kpts * 8 words), n_kps (nframes).  The ring
+ * slots are reused, so the trajectory state is reset (as by vo_reset) before and after. */
+int  vo_extract_frames_device(vo_ctx* ctx, const uint8_t* d_frames, size_t frame_bytes, int nframes,
+                              vo_kp* kps, uint64_t* desc, int32_t* n_kps);
+
+/* Host-frame streaming variant (the drop-in path of VisualOdometry::run, whose loop reads one
+ * image per iteration, VisualOdometry.cpp:68-189): nframes dense W x H u8 frames in HOST memory
+ * at frames + f * frame_bytes.  Batch k + 1's H2D copy runs on a copy queue while batch k is
+ * extracted and earlier windows are posed; nothing synchronises the host until the chunk ends.
+ * Pinned memory (vo_host_alloc, or the caller's own hipHostMalloc / hipHostRegister) is DMA'd
+ * directly; pageable memory is registered for the duration of the call, or staged through a
+ * pinned ring if registration fails.  Results are those of nframes vo_process_frame calls. */
+int  vo_process_frames_host(vo_ctx* ctx, const uint8_t* frames, size_t frame_bytes, int nframes,
+                            double* poses_out, int* status_out, int32_t* info_out);
+
+/* cv::imread(path, cv::IMREAD_GRAYSCALE)  VisualOdometry.cpp:65,76, for PNG (any bit depth /
+ * colour type, Adam7) and binary PGM.  Writes width x height u8 pixels to out when out != NULL
+ * and cap >= width * height (VO_ERR_CAPACITY otherwise; the dimensions are always set on a
+ * successful decode).  VO_ERR_IO where imread returns an empty Mat. */
+int  vo_imread_gray(const char* path, uint8_t* out, size_t cap, int* width, int* height);
+
+/* Pinned host memory for vo_process_frames_host sources. */
+int  vo_host_alloc(vo_ctx* ctx, size_t bytes, void** hptr);
+int  vo_host_free(vo_ctx* ctx, void* hptr);
+
 /* Device memory helpers for callers without their own allocator (bench, tests). */
 int  vo_device_alloc(vo_ctx* ctx, size_t bytes, void** dptr);
 int  vo_device_free(vo_ctx* ctx, void* dptr);
@@ -152,7 +180,8 @@ int  vo_last_kernel_stats(vo_ctx* ctx, const char** names, float* ms_per_launch,
 int  vo_enable_kernel_timing(vo_ctx* ctx, int on);
 
 /* desc512 (8 words) -> 512 bytes in {0,1}: the reference's byte-per-test layout
- * (FREAK_feature_descriptor_parallel_GPU.cpp:334-336). */
+ * (desc[kp * 512 + t] = I(p1) > I(p2), kernels/feature_extraction_kernel_functions.c:223, read
+ * back as vector<vector<uint8_t>> at FREAK_feature_descriptor_parallel_GPU.cpp:179,196-198). */
 void vo_unpack_descriptor(const uint64_t words[8], uint8_t bytes[512]);
 
 #ifdef __cplusplus
