@@ -335,10 +335,14 @@ void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int cap)
 // shorter).  Pass k's window starts at or before batch k's first frame, so its frames are
 // extracted once batch k is.  (Smaller first batches to start the pose queue earlier were
 // measured slower: more passes, each with a fixed latency.)
-std::vector<int> batch_schedule(int nf, int B)
+// Host streaming (first_default > 0): the first batch is short, so its H2D copy (the pipeline
+// fill: 64 KITTI frames are 30 MB, ~0.5 ms at PCIe's ~56 GB/s) does not hold back the first extract
+// (tools/host_stream_diag.py: first batch 8/16/32 measured +5 % over 64).
+std::vector<int> batch_schedule(int nf, int B, int first_default = 0)
 {
     // experiment knob: VO_FIRST = size of the first batch (pipeline fill), default B
-    static const int first = getenv("VO_FIRST") ? atoi(getenv("VO_FIRST")) : 0;
+    static const int env_first = getenv("VO_FIRST") ? atoi(getenv("VO_FIRST")) : -1;
+    const int first = env_first >= 0 ? env_first : first_default;
     std::vector<int> v;
     for (int done = 0; done < nf;) {
         const int want = (done == 0 && first > 0 && first < B) ? first : B;
@@ -364,7 +368,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         c->reset_pending = false;
     }
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&c->d.st->end, end, 1, s));
-    const std::vector<int> sched = batch_schedule(nf, B);
+    const std::vector<int> sched = batch_schedule(nf, B, hs ? VO_HOST_FIRST_BATCH : 0);
     if (!img0 && !hs) {
         vo::launch_ext_missing(c->d, base % VO_RING, s);
     } else {
@@ -575,6 +579,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     auto bail = [&](int r) { vo_destroy(c); return r; };
     c->serial = getenv("VO_SERIAL") && atoi(getenv("VO_SERIAL")) != 0;
     c->event_wait = getenv("VO_EVENT_WAIT") && atoi(getenv("VO_EVENT_WAIT")) != 0;
+    d.xcd_map = getenv("VO_XCD") ? atoi(getenv("VO_XCD")) : 1;
     if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
     for (hipStream_t& q : c->se)
         if (hip_ok(hipStreamCreateWithFlags(&q, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);

@@ -62,6 +62,7 @@
 #define VO_CTR_WORDS 64
 // host-frame streaming (vo_process_frames_host): device ring of VO_HRING slots of B frames
 #define VO_HRING 3
+#define VO_HOST_FIRST_BATCH 16 // host streaming: frames in a chunk's first batch (shorter pipeline fill)
 #define VO_EV_WAIT 0           // per-batch event pools of a chunk (vo_api.cpp)
 #define VO_EV_COPY 1
 #define VO_EV_STENCIL 2
@@ -133,6 +134,7 @@ struct VoDev {
     int max_hyp;
     int B;                // window / extract batch capacity (frames)
     int eq;               // extract queue of this launch (its scratch copy and counters)
+    int xcd_map;          // extract kernels place a frame's workgroups on one XCD (VO_XCD=0: off)
     uint64_t seed;
     double K[9];
     uint32_t cand_cap;    // per frame

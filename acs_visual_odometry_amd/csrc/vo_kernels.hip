@@ -391,20 +391,41 @@ __device__ __forceinline__ int from_right(int v)
 
 // SEGT tiles (16 SEGT output rows) per wave, source rows in unrolled blocks of U; rows past
 // the segment's 16 SEGT + 14 in the last block only feed masked outputs
+// XCD-aware workgroup -> (frame, workgroup of the frame) for the extract kernels: a 1-D grid of
+// nx * ceil8(nb) workgroups.  Workgroup L is dispatched to XCD L % 8 (round-robin; used for
+// speed only, MI355X_MICROARCH.md "Dispatch order ... block->XCD map"), so with d.xcd_map frame z's
+// nx workgroups all run on XCD z % 8 and share that XCD's L2: the frame's image and blurred
+// plane are fetched into one L2 instead of eight.  false: a padding workgroup of the last group.
+__device__ __forceinline__ bool xcd_frame(const VoDev& d, int nx, int nb, int& z, int& bx)
+{
+    const int L = blockIdx.x;
+    if (d.xcd_map) {
+        const int k = L >> 3;
+        z = (k / nx) * 8 + (L & 7);
+        bx = k % nx;
+    } else {
+        z = L / nx;
+        bx = L % nx;
+    }
+    return z < nb;
+}
+__host__ inline int xcd_grid(int nx, int nb) { return nx * ((nb + 7) / 8) * 8; }
+
 template <int SEGT, int U>
 __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restrict__ img0, size_t frame_bytes,
-                                                  int write_response)
+                                                  int write_response, int nb)
 {
     constexpr int ST_SEGT = SEGT, ST_SEG = ST_TH * SEGT, ST_ROWS = ST_SEG + 2 * ST_HALO, ST_U = U;
     const int W = d.W, H = d.H;
     const int ntx = (W + ST_TW - 1) / ST_TW, nty = (H + ST_TH - 1) / ST_TH;
     const int nseg = (nty + ST_SEGT - 1) / ST_SEGT;
-    const int g = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
+    // frame z of the batch (its image and its scratch copy), workgroup bx of the frame
+    int z, bx;
+    if (!xcd_frame(d, (ntx * nseg + 3) / 4, nb, z, bx)) return;
+    const int g = bx * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
     if (g >= ntx * nseg) return;
     const int strip = g % ntx, seg = g / ntx;
     const int lane = threadIdx.x & 63;
-    // frame z of the batch: its image and its scratch copy
-    const int z = blockIdx.y;
     const uint8_t* __restrict__ img = img0 + (size_t)z * frame_bytes;
     uint8_t* __restrict__ blurred = d.blurred + (size_t)z * W * H;
     uint64_t* __restrict__ cand = d.cand + (size_t)z * d.cand_cap;
@@ -1079,25 +1100,29 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
     }
 }
 
-// grid (N / DS_KPB, nb): frame z = blockIdx.y of the batch.  publish > 0: the last
-// workgroup of the launch tells the pose queue that frames < publish are extracted
-__global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int slot_override, unsigned publish)
+// grid xcd_grid(N / DS_KPB, nb) (frame z of the batch, workgroup bx of the frame, xcd_frame).
+// publish > 0: the last workgroup of the launch tells the pose queue that frames < publish are
+// extracted (every workgroup of the grid arrives, padding included)
+__global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int slot_override, unsigned publish,
+                                                            int nb)
 {
     __shared__ float s_I0[DS_WAVES][DS_KPW][VO_FREAK_NPOINTS];
     __shared__ uint8_t s_I1[DS_WAVES][DS_KPW][DS_I1W];
-    const int z = blockIdx.y;
-    const int cur = ext_slot(f0, z, slot_override);
-    const int n = d.ext->n_kps[cur];
-    const int wave = threadIdx.x >> 6;
-    const int base = blockIdx.x * DS_KPB + wave * DS_KPW;
-    if (blockIdx.x * DS_KPB < n)             // workgroup-uniform: the barriers inside are met by all
-        describe_wave(d, d.blurred + (size_t)z * d.W * d.H, cur, n, base, s_I0[wave], s_I1[wave]);
+    int z, bx;
+    if (xcd_frame(d, (d.N + DS_KPB - 1) / DS_KPB, nb, z, bx)) {
+        const int cur = ext_slot(f0, z, slot_override);
+        const int n = d.ext->n_kps[cur];
+        const int wave = threadIdx.x >> 6;
+        const int base = bx * DS_KPB + wave * DS_KPW;
+        if (bx * DS_KPB < n)             // workgroup-uniform: the barriers inside are met by all
+            describe_wave(d, d.blurred + (size_t)z * d.W * d.H, cur, n, base, s_I0[wave], s_I1[wave]);
+    }
     if (!publish) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __shared__ unsigned s_last;
-    if (!arrive_last(d.ctr + VO_CTR_DESCRIBE + 16 * d.eq, gridDim.x * gridDim.y, &s_last)) return;
+    if (!arrive_last(d.ctr + VO_CTR_DESCRIBE + 16 * d.eq, gridDim.x, &s_last)) return;
     if (threadIdx.x == 0) d.ctr[VO_CTR_DESCRIBE + 16 * d.eq] = 0u;
     publish_seq(d.ctr + VO_SYNC_EXT + 16 * d.eq, publish);
 }
@@ -2600,13 +2625,13 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
     static const int segt = getenv("VO_STSEG") ? atoi(getenv("VO_STSEG")) : ST_SEGT_DEFAULT;
     const int st = segt == 6 || segt == 8 ? segt : 4;
     const int waves = ntx * ((nty + st - 1) / st);                 // one (strip, segment) per wave
-    dim3 g((waves + 3) / 4, nb);
+    dim3 g(xcd_grid((waves + 3) / 4, nb));
     if (st == 8)
-        hipLaunchKernelGGL((k_stencil<8, 24>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response);
+        hipLaunchKernelGGL((k_stencil<8, 24>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response, nb);
     else if (st == 6)
-        hipLaunchKernelGGL((k_stencil<6, 22>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response);
+        hipLaunchKernelGGL((k_stencil<6, 22>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response, nb);
     else
-        hipLaunchKernelGGL((k_stencil<4, 26>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response);
+        hipLaunchKernelGGL((k_stencil<4, 26>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response, nb);
 }
 void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s)
 {
@@ -2632,8 +2657,8 @@ int select_lds_bytes(int W, int H, int* key_cap)
 void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned publish, hipStream_t s)
 {
     ensure_tables();
-    hipLaunchKernelGGL(k_describe, dim3((d.N + DS_KPB - 1) / DS_KPB, nb), dim3(64 * DS_WAVES), 0, s, d, f0, slot_override,
-                       publish);
+    hipLaunchKernelGGL(k_describe, dim3(xcd_grid((d.N + DS_KPB - 1) / DS_KPB, nb)), dim3(64 * DS_WAVES), 0, s, d, f0,
+                       slot_override, publish, nb);
 }
 void launch_match(const VoDev& d, int stage, hipStream_t s)
 {

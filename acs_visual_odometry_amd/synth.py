@@ -116,3 +116,34 @@ def noise_frames(width=KITTI_W, height=KITTI_H, nframes=8, seq=0) -> np.ndarray:
         rng = np.random.default_rng(frame_seed(seq, f))
         out[f] = rng.integers(0, 256, size=(height, width), dtype=np.uint8)
     return out
+
+
+# -- parallel rendering (bench: several sequences of 200+ frames) ------------------------
+_SEQ_CACHE: dict = {}
+
+
+def _render(args):
+    W, H, n, seq, step, f = args
+    key = (W, H, n, seq, step)
+    s = _SEQ_CACHE.get(key)
+    if s is None:
+        s = _SEQ_CACHE[key] = SceneSequence(W, H, nframes=n, seq=seq, step=step)
+    return s.frame(f)
+
+
+def render_sequences(specs, workers: int = 1):
+    """Frames of several scene sequences, specs = [(W, H, nframes, seq, step), ...], rendered by
+    `workers` forked processes (call before the process touches the GPU).  Identical to
+    SceneSequence(W, H, nframes=n, seq=seq, step=step).frames() for each spec."""
+    tasks = [(W, H, n, s, st, f) for (W, H, n, s, st) in specs for f in range(n)]
+    if workers <= 1:
+        flat = [_render(t) for t in tasks]
+    else:
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(workers) as pool:
+            flat = pool.map(_render, tasks, chunksize=max(1, len(tasks) // (4 * workers)))
+    out, k = [], 0
+    for (W, H, n, s, st) in specs:
+        out.append(np.stack(flat[k:k + n]))
+        k += n
+    return out

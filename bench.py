@@ -1,28 +1,39 @@
 #!/usr/bin/env python3
 """VO frames/sec (extract + match + pose) at 1241x376, 2000 keypoints/frame.
 
-One step = one pass of the full per-frame hot path (blur -> response -> NMS/top-N ->
-orientation/descriptor -> Hamming match -> 8-point RANSAC -> refit -> getPose ->
-trajectory update) over a synthetic KITTI-shape sequence of --frames frames that is
-already resident in HBM (uploaded before the timed region).  Frames are enqueued back
-to back on the ctx's HIP stream; the step ends with one stream synchronisation.
+Workload: S = 8 synthetic KITTI-shape scene
+sequences (camera +1.0 m/frame along z, 0.1 deg/frame yaw; seed = splitmix64(0xACE0 ^ seq<<32 ^
+frame)), --frames frames each.  Sequence s runs on rank s mod G (config 5's partition: at G < 8
+a GPU runs 8/G sequences, one after another on its context).  One step = every sequence of the
+rank through the full per-frame path (blur -> response -> NMS/top-N -> orientation/descriptor ->
+Hamming match -> 8-point RANSAC -> refit -> getPose -> trajectory update), from vo_reset, with the
+frames already resident in HBM (uploaded before the timed region).  value = all ranks' frames /
+the slowest rank's time.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-replicas -- rank r processes its own sequence (seq = r) on GPU LOCAL_RANK with no
-data-path collective; the barrier and the max-over-ranks step time go over RCCL
-("nccl" backend).  value = frames processed by all ranks / max rank time (weak scaling).
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process
+per GPU, no data-path collective; RCCL ("nccl") carries the barrier, the max-over-ranks time and
+one all-reduce that assembles every sequence's poses on every rank, after which rank 0 re-runs
+all sequences on its own GPU and checks the gathered rows bit for bit.
 
-Also reported, on the same JSON line:
-  roofline      -- the dominant kernel's algorithmic bytes per launch / its average
-                   launch time (HIP events on the ctx stream, inside the timed region)
-                   against the MI355X HBM peak (8 TB/s)
-  cpu_baseline  -- the CPU oracle (a plain-C restatement of the reference path, one host
-                   core) timed on a bounded sample of the same sequence (rank 0, N=1)
+Also on the JSON line:
+  roofline      the critical-path kernel (the largest per-frame time on the pose queue, which
+                serialises the path; the extract kernels overlap it on their own queue):
+                SURVEY 8(d)'s algorithmic bytes per launch / its average launch time (HIP events on
+                its stream inside the timed region) against 8 TB/s; traffic = PMC HBM bytes per
+                launch from the committed profile; valu = VALU issue from the PMC profile
+  kernels       every kernel's per-frame time, algorithmic bytes and VALU issue fraction
+  variants      (N = 1) the 0.05 m/frame and low-inlier (0.12 m/frame) sequences, extract only
+                (config 2), host-frame streaming from pinned memory (H2D inside the timing), the
+                per-frame vo_process_frame rate, and 1920x1080 / N=4096 (config 4) with the 32-test
+                and the 512-test matcher
+  cpu_baseline  the CPU oracle (plain-C restatement of the reference path) on the host's cores:
+                one process per core over the same sequence (cores stated), plus one core
 """
 from __future__ import annotations
 
 import argparse
 import json
+import multiprocessing as mp
 import os
 import sys
 import time
@@ -33,60 +44,77 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 METRIC = "VO frames/sec (extract+match+pose), 1241×376 mono, 2000 kpts/frame"
-# committed rocprofv3 FETCH_SIZE / WRITE_SIZE summaries of the two bench configs (tools/profile.sh
-# -> tools/rocprof_summary.py --fetch-x2 --json): the source of roofline.traffic
-PMC_PROFILES = {(1241, 376): "r1_batched_kitti_kernels.json", (1920, 1080): "r1_batched_1080_kernels.json"}
+HBM_PEAK_GBS = 8000.0
+# VALU issue peak: 256 CUs x 4 SIMD-32, a wave64 VALU instruction every 2 cycles per SIMD
+VALU_SIMDS = 1024
+KERNELS = ["stencil", "select", "describe", "match", "ransac", "refit", "triangulate", "finalize"]
+POSE_QUEUE = ["match", "ransac", "refit", "triangulate", "finalize"]
 ROCPROF_NAME = {"stencil": "k_stencil", "select": "k_select", "describe": "k_describe", "match": "k_match",
                 "ransac": "k_ransac_hyp", "refit": "k_refit", "triangulate": "k_triangulate",
                 "finalize": "k_finalize"}
-HBM_PEAK_GBS = 8000.0
-KERNELS = ["stencil", "select", "describe", "match", "ransac", "refit", "triangulate", "finalize"]
+# committed rocprofv3 summaries (tools/profile.sh -> tools/rocprof_summary.py --json): kernel
+# durations, PMC HBM bytes and VALU counters per launch
+PROFILES = {(1241, 376, 32): "r2_kitti_kernels.json", (1920, 1080, 32): "r2_1080_kernels.json",
+            (1920, 1080, 512): "r2_1080_512_kernels.json"}
 
 
-def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray, N: int) -> float:
-    """Algorithmic HBM bytes per frame of `kernel` (one launch, two for ransac), averaged
-    over the frames in `info` (n_kps, n_matches, n_inliers, ...).  DESIGN.md section 4
-    derives each figure; n = keypoints, M = matches, I = inliers."""
+def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray) -> float:
+    """SURVEY 8(d)'s algorithmic HBM bytes per frame, B = W*H + 80n + 24M + 96, split by the
+    kernel that moves each term (n = keypoints, M = matches, I = inliers, averaged over info):
+    the image read (stencil), 8n keypoints written (select), 64n descriptors written (describe),
+    8n prefixes read + 8M matches written (match), 16M match coordinates read (RANSAC), 96 B of
+    R, t (finalize).  Refit and triangulate have no term of their own in 8(d); they are given
+    their 16I inlier coordinates read."""
     n = float(info[:, 0].mean())
     M = float(info[:, 1].mean())
     I = float(info[:, 2].mean())
-    if kernel == "stencil":
-        return 2.0 * W * H + 4 * 8 * n                # frame in + blurred out + ~4n candidate keys
-    if kernel == "select":
-        return 4 * 8 * n + 8 * n                      # ~4n candidate keys in, n keypoints out
-    if kernel == "describe":
-        return (86 + 8 + 64 + 4) * n                  # 86 sampled px + kp in; descriptor + prefix out
-    if kernel == "match":
-        return 3 * 4 * n + 8 * M                      # two 32-bit prefix sets + best index; pairs out
-    if kernel == "ransac":
-        return 32 * M + 36 * 4                        # match coords once (L2 re-reads excluded)
-    if kernel == "refit":
-        return 32 * M + 4 * I + 72 + 16 * I           # coords + inlier ids; F + f32 inlier points out
-    if kernel == "triangulate":
-        return 16 * I + 96 + 96                       # f32 inlier points in; candidate counts out
-    if kernel == "finalize":
-        return 2 * 96 + 96 + 128                      # two GT rows + R, t in; the output row
-    return float(W * H + 80 * n + 24 * M + 96)       # whole path (SURVEY 8(d))
+    return {"stencil": W * H, "select": 8 * n, "describe": 64 * n, "match": 8 * n + 8 * M, "ransac": 16 * M,
+            "refit": 16 * I, "triangulate": 16 * I, "finalize": 96.0,
+            "path": W * H + 80 * n + 24 * M + 96}[kernel]
 
 
-def pmc_traffic(kernel: str, W: int, H: int):
-    """HBM bytes per launch of `kernel` from the committed PMC profile of this frame size (None
-    if absent); the RANSAC launches of a pass count as one launch, as in the live timing."""
-    if (W, H) not in PMC_PROFILES:
+def load_profile(W: int, H: int, bits: int):
+    name = PROFILES.get((W, H, bits))
+    if not name:
         return None, None
-    PMC_PROFILE = os.path.join(ROOT, "profiles", PMC_PROFILES[(W, H)])
+    path = os.path.join(ROOT, "profiles", name)
     try:
-        prof = json.load(open(PMC_PROFILE))["kernels"]
-        rows = [r for k, r in prof.items() if k.split("<")[0] == ROCPROF_NAME[kernel]]   # template instances
-        total = sum(r["hbm_bytes_per_launch"] for r in rows)
-        return (total if rows else None), os.path.relpath(PMC_PROFILE, ROOT)
-    except (OSError, KeyError, TypeError, ZeroDivisionError, ValueError):
+        return json.load(open(path))["kernels"], os.path.relpath(path, ROOT)
+    except (OSError, KeyError, ValueError):
         return None, None
+
+
+def profile_row(prof, kernel: str):
+    """The profile's per-launch figures of `kernel`, a launch as the live timing counts it: one
+    pose pass launches k_ransac_hyp three times (hypothesis chunks), so the pose-queue kernels are
+    normalised by the passes (k_match calls) and the extract kernels by the batches (k_stencil)."""
+    if not prof:
+        return None
+    rows = [r for k, r in prof.items() if k.split("<")[0] == ROCPROF_NAME[kernel]]
+    if not rows:
+        return None
+    ref = "k_match" if kernel in POSE_QUEUE else "k_stencil"
+    ref_calls = [r["calls"] for k, r in prof.items() if k.split("<")[0] == ref]
+    launches = max(ref_calls) if ref_calls else max(r["calls"] for r in rows)
+
+    def per(key):
+        if any(r.get(key) is None for r in rows):
+            return None
+        return sum(r[key] * r["calls"] for r in rows) / launches
+    vi, gc = per("valu_insts"), per("grbm_cycles")
+    return {"avg_us": per("avg_us"), "hbm_bytes": per("hbm_bytes_per_launch"), "valu_insts": vi,
+            "valu_issue_frac": vi * 2 / (VALU_SIMDS * gc / 8) if vi is not None and gc else None}
+
+
+# -- multi-GPU harness (config 5) --------------------------------------------------------
+def rank_sequences(n_seq: int, rank: int, world: int):
+    """Sequence s runs on rank s mod G."""
+    return [s for s in range(n_seq) if s % world == rank]
 
 
 def dist_init(world: int, local: int, backend: str = "nccl"):
-    """One process per GPU; RCCL ("nccl") carries only the barrier and the max-time
-    reduction (replicas: no data-path collective).  gloo is used by the CPU tests."""
+    """One process per GPU; RCCL ("nccl") carries the barrier, the max-time reduction and the
+    pose gather (replicas: no data-path collective).  gloo is used by the CPU tests."""
     if world <= 1:
         return None
     import torch
@@ -104,34 +132,199 @@ def aggregate(dist, dt: float, frames_per_rank: int, world: int, backend: str = 
     if dist is not None:
         import torch
         dev = f"cuda:{local}" if backend == "nccl" else "cpu"
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+        tt = torch.tensor([dt, float(frames_per_rank)], dtype=torch.float64, device=dev)
+        t_max = tt[:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        f_sum = tt[1:].clone()
+        dist.all_reduce(f_sum, op=dist.ReduceOp.SUM)
+        return float(t_max.item()), float(f_sum.item()) / float(t_max.item())
     return dt, frames_per_rank * world / dt
 
 
-def cpu_baseline(frames: np.ndarray, seq, budget_s: float, max_kpts: int) -> dict:
-    """The CPU oracle over the same sequence, restarted from frame 0 after each pass, until
-    the time budget is spent."""
+def gather_poses(dist, local_rows: dict, n_seq: int, nframes: int, backend: str = "nccl", local: int = 0):
+    """Every sequence's (nframes, 13) rows -- 12 pose values and the status -- on every rank:
+    each rank fills its own sequences into a zero (n_seq, nframes, 13) f64 tensor and one SUM
+    all-reduce assembles them (each sequence is owned by exactly one rank)."""
+    out = np.zeros((n_seq, nframes, 13))
+    for s, rows in local_rows.items():
+        out[s] = rows
+    if dist is None:
+        return out
+    import torch
+    dev = f"cuda:{local}" if backend == "nccl" else "cpu"
+    t = torch.from_numpy(out).to(dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.cpu().numpy()
+
+
+# -- CPU baseline ------------------------------------------------------------------------
+_CPU = {}
+
+
+def _cpu_worker(budget_s: float):
     import oracle as O
-    cfg = O.config(seq.W, seq.H, K=seq.K.reshape(9), max_kpts=max_kpts)
+    frames, W, H, K, gt, N = (_CPU[k] for k in ("frames", "W", "H", "K", "gt", "N"))
+    cfg = O.config(W, H, K=K.reshape(9), max_kpts=N)
     t0 = time.perf_counter()
-    done = passes = 0
+    done = 0
     while True:
-        vo = O.VO(cfg, gt=seq.gt())
+        vo = O.VO(cfg, gt=gt)
         for f in range(frames.shape[0]):
             vo.process(frames[f])
             done += 1
             if time.perf_counter() - t0 > budget_s and done >= 2:
                 break
         vo.close()
-        passes += 1
         if time.perf_counter() - t0 > budget_s:
             break
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{done} frames ({passes} pass(es) over the {frames.shape[0]}-frame sequence, seq 0, "
-                      f"{seq.W}x{seq.H}, N={max_kpts}), oracle/vo_oracle.c single thread, {dt:.1f} s"}
+    return done, time.perf_counter() - t0
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(frames, seq, budget_s: float, max_kpts: int, procs: int) -> dict:
+    """The CPU oracle over the bench sequence (restarted at frame 0 after each pass) for about
+    budget_s seconds: `procs` forked processes, one per host core, each running the sequence
+    (throughput = all frames / the slowest process), and one process alone.  Runs before the
+    process touches the GPU."""
+    _CPU.update(frames=frames, W=seq.W, H=seq.H, K=seq.K, gt=seq.gt(), N=max_kpts)
+    one_done, one_dt = _cpu_worker(budget_s)
+    single = {"value": one_done / one_dt, "unit": "frames/s", "cores": 1, "kind": "port",
+              "sample": f"{one_done} frames of the {frames.shape[0]}-frame sequence (restarted at frame 0 after "
+                        f"each pass), oracle/vo_oracle.c in one process, {one_dt:.1f} s"}
+    if procs <= 1:
+        return dict(single, cpu_model=cpu_model())
+    with mp.get_context("fork").Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [budget_s] * procs)
+    done = sum(r[0] for r in res)
+    dt = max(r[1] for r in res)
+    return {"value": done / dt, "unit": "frames/s", "cores": procs, "kind": "port",
+            "sample": f"{procs} processes (one per host core), each running oracle/vo_oracle.c over the same "
+                      f"{frames.shape[0]}-frame sequence for ~{budget_s:.0f} s: {done} frames in {dt:.1f} s",
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "single_thread": single}
+
+
+# -- GPU measurement helpers ---------------------------------------------------------------
+def timed_rate(fn, frames_per_call: int, steps: int, warmup: int = 1) -> float:
+    for _ in range(warmup):
+        fn()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    return frames_per_call * steps / (time.perf_counter() - t0)
+
+
+def breakdown(ctx, call) -> dict:
+    """{kernel: (ms per launch, frames per launch)} of one call with every launch timed."""
+    call(1)
+    return ctx.kernel_stats()
+
+
+def run_variants(args, ctx, W, H, frames0, gt0, extra, Context) -> dict:
+    """Secondary lines (N = 1): other motions, extract only, host streaming, per-frame calls,
+    and config 4 at 1920x1080."""
+    out = {}
+    steps = max(3, args.steps // 2)
+    for tag, (fr, seq) in extra.items():
+        if tag in ("x1080", "stream"):
+            continue
+        df = ctx.device_frames(fr)
+        ctx.set_ground_truth(seq.gt())
+
+        def go(timing=0, df=df):
+            ctx.reset()
+            return ctx.process_frames_device(df, timing=timing)
+        rate = timed_rate(go, fr.shape[0], steps)
+        _, st, info = go()
+        ks = breakdown(ctx, go)
+        out[tag] = {"fps": rate, "motion_m_per_frame": seq.step, "frames": fr.shape[0],
+                    "mean_hypotheses": float(info[1:, 4].mean()), "mean_matches": float(info[1:, 1].mean()),
+                    "mean_inliers": float(info[1:, 2].mean()), "frames_ok": int((st == 0).sum()),
+                    "kernels_us_per_frame": {k: round(v[0] / v[1] * 1e3, 3) for k, v in ks.items() if v[1] > 0}}
+        df.free()
+    # extract only (config 2), device-resident frames of sequence 0
+    df = ctx.device_frames(frames0)
+    rate = timed_rate(lambda: ctx.extract_frames_device(df), frames0.shape[0], steps)
+    ks = breakdown(ctx, lambda t: ctx.extract_frames_device(df, timing=t))
+    out["extract_only"] = {"fps": rate, "frames": frames0.shape[0], "config": "2: extract only, device-resident",
+                           "kernels_us_per_frame": {k: round(v[0] / v[1] * 1e3, 3) for k, v in ks.items()
+                                                    if v[1] > 0},
+                           "roofline_stencil_frac": None}
+    if "stencil" in ks:
+        ms, fpl = ks["stencil"]
+        out["extract_only"]["roofline_stencil_frac"] = W * H * fpl / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    df.free()
+    # host-frame streaming from pinned memory (H2D inside the timed region) against the same
+    # frames device-resident: one 1000-frame sequence, so the per-call pipeline fill (the first
+    # batch's copy) and drain (the last batch's extract and pass) are amortised as in a KITTI run
+    if "stream" in extra:
+        fr, seq = extra["stream"]
+        ctx.set_ground_truth(seq.gt())
+        dl = ctx.device_frames(fr)
+
+        def dev(dl=dl):
+            ctx.reset()
+            return ctx.process_frames_device(dl)
+        dev_rate = timed_rate(dev, fr.shape[0], 3)
+        ref = dev()
+        dl.free()
+        hf = ctx.host_frames(fr)
+
+        def host():
+            ctx.reset()
+            return ctx.process_frames_host(hf)
+        host_rate = timed_rate(host, fr.shape[0], 3)
+        got = host()
+        same = bool(np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]))
+        out["host_stream"] = {"fps": host_rate, "device_resident_fps": dev_rate, "ratio": host_rate / dev_rate,
+                              "h2d_GBs": host_rate * W * H / 1e9, "rows_equal_device_path": same,
+                              "frames": fr.shape[0], "motion_m_per_frame": seq.step,
+                              "source": "pinned host memory (vo_host_alloc), vo_process_frames_host, one call per "
+                                        "sequence pass"}
+        hf.free()
+    # per-frame calls (vo_process_frame: host frame in, pose out, one frame per call)
+    nf = min(100, frames0.shape[0])
+
+    def per_frame():
+        ctx.reset()
+        for f in range(nf):
+            ctx.process_frame(frames0[f])
+    out["process_frame"] = {"fps": timed_rate(per_frame, nf, 2), "frames": nf,
+                            "note": "one vo_process_frame call per frame (H2D + extract + pose + D2H, host sync)"}
+    # config 4: 1920x1080, N = 4096, 32-test and 512-test matching
+    if "x1080" in extra:
+        fr, seq = extra["x1080"]
+        for bits in (32, 512):
+            cx = Context(seq.W, seq.H, K=seq.K, max_kpts=4096, match_bits=bits)
+            cx.set_ground_truth(seq.gt())
+            dx = cx.device_frames(fr)
+
+            def g(timing=0, cx=cx, dx=dx):
+                cx.reset()
+                return cx.process_frames_device(dx, timing=timing)
+            rate = timed_rate(g, fr.shape[0], steps)
+            _, st, info = g()
+            ks = breakdown(cx, g)
+            prof, src = load_profile(seq.W, seq.H, bits)
+            prow = profile_row(prof, "match")
+            out[f"x1080_{bits}bit"] = {
+                "fps": rate, "frames": fr.shape[0], "match_bits": bits, "motion_m_per_frame": seq.step,
+                "frames_ok": int((st == 0).sum()), "mean_matches": float(info[1:, 1].mean()),
+                "match_us_per_launch": ks.get("match", (float("nan"), 0))[0] * 1e3,
+                "match_frames_per_launch": ks.get("match", (0, 0))[1],
+                "match_rocprof_avg_us": prow["avg_us"] if prow else None, "profile": src,
+                "kernels_us_per_frame": {k: round(v[0] / v[1] * 1e3, 3) for k, v in ks.items() if v[1] > 0}}
+            dx.free()
+            cx.close()
+    return out
 
 
 def main():
@@ -139,14 +332,17 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=200, help="frames per step (one sequence pass)")
+    ap.add_argument("--frames", type=int, default=200, help="frames per sequence")
+    ap.add_argument("--sequences", type=int, default=8, help="sequences of the job (config 5: 8)")
     ap.add_argument("--width", type=int, default=1241)
     ap.add_argument("--height", type=int, default=376)
     ap.add_argument("--max-kpts", type=int, default=2000)
-    ap.add_argument("--motion", type=float, default=0.05, help="metres per frame of the synthetic camera")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--match-bits", type=int, default=32)
+    ap.add_argument("--motion", type=float, default=1.0, help="metres per frame of the synthetic camera")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--batch", type=int, default=0, help="frames per extract batch / pose window (0: default)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--breakdown", action="store_true", help="print the per-kernel table to stderr")
     args = ap.parse_args()
 
@@ -155,21 +351,47 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     if world != args.gpus:
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    W, H, F = args.width, args.height, args.frames
+    S = max(args.sequences, world)          # every rank gets at least one sequence
+    my_seqs = rank_sequences(S, rank, world)
+    lead = rank == 0 and world == 1
+
+    # -- host-side preparation, before anything touches the GPU (forked workers) --
+    from acs_visual_odometry_amd.synth import SceneSequence, render_sequences
+    workers = max(1, min(16, (os.cpu_count() or 4) // max(world, 1)))
+    specs = [(W, H, F, s, args.motion) for s in my_seqs]
+    extra_specs = {}
+    if lead and not args.no_variants:
+        extra_specs = {"motion_0.05": (W, H, F, 0, 0.05), "low_inlier_0.12": (W, H, F, 0, 0.12),
+                       "x1080": (1920, 1080, 64, 0, args.motion), "stream": (W, H, 1000, 0, args.motion)}
+    if rank == 0 and world > 1:        # rank 0 re-runs every sequence to check the gather
+        specs += [(W, H, F, s, args.motion) for s in range(S) if s not in my_seqs]
+    rendered = render_sequences(specs + list(extra_specs.values()), workers)
+    seqs = {sp[3]: (SceneSequence(W, H, nframes=F, seq=sp[3], step=args.motion), rendered[i])
+            for i, sp in enumerate(specs)}
+    extra = {tag: (rendered[len(specs) + i], SceneSequence(sp[0], sp[1], nframes=sp[2], seq=sp[3], step=sp[4]))
+             for i, (tag, sp) in enumerate(extra_specs.items())}
+    cpu = None
+    if lead and not args.no_cpu:
+        s0, fr0 = seqs[my_seqs[0]]
+        cpu = cpu_baseline(fr0, s0, args.cpu_seconds, args.max_kpts, workers)
 
     dist = dist_init(world, local)
-
     from acs_visual_odometry_amd import Context
-    from acs_visual_odometry_amd.synth import SceneSequence
 
-    seq = SceneSequence(args.width, args.height, nframes=args.frames, seq=rank, step=args.motion)
-    frames = seq.frames()
-    ctx = Context(seq.W, seq.H, K=seq.K, max_kpts=args.max_kpts, device=local, frame_batch=args.batch)
-    ctx.set_ground_truth(seq.gt())
-    dframes = ctx.device_frames(frames)
+    ctx = Context(W, H, K=seqs[my_seqs[0]][0].K, max_kpts=args.max_kpts, device=local, frame_batch=args.batch,
+                  match_bits=args.match_bits)
+    dframes = {s: ctx.device_frames(seqs[s][1]) for s in my_seqs}
+    gts = {s: seqs[s][0].gt() for s in my_seqs}
+    last = {}
 
-    def step(timing=0):
-        ctx.reset()
-        return ctx.process_frames_device(dframes, timing=timing)
+    def step(timing=0, stats=None):
+        for s in my_seqs:
+            ctx.reset()
+            ctx.set_ground_truth(gts[s])
+            last[s] = ctx.process_frames_device(dframes[s], timing=timing)
+            if stats is not None:
+                stats.append(ctx.kernel_stats())
 
     def barrier():
         if dist is not None:
@@ -177,56 +399,107 @@ def main():
 
     for _ in range(max(args.warmup, 1)):
         step()
-    # per-kernel breakdown (untimed pass): every launch bracketed by events; a launch covers
-    # frames_per_launch frames (an extract batch or a pose-pass window)
-    _, st, info = step(timing=1)
-    ks = ctx.kernel_stats()
-    per_frame = {k: (ks[k][0] / ks[k][1] if k in ks and ks[k][1] > 0 else 0.0) for k in KERNELS}
-    dominant = max(per_frame, key=lambda k: per_frame[k])
+    warm = {s: (last[s][0].copy(), last[s][1].copy()) for s in my_seqs}
+    # per-kernel breakdown (untimed): every launch bracketed by events
+    bd = []
+    step(timing=1, stats=bd)
+    ks = {k: (float(np.mean([b[k][0] for b in bd if k in b])), float(np.mean([b[k][1] for b in bd if k in b])))
+          for k in KERNELS if any(k in b for b in bd)}
+    info_all = np.concatenate([last[s][2] for s in my_seqs])
+    per_frame = {k: ks[k][0] / ks[k][1] if k in ks and ks[k][1] > 0 else 0.0 for k in KERNELS}
+    dominant = max(POSE_QUEUE, key=lambda k: per_frame[k])
     kidx = KERNELS.index(dominant)
 
     barrier()
+    live = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        poses, st, info = step(timing=100 + kidx)       # two events around the dominant kernel
+        step(timing=100 + kidx, stats=live)          # two events around every 4th dominant launch
     t1 = time.perf_counter()
     barrier()
     dt = t1 - t0
-    dom_ms, dom_fpl = ctx.kernel_stats().get(dominant, (float("nan"), float("nan")))
+    frames_rank = args.steps * F * len(my_seqs)
+    dt, value = aggregate(dist, dt, frames_rank, world, local=local)
+    repeat_equal = all(np.array_equal(warm[s][0], last[s][0]) and np.array_equal(warm[s][1], last[s][1])
+                       for s in my_seqs)
+    rows = {s: np.concatenate([last[s][0].reshape(F, 12), last[s][1].reshape(F, 1).astype(np.float64)], axis=1)
+            for s in my_seqs}
+    gathered = gather_poses(dist, rows, S, F, local=local)
+    gather_ok = None
+    if rank == 0 and world > 1:
+        gather_ok = True
+        for s in range(S):
+            if s not in my_seqs:
+                df = ctx.device_frames(seqs[s][1])
+                ctx.reset()
+                ctx.set_ground_truth(seqs[s][0].gt())
+                p, st, _ = ctx.process_frames_device(df)
+                df.free()
+            else:
+                p, st = last[s][0], last[s][1]
+            mine = np.concatenate([p.reshape(F, 12), st.reshape(F, 1).astype(np.float64)], axis=1)
+            gather_ok = gather_ok and bool(np.array_equal(mine, gathered[s]))
 
-    dt, value = aggregate(dist, dt, args.steps * args.frames, world, local=local)
+    variants = None
+    if lead and not args.no_variants:
+        s0 = my_seqs[0]
+        variants = run_variants(args, ctx, W, H, seqs[s0][1], gts[s0], extra, Context)
 
     if rank == 0:
-        abytes = algorithmic_bytes(dominant, seq.W, seq.H, info, args.max_kpts) * dom_fpl   # per launch
+        live_ms = [b[dominant][0] for b in live if dominant in b]
+        live_fpl = [b[dominant][1] for b in live if dominant in b]
+        dom_ms = float(np.mean(live_ms)) if live_ms else float("nan")
+        dom_fpl = float(np.mean(live_fpl)) if live_fpl else float("nan")
+        prof, psrc = load_profile(W, H, args.match_bits)
+        abytes = algorithmic_bytes(dominant, W, H, info_all) * dom_fpl
         achieved = abytes / (dom_ms * 1e-3) / 1e9
-        traffic, tsrc = pmc_traffic(dominant, seq.W, seq.H)
+        prow = profile_row(prof, dominant)
         roof = {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
-                "avg_launch_ms": dom_ms, "frames_per_launch": dom_fpl, "algorithmic_bytes_per_launch": abytes}
-        path_bytes = algorithmic_bytes("path", seq.W, seq.H, info, args.max_kpts)
-        cpu = None
-        if not args.no_cpu and world == 1:
-            cpu = cpu_baseline(frames, seq, args.cpu_seconds, args.max_kpts)
-        ok = int((st == 0).sum())
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": prow["hbm_bytes"] if prow else None, "traffic_source": psrc,
+                "avg_launch_ms": dom_ms, "frames_per_launch": dom_fpl, "algorithmic_bytes_per_launch": abytes,
+                "rocprof_avg_launch_us": prow["avg_us"] if prow else None,
+                "choice": "largest per-frame time among the pose-queue kernels (the serial critical path)",
+                "valu": None if not prow else {
+                    "insts_per_launch": prow["valu_insts"], "issue_frac": prow["valu_issue_frac"],
+                    "peak": f"{VALU_SIMDS} SIMDs x 1 wave64 VALU instruction / 2 cycles (PMC: SQ_INSTS_VALU, "
+                            f"GRBM_GUI_ACTIVE)"}}
+        path_bytes = algorithmic_bytes("path", W, H, info_all)
+        kern = {}
+        for k in KERNELS:
+            if k not in ks:
+                continue
+            r = profile_row(prof, k)
+            kern[k] = {"us_per_frame": round(per_frame[k] * 1e3, 4), "us_per_launch": round(ks[k][0] * 1e3, 2),
+                       "frames_per_launch": round(ks[k][1], 2),
+                       "algorithmic_bytes_per_frame": round(algorithmic_bytes(k, W, H, info_all), 1),
+                       "queue": "pose" if k in POSE_QUEUE else "extract",
+                       "pmc_hbm_bytes_per_launch": r["hbm_bytes"] if r else None,
+                       "valu_issue_frac": r["valu_issue_frac"] if r else None}
+        st_all = np.concatenate([last[s][1] for s in my_seqs])
         line = {
             "metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8/f32/u32/f64", "data": "synthetic",
-            "config": {"workload": "kitti_1241x376_2000kpts_full_path" if (seq.W, seq.H) == (1241, 376)
-                       else f"{seq.W}x{seq.H}_{args.max_kpts}kpts_full_path",
-                       "frames_per_step": args.frames, "width": seq.W, "height": seq.H,
-                       "max_kpts": args.max_kpts, "sequence": f"scene seq=rank, {args.motion} m/frame",
-                       "parallelism": f"replicas: 1 sequence per GPU x {world}",
-                       "frame_batch": ctx.cfg.frame_batch or 64,
-                       "mean_kpts": float(info[:, 0].mean()), "mean_matches": float(info[:, 1].mean()),
-                       "mean_inliers": float(info[:, 2].mean()), "mean_hypotheses": float(info[:, 4].mean()),
-                       "frames_ok": ok},
+            "scaling": "strong", "vs_baseline": None, "dtype": "u8/f32/u32/f64", "data": "synthetic",
+            "config": {"workload": ("kitti_1241x376_2000kpts_full_path" if (W, H) == (1241, 376)
+                                    else f"{W}x{H}_{args.max_kpts}kpts_full_path"),
+                       "sequences": S, "frames_per_sequence": F, "sequences_per_gpu": len(my_seqs),
+                       "width": W, "height": H, "max_kpts": args.max_kpts, "match_bits": args.match_bits,
+                       "motion": f"+{args.motion} m/frame along z, 0.1 deg/frame yaw (SURVEY 8(d) scene generator)",
+                       "parallelism": f"config 5: sequence s on GPU s mod {world}, no data-path collective",
+                       "frame_batch": ctx.cfg.frame_batch or 64, "inputs": "device-resident (HBM) before timing",
+                       "mean_kpts": float(info_all[:, 0].mean()), "mean_matches": float(info_all[:, 1].mean()),
+                       "mean_inliers": float(info_all[:, 2].mean()),
+                       "mean_hypotheses": float(info_all[:, 4].mean()),
+                       "frames_ok": int((st_all == 0).sum()), "frames": int(st_all.size)},
             "roofline": roof,
             "path_roofline": {"algorithmic_bytes_per_frame": path_bytes,
                               "achieved_GBs": path_bytes * value / world / 1e9,
                               "frac": path_bytes * value / world / 1e9 / HBM_PEAK_GBS},
-            "kernels_ms_per_frame": {k: round(v, 5) for k, v in per_frame.items()},
-            "kernels_ms_per_launch": {k: round(ks[k][0], 5) for k in KERNELS if k in ks},
+            "kernels": kern,
+            "determinism": {"timed_rows_equal_warmup_rows": bool(repeat_equal),
+                            "gathered_rows_equal_rank0_rerun": gather_ok},
+            "variants": variants,
             "cpu_baseline": cpu,
         }
         if args.breakdown:
@@ -235,7 +508,8 @@ def main():
                     print(f"{k:14s} {per_frame[k] * 1e3:9.2f} us/frame  {ks[k][0] * 1e3:9.1f} us/launch  "
                           f"{ks[k][1]:5.1f} frames/launch", file=sys.stderr)
         print(json.dumps(line))
-    dframes.free()
+    for d in dframes.values():
+        d.free()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
