@@ -159,14 +159,14 @@ int write_work0(vo_ctx* c, const VoWork* w)
 }
 
 // work[0] of a stage call: status OK, counters clear
-void stage_work(VoWork* w)
+void stage_work(VoWork* w, int ring)
 {
     std::memset(w, 0, sizeof(*w));
     w->status = VO_STATUS_OK;
     w->frame = -1;
     w->bestk = -1;
-    w->prev = VO_STAGE_SLOT;
-    w->cur = VO_STAGE_SLOT + 1;
+    w->prev = ring + 1;          // the two stage slots after the ring and the carry slot
+    w->cur = ring + 2;
 }
 
 // host frame (any stride) -> frame_in on stream `st`, via the pinned staging buffer
@@ -188,8 +188,8 @@ int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride, hipStream_t st)
 void enqueue_stage_extract(vo_ctx* c)
 {
     vo::launch_stencil(c->d, c->d.frame_in, 0, 1, 0, c->s);
-    vo::launch_select(c->d, 0, 1, VO_STAGE_SLOT, c->s);
-    vo::launch_describe(c->d, 0, 1, VO_STAGE_SLOT, 0u, c->s);
+    vo::launch_select(c->d, 0, 1, c->d.ring + 1, c->s);
+    vo::launch_describe(c->d, 0, 1, c->d.ring + 1, 0u, c->s);
 }
 
 // Timing: every timed launch is bracketed by two events on the stream it runs on (all
@@ -370,7 +370,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&c->d.st->end, end, 1, s));
     const std::vector<int> sched = batch_schedule(nf, B, hs ? VO_HOST_FIRST_BATCH : 0);
     if (!img0 && !hs) {
-        vo::launch_ext_missing(c->d, base % VO_RING, s);
+        vo::launch_ext_missing(c->d, base % c->d.ring, s);
     } else {
         int f0 = 0, j = 0;
         for (int cnt : sched) {
@@ -558,6 +558,8 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     c->B = B;
     d.B = B;
     d.W = W; d.H = H; d.N = N;
+    d.ring = VO_RING_DEFAULT;
+    if (getenv("VO_RING_SLOTS")) d.ring = std::max(2 * VO_MAX_BATCH, std::min(1 << 16, atoi(getenv("VO_RING_SLOTS"))));
     d.nms_k = k.nms_k; d.brow = k.border_row; d.bcol = k.border_col;
     d.resp_thr = k.resp_thr;
     std::memcpy(&d.thr_bits, &k.resp_thr, 4);
@@ -609,7 +611,9 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc(&d.model_p, (size_t)N * 4 * B);
     rc |= dalloc(&d.work, B);
     rc |= dalloc(&d.st, 1);
-    rc |= dalloc(&d.ext, 1);
+    rc |= dalloc(&d.ext_n, VO_SLOTS);
+    rc |= dalloc(&d.ext_st, VO_SLOTS);
+    rc |= dalloc(&d.seq_starts, VO_MAX_SEQ_STARTS);
     rc |= dalloc(&d.ctr, VO_CTR_WORDS);
 #ifdef VO_STAMPS
     rc |= dalloc(&d.dbg, (size_t)d.max_hyp * 16);
@@ -627,6 +631,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     (void)hipMemset(d.kps, 0, sizeof(int2) * N * VO_SLOTS);
     (void)hipMemset(d.desc, 0, sizeof(uint64_t) * 8 * N * VO_SLOTS);
     (void)hipMemset(d.pre, 0, sizeof(uint32_t) * N * VO_SLOTS);
+    d.n_seq_starts = 0;
     if (ensure_out(c, 16) != VO_OK) return bail(VO_ERR_HIP);
     c->klaunch.assign(vo::kernel_count(), 0);
     if (vo_reset(c) != VO_OK) return bail(VO_ERR_HIP);
@@ -643,7 +648,7 @@ void vo_destroy(vo_ctx* c)
         if (q) (void)hipStreamSynchronize(q);
     if (c->s) (void)hipStreamSynchronize(c->s);
     VoDev& d = c->d;
-    void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.tilerows, d.ckeys, d.selbits, d.hist, d.ext,
+    void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.tilerows, d.ckeys, d.selbits, d.hist, d.ext_n, d.ext_st, (void*)d.seq_starts,
                     d.kps, d.desc, d.pre, d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.inlmask,
                     d.model_p, d.work, d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr, d.dbg};
     for (void* p : ptrs)
@@ -678,6 +683,18 @@ int vo_reset(vo_ctx* c)
     return VO_OK;
 }
 
+int vo_set_sequence_starts(vo_ctx* c, const int32_t* starts, int n)
+{
+    if (!c || n < 0 || n > VO_MAX_SEQ_STARTS || (n > 0 && !starts)) return VO_ERR_ARG;
+    for (int i = 0; i < n; ++i)
+        if (starts[i] < 1 || (i > 0 && starts[i] <= starts[i - 1])) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    SYNC_ALL(c);
+    if (n) HIPCHK(hipMemcpy((void*)c->d.seq_starts, starts, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice));
+    c->d.n_seq_starts = n;
+    return VO_OK;
+}
+
 int vo_set_ground_truth(vo_ctx* c, const double* poses12, int n)
 {
     if (!c || n < 0 || (n > 0 && !poses12)) return VO_ERR_ARG;
@@ -701,18 +718,19 @@ int vo_extract(vo_ctx* c, const uint8_t* gray, size_t stride, vo_kp* kps, uint64
     HIPCHK(hipSetDevice(c->cfg.device));
     int rc = upload_frame(c, gray, stride, c->s);
     if (rc) return rc;
-    enqueue_stage_extract(c);      // slot VO_STAGE_SLOT: the trajectory's slots are untouched
+    enqueue_stage_extract(c);      // stage slot ring + 1: the trajectory's slots are untouched
     HIPCHK(hipGetLastError());
     SYNC_ALL(c);
     int32_t nk = 0, status = 0;
-    HIPCHK(hipMemcpy(&nk, &c->d.ext->n_kps[VO_STAGE_SLOT], sizeof(int32_t), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(&status, &c->d.ext->status[VO_STAGE_SLOT], sizeof(int32_t), hipMemcpyDeviceToHost));
+    const size_t stg = (size_t)c->d.ring + 1;
+    HIPCHK(hipMemcpy(&nk, &c->d.ext_n[stg], sizeof(int32_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&status, &c->d.ext_st[stg], sizeof(int32_t), hipMemcpyDeviceToHost));
     if (status != VO_STATUS_OK) return VO_ERR_CAPACITY;
     *n = nk;
     const size_t N = (size_t)c->cfg.max_kpts;
-    if (kps && nk) HIPCHK(hipMemcpy(kps, c->d.kps + VO_STAGE_SLOT * N, sizeof(vo_kp) * nk, hipMemcpyDeviceToHost));
+    if (kps && nk) HIPCHK(hipMemcpy(kps, c->d.kps + stg * N, sizeof(vo_kp) * nk, hipMemcpyDeviceToHost));
     if (desc && nk)
-        HIPCHK(hipMemcpy(desc, c->d.desc + VO_STAGE_SLOT * N * 8, sizeof(uint64_t) * 8 * nk, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(desc, c->d.desc + stg * N * 8, sizeof(uint64_t) * 8 * nk, hipMemcpyDeviceToHost));
     if (blurred)
         HIPCHK(hipMemcpy(blurred, c->d.blurred, (size_t)c->cfg.width * c->cfg.height, hipMemcpyDeviceToHost));
     return VO_OK;
@@ -746,15 +764,15 @@ int vo_match(vo_ctx* c, const uint64_t* d_prev, int n_prev, const uint64_t* d_cu
     for (int i = 0; i < n_cur; ++i) p1[i] = (uint32_t)d_cur[8 * (size_t)i];
     SYNC_ALL(c);
     const size_t N = (size_t)c->cfg.max_kpts;
-    const int a = VO_STAGE_SLOT, b = VO_STAGE_SLOT + 1;     // stage slots: the trajectory's stay intact
+    const int a = c->d.ring + 1, b = c->d.ring + 2;     // stage slots: the trajectory's stay intact
     HIPCHK(hipMemcpy(c->d.desc + a * N * 8, d_prev, sizeof(uint64_t) * 8 * n_prev, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d.desc + b * N * 8, d_cur, sizeof(uint64_t) * 8 * n_cur, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d.pre + a * N, p0.data(), sizeof(uint32_t) * n_prev, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d.pre + b * N, p1.data(), sizeof(uint32_t) * n_cur, hipMemcpyHostToDevice));
     const int nk2[2] = {n_prev, n_cur};
-    HIPCHK(hipMemcpy(c->d.ext->n_kps + a, nk2, sizeof(nk2), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d.ext_n + a, nk2, sizeof(nk2), hipMemcpyHostToDevice));
     VoWork w;
-    stage_work(&w);
+    stage_work(&w, c->d.ring);
     int rc = write_work0(c, &w);
     if (rc) return rc;
     vo::launch_match(c->d, 1, c->s);
@@ -774,7 +792,7 @@ int vo_ransac_F(vo_ctx* c, const double* pts, int m, uint64_t seed, double F[9],
     SYNC_ALL(c);
     HIPCHK(hipMemcpy(c->d.pts, pts, sizeof(double) * 4 * (size_t)m, hipMemcpyHostToDevice));
     VoWork w;
-    stage_work(&w);
+    stage_work(&w, c->d.ring);
     w.M = m;
     w.scored = (m / c->cfg.ransac_chunk_threads) * c->cfg.ransac_chunk_threads;
     w.frame_seed = seed;
@@ -813,7 +831,7 @@ int vo_pose(vo_ctx* c, const double F[9], const float* p1, const float* p2, int 
     HIPCHK(hipMemcpy(c->d.model_p, mp.data(), sizeof(float) * mp.size(), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(&c->d.st->scale_override, &scale, sizeof(double), hipMemcpyHostToDevice));
     VoWork w;
-    stage_work(&w);
+    stage_work(&w, c->d.ring);
     w.fitted = 1;
     w.n_fit = n;
     std::memcpy(w.F, F, sizeof(w.F));
@@ -889,8 +907,9 @@ int run_frames(vo_ctx* c, const uint8_t* dev, const uint8_t* host, bool pinned, 
     EvRec rec{&c->ev_pool, 0, c->timing >= 100 ? c->timing - 100 : -1, &c->klaunch, {}};
     EvRec* evp = c->timing ? &rec : nullptr;
     const int base = c->fidx;
-    for (int f0 = 0; f0 < nframes; f0 += VO_CHUNK) {
-        const int nf = std::min(VO_CHUNK, nframes - f0);
+    const int chunk = c->d.ring - 1;
+    for (int f0 = 0; f0 < nframes; f0 += chunk) {
+        const int nf = std::min(chunk, nframes - f0);
         if (host) {
             const HostSrc hs{host + (size_t)f0 * frame_bytes, frame_bytes, pinned};
             rc = run_chunk(c, nullptr, frame_bytes, nf, c->out_dev, base, evp, false, &hs);
@@ -982,8 +1001,8 @@ int vo_extract_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
     EvRec rec{&c->ev_pool, 0, c->timing >= 100 ? c->timing - 100 : -1, &c->klaunch, {}};
     EvRec* evp = c->timing ? &rec : nullptr;
     const size_t N = (size_t)c->cfg.max_kpts;
-    for (int f0 = 0; f0 < nframes; f0 += VO_RING) {
-        const int nf = std::min(VO_RING, nframes - f0);
+    for (int f0 = 0; f0 < nframes; f0 += c->d.ring) {
+        const int nf = std::min(c->d.ring, nframes - f0);
         int off = 0;
         for (int cnt : batch_schedule(nf, c->B)) {
             rc = enqueue_extract(c, d_frames + (size_t)(f0 + off) * frame_bytes, frame_bytes, off, cnt, false, c->s,
@@ -995,8 +1014,8 @@ int vo_extract_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
         if (n_kps || kps || desc) {
             HIPCHK(hipStreamSynchronize(c->s));
             std::vector<int32_t> nk(nf), stt(nf);
-            HIPCHK(hipMemcpy(nk.data(), c->d.ext->n_kps, sizeof(int32_t) * nf, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(stt.data(), c->d.ext->status, sizeof(int32_t) * nf, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(nk.data(), c->d.ext_n, sizeof(int32_t) * nf, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(stt.data(), c->d.ext_st, sizeof(int32_t) * nf, hipMemcpyDeviceToHost));
             for (int z = 0; z < nf; ++z) {
                 const size_t f = (size_t)(f0 + z);
                 if (stt[z] != VO_STATUS_OK) return VO_ERR_CAPACITY;      // top-N boundary overflow

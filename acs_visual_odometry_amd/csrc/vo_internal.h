@@ -44,15 +44,19 @@
 #define VO_TILE_H 16
 // keypoint/descriptor slots: frame f (since vo_reset) is extracted into ring slot
 // f % VO_RING; the last valid frame's copy lives in the carry slot during a skip run; the
-// stage APIs (vo_extract / vo_match) use their own two slots
-#define VO_RING 1024
-#define VO_CARRY_SLOT VO_RING
-#define VO_STAGE_SLOT (VO_RING + 1)
-#define VO_SLOTS (VO_RING + 3)
+// stage APIs (vo_extract / vo_match) use their own two slots.  The ring holds d.ring slots
+// (VO_RING_DEFAULT = 4096: 0.6 GB at N = 2000, sized for HBM; VO_RING_SLOTS overrides it, the
+// tests use small rings to exercise wrap-around)
+#define VO_RING_DEFAULT 4096
+#define VO_RING (d.ring)
+#define VO_CARRY_SLOT (d.ring)
+#define VO_STAGE_SLOT (d.ring + 1)
+#define VO_SLOTS (d.ring + 3)
 // frames per host chunk: a chunk never extracts over a slot one of its passes still reads
 // (frame f's slot is rewritten by frame f + VO_RING; passes read frames >= lo - 1)
-#define VO_CHUNK (VO_RING - 1)
+#define VO_CHUNK (d.ring - 1)
 #define VO_MAX_BATCH 64
+#define VO_MAX_SEQ_STARTS 4096     // vo_set_sequence_starts capacity
 #define VO_DEFAULT_BATCH 64
 // ctr words: cross-queue counters on lines of their own
 #define VO_EXT_QUEUES 1        // extract queues (batch j on queue j % n, own scratch); 2 measured no faster
@@ -76,11 +80,6 @@ struct VoFrameOut {
     double pose[12];
 };
 
-// Extract-side state, per keypoint/descriptor slot.
-struct VoExt {
-    int32_t n_kps[VO_SLOTS];
-    int32_t status[VO_SLOTS];   // VO_STATUS_OK, VO_STATUS_OVERFLOW (select capacity), VO_STATUS_MISSING
-};
 
 // Per-frame control state of a pose pass (one per window frame).  k_match writes the
 // header, the RANSAC launches their counters and the replay's result, k_refit the model,
@@ -165,7 +164,11 @@ struct VoDev {
     const uint16_t* maxit_tab;
     const double* gt;
     VoState* st;
-    VoExt* ext;
+    int ring;             // ring slots (VO_RING)
+    int32_t* ext_n;       // x SLOTS: keypoints extracted into the slot
+    int32_t* ext_st;      // x SLOTS: VO_STATUS_OK, VO_STATUS_OVERFLOW (select capacity), VO_STATUS_MISSING
+    const int32_t* seq_starts;   // sorted frame indices (since vo_reset) where a new sequence begins
+    int n_seq_starts;
     unsigned* ctr;
     unsigned long long* dbg;   // diagnostic s_memtime stamps (VO_STAMPS builds only)
 };

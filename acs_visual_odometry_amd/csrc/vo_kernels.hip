@@ -618,7 +618,7 @@ __device__ __forceinline__ uint32_t sel_bin(uint64_t key, uint32_t thr_bits)
 //   E  chunked block scan over the (row, tile) segments in raster order
 //   F  each selected key computes its raster position directly and writes its keypoint
 // slot of frame f0 + z of an extract batch (vo_internal.h: ring slot, or a stage slot)
-__device__ __forceinline__ int ext_slot(int f0, int z, int slot_override)
+__device__ __forceinline__ int ext_slot(const VoDev& d, int f0, int z, int slot_override)
 {
     return slot_override >= 0 ? slot_override : (f0 + z) % VO_RING;
 }
@@ -654,7 +654,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     const size_t TCAP = ST_TW * ST_TH / 4;
     if (tid == 0) {
         s_nbnd = 0; s_b = -1; s_above = 0;
-        s_slot = ext_slot(f0, z, slot_override);
+        s_slot = ext_slot(d, f0, z, slot_override);
     }
     VO_STAMP(d, 1990, 0);
     // A
@@ -919,8 +919,8 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     // select is the histogram's only reader: leave it zeroed for the next frame's stencil
     for (int i = tid; i < VO_HIST_BINS; i += 1024) hist[i] = 0u;
     if (tid == 0) {
-        d.ext->n_kps[slot] = ovf ? 0 : (C < N ? C : N);
-        d.ext->status[slot] = ovf ? VO_STATUS_OVERFLOW : VO_STATUS_OK;
+        d.ext_n[slot] = ovf ? 0 : (C < N ? C : N);
+        d.ext_st[slot] = ovf ? VO_STATUS_OVERFLOW : VO_STATUS_OK;
     }
 }
 
@@ -972,8 +972,8 @@ __device__ __forceinline__ void publish_seq(unsigned* flag, unsigned v)
 __global__ void k_ext_missing(VoDev d, int slot)
 {
     if (threadIdx.x == 0) {
-        d.ext->n_kps[slot] = 0;
-        d.ext->status[slot] = VO_STATUS_MISSING;
+        d.ext_n[slot] = 0;
+        d.ext_st[slot] = VO_STATUS_MISSING;
     }
 }
 
@@ -1110,8 +1110,8 @@ __global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int
     __shared__ uint8_t s_I1[DS_WAVES][DS_KPW][DS_I1W];
     int z, bx;
     if (xcd_frame(d, (d.N + DS_KPB - 1) / DS_KPB, nb, z, bx)) {
-        const int cur = ext_slot(f0, z, slot_override);
-        const int n = d.ext->n_kps[cur];
+        const int cur = ext_slot(d, f0, z, slot_override);
+        const int n = d.ext_n[cur];
         const int wave = threadIdx.x >> 6;
         const int base = bx * DS_KPB + wave * DS_KPW;
         if (bx * DS_KPB < n)             // workgroup-uniform: the barriers inside are met by all
@@ -1191,6 +1191,19 @@ __device__ __forceinline__ uint64_t frame_seed_of(const VoDev& d, int f)
     return mix64(d.seed + 0x632BE59BD9B4E019ULL * (uint64_t)(f + 1));
 }
 
+// First frame (since vo_reset) of the sequence holding frame f: 0, or the largest of the sorted
+// vo_set_sequence_starts entries <= f (binary search; block-uniform).  A frame is its sequence's
+// frame f - base: the FIRST status and the RANSAC sampler's frame index follow it.
+__device__ __forceinline__ int seq_base(const VoDev& d, int f)
+{
+    int lo = 0, hi = d.n_seq_starts;               // first entry > f
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (d.seq_starts[mid] <= f) lo = mid + 1; else hi = mid;
+    }
+    return lo > 0 ? d.seq_starts[lo - 1] : 0;
+}
+
 // Header of a window frame's match: slots and status (speculation: the previous frame of
 // window frame wf > 0 is frame f - 1; k_finalize re-runs f when that was skipped).  Block 0
 // initialises the frame's VoWork.  Returns false if the frame has nothing to match.
@@ -1202,15 +1215,16 @@ struct MatchFrame {
 __device__ __forceinline__ bool match_header(const VoDev& d, int stage, int wf, MatchFrame& m)
 {
     VoWork* w = d.work + wf;
-    int f, cur, prev, status = VO_STATUS_OK;
+    int f, fl = -1, cur, prev, status = VO_STATUS_OK;
     if (stage) {
         f = -1; prev = VO_STAGE_SLOT; cur = VO_STAGE_SLOT + 1;
     } else {
         f = d.st->lo + wf;
         cur = f % VO_RING;
         prev = wf == 0 ? d.st->prev_slot : (f - 1) % VO_RING;
-        const int es = d.ext->status[cur];
-        if (f == 0) status = VO_STATUS_FIRST;                 // VisualOdometry.cpp:58,64-66
+        const int es = d.ext_st[cur];
+        fl = f - seq_base(d, f);
+        if (fl == 0) status = VO_STATUS_FIRST;                 // VisualOdometry.cpp:58,64-66
         else if (es != VO_STATUS_OK) status = es;              // MISSING / OVERFLOW
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1218,12 +1232,12 @@ __device__ __forceinline__ bool match_header(const VoDev& d, int stage, int wf, 
         w->bestk = -1; w->n_eval = 0; w->n_inl = 0; w->fitted = 0; w->n_fit = 0; w->degenerate = 0;
         w->need_more = 0;
         for (int c = 0; c < 4; ++c) w->counts4[c] = 0;
-        if (!stage) w->frame_seed = frame_seed_of(d, f);
+        if (!stage) w->frame_seed = frame_seed_of(d, fl);
         if (status != VO_STATUS_OK) { w->status = status; w->M = 0; w->scored = 0; }
     }
     m.w = w; m.f = f; m.cur = cur; m.prev = prev;
-    m.n1 = d.ext->n_kps[prev];
-    m.n2 = d.ext->n_kps[cur];
+    m.n1 = d.ext_n[prev];
+    m.n2 = d.ext_n[cur];
     m.match_j = d.match_j + (size_t)wf * d.N;
     return status == VO_STATUS_OK;
 }
@@ -1748,8 +1762,18 @@ __global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, 
     const double* pts = d.pts + (size_t)wf * 4 * d.N;
     int32_t* counts = d.counts + (size_t)wf * d.max_hyp;
     int k = k0 + blockIdx.x * HPB + h;                 // (WPH > 1 only with reps == 1: s_cnt below)
+    // Hypotheses at or past the previous replay's bound are never evaluated by the sequential
+    // loop: once an improvement updated maxIterations (best > 0 and its table entry is not the
+    // 'denom == 0: no update' mark) and the loop went on past k0 (maxit > 100), the inlier ratio
+    // is in the band where maxIterations only falls as best rises (below it the x86 INT_MIN clamp
+    // gives 100, quirk 8), so maxit bounds every later hypothesis.  Otherwise maxit is still the
+    // initial 1176 and the next improvement may raise it to 2000.  Waves past the bound skip
+    // straight to the arrival.
+    int kbound = k1;
+    if (k0 > 0 && w->best > 0 && d.maxit_tab[(size_t)M * (M + 1) / 2 + w->best] != 0xFFFFu)
+        kbound = min(w->maxit, k1);
     for (int rep = 0; rep < reps; ++rep, k += gridDim.x * HPB) {
-    if (k < k1) {
+    if (k < kbound) {
         VO_STAMP(d, k, 0);
         int s8[8];
         sample8(w->frame_seed, k, M, s8);
@@ -1772,11 +1796,13 @@ __global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, 
             s_cnt[h][sw] = cnt;
         }
         VO_STAMP(d, k, 6);
+    } else if (k < k1 && sw == 0 && lane == 0) {
+        st_sc1(counts + k, -1);                    // skipped: the replay never takes it
     }
     }
     if (WPH > 1) {
         __syncthreads();
-        if (k < k1 && sw == 0 && lane == 0) {
+        if (k < kbound && sw == 0 && lane == 0) {
             int t = 0;
 #pragma unroll
             for (int w = 0; w < WPH; ++w) t += s_cnt[h][w];
@@ -1799,7 +1825,7 @@ __global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, 
     while (kk < maxit && kk < lim) {
         const int base = kk, idx = base + lane;
         const int c = idx < lim ? ld_sc1(counts + idx) : -1;
-        const int u = c >= 0 ? (int)tab[c] : 0xFFFF;
+        const int u = (c >= 0 && c <= M) ? (int)tab[c] : 0xFFFF;
         for (;;) {
             const unsigned long long bal = ballot64(idx >= kk && idx < maxit && idx < lim && c > best);
             if (bal == 0ull) {
@@ -2390,7 +2416,7 @@ __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d, int stage)
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int out_base)
 {
-    __shared__ int s_n, s_ncommit, s_lo, s_copy, s_model_wf, s_newlv, s_newprev;
+    __shared__ int s_n, s_ncommit, s_lo, s_copy, s_model_wf, s_model_clear, s_newlv, s_newprev;
     __shared__ int s_status[VO_MAX_BATCH], s_kind[VO_MAX_BATCH], s_src[VO_MAX_BATCH], s_lvb[VO_MAX_BATCH];
     __shared__ int s_flip[VO_MAX_BATCH], s_fitted[VO_MAX_BATCH], s_degen[VO_MAX_BATCH], s_cur[VO_MAX_BATCH];
     __shared__ double s_R[VO_MAX_BATCH + 1][9], s_t[VO_MAX_BATCH + 1][3];   // [B]: the model before the window
@@ -2443,7 +2469,8 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
             int s = s_status[wf], kind = 0, flip = 1;
             adv = 0;
             if (s == VO_STATUS_FIRST) {                 // :58 identity, desc1 = frame 0
-                flip = 0; adv = 1; lv = 0; prev = s_cur[wf];
+                // frame 0 of a sequence: a fresh run()'s state (T_curr = I in step 3, no model)
+                flip = 0; adv = 1; lv = f; prev = s_cur[wf]; msrc = -1;
             } else if (s == VO_STATUS_MISSING) {        // :77-82 T_curr pushed unflipped
                 flip = 0;
             } else if (s == VO_STATUS_OK) {
@@ -2462,6 +2489,7 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
         }
         s_ncommit = wf;
         if (msrc >= 0 && msrc < MB) s_model_wf = msrc;
+        s_model_clear = msrc < 0;                       // no model (never fitted, or a new sequence)
         if (!adv && prev < VO_RING) { s_copy = prev; prev = VO_CARRY_SLOT; }
         s_newlv = lv; s_newprev = prev;
     }
@@ -2501,6 +2529,8 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
                 const double a2 = __shfl(Tv, i * 4 + 2), a3 = __shfl(Tv, i * 4 + 3);
                 const double* B = s_Trel[wf];
                 Tv = ((a0 * B[0 * 4 + j] + a1 * B[1 * 4 + j]) + a2 * B[2 * 4 + j]) + a3 * B[3 * 4 + j];
+            } else if (s_status[wf] == VO_STATUS_FIRST) {
+                Tv = (e % 5 == 0) ? 1.0 : 0.0;          // VisualOdometry.cpp:57 T_curr = eye(4)
             }
             if (tid < 12) s_row[wf][tid] = (s_flip[wf] && i == 2) ? -Tv : Tv;
         }
@@ -2514,7 +2544,7 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
         VoFrameOut* o = out + (lo + tid - out_base);
         for (int r = 0; r < 12; ++r) o->pose[r] = s_row[tid][r];
         o->status = s;
-        o->n_kps = s == VO_STATUS_MISSING ? 0 : d.ext->n_kps[s_cur[tid]];
+        o->n_kps = s == VO_STATUS_MISSING ? 0 : d.ext_n[s_cur[tid]];
         o->n_matches = w->M;
         o->n_inl = w->n_inl;
         o->best_k = w->bestk;
@@ -2534,10 +2564,13 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
             for (int i = 0; i < 9; ++i) st->model_F[i] = w->F[i];
             for (int i = 0; i < 9; ++i) st->model_R[i] = s_R[m][i];
             for (int i = 0; i < 3; ++i) st->model_t[i] = s_t[m][i];
+        } else if (s_model_clear) {
+            st->model_n = 0;
+            st->model_degenerate = 0;
         }
     }
     if (s_copy >= 0) {
-        const int src = s_copy, nk = d.ext->n_kps[src];
+        const int src = s_copy, nk = d.ext_n[src];
         const size_t N = (size_t)d.N;
         for (int i = tid; i < nk; i += blockDim.x) {
             d.kps[VO_CARRY_SLOT * N + i] = d.kps[src * N + i];
@@ -2545,8 +2578,8 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
         }
         for (int i = tid; i < 8 * nk; i += blockDim.x) d.desc[VO_CARRY_SLOT * N * 8 + i] = d.desc[src * N * 8 + i];
         if (tid == 0) {
-            d.ext->n_kps[VO_CARRY_SLOT] = nk;
-            d.ext->status[VO_CARRY_SLOT] = VO_STATUS_OK;
+            d.ext_n[VO_CARRY_SLOT] = nk;
+            d.ext_st[VO_CARRY_SLOT] = VO_STATUS_OK;
         }
     }
 }
@@ -2565,8 +2598,7 @@ __global__ void __launch_bounds__(256) k_reset(VoDev d)
         for (int i = 0; i < 16; ++i) st->Tcurr[i] = (i % 5 == 0) ? 1.0 : 0.0;
         st->scale_override = __longlong_as_double(0x7FF8000000000000ll);
     }
-    int32_t* ext = reinterpret_cast<int32_t*>(d.ext);
-    for (int i = tid; i < (int)(sizeof(VoExt) / 4); i += nth) ext[i] = 0;   // n_kps 0, status OK
+    for (int i = tid; i < VO_SLOTS; i += nth) { d.ext_n[i] = 0; d.ext_st[i] = VO_STATUS_OK; }
     for (int i = tid; i < VO_HIST_BINS * d.B * VO_EXT_QUEUES; i += nth) d.hist[i] = 0u;
     uint32_t* w = reinterpret_cast<uint32_t*>(d.work);
     for (int i = tid; i < (int)(sizeof(VoWork) / 4) * d.B; i += nth) w[i] = 0u;

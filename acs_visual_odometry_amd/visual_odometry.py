@@ -109,6 +109,11 @@ class Context:
         g = np.ascontiguousarray(gt, dtype=np.float64).reshape(-1, 12)
         check(self.lib.vo_set_ground_truth(self.h, _p(g), g.shape[0]), "vo_set_ground_truth")
 
+    def set_sequence_starts(self, starts):
+        """Frames (since reset) that begin a new independent sequence (vo_set_sequence_starts)."""
+        a = np.ascontiguousarray(np.asarray(starts, dtype=np.int32).reshape(-1))
+        check(self.lib.vo_set_sequence_starts(self.h, _p(a) if a.size else None, a.size), "vo_set_sequence_starts")
+
     def reset(self):
         check(self.lib.vo_reset(self.h), "vo_reset")
 

@@ -4,16 +4,18 @@
 Workload: S = 8 synthetic KITTI-shape scene
 sequences (camera +1.0 m/frame along z, 0.1 deg/frame yaw; seed = splitmix64(0xACE0 ^ seq<<32 ^
 frame)), --frames frames each.  Sequence s runs on rank s mod G (config 5's partition: at G < 8
-a GPU runs 8/G sequences, one after another on its context).  One step = every sequence of the
-rank through the full per-frame path (blur -> response -> NMS/top-N -> orientation/descriptor ->
+a GPU runs 8/G sequences as one frame stream on its context, vo_set_sequence_starts resetting
+the trajectory at each sequence's first frame).  One step = every sequence of the rank through the
+full per-frame path (blur -> response -> NMS/top-N -> orientation/descriptor ->
 Hamming match -> 8-point RANSAC -> refit -> getPose -> trajectory update), from vo_reset, with the
 frames already resident in HBM (uploaded before the timed region).  value = all ranks' frames /
 the slowest rank's time.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process
 per GPU, no data-path collective; RCCL ("nccl") carries the barrier, the max-over-ranks time and
-one all-reduce that assembles every sequence's poses on every rank, after which rank 0 re-runs
-all sequences on its own GPU and checks the gathered rows bit for bit.
+one all-reduce that assembles every sequence's poses on every rank, after which rank 0 runs each
+sequence alone on its own GPU (one vo_reset + call per sequence, as the reference's one run() per
+sequence) and checks the gathered rows bit for bit.
 
 Also on the JSON line:
   roofline      the critical-path kernel (the largest per-frame time on the pose queue, which
@@ -364,7 +366,7 @@ def main():
     if lead and not args.no_variants:
         extra_specs = {"motion_0.05": (W, H, F, 0, 0.05), "low_inlier_0.12": (W, H, F, 0, 0.12),
                        "x1080": (1920, 1080, 64, 0, args.motion), "stream": (W, H, 1000, 0, args.motion)}
-    if rank == 0 and world > 1:        # rank 0 re-runs every sequence to check the gather
+    if rank == 0 and world > 1:        # rank 0 runs every sequence alone to check the gather
         specs += [(W, H, F, s, args.motion) for s in range(S) if s not in my_seqs]
     rendered = render_sequences(specs + list(extra_specs.values()), workers)
     seqs = {sp[3]: (SceneSequence(W, H, nframes=F, seq=sp[3], step=args.motion), rendered[i])
@@ -381,17 +383,34 @@ def main():
 
     ctx = Context(W, H, K=seqs[my_seqs[0]][0].K, max_kpts=args.max_kpts, device=local, frame_batch=args.batch,
                   match_bits=args.match_bits)
-    dframes = {s: ctx.device_frames(seqs[s][1]) for s in my_seqs}
+    # the rank's sequences as one frame stream: frames and GT rows concatenated, each sequence's
+    # first frame marked (vo_set_sequence_starts), so the next sequence's extract overlaps the
+    # previous one's last pose passes; rows are split back per sequence
+    dall = ctx.device_frames(np.concatenate([seqs[s][1] for s in my_seqs]))
     gts = {s: seqs[s][0].gt() for s in my_seqs}
+    gt_all = np.concatenate([gts[s] for s in my_seqs])
+    starts = [F * i for i in range(1, len(my_seqs))]
     last = {}
 
     def step(timing=0, stats=None):
-        for s in my_seqs:
-            ctx.reset()
-            ctx.set_ground_truth(gts[s])
-            last[s] = ctx.process_frames_device(dframes[s], timing=timing)
-            if stats is not None:
-                stats.append(ctx.kernel_stats())
+        ctx.reset()
+        ctx.set_ground_truth(gt_all)
+        ctx.set_sequence_starts(starts)
+        poses, st, info = ctx.process_frames_device(dall, timing=timing)
+        for i, s in enumerate(my_seqs):
+            last[s] = (poses[i * F:(i + 1) * F], st[i * F:(i + 1) * F], info[i * F:(i + 1) * F])
+        if stats is not None:
+            stats.append(ctx.kernel_stats())
+
+    def separate(s, frames):
+        """Sequence s alone (its own stream: the reference's one run() per sequence)."""
+        df = ctx.device_frames(frames)
+        ctx.reset()
+        ctx.set_sequence_starts([])
+        ctx.set_ground_truth(seqs[s][0].gt())
+        p, st, _ = ctx.process_frames_device(df)
+        df.free()
+        return np.concatenate([p.reshape(F, 12), st.reshape(F, 1).astype(np.float64)], axis=1)
 
     def barrier():
         if dist is not None:
@@ -425,24 +444,16 @@ def main():
     rows = {s: np.concatenate([last[s][0].reshape(F, 12), last[s][1].reshape(F, 1).astype(np.float64)], axis=1)
             for s in my_seqs}
     gathered = gather_poses(dist, rows, S, F, local=local)
+    # rank 0 runs every sequence of the job alone, as the reference would (one run() each), and
+    # checks the gathered rows of the stream(s) against them bit for bit
     gather_ok = None
-    if rank == 0 and world > 1:
-        gather_ok = True
-        for s in range(S):
-            if s not in my_seqs:
-                df = ctx.device_frames(seqs[s][1])
-                ctx.reset()
-                ctx.set_ground_truth(seqs[s][0].gt())
-                p, st, _ = ctx.process_frames_device(df)
-                df.free()
-            else:
-                p, st = last[s][0], last[s][1]
-            mine = np.concatenate([p.reshape(F, 12), st.reshape(F, 1).astype(np.float64)], axis=1)
-            gather_ok = gather_ok and bool(np.array_equal(mine, gathered[s]))
+    if rank == 0:
+        gather_ok = all(bool(np.array_equal(separate(s, seqs[s][1]), gathered[s])) for s in range(S))
 
     variants = None
     if lead and not args.no_variants:
         s0 = my_seqs[0]
+        ctx.set_sequence_starts([])
         variants = run_variants(args, ctx, W, H, seqs[s0][1], gts[s0], extra, Context)
 
     if rank == 0:
@@ -498,7 +509,7 @@ def main():
                               "frac": path_bytes * value / world / 1e9 / HBM_PEAK_GBS},
             "kernels": kern,
             "determinism": {"timed_rows_equal_warmup_rows": bool(repeat_equal),
-                            "gathered_rows_equal_rank0_rerun": gather_ok},
+                            "gathered_rows_equal_separate_runs": gather_ok},
             "variants": variants,
             "cpu_baseline": cpu,
         }
@@ -508,8 +519,7 @@ def main():
                     print(f"{k:14s} {per_frame[k] * 1e3:9.2f} us/frame  {ks[k][0] * 1e3:9.1f} us/launch  "
                           f"{ks[k][1]:5.1f} frames/launch", file=sys.stderr)
         print(json.dumps(line))
-    for d in dframes.values():
-        d.free()
+    dall.free()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

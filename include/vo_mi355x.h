@@ -117,6 +117,15 @@ int  vo_pose(vo_ctx* ctx, const double F[9], const float* p1, const float* p2, i
  * 12 doubles (KITTI 3x4 row-major).  Without it the scale is 1. */
 int  vo_set_ground_truth(vo_ctx* ctx, const double* poses12, int n);
 
+/* Independent sequences in one frame stream (config 5 on one GPU): frames starts[0..n) (counted
+ * since vo_reset, strictly ascending, >= 1) each begin a new sequence -- the trajectory state is
+ * reset there as at the start of a new VisualOdometry::run (identity pose, no model, desc1 = that
+ * frame; VisualOdometry.cpp:46-66) -- so a batched call over several sequences' frames, with their
+ * ground-truth rows concatenated in the same order, returns each sequence's own rows while the
+ * extract of the next sequence overlaps the last pose passes of the previous one.  n = 0: one
+ * sequence.  Kept across vo_reset. */
+int  vo_set_sequence_starts(vo_ctx* ctx, const int32_t* starts, int n);
+
 /* One iteration of VisualOdometry::run's loop (VisualOdometry.cpp:68-189): frame in,
  * pose out.  gray == NULL marks a missing image.  pose_out: 12 doubles, the row the
  * reference appends to estimated_poses.  info (optional, 8 ints): n_kpts, n_matches,
@@ -128,7 +137,7 @@ int  vo_process_frame(vo_ctx* ctx, const uint8_t* gray, size_t stride, double po
  * d_frames + f * frame_bytes (dense W x H u8).  Frames are extracted frame_batch at a time
  * on one queue and posed in windows of frame_batch frames on another (each frame matched
  * speculatively against its predecessor; a frame after a skipped one is re-run), with one
- * host synchronisation per VO_CHUNK = 1023 frames (more only after skipped frames).  Results
+ * host synchronisation per chunk of ring - 1 = 4095 frames (more only after skipped frames).  Results
  * are those of nframes vo_process_frame calls.  poses_out: nframes*12, status_out: nframes,
  * info_out: nframes*8 (all host, optional). */
 int  vo_process_frames_device(vo_ctx* ctx, const uint8_t* d_frames, size_t frame_bytes, int nframes,

@@ -52,6 +52,7 @@ class RefKernels:
     """One OpenCL context/queue on GPU 0 with the reference program loaded from a binary."""
 
     def __init__(self, variant: str = "strict"):
+        self.name = variant
         path = os.path.join(REF_DIR, f"fe_kernels_{variant}.co")
         if not os.path.exists(path):
             raise FileNotFoundError(path)

@@ -329,9 +329,11 @@ def test_windowed_batch_matches_oracle(blank, batch):
     _device_vs_oracle(seq, frames, frame_batch=batch)
 
 
-def test_windowed_batch_across_chunks_and_ring_wrap():
-    """1100 frames: two host chunks (VO_CHUNK = 1023) and a wrap of the 1024-slot ring, with a
-    skip run that straddles the chunk boundary (the carry slot outlives the chunk)."""
+def test_windowed_batch_across_chunks_and_ring_wrap(monkeypatch):
+    """1100 frames on a 256-slot ring (VO_RING_SLOTS; the default is 4096): five host chunks of
+    255 frames and four ring wraps, with a skip run that straddles the chunk boundary at 1020 (the
+    carry slot outlives the chunk)."""
+    monkeypatch.setenv("VO_RING_SLOTS", "256")
     seq = SceneSequence(320, 192, nframes=1100, step=0.05)
     frames = seq.frames()
     for b in range(1015, 1030):

@@ -109,9 +109,10 @@ def test_host_streaming_matches_oracle(leak_case, host, batch, monkeypatch):
     _device_run(seq, frames, ref=ref, host="pinned" if host == "pinned" else "pageable", frame_batch=batch)
 
 
-def test_host_streaming_across_chunks():
-    """1100 host frames: two host chunks, a ring wrap, and the device batch ring reused across
-    both, with a skip run over the chunk boundary."""
+def test_host_streaming_across_chunks(monkeypatch):
+    """1100 host frames on a 256-slot ring: five host chunks, ring wraps, and the device batch
+    ring reused across them, with a skip run over a chunk boundary."""
+    monkeypatch.setenv("VO_RING_SLOTS", "256")
     seq = SceneSequence(320, 192, nframes=1100, step=0.05)
     frames = seq.frames()
     for b in range(1015, 1030):
@@ -239,4 +240,50 @@ def test_config2_batched_extract():
     poses, st, info = ctx.process_frames_device(df)
     assert st[0] == 1 and info[0, 6] == 0
     df.free()
+    ctx.close()
+
+
+@pytest.mark.parametrize("batch,host", [(64, None), (8, None), (16, "pinned")])
+def test_sequence_starts(batch, host):
+    """Several independent sequences in one frame stream (vo_set_sequence_starts): each
+    sequence's rows equal its own oracle run (a fresh VisualOdometry::run), including a sequence
+    whose first frames give < 8 inliers (FEW_INLIERS before its first fit: the previous
+    sequence's model must not leak into it), a one-frame sequence and a blank frame."""
+    parts = []
+    a = SceneSequence(nframes=23, step=0.05, seq=1)
+    parts.append((a, a.frames()))
+    b_seq, b_frames = _leak_sequence()
+    parts.append((b_seq, b_frames[:40]))
+    c = SceneSequence(nframes=1, step=0.05, seq=2)
+    parts.append((c, c.frames()))
+    d = SceneSequence(nframes=17, step=0.05, seq=4)
+    df_ = d.frames()
+    df_[5] = 128
+    parts.append((d, df_))
+    refs, starts, gts, frames = [], [], [], []
+    n = 0
+    for sq, fr in parts:
+        cfg = O.config(sq.W, sq.H, K=sq.K.reshape(9))
+        vo = O.VO(cfg, gt=sq.gt()[:len(fr)])
+        refs += [vo.process(fr[f]) for f in range(len(fr))]
+        vo.close()
+        if n:
+            starts.append(n)
+        gts.append(sq.gt()[:len(fr)])
+        frames.append(fr)
+        n += len(fr)
+    frames = np.concatenate(frames)
+    ctx = Context(a.W, a.H, K=a.K, frame_batch=batch)
+    ctx.set_ground_truth(np.concatenate(gts))
+    ctx.set_sequence_starts(starts)
+    if host:
+        hf = ctx.host_frames(frames)
+        out = ctx.process_frames_host(hf)
+        hf.free()
+    else:
+        dfr = ctx.device_frames(frames)
+        out = ctx.process_frames_device(dfr)
+        dfr.free()
+    assert [out[1][s] for s in [0] + starts] == [1] * (len(starts) + 1)
+    _check(refs, *out)
     ctx.close()

@@ -123,3 +123,46 @@ def test_ref_stock_build_differences(images):
         assert flips <= 1e-3 * both.sum()
         assert common >= 0.99 * len(kps)
         assert bits < 1e-2
+
+
+def a6_agreement(variant):
+    """SURVEY A.6 secondary numbers: the reference's own compute_all_orientations (CAS-atomic
+    order) and merge_all_orientations (OCML f32 atan2/cos/sin), compiled `variant`, drive its
+    compute_all_descriptors on the oracle's keypoints and blurred images of factory1 -> factory2;
+    returns the descriptor-bit agreement with the oracle (whose f64 det-math rotations the HIP
+    path reproduces bit for bit) and the agreement of the 32-test match pairs."""
+    imgs = [read_gray(os.path.join(GOLD, f"factory{i}.png")) for i in (1, 2)]
+    out = {"variant": variant.name}
+    descs_ref, descs_our = [], []
+    bits_total = bits_same = 0
+    for k, img in enumerate(imgs):
+        H, W = img.shape
+        kps, desc, bl = O.extract(img, O.config(W, H))
+        _, _, rot_cl, dcl = variant.orient_describe(bl, kps)
+        ours = unpack_descriptor(desc)
+        bits_total += ours.size
+        bits_same += int((dcl == ours).sum())
+        descs_ref.append(np.packbits(dcl.astype(np.uint8), axis=1, bitorder="little").view(np.uint64))
+        descs_our.append(desc)
+        _, rot_or = O.describe(bl, kps, with_rot=True)
+        out[f"factory{k + 1}_keypoints"] = int(kps.shape[0])
+        out[f"factory{k + 1}_rotation_max_abs_diff"] = float(np.abs(rot_cl - rot_or).max())
+        out[f"factory{k + 1}_descriptors_identical"] = float(np.mean((dcl == ours).all(1)))
+    out["descriptor_bit_agreement"] = bits_same / bits_total
+    m_ref = O.match(descs_ref[0], descs_ref[1])
+    m_our = O.match(descs_our[0], descs_our[1])
+    a, b = set(map(tuple, m_ref)), set(map(tuple, m_our))
+    out["match_pairs_reference_driven"] = len(a)
+    out["match_pairs_oracle"] = len(b)
+    out["match_pairs_common"] = len(a & b)
+    out["match_pair_agreement"] = len(a & b) / max(1, len(a | b))
+    return out
+
+
+@pytest.mark.parametrize("name", ["strict", "stock"])
+def test_a6_reference_driven_descriptor_agreement(name):
+    v = _variant(name)
+    out = a6_agreement(v)
+    print("A.6", out)
+    assert out["descriptor_bit_agreement"] > 0.99
+    assert out["match_pair_agreement"] > 0.9
