@@ -1162,15 +1162,8 @@ __device__ __forceinline__ int ratio_accept(uint32_t m1, uint32_t m2, float rati
     return ((float)d1 < ratio * (float)d2) ? (int)(m1 & 0xFFFF) : -1;
 }
 
-// 32-bit prefix mode: the cur frame's prefixes are staged once per workgroup in LDS
-// (16 KB at N = 4096), and each wave scores MT_QPW queries per candidate read.
-#ifndef MT_UNROLL
-#define MT_UNROLL 4    // candidate loop unroll
-#endif
-#ifndef MT_QPW
-#define MT_QPW 16
-#endif
-#define MT_QPB (4 * MT_QPW)
+// 32-bit prefix mode: 64 queries per workgroup (k_match)
+#define MT_QPB 64
 #define MT512_QPB 256                 // 512-test matcher: queries per workgroup (one per thread)
 __host__ __device__ inline int match_blocks(int N, int match_bits)
 {
@@ -1306,7 +1299,19 @@ __device__ void match_compact(const VoDev& d, int wf, const MatchFrame& m, int* 
 }
 
 // 32-test matcher (the reference's quirk 1, feature_matching_parallel.cpp:39-47).
-// grid (match_blocks, B): frame wf = blockIdx.y of the window.
+// grid (match_blocks, B): frame wf = blockIdx.y of the window.  A workgroup owns 64 queries,
+// lane = query (the same 64 in each of its 4 waves); the cur frame's prefixes are staged in LDS
+// (16 KB at N = 4096) and wave w walks candidate quarter w with wave-uniform ds_read_b128s, four
+// candidates per read, keeping two top-2 key sets per lane (even / odd candidates: independent
+// chains).  The four quarters' sets merge through LDS: keys are (dist << 16 | j), so the merged
+// minimum is the first-index minimum the sequential loop keeps.
+__device__ __forceinline__ void top2_merge(uint32_t& m1, uint32_t& m2, uint32_t o1, uint32_t o2)
+{
+    const uint32_t n1v = min(m1, o1);
+    m2 = min(max(m1, o1), min(m2, o2));
+    m1 = n1v;
+}
+
 __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
 {
     const int wf = blockIdx.y;
@@ -1315,9 +1320,12 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
     if (!match_header(d, stage, wf, m)) return;
     __shared__ unsigned s_last;
     __shared__ int s_wsum[4];
-    __shared__ uint32_t s_cand[4096];
+    __shared__ uint4 s_cand4[1024];                  // 4096 prefixes
+    __shared__ uint2 s_top[3][64];
+    uint32_t* s_cand = reinterpret_cast<uint32_t*>(s_cand4);
     const int N = d.N, n1 = m.n1, n2 = m.n2;
-    const int lane = threadIdx.x & 63;
+    // wave-uniform candidate range: scalar loop counter, key index an SGPR operand
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (blockIdx.x * MT_QPB < n1) {
         const uint32_t* cand = d.pre + (size_t)m.cur * N;
         for (int j0 = threadIdx.x; j0 < n2; j0 += 4 * 256) {
@@ -1328,26 +1336,33 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
             for (int u = 0; u < 4; ++u)
                 if (j0 + u * 256 < n2) s_cand[j0 + u * 256] = v[u];
         }
-        const int q0 = blockIdx.x * MT_QPB + (threadIdx.x >> 6) * MT_QPW;
-        uint32_t qv[MT_QPW], m1[MT_QPW], m2[MT_QPW];
-#pragma unroll
-        for (int u = 0; u < MT_QPW; ++u) {
-            qv[u] = q0 + u < n1 ? d.pre[(size_t)m.prev * N + q0 + u] : 0u;
-            m1[u] = 0xFFFFFFFFu;
-            m2[u] = 0xFFFFFFFFu;
-        }
+        const int q = blockIdx.x * MT_QPB + lane;
+        const uint32_t qv = q < n1 ? d.pre[(size_t)m.prev * N + q] : 0u;
+        // quarter of the candidates: [j0, j1), j0 a multiple of 4
+        const int qs = ((n2 + 15) >> 4) << 2;
+        const int j0 = min(wave * qs, n2), j1 = min(j0 + qs, n2);
+        uint32_t a1 = 0xFFFFFFFFu, a2 = 0xFFFFFFFFu, b1 = 0xFFFFFFFFu, b2 = 0xFFFFFFFFu;
         __syncthreads();
-#pragma unroll MT_UNROLL
-        for (int j = lane; j < n2; j += 64) {
-            const uint32_t c = s_cand[j];
-#pragma unroll
-            for (int u = 0; u < MT_QPW; ++u)
-                top2_insert(((uint32_t)__popc(qv[u] ^ c) << 16) | (uint32_t)j, m1[u], m2[u]);
+        int j = j0;
+#pragma unroll 2
+        for (; j + 4 <= j1; j += 4) {
+            const uint4 c = s_cand4[j >> 2];
+            top2_insert(((uint32_t)__popc(qv ^ c.x) << 16) | (uint32_t)j, a1, a2);
+            top2_insert(((uint32_t)__popc(qv ^ c.y) << 16) | (uint32_t)(j + 1), b1, b2);
+            top2_insert(((uint32_t)__popc(qv ^ c.z) << 16) | (uint32_t)(j + 2), a1, a2);
+            top2_insert(((uint32_t)__popc(qv ^ c.w) << 16) | (uint32_t)(j + 3), b1, b2);
         }
+        for (; j < j1; ++j) top2_insert(((uint32_t)__popc(qv ^ s_cand[j]) << 16) | (uint32_t)j, a1, a2);
+        top2_merge(a1, a2, b1, b2);
+        if (wave > 0) s_top[wave - 1][lane] = make_uint2(a1, a2);
+        __syncthreads();
+        if (wave == 0) {
 #pragma unroll
-        for (int u = 0; u < MT_QPW; ++u) {
-            top2_wave(m1[u], m2[u]);
-            if (lane == 0 && q0 + u < n1) st_sc1(m.match_j + q0 + u, ratio_accept(m1[u], m2[u], d.ratio));
+            for (int w = 0; w < 3; ++w) {
+                const uint2 o = s_top[w][lane];
+                top2_merge(a1, a2, o.x, o.y);
+            }
+            if (q < n1) st_sc1(m.match_j + q, ratio_accept(a1, a2, d.ratio));
         }
     }
     if (blockIdx.x == 0) VO_STAMP(d, 1993, 1);
@@ -1463,6 +1478,7 @@ __device__ __forceinline__ double dpp_f64(double v, int ctrl_sel)
 }
 
 __device__ __forceinline__ double rdlane(double v, int l);
+
 
 __device__ __forceinline__ double wave_max_f64(double v)
 {
