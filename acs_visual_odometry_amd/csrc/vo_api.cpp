@@ -40,9 +40,9 @@ struct vo_ctx {
     int fidx = 0;                     // frames enqueued since vo_reset
     bool serial = false;              // VO_SERIAL=1: every kernel on one queue, no cross-queue
                                       // waits (for profilers that serialize dispatches: PMC passes)
-    bool event_wait = false;          // pose queue waits for extract batches on events instead of
-                                      // the stream-wait-value packet (VO_EVENT_WAIT=1, or after the
-                                      // runtime refused a wait-value packet)
+    bool event_wait = true;           // pose queue waits for extract batches on events (default)
+                                      // or on the stream-wait-value packet (VO_EVENT_WAIT=0; events
+                                      // again after the runtime refused a wait-value packet)
     // per-batch event pools of a chunk: [VO_EV_WAIT] extract done (event_wait mode),
     // [VO_EV_COPY] H2D copy done, [VO_EV_STENCIL] stencil done (host streaming)
     std::vector<hipEvent_t> ev_batch[3];
@@ -369,75 +369,86 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     }
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&c->d.st->end, end, 1, s));
     const std::vector<int> sched = batch_schedule(nf, B, hs ? VO_HOST_FIRST_BATCH : 0);
-    if (!img0 && !hs) {
-        vo::launch_ext_missing(c->d, base % c->d.ring, s);
-    } else {
-        int f0 = 0, j = 0;
-        for (int cnt : sched) {
-            const int eq = multi ? j % nq : 0;
-            hipStream_t q = multi ? c->se[eq] : s;
-            if (hs) {
-                uint8_t* dimg = nullptr;
-                hipEvent_t e_cp, e_st;
-                int rc = enqueue_h2d(c, *hs, f0, cnt, j, &dimg);
-                if (rc == VO_OK) rc = batch_event(c, VO_EV_COPY, (size_t)j, &e_cp);
-                if (rc == VO_OK) rc = batch_event(c, VO_EV_STENCIL, (size_t)j, &e_st);
-                if (rc) return rc;
-                HIPCHK(hipStreamWaitEvent(q, e_cp, 0));
-                rc = enqueue_extract(c, dimg, (size_t)c->cfg.width * c->cfg.height, base + f0, cnt, multi, q, ev, eq,
-                                     e_st);
-                if (rc) return rc;
-            } else {
-                int rc = enqueue_extract(c, img0 + (size_t)f0 * frame_bytes, frame_bytes, base + f0, cnt, multi, q,
-                                         ev, eq);
-                if (rc) return rc;
-            }
-            if (multi && c->event_wait) {
-                hipEvent_t e;
-                int rc = batch_event(c, VO_EV_WAIT, (size_t)j, &e);
-                if (rc) return rc;
-                HIPCHK(hipEventRecord(e, c->se[eq]));
-            }
-            f0 += cnt;
-            ++j;
+    // extract batch j on its queue (+ its event in event-wait mode)
+    std::vector<int> f0s(sched.size() + 1, 0);
+    for (size_t j = 0; j < sched.size(); ++j) f0s[j + 1] = f0s[j] + sched[j];
+    auto extract = [&](int j) -> int {
+        const int f0 = f0s[j], cnt = sched[j];
+        // describe publishes the extracted-frame count only for the wait-value packet
+        const bool publish = multi && !c->event_wait;
+        const int eq = multi ? j % nq : 0;
+        hipStream_t q = multi ? c->se[eq] : s;
+        if (hs) {
+            uint8_t* dimg = nullptr;
+            hipEvent_t e_cp, e_st;
+            int rc = enqueue_h2d(c, *hs, f0, cnt, j, &dimg);
+            if (rc == VO_OK) rc = batch_event(c, VO_EV_COPY, (size_t)j, &e_cp);
+            if (rc == VO_OK) rc = batch_event(c, VO_EV_STENCIL, (size_t)j, &e_st);
+            if (rc) return rc;
+            HIPCHK(hipStreamWaitEvent(q, e_cp, 0));
+            rc = enqueue_extract(c, dimg, (size_t)c->cfg.width * c->cfg.height, base + f0, cnt, publish, q, ev, eq,
+                                 e_st);
+            if (rc) return rc;
+        } else {
+            int rc = enqueue_extract(c, img0 + (size_t)f0 * frame_bytes, frame_bytes, base + f0, cnt, publish, q, ev,
+                                     eq);
+            if (rc) return rc;
         }
-    }
-    c->fidx = end;
-    {
-        // pass k waits for batch k on its queue; batch k-1 (the other queue) was waited for
-        // by pass k-1, which precedes pass k on the pose queue
-        int f1 = 0, k = 0;
-        for (int cnt : sched) {
-            f1 += cnt;
-            if (multi) {
-                const int eq = k % nq;
-                hipEvent_t e;
-                if (!c->event_wait) {
-                    const hipError_t we = hipStreamWaitValue32(s, c->d.ctr + VO_SYNC_EXT + 16 * eq,
-                                                               (uint32_t)(base + f1), hipStreamWaitValueGte,
-                                                               0xFFFFFFFFu);
-                    if (we != hipSuccess) {
-                        // the packet was refused: events from now on.  This chunk's batches are
-                        // all enqueued, so the fallback event (recorded now) covers every batch
-                        // of queue eq -- later passes of the chunk wait for them all (correct,
-                        // less overlap); later chunks record one event per batch
-                        fprintf(stderr, "[vo_mi355x] hipStreamWaitValue32 failed (%s): event waits\n",
-                                hipGetErrorString(we));
-                        (void)hipGetLastError();
-                        c->event_wait = true;
-                        int rc = batch_event(c, VO_EV_WAIT, 0, &e);
-                        if (rc) return rc;
-                        HIPCHK(hipEventRecord(e, c->se[eq]));
-                        HIPCHK(hipStreamWaitEvent(s, e, 0));
-                    }
-                } else {
+        if (multi && c->event_wait) {
+            hipEvent_t e;
+            int rc = batch_event(c, VO_EV_WAIT, (size_t)j, &e);
+            if (rc) return rc;
+            HIPCHK(hipEventRecord(e, c->se[eq]));
+        }
+        return VO_OK;
+    };
+    // pass k waits for batch k on its queue; batch k-1 (the other queue) was waited for by pass
+    // k-1, which precedes pass k on the pose queue
+    auto pass = [&](int k) -> int {
+        if (multi) {
+            const int eq = k % nq;
+            hipEvent_t e;
+            if (!c->event_wait) {
+                const hipError_t we = hipStreamWaitValue32(s, c->d.ctr + VO_SYNC_EXT + 16 * eq,
+                                                           (uint32_t)(base + f0s[k + 1]), hipStreamWaitValueGte,
+                                                           0xFFFFFFFFu);
+                if (we != hipSuccess) {
+                    // the packet was refused: events from now on.  The fallback event, recorded
+                    // now, covers every batch of queue eq enqueued so far (correct, less overlap);
+                    // later batches record one event each
+                    fprintf(stderr, "[vo_mi355x] hipStreamWaitValue32 failed (%s): event waits\n",
+                            hipGetErrorString(we));
+                    (void)hipGetLastError();
+                    c->event_wait = true;
                     int rc = batch_event(c, VO_EV_WAIT, (size_t)k, &e);
                     if (rc) return rc;
+                    HIPCHK(hipEventRecord(e, c->se[eq]));
                     HIPCHK(hipStreamWaitEvent(s, e, 0));
                 }
+            } else {
+                int rc = batch_event(c, VO_EV_WAIT, (size_t)k, &e);
+                if (rc) return rc;
+                HIPCHK(hipStreamWaitEvent(s, e, 0));
             }
-            enqueue_pass(c, out, out_base, ev, cnt);
-            ++k;
+        }
+        enqueue_pass(c, out, out_base, ev, sched[k]);
+        return VO_OK;
+    };
+    if (!img0 && !hs) {
+        vo::launch_ext_missing(c->d, base % c->d.ring, s);
+        c->fidx = end;
+        int rc = pass(0);
+        if (rc) return rc;
+    } else {
+        // enqueue order: the extract queue one batch ahead of the pose queue, so pass k is
+        // queued as soon as batch k is (all extracts first would hold the first pass back by
+        // the host time of every extract launch of the chunk)
+        int rc = extract(0);
+        if (rc) return rc;
+        c->fidx = end;
+        for (size_t k = 0; k < sched.size(); ++k) {
+            if (k + 1 < sched.size() && (rc = extract((int)k + 1)) != VO_OK) return rc;
+            if ((rc = pass((int)k)) != VO_OK) return rc;
         }
     }
     // every pass commits at least its first frame, so nf re-pass rounds bound the loop
@@ -580,7 +591,10 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     int rc = VO_OK;
     auto bail = [&](int r) { vo_destroy(c); return r; };
     c->serial = getenv("VO_SERIAL") && atoi(getenv("VO_SERIAL")) != 0;
-    c->event_wait = getenv("VO_EVENT_WAIT") && atoi(getenv("VO_EVENT_WAIT")) != 0;
+    // the pose queue waits for extract batches on events by default (barrier packets the queue
+    // processes itself); VO_EVENT_WAIT=0 selects the stream-wait-value packet on the describe
+    // counter, which ROCm runs as a polling blit kernel (measured equal or slightly slower)
+    c->event_wait = !(getenv("VO_EVENT_WAIT") && atoi(getenv("VO_EVENT_WAIT")) == 0);
     d.xcd_map = getenv("VO_XCD") ? atoi(getenv("VO_XCD")) : 1;
     if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
     for (hipStream_t& q : c->se)

@@ -2417,6 +2417,21 @@ __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d, int stage)
                                __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// lane 4q + k of each quad -> every lane of the quad (DPP quad_perm [k, k, k, k])
+__device__ __forceinline__ double dpp_quad_bcast(double v, int k)
+{
+    const long long x = __double_as_longlong(v);
+    const int lo = (int)(x & 0xFFFFFFFFll), hi = (int)(x >> 32);
+    int lo2, hi2;
+    switch (k) {
+    case 0: lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0x00, 0xF, 0xF, false); hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0x00, 0xF, 0xF, false); break;
+    case 1: lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0x55, 0xF, 0xF, false); hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0x55, 0xF, 0xF, false); break;
+    case 2: lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0xAA, 0xF, 0xF, false); hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0xAA, 0xF, 0xF, false); break;
+    default: lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0xFF, 0xF, 0xF, false); hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0xFF, 0xF, 0xF, false); break;
+    }
+    return __longlong_as_double(((long long)hi2 << 32) | (unsigned)lo2);
+}
+
 // ---------------------------------------------------------------------------
 // finalize: the trajectory loop's bookkeeping over the window, in frame order
 // (VisualOdometry.cpp:68-189, PoseUpdate.hpp:142-178).  One workgroup:
@@ -2473,8 +2488,16 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
         for (int i = 0; i < 16; ++i) s_T[i] = st->Tcurr[i];
     }
     __syncthreads();
-    // 1
-    if (tid == 0) {
+    // 1 (wave 0): frame wf's inputs sit in lane wf; the rules run on wave-uniform scalar state,
+    //   reading lane wf by v_readlane and writing frame wf's results into lane wf (one wave,
+    //   no LDS round trip per frame)
+    if (tid < 64) {
+        const int lane = tid;
+        const int st_l = lane < n ? s_status[lane] : 0;
+        const int fit_l = lane < n ? s_fitted[lane] : 0;
+        const int dg_l = lane < n ? s_degen[lane] : 0;
+        const int cur_l = lane < n ? s_cur[lane] : 0;
+        int o_s = st_l, o_kind = 0, o_flip = 1, o_src = 0, o_lvb = 0;
         int lv = st->last_valid, prev = st->prev_slot;
         int msrc = st->model_n >= 8 ? MB : -1;          // MB: the model fitted before this window
         const int mdeg = st->model_degenerate;
@@ -2482,32 +2505,39 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
         for (; wf < n; ++wf) {
             if (wf > 0 && !adv) break;                  // matched against frame f-1, which was not desc1
             const int f = lo + wf;
-            int s = s_status[wf], kind = 0, flip = 1;
+            int s = __builtin_amdgcn_readlane(st_l, wf), kind = 0, flip = 1, lvb = 0, src = 0;
+            const int cur = __builtin_amdgcn_readlane(cur_l, wf);
             adv = 0;
             if (s == VO_STATUS_FIRST) {                 // :58 identity, desc1 = frame 0
                 // frame 0 of a sequence: a fresh run()'s state (T_curr = I in step 3, no model)
-                flip = 0; adv = 1; lv = f; prev = s_cur[wf]; msrc = -1;
+                flip = 0; adv = 1; lv = f; prev = cur; msrc = -1;
             } else if (s == VO_STATUS_MISSING) {        // :77-82 T_curr pushed unflipped
                 flip = 0;
             } else if (s == VO_STATUS_OK) {
-                if (s_fitted[wf]) msrc = wf;            // fit() ran: the model is this frame's
+                if (__builtin_amdgcn_readlane(fit_l, wf)) msrc = wf;   // fit() ran: the model is this frame's
                 if (msrc < 0) {
                     s = VO_STATUS_FEW_INLIERS;          // :147-153 (no model was ever fitted)
                 } else {
-                    s_lvb[wf] = lv;                     // :161-166 precede getPose
-                    lv = f; prev = s_cur[wf]; adv = 1;
-                    s_src[wf] = msrc;
-                    const int dg = msrc == MB ? mdeg : s_degen[msrc];
+                    lvb = lv;                           // :161-166 precede getPose
+                    lv = f; prev = cur; adv = 1;
+                    src = msrc;
+                    const int dg = msrc == MB ? mdeg : __builtin_amdgcn_readlane(dg_l, msrc);
                     if (dg) s = VO_STATUS_DEGENERATE; else kind = 1;
                 }
             }                                           // FEW_MATCHES / OVERFLOW: :108-115
-            s_status[wf] = s; s_kind[wf] = kind; s_flip[wf] = flip;
+            if (lane == wf) { o_s = s; o_kind = kind; o_flip = flip; o_src = src; o_lvb = lvb; }
         }
-        s_ncommit = wf;
-        if (msrc >= 0 && msrc < MB) s_model_wf = msrc;
-        s_model_clear = msrc < 0;                       // no model (never fitted, or a new sequence)
-        if (!adv && prev < VO_RING) { s_copy = prev; prev = VO_CARRY_SLOT; }
-        s_newlv = lv; s_newprev = prev;
+        if (lane < n) {
+            s_status[lane] = o_s; s_kind[lane] = o_kind; s_flip[lane] = o_flip; s_src[lane] = o_src;
+            s_lvb[lane] = o_lvb;
+        }
+        if (lane == 0) {
+            s_ncommit = wf;
+            if (msrc >= 0 && msrc < MB) s_model_wf = msrc;
+            s_model_clear = msrc < 0;                   // no model (never fitted, or a new sequence)
+            if (!adv && prev < VO_RING) { s_copy = prev; prev = VO_CARRY_SLOT; }
+            s_newlv = lv; s_newprev = prev;
+        }
     }
     __syncthreads();
     const int nc = s_ncommit;
@@ -2538,11 +2568,13 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
     // 3
     if (tid < 64) {
         const int e = tid & 15, i = e >> 2, j = e & 3;
+        (void)i;
         double Tv = s_T[e];
         for (int wf = 0; wf < nc; ++wf) {
             if (s_kind[wf] == 1) {
-                const double a0 = __shfl(Tv, i * 4 + 0), a1 = __shfl(Tv, i * 4 + 1);
-                const double a2 = __shfl(Tv, i * 4 + 2), a3 = __shfl(Tv, i * 4 + 3);
+                // row i of T_curr: entry k from lane 4i + k of the quad (DPP quad broadcast)
+                const double a0 = dpp_quad_bcast(Tv, 0), a1 = dpp_quad_bcast(Tv, 1);
+                const double a2 = dpp_quad_bcast(Tv, 2), a3 = dpp_quad_bcast(Tv, 3);
                 const double* B = s_Trel[wf];
                 Tv = ((a0 * B[0 * 4 + j] + a1 * B[1 * 4 + j]) + a2 * B[2 * 4 + j]) + a3 * B[3 * 4 + j];
             } else if (s_status[wf] == VO_STATUS_FIRST) {

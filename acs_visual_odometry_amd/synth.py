@@ -140,8 +140,14 @@ def render_sequences(specs, workers: int = 1):
         flat = [_render(t) for t in tasks]
     else:
         import multiprocessing as mp
-        with mp.get_context("fork").Pool(workers) as pool:
+        # close + join (not the context manager's terminate): workers exit normally, no SIGTERM
+        # (a profiler preloaded into the forked workers handles SIGTERM badly)
+        pool = mp.get_context("fork").Pool(workers)
+        try:
             flat = pool.map(_render, tasks, chunksize=max(1, len(tasks) // (4 * workers)))
+        finally:
+            pool.close()
+            pool.join()
     out, k = [], 0
     for (W, H, n, s, st) in specs:
         out.append(np.stack(flat[k:k + n]))

@@ -204,8 +204,12 @@ def cpu_baseline(frames, seq, budget_s: float, max_kpts: int, procs: int) -> dic
                         f"each pass), oracle/vo_oracle.c in one process, {one_dt:.1f} s"}
     if procs <= 1:
         return dict(single, cpu_model=cpu_model())
-    with mp.get_context("fork").Pool(procs) as pool:
+    pool = mp.get_context("fork").Pool(procs)
+    try:
         res = pool.map(_cpu_worker, [budget_s] * procs)
+    finally:
+        pool.close()                       # workers exit normally (no terminate / SIGTERM)
+        pool.join()
     done = sum(r[0] for r in res)
     dt = max(r[1] for r in res)
     return {"value": done / dt, "unit": "frames/s", "cores": procs, "kind": "port",

@@ -90,11 +90,13 @@ def test_finalize_leak_and_few_inliers_paths(leak_case, batch):
     _device_run(seq, frames, ref=ref, frame_batch=batch)
 
 
-def test_event_wait_fallback(leak_case, monkeypatch):
-    """VO_EVENT_WAIT=1: the pose queue waits for extract batches on events (the fallback taken
-    when the runtime refuses hipStreamWaitValue32); results are unchanged."""
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_cross_queue_wait_modes(leak_case, monkeypatch, mode):
+    """The pose queue waits for extract batches on events (VO_EVENT_WAIT=1, the default, also
+    the fallback when the runtime refuses a wait-value packet) or on a stream-wait-value packet
+    on the describe counter (VO_EVENT_WAIT=0); results are the same."""
     seq, frames, ref = leak_case
-    monkeypatch.setenv("VO_EVENT_WAIT", "1")
+    monkeypatch.setenv("VO_EVENT_WAIT", mode)
     _device_run(seq, frames, ref=ref, frame_batch=16)
 
 

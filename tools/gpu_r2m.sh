@@ -1,0 +1,12 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r2m; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for r in 1 2; do
+timeout -k 10 300 python -u bench.py --no-cpu --no-variants > $O/b.json 2> $O/b.err || { echo BENCH_FAIL; tail $O/b.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/b.json'));print(round(d['value']), d['ms_per_step'])"
+done
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/tr -o trace -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-variants > $O/tr.json 2>&1 || { echo TRACE_FAIL; tail $O/tr.json; exit 1; }
+python3 tools/pass_timeline.py $O/tr/trace_kernel_trace.csv | head -30
