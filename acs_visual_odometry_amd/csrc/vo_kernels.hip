@@ -2451,10 +2451,11 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
     __shared__ int s_status[VO_MAX_BATCH], s_kind[VO_MAX_BATCH], s_src[VO_MAX_BATCH], s_lvb[VO_MAX_BATCH];
     __shared__ int s_flip[VO_MAX_BATCH], s_fitted[VO_MAX_BATCH], s_degen[VO_MAX_BATCH], s_cur[VO_MAX_BATCH];
     __shared__ double s_R[VO_MAX_BATCH + 1][9], s_t[VO_MAX_BATCH + 1][3];   // [B]: the model before the window
-    __shared__ double s_Trel[VO_MAX_BATCH][16];
+    __shared__ double s_Trel[VO_MAX_BATCH + 2][16];   // + 2: step 3 reads two frames ahead
     __shared__ double s_row[VO_MAX_BATCH][12];
     __shared__ double s_T[16];
     const int tid = threadIdx.x;
+    VO_STAMP(d, 1996, 7);
     VoState* st = d.st;
     if (tid == 0) {
         const int lo = st->lo;
@@ -2465,6 +2466,7 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
         s_model_wf = -1;
     }
     __syncthreads();
+    VO_STAMP(d, 1996, 0);
     const int n = s_n, lo = s_lo;
     if (n <= 0) return;
     const int MB = VO_MAX_BATCH;
@@ -2488,58 +2490,63 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
         for (int i = 0; i < 16; ++i) s_T[i] = st->Tcurr[i];
     }
     __syncthreads();
-    // 1 (wave 0): frame wf's inputs sit in lane wf; the rules run on wave-uniform scalar state,
-    //   reading lane wf by v_readlane and writing frame wf's results into lane wf (one wave,
-    //   no LDS round trip per frame)
+    VO_STAMP(d, 1996, 1);
+    // 1 (wave 0, lane = window frame): the sequential rules as prefix operations over ballots --
+    //   the model source of a frame is its latest fit, unless a sequence start (FIRST) came
+    //   after it; desc1 / last_valid advance on FIRST and on OK frames with a model; the commit
+    //   stops after the first frame that did not advance (the next one was matched against it)
     if (tid < 64) {
         const int lane = tid;
-        const int st_l = lane < n ? s_status[lane] : 0;
-        const int fit_l = lane < n ? s_fitted[lane] : 0;
-        const int dg_l = lane < n ? s_degen[lane] : 0;
-        const int cur_l = lane < n ? s_cur[lane] : 0;
-        int o_s = st_l, o_kind = 0, o_flip = 1, o_src = 0, o_lvb = 0;
-        int lv = st->last_valid, prev = st->prev_slot;
-        int msrc = st->model_n >= 8 ? MB : -1;          // MB: the model fitted before this window
+        const bool in = lane < n;
+        const int s0 = in ? s_status[lane] : -1;
+        const int cur_l = in ? s_cur[lane] : 0;
+        const int dg_l = in ? s_degen[lane] : 0;
+        const bool first = s0 == VO_STATUS_FIRST;
+        const bool ok = s0 == VO_STATUS_OK;
+        const bool fitok = ok && s_fitted[lane];
+        const unsigned long long Mfirst = ballot64(first), Mfit = ballot64(fitok);
+        const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);   // bits <= lane
+        const unsigned long long below = (1ull << lane) - 1ull;                          // bits < lane
+        auto hibit = [](unsigned long long x) { return x ? 63 - __clzll((long long)x) : -1; };
+        const int msrc0 = st->model_n >= 8 ? MB : -1;   // MB: the model fitted before this window
         const int mdeg = st->model_degenerate;
-        int wf = 0, adv = 1;
-        for (; wf < n; ++wf) {
-            if (wf > 0 && !adv) break;                  // matched against frame f-1, which was not desc1
-            const int f = lo + wf;
-            int s = __builtin_amdgcn_readlane(st_l, wf), kind = 0, flip = 1, lvb = 0, src = 0;
-            const int cur = __builtin_amdgcn_readlane(cur_l, wf);
-            adv = 0;
-            if (s == VO_STATUS_FIRST) {                 // :58 identity, desc1 = frame 0
-                // frame 0 of a sequence: a fresh run()'s state (T_curr = I in step 3, no model)
-                flip = 0; adv = 1; lv = f; prev = cur; msrc = -1;
-            } else if (s == VO_STATUS_MISSING) {        // :77-82 T_curr pushed unflipped
-                flip = 0;
-            } else if (s == VO_STATUS_OK) {
-                if (__builtin_amdgcn_readlane(fit_l, wf)) msrc = wf;   // fit() ran: the model is this frame's
-                if (msrc < 0) {
-                    s = VO_STATUS_FEW_INLIERS;          // :147-153 (no model was ever fitted)
-                } else {
-                    lvb = lv;                           // :161-166 precede getPose
-                    lv = f; prev = cur; adv = 1;
-                    src = msrc;
-                    const int dg = msrc == MB ? mdeg : __builtin_amdgcn_readlane(dg_l, msrc);
-                    if (dg) s = VO_STATUS_DEGENERATE; else kind = 1;
-                }
-            }                                           // FEW_MATCHES / OVERFLOW: :108-115
-            if (lane == wf) { o_s = s; o_kind = kind; o_flip = flip; o_src = src; o_lvb = lvb; }
+        const int lfit = hibit(Mfit & upto), lfirst = hibit(Mfirst & upto);
+        const int msrc_l = lfit > lfirst ? lfit : (lfirst >= 0 ? -1 : msrc0);
+        const int dgv = __shfl(dg_l, msrc_l >= 0 && msrc_l < MB ? msrc_l : 0);
+        const int dg = msrc_l == MB ? mdeg : (msrc_l >= 0 ? dgv : 0);
+        const bool okm = ok && msrc_l >= 0;
+        const bool adv = first || okm;
+        const unsigned long long Madv = ballot64(in && adv);
+        int o_s = s0;
+        if (ok) o_s = !okm ? VO_STATUS_FEW_INLIERS : (dg ? VO_STATUS_DEGENERATE : VO_STATUS_OK);   // :147-153
+        const int lv0 = st->last_valid, prev0 = st->prev_slot;
+        const int la = hibit(Madv & below);
+        if (in) {
+            s_status[lane] = o_s;
+            s_kind[lane] = (okm && !dg) ? 1 : 0;
+            s_flip[lane] = (first || s0 == VO_STATUS_MISSING) ? 0 : 1;   // :58, :79 unflipped
+            s_src[lane] = msrc_l;
+            s_lvb[lane] = la >= 0 ? lo + la : lv0;      // :161-166 precede getPose
         }
-        if (lane < n) {
-            s_status[lane] = o_s; s_kind[lane] = o_kind; s_flip[lane] = o_flip; s_src[lane] = o_src;
-            s_lvb[lane] = o_lvb;
-        }
+        // commit point: after the first frame (of frames 0 .. n-2) that did not advance
+        const unsigned long long nadv = ~Madv & (n >= 64 ? ~0ull : ((1ull << n) - 1ull)) &
+                                        ((1ull << (n - 1)) - 1ull);
+        const int nc = nadv ? __ffsll((long long)nadv) : n;        // (lowest bit) + 1
+        const unsigned long long Mc = nc >= 64 ? ~0ull : ((1ull << nc) - 1ull);
+        const int lend = hibit(Madv & Mc);
+        const int cur_end = __shfl(cur_l, lend >= 0 ? lend : 0);
+        const int msrc_end = __shfl(msrc_l, nc - 1);
         if (lane == 0) {
-            s_ncommit = wf;
-            if (msrc >= 0 && msrc < MB) s_model_wf = msrc;
-            s_model_clear = msrc < 0;                   // no model (never fitted, or a new sequence)
-            if (!adv && prev < VO_RING) { s_copy = prev; prev = VO_CARRY_SLOT; }
+            int lv = lend >= 0 ? lo + lend : lv0, prev = lend >= 0 ? cur_end : prev0;
+            s_ncommit = nc;
+            if (msrc_end >= 0 && msrc_end < MB) s_model_wf = msrc_end;
+            s_model_clear = msrc_end < 0;               // no model (never fitted, or a new sequence)
+            if (!((Madv >> (nc - 1)) & 1ull) && prev < VO_RING) { s_copy = prev; prev = VO_CARRY_SLOT; }
             s_newlv = lv; s_newprev = prev;
         }
     }
     __syncthreads();
+    VO_STAMP(d, 1996, 2);
     const int nc = s_ncommit;
     // 2
     if (tid < nc && s_kind[tid] == 1) {
@@ -2565,26 +2572,41 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
         T[12] = 0.0; T[13] = 0.0; T[14] = 0.0; T[15] = 1.0;
     }
     __syncthreads();
-    // 3
+    VO_STAMP(d, 1996, 3);
+    // 3 (wave 0): the frame kinds as wave-uniform bit masks, T_rel columns read from LDS two
+    //   frames ahead, so each step's critical path is the quad broadcasts and the four products
     if (tid < 64) {
         const int e = tid & 15, i = e >> 2, j = e & 3;
-        (void)i;
+        const bool inc = tid < nc;
+        const unsigned long long Mkind = ballot64(inc && s_kind[tid] == 1);
+        const unsigned long long Mfirst = ballot64(inc && s_status[tid] == VO_STATUS_FIRST);
+        const unsigned long long Mflip = ballot64(inc && s_flip[tid] != 0);
         double Tv = s_T[e];
+        const double ident = (e % 5 == 0) ? 1.0 : 0.0;  // VisualOdometry.cpp:57 T_curr = eye(4)
+        double b[3][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) b[u][k] = s_Trel[u][k * 4 + j];
+        // branch-free: every step computes the product and selects (s_Trel rows past nc are
+        // never used); the loads of frame wf + 2 are unconditional
         for (int wf = 0; wf < nc; ++wf) {
-            if (s_kind[wf] == 1) {
-                // row i of T_curr: entry k from lane 4i + k of the quad (DPP quad broadcast)
-                const double a0 = dpp_quad_bcast(Tv, 0), a1 = dpp_quad_bcast(Tv, 1);
-                const double a2 = dpp_quad_bcast(Tv, 2), a3 = dpp_quad_bcast(Tv, 3);
-                const double* B = s_Trel[wf];
-                Tv = ((a0 * B[0 * 4 + j] + a1 * B[1 * 4 + j]) + a2 * B[2 * 4 + j]) + a3 * B[3 * 4 + j];
-            } else if (s_status[wf] == VO_STATUS_FIRST) {
-                Tv = (e % 5 == 0) ? 1.0 : 0.0;          // VisualOdometry.cpp:57 T_curr = eye(4)
-            }
-            if (tid < 12) s_row[wf][tid] = (s_flip[wf] && i == 2) ? -Tv : Tv;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) b[2][k] = s_Trel[wf + 2][k * 4 + j];
+            // row i of T_curr: entry k from lane 4i + k of the quad (DPP quad broadcast)
+            const double a0 = dpp_quad_bcast(Tv, 0), a1 = dpp_quad_bcast(Tv, 1);
+            const double a2 = dpp_quad_bcast(Tv, 2), a3 = dpp_quad_bcast(Tv, 3);
+            const double pv = ((a0 * b[0][0] + a1 * b[0][1]) + a2 * b[0][2]) + a3 * b[0][3];
+            const bool kind = (Mkind >> wf) & 1ull, firstf = (Mfirst >> wf) & 1ull;
+            Tv = kind ? pv : (firstf ? ident : Tv);
+            if (tid < 12) s_row[wf][tid] = (((Mflip >> wf) & 1ull) && i == 2) ? -Tv : Tv;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { b[0][k] = b[1][k]; b[1][k] = b[2][k]; }
         }
         if (tid < 16) s_T[tid] = Tv;
     }
     __syncthreads();
+    VO_STAMP(d, 1996, 4);
     // 4
     if (tid < nc) {
         const VoWork* w = d.work + tid;
@@ -2617,6 +2639,7 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
             st->model_degenerate = 0;
         }
     }
+    VO_STAMP(d, 1996, 5);
     if (s_copy >= 0) {
         const int src = s_copy, nk = d.ext_n[src];
         const size_t N = (size_t)d.N;
