@@ -256,9 +256,9 @@ int enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, 
                     hipStream_t q, EvRec* ev, int eq, hipEvent_t ev_stencil = nullptr)
 {
     VoDev d = c->d;
-    const size_t B = (size_t)c->B, np = (size_t)d.W * d.H;
+    const size_t B = (size_t)c->B;
     d.eq = eq;
-    d.blurred += np * B * eq;
+    d.blurred += d.bplane * B * eq;
     d.cand += (size_t)d.cand_cap * B * eq;
     d.tilerows += (size_t)d.ntiles * 16 * B * eq;
     d.ckeys += (size_t)d.cand_cap * B * eq;
@@ -604,7 +604,9 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     if (d.sel_lds < 0) return bail(VO_ERR_HIP);
     const size_t np = (size_t)W * H;
     rc |= dalloc(&d.frame_in, np);
-    rc |= dalloc(&d.blurred, np * B * VO_EXT_QUEUES);
+    d.bstride = vo_blur_stride(W);
+    d.bplane = (size_t)d.bstride * vo_blur_rows(H);
+    rc |= dalloc(&d.blurred, d.bplane * B * VO_EXT_QUEUES);
     rc |= dalloc(&d.response, np);
     rc |= dalloc(&d.cand, (size_t)d.cand_cap * B * VO_EXT_QUEUES);
     rc |= dalloc(&d.tilerows, (size_t)ntiles * 16 * B * VO_EXT_QUEUES);
@@ -746,7 +748,8 @@ int vo_extract(vo_ctx* c, const uint8_t* gray, size_t stride, vo_kp* kps, uint64
     if (desc && nk)
         HIPCHK(hipMemcpy(desc, c->d.desc + stg * N * 8, sizeof(uint64_t) * 8 * nk, hipMemcpyDeviceToHost));
     if (blurred)
-        HIPCHK(hipMemcpy(blurred, c->d.blurred, (size_t)c->cfg.width * c->cfg.height, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy2D(blurred, (size_t)c->cfg.width, c->d.blurred, (size_t)c->d.bstride, (size_t)c->cfg.width,
+                           (size_t)c->cfg.height, hipMemcpyDeviceToHost));
     return VO_OK;
 }
 

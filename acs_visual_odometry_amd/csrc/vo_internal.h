@@ -14,7 +14,8 @@
 // cl::Buffer per frame, corner_detection_parallel_GPU.cpp:45-49,85 and
 // FREAK_feature_descriptor_parallel_GPU.cpp:53-78).  x B = one copy per frame of a batch.
 //   frame_in    u8  W*H            staging for host-supplied frames
-//   blurred     u8  W*H      x B   7x7 Gaussian output (read back by describe)
+//   blurred     u8  Wb*Hb    x B   7x7 Gaussian output (read back by describe); rows of
+//                                  Wb = whole stencil strips, Hb = whole tiles + 4 rows
 //   response    f32 W*H            optional dense R map (debug / parity only)
 //   cand        u64 192/tile x B   NMS survivors per 48x16 tile, key = Rbits<<32 | row<<16 | col
 //   tilerows    u8  16/tile  x B   survivors per tile row (select emits raster order from them)
@@ -42,6 +43,11 @@
 #define VO_HIST_BINS 4096
 #define VO_TILE_W 48       // stencil tile = one wave's strip width x 16 rows (k_stencil ST_TW, ST_TH)
 #define VO_TILE_H 16
+#define VO_STRIP_W 96      // stencil strip = one wave: two tiles side by side
+// blurred plane of a W x H frame: row stride and rows (every stencil wave stores whole rows of
+// its strip, up to 4 rows past its segment)
+inline int vo_blur_stride(int W) { return ((W + 2 * VO_TILE_W - 1) / (2 * VO_TILE_W)) * VO_STRIP_W; }
+inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_TILE_H + 4; }
 // keypoint/descriptor slots: frame f (since vo_reset) is extracted into ring slot
 // f % VO_RING; the last valid frame's copy lives in the carry slot during a skip run; the
 // stage APIs (vo_extract / vo_match) use their own two slots.  The ring holds d.ring slots
@@ -140,7 +146,9 @@ struct VoDev {
     int ntiles;
     int gt_n;
     uint8_t* frame_in;
-    uint8_t* blurred;     // x B
+    uint8_t* blurred;     // x B: bplane bytes per frame, rows of bstride
+    int bstride;
+    size_t bplane;
     float* response;
     uint64_t* cand;       // x B: per stencil tile up to 192 keys in tile-local raster order
     uint8_t* tilerows;    // x B: per stencil tile the candidate count of each of its 16 rows

@@ -8,6 +8,7 @@
 // small-f64 bound.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "vo_internal.h"
 #include "../../include/vo_freak_tables.h"
@@ -349,22 +350,28 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // stencil: blur7x7 -> gradients -> 5x5 response -> strict 3x3 NMS candidates
 // kernels/feature_extraction_kernel_functions.c:43-120, corner_detection_parallel_GPU.cpp:146-180
 //
-// Column-streaming form: one wave owns a strip of ST_TW = 48 output columns and walks down a
-// segment of ST_SEG = 64 output rows.  Lane L holds column x = xs - 7 + L in every stage, so
-// the 7 halo columns on each side cost 16 of the 64 lanes.  Vertical neighbours are register
-// histories (one new source row per step), horizontal neighbours are DPP wave shifts; there
-// is no LDS and no barrier.  Source row k of the segment (y = ys - 7 + k) completes blurred
-// row ys - 10 + k, gradient row ys - 11 + k, response row ys - 13 + k and NMS row ys - 14 + k;
-// 78 source rows give the 64 output rows.  Every stage but the response is exact integer
-// arithmetic, so the order of its sums is free.
+// Column-streaming form: one wave owns a strip of ST_SW = 96 output columns (two 48-column
+// tiles) and walks down a segment of 16 SEGT output rows.  Lane L holds the column PAIR
+// c0 = xs - 8 + 2L, c0 + 1 in every stage (128 columns: the strip, 7 halo columns on each
+// side, 18 spare).  Vertical neighbours are register histories (one new source row per step);
+// horizontal neighbours are the lane's other column or a DPP wave shift (v_mov_b32_dpp
+// wave_shr:1 / wave_shl:1), so a shift serves two columns.  No LDS, no barrier.
+// Source row k of the segment (y = ys - 7 + k) completes blurred row ys - 10 + k, gradient
+// row ys - 11 + k, response row ys - 13 + k and NMS row ys - 14 + k: 14 prologue rows, then
+// 16 rows per tile.  Every stage but the response is exact integer arithmetic, so the order
+// of its sums is free; the vertical blur runs on both columns at once in 16-bit halves.
+// The wave's row and column conditions are uniform branches or lane masks, so the scalar
+// unit (one per CU, shared by its four SIMDs) stays well below the VALU's issue rate.
 // ---------------------------------------------------------------------------
-#define ST_TW VO_TILE_W                // tile / strip width (output columns per wave): 48
+#define ST_TW VO_TILE_W                // tile width: 48
 #define ST_TH VO_TILE_H                // tile height (select reads 16 row counts per tile)
+#define ST_SW VO_STRIP_W               // strip width = two tiles: 96 output columns per wave
 #define ST_HALO 7                      // blur 3 + gradient 1 + window 2 + nms 1
+#define ST_TCAP (ST_TW * ST_TH / 4)    // candidates per tile (strict maxima: at most 1 in 4)
 #ifndef ST_SEGT_DEFAULT
-#define ST_SEGT_DEFAULT 4              // tiles per wave segment (VO_STSEG picks 4 / 6 / 8)
+#define ST_SEGT_DEFAULT 4              // tiles per wave segment (VO_STSEG picks 2 / 4 / 6 / 8)
 #endif
-static_assert(ST_TW + 2 * ST_HALO <= 64, "strip + halo within one wave");
+static_assert(ST_SW + 2 * ST_HALO + 1 <= 128, "strip + halo within one wave of column pairs");
 
 __device__ __forceinline__ int refl101(int i, int n)
 {
@@ -389,8 +396,6 @@ __device__ __forceinline__ int from_right(int v)
     return r;
 }
 
-// SEGT tiles (16 SEGT output rows) per wave, source rows in unrolled blocks of U; rows past
-// the segment's 16 SEGT + 14 in the last block only feed masked outputs
 // XCD-aware workgroup -> (frame, workgroup of the frame) for the extract kernels: a 1-D grid of
 // nx * ceil8(nb) workgroups.  Workgroup L is dispatched to XCD L % 8 (round-robin; used for
 // speed only, MI355X_MICROARCH.md "Dispatch order ... block->XCD map"), so with d.xcd_map frame z's
@@ -411,144 +416,303 @@ __device__ __forceinline__ bool xcd_frame(const VoDev& d, int nx, int nb, int& z
 }
 __host__ inline int xcd_grid(int nx, int nb) { return nx * ((nb + 7) / 8) * 8; }
 
-template <int SEGT, int U>
+// correctly rounded sqrtf for the response's argument: integer-valued (0 or |x| >= 1: every
+// term of tr * tr - 4 det is an integer-valued f32) or negative (NaN).  v_sqrt_f32 is within
+// 1 ulp; one residual test on each neighbour rounds it (the compiler's own sqrtf expansion
+// without its denormal scaling and its 0 / inf class test, which this range never needs).
+__device__ __forceinline__ float sqrt_cr_intval(float x)
+{
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __int_as_float(__float_as_int(s) - 1), sp = __int_as_float(__float_as_int(s) + 1);
+    const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
+    float r = rm <= 0.0f ? sm : s;
+    r = rp > 0.0f ? sp : r;
+    return r;
+}
+// kernel .c:108-114 (f32, in the reference's order)
+__device__ __forceinline__ float st_response(int sx, int sy, int ss)
+{
+    const float jx2 = (float)sx, jy2 = (float)sy, sxy = (float)ss;
+    const float det = (jx2 * jy2) - (sxy * sxy);
+    const float tr = jx2 + jy2;
+    // tr / 2 == tr * 0.5 exactly (both the correctly rounded halving)
+    return (tr * 0.5f) - (0.5f * sqrt_cr_intval(tr * tr - 4.0f * det));
+}
+
+typedef unsigned short st_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ st_u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(st_u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(st_u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+// wave shifts of 16-bit values (the range lets the blur's products use the 24-bit multiplier)
+__device__ __forceinline__ int from_left16(int v)
+{
+    const int r = from_left(v);
+    __builtin_assume((unsigned)r < 65536u);
+    return r;
+}
+__device__ __forceinline__ int from_right16(int v)
+{
+    const int r = from_right(v);
+    __builtin_assume((unsigned)r < 65536u);
+    return r;
+}
+// f(integral_constant<int, I>) for I = 0 .. N-1, unrolled at compile time
+template <typename F, int... I>
+__device__ __forceinline__ void st_for(F&& f, std::integer_sequence<int, I...>)
+{
+    (f(std::integral_constant<int, I>{}), ...);
+}
+#define ST_BUF_DW3 0x00020000      // gfx9 buffer descriptor word 3 (raw bytes, no format)
+
+// grid xcd_grid(ceil(waves / 4), nb): 4 waves per workgroup, one (strip, segment) per wave
+template <int SEGT, bool DBG>
 __global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restrict__ img0, size_t frame_bytes,
                                                   int write_response, int nb)
 {
-    constexpr int ST_SEGT = SEGT, ST_SEG = ST_TH * SEGT, ST_ROWS = ST_SEG + 2 * ST_HALO, ST_U = U;
+    constexpr int SEG = ST_TH * SEGT;
     const int W = d.W, H = d.H;
-    const int ntx = (W + ST_TW - 1) / ST_TW, nty = (H + ST_TH - 1) / ST_TH;
-    const int nseg = (nty + ST_SEGT - 1) / ST_SEGT;
+    const int ntx = (W + ST_TW - 1) / ST_TW, nsx = (ntx + 1) / 2, nty = (H + ST_TH - 1) / ST_TH;
+    const int nseg = (nty + SEGT - 1) / SEGT;
     // frame z of the batch (its image and its scratch copy), workgroup bx of the frame
     int z, bx;
-    if (!xcd_frame(d, (ntx * nseg + 3) / 4, nb, z, bx)) return;
+    if (!xcd_frame(d, (nsx * nseg + 3) / 4, nb, z, bx)) return;
     const int g = bx * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
-    if (g >= ntx * nseg) return;
-    const int strip = g % ntx, seg = g / ntx;
+    if (g >= nsx * nseg) return;
+    const int sxi = g % nsx, seg = g / nsx;
     const int lane = threadIdx.x & 63;
-    const uint8_t* __restrict__ img = img0 + (size_t)z * frame_bytes;
-    uint8_t* __restrict__ blurred = d.blurred + (size_t)z * W * H;
+    // image rows and blurred rows through buffer descriptors: the row offset is a scalar
+    // operand of the access (no per-row address arithmetic), and a lane whose offset is past
+    // the plane (the halo lanes' stores) is dropped by the range check
+    const __amdgpu_buffer_rsrc_t rimg =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(img0 + (size_t)z * frame_bytes), 0, W * H, ST_BUF_DW3);
+    const __amdgpu_buffer_rsrc_t rblur =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(d.blurred + (size_t)z * d.bplane), 0, (int)d.bplane, ST_BUF_DW3);
     uint64_t* __restrict__ cand = d.cand + (size_t)z * d.cand_cap;
     uint8_t* __restrict__ tilerows = d.tilerows + (size_t)z * d.ntiles * ST_TH;
     uint32_t* __restrict__ hist = d.hist + (size_t)z * VO_HIST_BINS;
-    float* __restrict__ response = d.response;
+    const int Wb = d.bstride;
 
-    const int xs = strip * ST_TW, ys = seg * ST_SEG;
-    const int x = xs - ST_HALO + lane;
-    const uint32_t xl = (uint32_t)refl101(x, W);              // BORDER_REFLECT_101 column
-    const int yend = min(ys + ST_SEG, H);                     // image rows of this segment
-    const int tend = min(ys + ST_SEG, nty * ST_TH);           // tile rows of this segment
-    const bool out_lane = lane >= ST_HALO && lane < ST_HALO + ST_TW && x < W;
-    const bool gx_ok = x >= 1 && x <= W - 2;                  // kernel .c:59-76
-    const bool rx_ok = x >= 2 && x <= W - 3;                  // kernel .c:97-114
-    const int hk = d.nms_k / 2;
-    const bool nx_ok = out_lane && x >= hk && x < W - hk && x >= d.bcol && x <= W - d.bcol;
+    const int xs = sxi * ST_SW, ys = seg * SEG;
+    const int c0 = xs - 8 + 2 * lane;                          // this lane's columns: c0, c0 + 1
+    const int xl0 = refl101(c0, W), xl1 = refl101(c0 + 1, W);  // BORDER_REFLECT_101
+    const bool out_lane = lane >= 4 && lane < 4 + ST_SW / 2;  // columns xs .. xs + 95
+    const int boff = out_lane ? c0 : 0x40000000;               // blurred store: out of range off the strip
+    const bool isB = lane >= 4 + ST_TW / 2;                   // the strip's second tile
+    const bool hasB = 2 * sxi + 1 < ntx;
+    // the wave's columns reach the image's outer two columns, where gradients (kernel .c:59-76)
+    // are 0: the lane masks apply only then
+    const bool colfix = xs - 8 < 2 || xs + 120 > W - 2;
+    const bool g0 = c0 >= 1 && c0 <= W - 2, g1 = c0 + 1 >= 1 && c0 + 1 <= W - 2;
+    // lane masks folded into lane constants, so a row's tests are one compare each: responses
+    // outside 2 <= j <= W-3 are 0 (kernel .c:97-114): their threshold is +inf; an NMS centre
+    // outside the margin meets a neighbour maximum of INT_MAX
     const float thr = d.resp_thr;
+    const float thr0 = c0 >= 2 && c0 <= W - 3 ? thr : __builtin_inff();
+    const float thr1 = c0 + 1 >= 2 && c0 + 1 <= W - 3 ? thr : __builtin_inff();
+    const int hk = d.nms_k / 2;
+    auto ncol = [&](int x) { return out_lane && x >= hk && x < W - hk && x >= d.bcol && x <= W - d.bcol; };
+    const int nmsk0 = ncol(c0) ? 0 : 0x7FFFFFFF, nmsk1 = ncol(c0 + 1) ? 0 : 0x7FFFFFFF;
+    const int nlo = max(hk, d.brow), nhi = max(nlo, min(H - hk, H - d.brow + 1));   // NMS rows [nlo, nhi)
     const uint32_t thr_bits = d.thr_bits;
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    constexpr unsigned long long mA = 0x000000000FFFFFF0ull;   // lanes 4..27: tile 2 sxi
+    constexpr unsigned long long mB = 0x000FFFFFF0000000ull;   // lanes 28..51: tile 2 sxi + 1
 
-    // register histories (index 0 oldest)
-    int s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0;          // source rows
-    int ba = 0, bm = 0, be = 0;                                          // blurred rows
-    int qx0 = 0, qx1 = 0, qx2 = 0, qx3 = 0, qx4 = 0, vx = 0;             // Jx^2 rows + vertical sum
-    int qy0 = 0, qy1 = 0, qy2 = 0, qy3 = 0, qy4 = 0, vy = 0;             // Jy^2
-    int qs0 = 0, qs1 = 0, qs2 = 0, qs3 = 0, qs4 = 0, vs = 0;             // Jxy
-    float ru = 0.0f, rm = 0.0f, rd = 0.0f;                               // response rows
-    int toff = 0;                                                        // candidates so far in the tile
+    // register histories (index 0 oldest); source rows packed: column c0 low half, c0 + 1 high
+    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0;
+    int ba0 = 0, bm0 = 0, be0 = 0, ba1 = 0, bm1 = 0, be1 = 0;               // blurred rows
+    int qx0[5] = {0, 0, 0, 0, 0}, qx1[5] = {0, 0, 0, 0, 0}, vx0 = 0, vx1 = 0;   // Jx^2 rows, vertical sums
+    int qy0[5] = {0, 0, 0, 0, 0}, qy1[5] = {0, 0, 0, 0, 0}, vy0 = 0, vy1 = 0;   // Jy^2
+    int qs0[5] = {0, 0, 0, 0, 0}, qs1[5] = {0, 0, 0, 0, 0}, vs0 = 0, vs1 = 0;   // Jxy
+    int ru0 = 0, rm0 = 0, rd0 = 0, ru1 = 0, rm1 = 0, rd1 = 0;               // response rows (f32 bits)
+    int toffA = 0, toffB = 0;                                                // candidates so far per tile
+    int trows = 0;                                                           // lane r (16 + r): tile A (B) row r count
 
-    for (int k0 = 0; k0 < ST_ROWS; k0 += ST_U) {
-        // every load of the block in flight before the first use
-        uint32_t src[ST_U];
-#pragma unroll
-        for (int u = 0; u < ST_U; ++u) {
-            const int yr = refl101(ys - ST_HALO + k0 + u, H);
-            src[u] = img[(uint32_t)yr * (uint32_t)W + xl];                 // frames < 2^32 px
+    // lane u of the result: byte offset of source row ys - 7 + k0 + u (u < 16)
+    auto row_offsets = [&](int k0) {
+        const int y = refl101(ys - ST_HALO + k0 + (lane & 15), H);
+        return y * W;                                          // frames < 2^31 px
+    };
+    auto load = [&](int soff) -> uint32_t {
+        const uint32_t a = __builtin_amdgcn_raw_buffer_load_b8(rimg, xl0, soff, 0);
+        const uint32_t b = __builtin_amdgcn_raw_buffer_load_b8(rimg, xl1, soff, 0);
+        return a | (b << 16);
+    };
+
+    // one source row through every stage that is live at step k (P: 1 blur, 2 + gradients,
+    // 3 + blurred store, 4 + response, 5 + NMS of tile row R)
+    auto step = [&](auto PH, int k, uint32_t src, auto R) {
+        constexpr int P = decltype(PH)::value;
+        constexpr int r = decltype(R)::value;
+        s0 = s1; s1 = s2; s2 = s3; s3 = s4; s4 = s5; s5 = s6; s6 = src;
+        if constexpr (P >= 1) {
+            // 1. 7x7 blur (cv::GaussianBlur 8U fixed point, A.1): vertical taps on both columns
+            //    in 16-bit halves (<= 65280), horizontal taps from the pair and its neighbours,
+            //    one rounding: (sum k_i k_j I + 2^15) >> 16
+            const st_u16x2 v = (as_u16x2(s0) + as_u16x2(s6)) * (unsigned short)8 +
+                               (as_u16x2(s1) + as_u16x2(s5)) * (unsigned short)28 +
+                               (as_u16x2(s2) + as_u16x2(s4)) * (unsigned short)56 + as_u16x2(s3) * (unsigned short)72;
+            const int va = (int)(as_u32(v) & 0xFFFFu), vb = (int)(as_u32(v) >> 16);
+            const int aL1 = from_left16(va), bL1 = from_left16(vb), aR1 = from_right16(va), bR1 = from_right16(vb);
+            const int bL2 = from_left16(bL1), aR2 = from_right16(aR1);
+            const int ha = 8 * (bL2 + bR1) + 28 * (aL1 + aR1) + 56 * (bL1 + vb) + 72 * va;   // < 2^24
+            const int hb = 8 * (aL1 + aR2) + 28 * (bL1 + bR1) + 56 * (va + aR1) + 72 * vb;
+            const int b0 = (ha + 32768) >> 16, b1 = (hb + 32768) >> 16;
+            ba0 = bm0; bm0 = be0; be0 = b0;
+            ba1 = bm1; bm1 = be1; be1 = b1;
+            if constexpr (P >= 3) {
+                // blurred row ys - 10 + k: the plane is padded to whole strips and 4 rows past the
+                // last tile, so every output lane stores (rows past the segment are the next
+                // segment's, the same values)
+                __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(b0 | (b1 << 8)), rblur, boff,
+                                                      (ys - 10 + k) * Wb, 0);
+            }
         }
-#pragma unroll
-        for (int u = 0; u < ST_U; ++u) {
-            const int k = k0 + u;
-            s0 = s1; s1 = s2; s2 = s3; s3 = s4; s4 = s5; s5 = s6; s6 = (int)src[u];
-            // 1. 7x7 blur (cv::GaussianBlur 8U fixed point, A.1): vertical taps in registers,
-            //    horizontal taps by wave shifts, one rounding: (sum k_i k_j I + 2^15) >> 16
-            const int vb = (int)(__umul24(8u, s0 + s6) + __umul24(28u, s1 + s5) + __umul24(56u, s2 + s4) + __umul24(72u, s3));     // <= 65280
-            const int l1 = from_left(vb), l2 = from_left(l1), l3 = from_left(l2);
-            const int r1 = from_right(vb), r2 = from_right(r1), r3 = from_right(r2);
-            const int hb = (int)(__umul24(8u, l3 + r3) + __umul24(28u, l2 + r2) + __umul24(56u, l1 + r1) + __umul24(72u, vb));   // < 2^24
-            const int b = (hb + 32768) >> 16;
-            const int yb = ys - 10 + k;
-            if (yb >= ys && yb < yend && out_lane) blurred[(uint32_t)yb * (uint32_t)W + (uint32_t)x] = (uint8_t)b;
-            ba = bm; bm = be; be = b;
-            // 2. gradients of row yb - 1 (kernel .c:59-76), 0 outside 1<=i<=H-2, 1<=j<=W-2; the
-            //    reference's f32 values are these integers (all below 2^11)
-            const int yg = yb - 1;
-            const int dv = ba - be, sv = (ba + 2 * bm) + be;
-            const int dl = from_left(dv), dr = from_right(dv), sl = from_left(sv), sr = from_right(sv);
-            const bool gm = gx_ok && yg >= 1 && yg <= H - 2;
-            const int jx = gm ? (dl + 2 * dv) + dr : 0;
-            const int jy = gm ? sl - sr : 0;
-            const int jxy = gm ? dl - dr : 0;
+        if constexpr (P >= 2) {
+            // 2. gradients of row yg (kernel .c:59-76), 0 outside 1 <= i <= H-2, 1 <= j <= W-2;
+            //    the reference's f32 values are these integers (all below 2^11)
+            const int yg = ys - 11 + k;
+            const int dv0 = ba0 - be0, sv0 = (ba0 + 2 * bm0) + be0;
+            const int dv1 = ba1 - be1, sv1 = (ba1 + 2 * bm1) + be1;
+            const int dL = from_left(dv1), dR = from_right(dv0), sL = from_left(sv1), sR = from_right(sv0);
+            int jx0 = (dL + 2 * dv0) + dv1, jy0 = sL - sv1, jxy0 = dL - dv1;
+            int jx1 = (dv0 + 2 * dv1) + dR, jy1 = sv0 - sR, jxy1 = dv0 - dR;
+            if (colfix) {
+                if (!g0) jx0 = jy0 = jxy0 = 0;
+                if (!g1) jx1 = jy1 = jxy1 = 0;
+            }
+            if ((unsigned)(yg - 1) > (unsigned)(H - 3)) jx0 = jy0 = jxy0 = jx1 = jy1 = jxy1 = 0;
             // 3. 5x5 window sums (kernel .c:97-107): |J| <= 512 after the blur, so a sum of 25
             //    squares is below 2^24 and the in-order f32 sum is this integer sum
-            const int qx = __mul24(jx, jx), qy = __mul24(jy, jy);
-            vx += qx - qx0; qx0 = qx1; qx1 = qx2; qx2 = qx3; qx3 = qx4; qx4 = qx;
-            vy += qy - qy0; qy0 = qy1; qy1 = qy2; qy2 = qy3; qy3 = qy4; qy4 = qy;
-            vs += jxy - qs0; qs0 = qs1; qs1 = qs2; qs2 = qs3; qs3 = qs4; qs4 = jxy;
-            int sx, sy, ss;
-            {
-                const int a1 = from_left(vx), c1 = from_right(vx);
-                sx = ((vx + a1) + c1) + (from_left(a1) + from_right(c1));
-                const int a2 = from_left(vy), c2 = from_right(vy);
-                sy = ((vy + a2) + c2) + (from_left(a2) + from_right(c2));
-                const int a3 = from_left(vs), c3 = from_right(vs);
-                ss = ((vs + a3) + c3) + (from_left(a3) + from_right(c3));
+            const int x20 = __mul24(jx0, jx0), y20 = __mul24(jy0, jy0);
+            const int x21 = __mul24(jx1, jx1), y21 = __mul24(jy1, jy1);
+            vx0 += x20 - qx0[0]; vy0 += y20 - qy0[0]; vs0 += jxy0 - qs0[0];
+            vx1 += x21 - qx1[0]; vy1 += y21 - qy1[0]; vs1 += jxy1 - qs1[0];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                qx0[i] = qx0[i + 1]; qy0[i] = qy0[i + 1]; qs0[i] = qs0[i + 1];
+                qx1[i] = qx1[i + 1]; qy1[i] = qy1[i + 1]; qs1[i] = qs1[i + 1];
             }
-            // 4. response of row yg - 2 (kernel .c:108-114), threshold (corner_detection_parallel_GPU.h:25)
-            const int yr = yg - 2;
-            float out = 0.0f;
-            if (yr >= 2 && yr <= H - 3) {
-                const float jx2 = (float)sx, jy2 = (float)sy, sxy = (float)ss;
-                const float det = (jx2 * jy2) - (sxy * sxy);
-                const float tr = jx2 + jy2;
-                // tr / 2 == tr * 0.5 exactly (both the correctly rounded halving)
-                const float rv = (tr * 0.5f) - (0.5f * sqrtf(tr * tr - 4.0f * det));
-                out = (rx_ok && rv > thr) ? rv : 0.0f;
+            qx0[4] = x20; qy0[4] = y20; qs0[4] = jxy0;
+            qx1[4] = x21; qy1[4] = y21; qs1[4] = jxy1;
+        }
+        if constexpr (P >= 4) {
+            // horizontal 5-sums: column c0 takes c0-2 .. c0+2 = the left pair, its own pair and
+            // the right lane's c0; column c0 + 1 the left lane's c0 + 1, its pair, the right pair
+            auto box = [](int a, int b, int& sa, int& sb) {
+                const int p = a + b;
+                sa = (from_left(p) + p) + from_right(a);
+                sb = (from_left(b) + p) + from_right(p);
+            };
+            int sxa, sxb, sya, syb, ssa, ssb;
+            box(vx0, vx1, sxa, sxb);
+            box(vy0, vy1, sya, syb);
+            box(vs0, vs1, ssa, ssb);
+            // 4. response of row yr (kernel .c:108-114), 0 outside 2 <= i <= H-3, 2 <= j <= W-3
+            const int yr = ys - 13 + k;
+            const bool rrow = (unsigned)(yr - 2) <= (unsigned)(H - 5);
+            const float rv0 = st_response(sxa, sya, ssa), rv1 = st_response(sxb, syb, ssb);
+            const int o0 = ((rv0 > thr0) & rrow) ? __float_as_int(rv0) : 0;
+            const int o1 = ((rv1 > thr1) & rrow) ? __float_as_int(rv1) : 0;
+            if constexpr (DBG) {
+                if (write_response && yr >= ys && yr < min(ys + SEG, H) && out_lane) {
+                    float* R = d.response + (size_t)yr * W;
+                    const float w0 = write_response == 2 ? (float)sxa : write_response == 3 ? (float)sya
+                                   : write_response == 4 ? (float)ssa : __int_as_float(o0);
+                    const float w1 = write_response == 2 ? (float)sxb : write_response == 3 ? (float)syb
+                                   : write_response == 4 ? (float)ssb : __int_as_float(o1);
+                    if (c0 < W) R[c0] = w0;
+                    if (c0 + 1 < W) R[c0 + 1] = w1;
+                }
             }
-            if (write_response == 1 && yr >= ys && yr < yend && out_lane)
-                response[(size_t)yr * W + x] = out;
-            if (write_response > 1 && yr >= ys && yr < yend && out_lane)
-                response[(size_t)yr * W + x] = write_response == 2 ? (float)sx : write_response == 3 ? (float)sy : write_response == 4 ? (float)ss : write_response == 5 ? (float)vx : (float)qx4;
-            ru = rm; rm = rd; rd = out;
-            // 5. strict 3x3 NMS of row yr - 1 inside the retinal margin
+            ru0 = rm0; rm0 = rd0; rd0 = o0;
+            ru1 = rm1; rm1 = rd1; rd1 = o1;
+        }
+        if constexpr (P >= 5) {
+            // 5. strict 3x3 NMS of row yn = tile row r inside the retinal margin
             //    (corner_detection_parallel_GPU.cpp:152-180): any neighbour >= the centre rejects
-            //    it (responses are never NaN: 0 or above the threshold)
-            const int yn = yr - 1;
-            if (yn >= ys && yn < tend) {
-                // responses are +0 or above resp_thr >= 0 (vo_create): their bit patterns order
-                // as the values do, so the window maximum is an integer max3
-                const int iu = __float_as_int(ru), im = __float_as_int(rm), id = __float_as_int(rd);
-                const int cm = max(max(iu, im), id);
-                const int cl = from_left(cm), cr = from_right(cm);
-                const int nb = max(max(cl, cr), max(iu, id));
-                const bool row_ok = yn < H && yn >= hk && yn < H - hk && yn >= d.brow && yn <= H - d.brow;
-                const bool mx = nx_ok && row_ok && nb < im;
-                const unsigned long long bal = ballot64(mx);
-                const int r = yn & (ST_TH - 1);
-                const int tile = (yn / ST_TH) * ntx + strip;
-                if (r == 0) toff = 0;
-                if (lane == 0) tilerows[tile * ST_TH + r] = (uint8_t)__popcll(bal);
-                if (mx) {
-                    // tile-local raster order: rows before this one, then lanes (= columns) before
-                    const int off = toff + __popcll(bal & lt_mask);
-                    const uint32_t bits = __float_as_uint(rm);
-                    cand[(size_t)tile * (ST_TW * ST_TH / 4) + off] =
-                        ((uint64_t)bits << 32) | ((uint64_t)yn << 16) | (uint64_t)x;
-                    uint32_t bin = (bits - thr_bits) >> 15;
-                    if (bin > VO_HIST_BINS - 1) bin = VO_HIST_BINS - 1;
+            //    it; responses are +0 or above resp_thr >= 0 (vo_create), so their bit patterns
+            //    order as the values do and the window maximum is an integer max3
+            const int yn = ys - 14 + k;
+            const int cm0 = max(max(ru0, rm0), rd0), cm1 = max(max(ru1, rm1), rd1);
+            const int cL = from_left(cm1), cR = from_right(cm0);
+            const int nb0 = max(max(cL, cm1), max(max(ru0, rd0), nmsk0));
+            const int nb1 = max(max(cm0, cR), max(max(ru1, rd1), nmsk1));
+            const bool rok = (unsigned)(yn - nlo) < (unsigned)(nhi - nlo);
+            const bool mx0 = (nb0 < rm0) & rok, mx1 = (nb1 < rm1) & rok;
+            const unsigned long long b0 = ballot64(mx0), b1 = ballot64(mx1);
+            const int cA = __popcll(b0 & mA) + __popcll(b1 & mA);
+            const int cB = __popcll(b0 & mB) + __popcll(b1 & mB);
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(trows) : "s"(cA), "n"(r));
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(trows) : "s"(cB), "n"(16 + r));
+            if (b0 | b1) {
+                // tile-local raster order: rows before this one, then columns before: the lower
+                // lanes' pairs, and c0 before c0 + 1
+                const uint32_t pos0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32),
+                                      __builtin_amdgcn_mbcnt_lo((uint32_t)b1,
+                                      __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32),
+                                      __builtin_amdgcn_mbcnt_lo((uint32_t)b0, 0u))));
+                const uint32_t base = (uint32_t)(isB ? ST_TCAP + toffB - cA : toffA) + pos0;
+                const int tileA = (yn / ST_TH) * ntx + 2 * sxi;
+                char* __restrict__ tc = (char*)(cand + (size_t)tileA * ST_TCAP);
+                const uint32_t key_lo = ((uint32_t)yn << 16) | (uint32_t)c0;
+                if (mx0) {
+                    *(uint64_t*)(tc + base * 8u) = ((uint64_t)(uint32_t)rm0 << 32) | key_lo;
+                    const uint32_t bin = min(((uint32_t)rm0 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1));
                     atomicAdd(&hist[bin], 1u);
                 }
-                toff += __popcll(bal);
+                if (mx1) {
+                    *(uint64_t*)(tc + (base + (mx0 ? 1u : 0u)) * 8u) = ((uint64_t)(uint32_t)rm1 << 32) | (key_lo + 1u);
+                    const uint32_t bin = min(((uint32_t)rm1 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1));
+                    atomicAdd(&hist[bin], 1u);
+                }
             }
+            toffA += cA; toffB += cB;
         }
+    };
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    using P2 = std::integral_constant<int, 2>;
+    using P3 = std::integral_constant<int, 3>;
+    using P4 = std::integral_constant<int, 4>;
+    using P5 = std::integral_constant<int, 5>;
+    using R0 = std::integral_constant<int, 0>;
+
+    // prologue: source rows ys-7 .. ys+6 (blurred rows from ys-4, gradients from ys-3,
+    // responses from ys-1: what the segment's first NMS row needs); then the first 8 rows of
+    // the main loop are requested
+    constexpr int LA = 8;                                      // source rows in flight ahead of the step
+    uint32_t ahead[LA];
+    {
+        const int rows = row_offsets(0);
+        uint32_t src[14];
+        st_for([&](auto U) { src[U] = load(__builtin_amdgcn_readlane(rows, U)); }, std::make_integer_sequence<int, 14>{});
+        const int rows2 = row_offsets(14);
+        st_for([&](auto U) { ahead[U] = load(__builtin_amdgcn_readlane(rows2, U)); }, std::make_integer_sequence<int, LA>{});
+        st_for([&](auto U) { step(P0{}, U, src[U], R0{}); }, std::make_integer_sequence<int, 6>{});
+        step(P1{}, 6, src[6], R0{});
+        step(P1{}, 7, src[7], R0{});
+        step(P2{}, 8, src[8], R0{});
+        step(P2{}, 9, src[9], R0{});
+        step(P3{}, 10, src[10], R0{});
+        step(P3{}, 11, src[11], R0{});
+        step(P4{}, 12, src[12], R0{});
+        step(P4{}, 13, src[13], R0{});
+    }
+    // one tile row group (16 rows) per iteration; the last segment may hold fewer tiles.  Row
+    // k0 + u + LA is requested as row k0 + u is consumed (the last group's requests past the
+    // segment read rows that are never used)
+    const int ntl = min(SEGT, nty - seg * SEGT);
+    for (int i = 0; i < ntl; ++i) {
+        const int k0 = 14 + ST_TH * i;
+        const int rows = row_offsets(k0 + LA);
+        toffA = 0; toffB = 0;
+        st_for([&](auto U) {
+            const uint32_t cur = ahead[U % LA];
+            ahead[U % LA] = load(__builtin_amdgcn_readlane(rows, U));
+            step(P5{}, k0 + U, cur, U);
+        }, std::make_integer_sequence<int, ST_TH>{});
+        // the 16 row counts of tile A (lanes 0..15) and B (16..31) are contiguous
+        const int tileA = (ys / ST_TH + i) * ntx + 2 * sxi;
+        if (lane < (hasB ? 2 * ST_TH : ST_TH)) tilerows[tileA * ST_TH + lane] = (uint8_t)trows;
     }
 }
 
@@ -999,7 +1163,7 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
 {
     constexpr int NP = VO_FREAK_NPOINTS, HALF = (NP + 1) / 2;     // points per component lane
     const int lane = threadIdx.x & 63, k = lane & 31, comp = lane >> 5;
-    const int W = d.W, H = d.H;
+    const int W = d.W, H = d.H, Wb = d.bstride;   // blurred plane: row stride Wb
     const bool valid = base + k < n;
     // lanes past n sample around a keypoint inside the margin: every address stays in bounds
     // and the gathers need no branches (their values are never used)
@@ -1018,7 +1182,7 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
         for (int u = 0; u < HALF; ++u) {
             int px, py;
             pt(u, px, py);
-            v[u] = img[(size_t)(kp.y + py) * W + (kp.x + px)];
+            v[u] = img[(size_t)(kp.y + py) * Wb + (kp.x + px)];
         }
 #pragma unroll
         for (int u = 0; u < HALF; ++u)
@@ -1070,7 +1234,7 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
             int y = (int)(((float)kp.y + (float)(-1 * px) * ms) + (float)py * c);
             x = min(max(x, 0), W - 1);   // in range for every keypoint inside the margin
             y = min(max(y, 0), H - 1);
-            v[u] = img[(size_t)y * W + x];
+            v[u] = img[(size_t)y * Wb + x];
         }
 #pragma unroll
         for (int u = 0; u < HALF; ++u)
@@ -1115,7 +1279,7 @@ __global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int
         const int wave = threadIdx.x >> 6;
         const int base = bx * DS_KPB + wave * DS_KPW;
         if (bx * DS_KPB < n)             // workgroup-uniform: the barriers inside are met by all
-            describe_wave(d, d.blurred + (size_t)z * d.W * d.H, cur, n, base, s_I0[wave], s_I1[wave]);
+            describe_wave(d, d.blurred + (size_t)z * d.bplane, cur, n, base, s_I0[wave], s_I1[wave]);
     }
     if (!publish) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2724,17 +2888,21 @@ const char* kernel_name(int i) { return g_names[i]; }
 void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int nb, int write_response, hipStream_t s)
 {
     ensure_tables();
-    const int ntx = (d.W + ST_TW - 1) / ST_TW, nty = (d.H + ST_TH - 1) / ST_TH;
+    const int ntx = (d.W + ST_TW - 1) / ST_TW, nsx = (ntx + 1) / 2, nty = (d.H + ST_TH - 1) / ST_TH;
     static const int segt = getenv("VO_STSEG") ? atoi(getenv("VO_STSEG")) : ST_SEGT_DEFAULT;
-    const int st = segt == 6 || segt == 8 ? segt : 4;
-    const int waves = ntx * ((nty + st - 1) / st);                 // one (strip, segment) per wave
+    const int st = write_response ? 4 : segt == 2 || segt == 6 || segt == 8 ? segt : 4;
+    const int waves = nsx * ((nty + st - 1) / st);                 // one (strip, segment) per wave
     dim3 g(xcd_grid((waves + 3) / 4, nb));
-    if (st == 8)
-        hipLaunchKernelGGL((k_stencil<8, 24>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response, nb);
+    if (write_response)
+        hipLaunchKernelGGL((k_stencil<4, true>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response, nb);
+    else if (st == 8)
+        hipLaunchKernelGGL((k_stencil<8, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
     else if (st == 6)
-        hipLaunchKernelGGL((k_stencil<6, 22>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response, nb);
+        hipLaunchKernelGGL((k_stencil<6, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
+    else if (st == 2)
+        hipLaunchKernelGGL((k_stencil<2, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
     else
-        hipLaunchKernelGGL((k_stencil<4, 26>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response, nb);
+        hipLaunchKernelGGL((k_stencil<4, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
 }
 void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s)
 {
