@@ -41,6 +41,7 @@ struct vo_ctx {
     bool serial = false;              // VO_SERIAL=1: every kernel on one queue, no cross-queue
                                       // waits (for profilers that serialize dispatches: PMC passes)
     bool event_wait = true;           // pose queue waits for extract batches on events (default)
+    int slack = 0;                    // VO_SLACK: extra passes enqueued per chunk (misses re-run without a host round trip)
                                       // or on the stream-wait-value packet (VO_EVENT_WAIT=0; events
                                       // again after the runtime refused a wait-value packet)
     // per-batch event pools of a chunk: [VO_EV_WAIT] extract done (event_wait mode),
@@ -317,13 +318,14 @@ int enqueue_h2d(vo_ctx* c, const HostSrc& hs, int f0, int nb, int j, uint8_t** d
     return VO_OK;
 }
 
-// one pose pass over the window [lo, lo + B) of the frames enqueued so far
-// cap: the window size of this pass (<= B); every kernel of the pass sees the same VoDev
-void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int cap)
+// one pose pass over the window [lo, lo + n) of the frames enqueued so far, n <= WB
+// gmax: frames < gmax are extracted once the pass runs (its wait covers them); every kernel of
+// the pass sees the same VoDev
+void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax)
 {
     hipStream_t s = c->s;
     VoDev d = c->d;
-    d.B = cap;
+    d.gmax = gmax;
     timed(c, ev, 3, s, [&] { vo::launch_match(d, 0, s); });
     timed(c, ev, 4, s, [&] { vo::launch_ransac(d, 0, s); });
     timed(c, ev, 5, s, [&] { vo::launch_refit(d, 1, 0, s); });
@@ -431,7 +433,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
                 HIPCHK(hipStreamWaitEvent(s, e, 0));
             }
         }
-        enqueue_pass(c, out, out_base, ev, sched[k]);
+        enqueue_pass(c, out, out_base, ev, base + f0s[k + 1]);
         return VO_OK;
     };
     if (!img0 && !hs) {
@@ -450,6 +452,10 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
             if (k + 1 < sched.size() && (rc = extract((int)k + 1)) != VO_OK) return rc;
             if ((rc = pass((int)k)) != VO_OK) return rc;
         }
+        // slack passes: the frames left behind by speculation misses, without a host round trip
+        // (a pass with nothing left to commit returns at once); long chunks only
+        if (sched.size() >= 4)
+            for (int k = 0; k < c->slack; ++k) enqueue_pass(c, out, out_base, ev, end);
     }
     // every pass commits at least its first frame, so nf re-pass rounds bound the loop
     for (int round = 0, prev_lo = base;; ++round) {
@@ -468,7 +474,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         }
         prev_lo = lo;
         // frames after skipped ones: their windows restart at lo (extracts are complete)
-        for (int k = 0; k < (end - lo + B - 1) / B; ++k) enqueue_pass(c, out, out_base, ev, B);
+        for (int k = 0; k < (end - lo + B - 1) / B; ++k) enqueue_pass(c, out, out_base, ev, end);
     }
     return ev && ev->err ? ev->err : VO_OK;
 }
@@ -568,6 +574,9 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     const int B = k.frame_batch ? k.frame_batch : VO_DEFAULT_BATCH;
     c->B = B;
     d.B = B;
+    d.WB = std::min(VO_MAX_WIN, 2 * B);
+    if (getenv("VO_WIN")) d.WB = std::max(1, std::min(VO_MAX_WIN, atoi(getenv("VO_WIN"))));
+    d.gmax = INT_MAX;
     d.W = W; d.H = H; d.N = N;
     d.ring = VO_RING_DEFAULT;
     if (getenv("VO_RING_SLOTS")) d.ring = std::max(2 * VO_MAX_BATCH, std::min(1 << 16, atoi(getenv("VO_RING_SLOTS"))));
@@ -596,6 +605,8 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     // counter, which ROCm runs as a polling blit kernel (measured equal or slightly slower)
     c->event_wait = !(getenv("VO_EVENT_WAIT") && atoi(getenv("VO_EVENT_WAIT")) == 0);
     d.xcd_map = getenv("VO_XCD") ? atoi(getenv("VO_XCD")) : 1;
+    c->slack = getenv("VO_SLACK") ? std::max(0, std::min(64, atoi(getenv("VO_SLACK")))) : VO_SLACK_DEFAULT;
+    d.repair_win = getenv("VO_REPAIR_WIN") ? std::max(1, std::min(d.WB, atoi(getenv("VO_REPAIR_WIN")))) : std::min(d.WB, VO_REPAIR_WIN_DEFAULT);
     if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
     for (hipStream_t& q : c->se)
         if (hip_ok(hipStreamCreateWithFlags(&q, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
@@ -616,16 +627,17 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc(&d.kps, (size_t)N * VO_SLOTS);
     rc |= dalloc(&d.desc, (size_t)N * 8 * VO_SLOTS);
     rc |= dalloc(&d.pre, (size_t)N * VO_SLOTS);
-    rc |= dalloc(&d.match_j, (size_t)N * B);
-    rc |= dalloc(&d.match_pairs, (size_t)N * B);
-    rc |= dalloc(&d.pts, (size_t)N * 4 * B);
-    rc |= dalloc(&d.hypF, (size_t)d.max_hyp * 9 * B);
-    rc |= dalloc(&d.counts, (size_t)d.max_hyp * B);
-    rc |= dalloc(&d.inl, (size_t)N * B);
+    const int WB = d.WB;                                       // pose window buffers
+    rc |= dalloc(&d.match_j, (size_t)N * WB);
+    rc |= dalloc(&d.match_pairs, (size_t)N * WB);
+    rc |= dalloc(&d.pts, (size_t)N * 4 * WB);
+    rc |= dalloc(&d.hypF, (size_t)d.max_hyp * 9 * WB);
+    rc |= dalloc(&d.counts, (size_t)d.max_hyp * WB);
+    rc |= dalloc(&d.inl, (size_t)N * WB);
     d.mask_words = (N + 63) / 64;
-    rc |= dalloc(&d.inlmask, (size_t)d.max_hyp * d.mask_words * B);
-    rc |= dalloc(&d.model_p, (size_t)N * 4 * B);
-    rc |= dalloc(&d.work, B);
+    rc |= dalloc(&d.inlmask, (size_t)d.max_hyp * d.mask_words * WB);
+    rc |= dalloc(&d.model_p, (size_t)N * 4 * WB);
+    rc |= dalloc(&d.work, WB);
     rc |= dalloc(&d.st, 1);
     rc |= dalloc(&d.ext_n, VO_SLOTS);
     rc |= dalloc(&d.ext_st, VO_SLOTS);

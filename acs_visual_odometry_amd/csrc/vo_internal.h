@@ -62,8 +62,11 @@ inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_T
 // (frame f's slot is rewritten by frame f + VO_RING; passes read frames >= lo - 1)
 #define VO_CHUNK (d.ring - 1)
 #define VO_MAX_BATCH 64
+#define VO_MAX_WIN 128       // pose window capacity: up to two extract batches (k_finalize LDS)
 #define VO_MAX_SEQ_STARTS 4096     // vo_set_sequence_starts capacity
 #define VO_DEFAULT_BATCH 64
+#define VO_REPAIR_WIN_DEFAULT 4   // pose window after a speculation miss (frames; 4 / 8 / 64 measured 162k / 160k / 158k KITTI frames/s)
+#define VO_SLACK_DEFAULT 4        // extra passes per chunk of >= 4 batches (VO_SLACK)
 // ctr words: cross-queue counters on lines of their own
 #define VO_EXT_QUEUES 1        // extract queues (batch j on queue j % n, own scratch); 2 measured no faster
 #define VO_CTR_DESCRIBE 0      // + 16 * queue: describe's in-launch arrival counter
@@ -117,7 +120,7 @@ struct VoState {
     int32_t model_n;      // FundamentalMatrix model (VisualOdometry.cpp:49): inliers of the last fit
     int32_t model_degenerate;
     int32_t pose_status;  // stage vo_pose result
-    int32_t pad;
+    int32_t win;          // frames in the next pass's window: B, or repair_win after a pass that stopped early
     double model_F[9];
     double model_R[9], model_t[3];   // getPose(model) before scaling: det-fixed R, signed unit t
     double Tcurr[16];
@@ -137,9 +140,12 @@ struct VoDev {
     int T;
     int maxit_initial;
     int max_hyp;
-    int B;                // window / extract batch capacity (frames)
+    int B;                // extract batch capacity (frames)
+    int WB;               // pose window capacity (frames): min(2 B, VO_MAX_WIN), VO_WIN overrides
+    int gmax;             // pose pass: frames < gmax are extracted (the pass's wait covers them)
     int eq;               // extract queue of this launch (its scratch copy and counters)
     int xcd_map;          // extract kernels place a frame's workgroups on one XCD (VO_XCD=0: off)
+    int repair_win;       // window after a pass whose commit stopped early (VO_REPAIR_WIN, default VO_REPAIR_WIN_DEFAULT)
     uint64_t seed;
     double K[9];
     uint32_t cand_cap;    // per frame

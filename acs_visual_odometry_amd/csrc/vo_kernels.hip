@@ -1334,13 +1334,20 @@ __host__ __device__ inline int match_blocks(int N, int match_bits)
     return match_bits == 32 ? (N + MT_QPB - 1) / MT_QPB : (N + MT512_QPB - 1) / MT512_QPB;
 }
 
-// Window of a pose pass: frames [st->lo, st->lo + n), n = min(B, st->end - st->lo); a stage
-// call works on work[0] alone.  st changes only in k_finalize, the pass's last kernel.
+// Window of a pose pass: frames [st->lo, st->lo + n), n = min(st->win, st->end - st->lo,
+// d.gmax - st->lo) with st->win <= d.WB: up to WB frames (2 extract batches), but only frames
+// the pass's extract wait covers (d.gmax), so the window grows when the pose queue lags behind
+// the extract queue and each pass's fixed latency is spread over more frames.  A stage call
+// works on work[0] alone.  st changes only in k_finalize, the pass's last kernel.
+// st->win is B, or d.repair_win after a pass whose commit stopped early: the frames after a
+// speculation miss (a frame that did not advance desc1) are re-run in a short window, since
+// misses come in runs (a new sequence's first frames without a model, quirk 9) and each
+// re-run window commits only up to the next miss.
 __device__ __forceinline__ int win_count(const VoDev& d, int stage)
 {
     if (stage) return 1;
-    const int n = d.st->end - d.st->lo;
-    return n < d.B ? n : d.B;
+    const int lo = d.st->lo, w = d.st->win;
+    return min(min(d.st->end, d.gmax) - lo, w > 0 && w < d.WB ? w : d.WB);
 }
 
 __device__ __forceinline__ uint64_t frame_seed_of(const VoDev& d, int f)
@@ -2611,19 +2618,20 @@ __device__ __forceinline__ double dpp_quad_bcast(double v, int k)
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int out_base)
 {
+    constexpr int MW = VO_MAX_WIN;                    // s_R / s_t [MW]: the model before the window
     __shared__ int s_n, s_ncommit, s_lo, s_copy, s_model_wf, s_model_clear, s_newlv, s_newprev;
-    __shared__ int s_status[VO_MAX_BATCH], s_kind[VO_MAX_BATCH], s_src[VO_MAX_BATCH], s_lvb[VO_MAX_BATCH];
-    __shared__ int s_flip[VO_MAX_BATCH], s_fitted[VO_MAX_BATCH], s_degen[VO_MAX_BATCH], s_cur[VO_MAX_BATCH];
-    __shared__ double s_R[VO_MAX_BATCH + 1][9], s_t[VO_MAX_BATCH + 1][3];   // [B]: the model before the window
-    __shared__ double s_Trel[VO_MAX_BATCH + 2][16];   // + 2: step 3 reads two frames ahead
-    __shared__ double s_row[VO_MAX_BATCH][12];
+    __shared__ int s_status[MW], s_kind[MW], s_src[MW], s_lvb[MW];
+    __shared__ int s_flip[MW], s_fitted[MW], s_degen[MW], s_cur[MW], s_adv[MW];
+    __shared__ double s_R[MW + 1][9], s_t[MW + 1][3];
+    __shared__ double s_Trel[MW + 2][16];             // + 2: step 3 reads two frames ahead
+    __shared__ double s_row[MW][12];
     __shared__ double s_T[16];
     const int tid = threadIdx.x;
     VO_STAMP(d, 1996, 7);
     VoState* st = d.st;
     if (tid == 0) {
         const int lo = st->lo;
-        const int n = min(st->end - lo, d.B);
+        const int n = win_count(d, 0);
         s_lo = lo;
         s_n = n;
         s_copy = -1;
@@ -2633,7 +2641,6 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
     VO_STAMP(d, 1996, 0);
     const int n = s_n, lo = s_lo;
     if (n <= 0) return;
-    const int MB = VO_MAX_BATCH;
     // 0
     if (tid < n) {
         const VoWork* w = d.work + tid;
@@ -2647,67 +2654,75 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
             for (int c = 0; c < 4; ++c) c4[c] = w->counts4[c];
             choose_pose(c4, w->R1, w->R2, w->t, s_R[tid], s_t[tid]);
         }
-    } else if (tid == 64) {
-        for (int i = 0; i < 9; ++i) s_R[MB][i] = st->model_R[i];
-        for (int i = 0; i < 3; ++i) s_t[MB][i] = st->model_t[i];
-    } else if (tid == 96) {
+    } else if (tid == 255) {
+        for (int i = 0; i < 9; ++i) s_R[MW][i] = st->model_R[i];
+        for (int i = 0; i < 3; ++i) s_t[MW][i] = st->model_t[i];
+    } else if (tid == 254) {
         for (int i = 0; i < 16; ++i) s_T[i] = st->Tcurr[i];
     }
     __syncthreads();
     VO_STAMP(d, 1996, 1);
-    // 1 (wave 0, lane = window frame): the sequential rules as prefix operations over ballots --
-    //   the model source of a frame is its latest fit, unless a sequence start (FIRST) came
-    //   after it; desc1 / last_valid advance on FIRST and on OK frames with a model; the commit
-    //   stops after the first frame that did not advance (the next one was matched against it)
+    // 1 (wave 0, lane = window frame of a 64-frame chunk, chunks in order with wave-uniform
+    //   carries): the sequential rules as prefix operations over ballots -- the model source of
+    //   a frame is its latest fit, unless a sequence start (FIRST) came after it; desc1 /
+    //   last_valid advance on FIRST and on OK frames with a model; the commit stops after the
+    //   first frame that did not advance (the next one was matched against it)
     if (tid < 64) {
         const int lane = tid;
-        const bool in = lane < n;
-        const int s0 = in ? s_status[lane] : -1;
-        const int cur_l = in ? s_cur[lane] : 0;
-        const int dg_l = in ? s_degen[lane] : 0;
-        const bool first = s0 == VO_STATUS_FIRST;
-        const bool ok = s0 == VO_STATUS_OK;
-        const bool fitok = ok && s_fitted[lane];
-        const unsigned long long Mfirst = ballot64(first), Mfit = ballot64(fitok);
         const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);   // bits <= lane
         const unsigned long long below = (1ull << lane) - 1ull;                          // bits < lane
         auto hibit = [](unsigned long long x) { return x ? 63 - __clzll((long long)x) : -1; };
-        const int msrc0 = st->model_n >= 8 ? MB : -1;   // MB: the model fitted before this window
+        const int msrc0 = st->model_n >= 8 ? MW : -1;   // MW: the model fitted before this window
         const int mdeg = st->model_degenerate;
-        const int lfit = hibit(Mfit & upto), lfirst = hibit(Mfirst & upto);
-        const int msrc_l = lfit > lfirst ? lfit : (lfirst >= 0 ? -1 : msrc0);
-        const int dgv = __shfl(dg_l, msrc_l >= 0 && msrc_l < MB ? msrc_l : 0);
-        const int dg = msrc_l == MB ? mdeg : (msrc_l >= 0 ? dgv : 0);
-        const bool okm = ok && msrc_l >= 0;
-        const bool adv = first || okm;
-        const unsigned long long Madv = ballot64(in && adv);
-        int o_s = s0;
-        if (ok) o_s = !okm ? VO_STATUS_FEW_INLIERS : (dg ? VO_STATUS_DEGENERATE : VO_STATUS_OK);   // :147-153
-        const int lv0 = st->last_valid, prev0 = st->prev_slot;
-        const int la = hibit(Madv & below);
-        if (in) {
-            s_status[lane] = o_s;
-            s_kind[lane] = (okm && !dg) ? 1 : 0;
-            s_flip[lane] = (first || s0 == VO_STATUS_MISSING) ? 0 : 1;   // :58, :79 unflipped
-            s_src[lane] = msrc_l;
-            s_lvb[lane] = la >= 0 ? lo + la : lv0;      // :161-166 precede getPose
+        const int lv0 = st->last_valid;
+        int cfit = -1, cfirst = -1, cadv = -1;          // latest fit / FIRST / advance before the chunk
+        int nc = n;                                     // commit: after the first frame of 0 .. n-2 that did not advance
+        for (int c0 = 0; c0 < n; c0 += 64) {
+            const int wf = c0 + lane;
+            const bool in = wf < n;
+            const int s0 = in ? s_status[wf] : -1;
+            const bool first = s0 == VO_STATUS_FIRST;
+            const bool ok = s0 == VO_STATUS_OK;
+            const bool fitok = ok && s_fitted[wf];
+            const unsigned long long Mfirst = ballot64(first), Mfit = ballot64(fitok);
+            const int lf = hibit(Mfit & upto), lr = hibit(Mfirst & upto);
+            const int lfit = lf >= 0 ? c0 + lf : cfit, lfirst = lr >= 0 ? c0 + lr : cfirst;
+            const int msrc_l = lfit > lfirst ? lfit : (lfirst >= 0 ? -1 : msrc0);
+            const int dg = msrc_l == MW ? mdeg : (msrc_l >= 0 ? s_degen[msrc_l] : 0);
+            const bool okm = ok && msrc_l >= 0;
+            const bool adv = first || okm;
+            const unsigned long long Madv = ballot64(in && adv);
+            const int la_c = hibit(Madv & below), la = la_c >= 0 ? c0 + la_c : cadv;
+            if (in) {
+                int o_s = s0;
+                if (ok) o_s = !okm ? VO_STATUS_FEW_INLIERS : (dg ? VO_STATUS_DEGENERATE : VO_STATUS_OK);   // :147-153
+                s_status[wf] = o_s;
+                s_kind[wf] = (okm && !dg) ? 1 : 0;
+                s_flip[wf] = (first || s0 == VO_STATUS_MISSING) ? 0 : 1;   // :58, :79 unflipped
+                s_src[wf] = msrc_l;
+                s_lvb[wf] = la >= 0 ? lo + la : lv0;      // :161-166 precede getPose
+                s_adv[wf] = adv;
+            }
+            const unsigned long long nadv = ballot64(wf < n - 1 && !adv);
+            if (nc == n && nadv) nc = c0 + __ffsll((long long)nadv);   // (lowest bit) + 1
+            if (Mfit) cfit = c0 + hibit(Mfit);
+            if (Mfirst) cfirst = c0 + hibit(Mfirst);
+            if (Madv) cadv = c0 + hibit(Madv);
+            if (nc < n) break;                          // later chunks are not committed
         }
-        // commit point: after the first frame (of frames 0 .. n-2) that did not advance
-        const unsigned long long nadv = ~Madv & (n >= 64 ? ~0ull : ((1ull << n) - 1ull)) &
-                                        ((1ull << (n - 1)) - 1ull);
-        const int nc = nadv ? __ffsll((long long)nadv) : n;        // (lowest bit) + 1
-        const unsigned long long Mc = nc >= 64 ? ~0ull : ((1ull << nc) - 1ull);
-        const int lend = hibit(Madv & Mc);
-        const int cur_end = __shfl(cur_l, lend >= 0 ? lend : 0);
-        const int msrc_end = __shfl(msrc_l, nc - 1);
-        if (lane == 0) {
-            int lv = lend >= 0 ? lo + lend : lv0, prev = lend >= 0 ? cur_end : prev0;
-            s_ncommit = nc;
-            if (msrc_end >= 0 && msrc_end < MB) s_model_wf = msrc_end;
-            s_model_clear = msrc_end < 0;               // no model (never fitted, or a new sequence)
-            if (!((Madv >> (nc - 1)) & 1ull) && prev < VO_RING) { s_copy = prev; prev = VO_CARRY_SLOT; }
-            s_newlv = lv; s_newprev = prev;
-        }
+        if (lane == 0) s_ncommit = nc;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        // every frame before nc - 1 advanced: the last advance is nc - 1 or nc - 2
+        const int nc = s_ncommit, prev0 = st->prev_slot, lv0 = st->last_valid;
+        const int lend = s_adv[nc - 1] ? nc - 1 : nc - 2;
+        const int msrc_end = s_src[nc - 1];
+        int lv = lend >= 0 ? lo + lend : lv0, prev = lend >= 0 ? s_cur[lend] : prev0;
+        if (msrc_end >= 0 && msrc_end < MW) s_model_wf = msrc_end;
+        s_model_clear = msrc_end < 0;                   // no model (never fitted, or a new sequence)
+        if (!s_adv[nc - 1] && prev < VO_RING) { s_copy = prev; prev = VO_CARRY_SLOT; }
+        s_newlv = lv; s_newprev = prev;
     }
     __syncthreads();
     VO_STAMP(d, 1996, 2);
@@ -2741,10 +2756,14 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
     //   frames ahead, so each step's critical path is the quad broadcasts and the four products
     if (tid < 64) {
         const int e = tid & 15, i = e >> 2, j = e & 3;
-        const bool inc = tid < nc;
-        const unsigned long long Mkind = ballot64(inc && s_kind[tid] == 1);
-        const unsigned long long Mfirst = ballot64(inc && s_status[tid] == VO_STATUS_FIRST);
-        const unsigned long long Mflip = ballot64(inc && s_flip[tid] != 0);
+        // frame kinds of window frames tid (chunk 0) and 64 + tid (chunk 1)
+        const bool inc = tid < nc, inc1 = 64 + tid < nc;
+        const unsigned long long Mkind0 = ballot64(inc && s_kind[tid] == 1);
+        const unsigned long long Mfirst0 = ballot64(inc && s_status[tid] == VO_STATUS_FIRST);
+        const unsigned long long Mflip0 = ballot64(inc && s_flip[tid] != 0);
+        const unsigned long long Mkind1 = ballot64(inc1 && s_kind[64 + tid] == 1);
+        const unsigned long long Mfirst1 = ballot64(inc1 && s_status[64 + tid] == VO_STATUS_FIRST);
+        const unsigned long long Mflip1 = ballot64(inc1 && s_flip[64 + tid] != 0);
         double Tv = s_T[e];
         const double ident = (e % 5 == 0) ? 1.0 : 0.0;  // VisualOdometry.cpp:57 T_curr = eye(4)
         double b[3][4];
@@ -2761,9 +2780,12 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
             const double a0 = dpp_quad_bcast(Tv, 0), a1 = dpp_quad_bcast(Tv, 1);
             const double a2 = dpp_quad_bcast(Tv, 2), a3 = dpp_quad_bcast(Tv, 3);
             const double pv = ((a0 * b[0][0] + a1 * b[0][1]) + a2 * b[0][2]) + a3 * b[0][3];
-            const bool kind = (Mkind >> wf) & 1ull, firstf = (Mfirst >> wf) & 1ull;
+            const int sh = wf & 63;
+            const bool kind = ((wf < 64 ? Mkind0 : Mkind1) >> sh) & 1ull;
+            const bool firstf = ((wf < 64 ? Mfirst0 : Mfirst1) >> sh) & 1ull;
+            const bool flip = ((wf < 64 ? Mflip0 : Mflip1) >> sh) & 1ull;
             Tv = kind ? pv : (firstf ? ident : Tv);
-            if (tid < 12) s_row[wf][tid] = (((Mflip >> wf) & 1ull) && i == 2) ? -Tv : Tv;
+            if (tid < 12) s_row[wf][tid] = (flip && i == 2) ? -Tv : Tv;
 #pragma unroll
             for (int k = 0; k < 4; ++k) { b[0][k] = b[1][k]; b[1][k] = b[2][k]; }
         }
@@ -2785,8 +2807,9 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
         o->n_eval = w->n_eval;
         o->fitted = s_fitted[tid];
         o->frame = lo + tid;
-    } else if (tid == 64) {
+    } else if (tid == 255) {
         st->lo = lo + nc;
+        st->win = nc < n ? d.repair_win : d.WB;
         st->last_valid = s_newlv;
         st->prev_slot = s_newprev;
         for (int i = 0; i < 16; ++i) st->Tcurr[i] = s_T[i];
@@ -2826,7 +2849,7 @@ __global__ void __launch_bounds__(256) k_reset(VoDev d)
     const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
     if (tid == 0) {
         VoState* st = d.st;
-        st->lo = 0; st->end = 0; st->prev_slot = 0; st->last_valid = 0;
+        st->lo = 0; st->end = 0; st->prev_slot = 0; st->last_valid = 0; st->win = d.WB;
         st->model_n = 0; st->model_degenerate = 0; st->pose_status = 0;
         for (int i = 0; i < 9; ++i) { st->model_F[i] = 0.0; st->model_R[i] = 0.0; st->pose_R[i] = 0.0; }
         for (int i = 0; i < 3; ++i) { st->model_t[i] = 0.0; st->pose_t[i] = 0.0; }
@@ -2836,7 +2859,7 @@ __global__ void __launch_bounds__(256) k_reset(VoDev d)
     for (int i = tid; i < VO_SLOTS; i += nth) { d.ext_n[i] = 0; d.ext_st[i] = VO_STATUS_OK; }
     for (int i = tid; i < VO_HIST_BINS * d.B * VO_EXT_QUEUES; i += nth) d.hist[i] = 0u;
     uint32_t* w = reinterpret_cast<uint32_t*>(d.work);
-    for (int i = tid; i < (int)(sizeof(VoWork) / 4) * d.B; i += nth) w[i] = 0u;
+    for (int i = tid; i < (int)(sizeof(VoWork) / 4) * d.WB; i += nth) w[i] = 0u;
     for (int i = tid; i < VO_CTR_WORDS; i += nth) d.ctr[i] = 0u;
 }
 
@@ -2934,14 +2957,14 @@ void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned
 void launch_match(const VoDev& d, int stage, hipStream_t s)
 {
     if (d.match_bits == 32)
-        hipLaunchKernelGGL(k_match, dim3(match_blocks(d.N, 32), stage ? 1 : d.B), dim3(256), 0, s, d, stage);
+        hipLaunchKernelGGL(k_match, dim3(match_blocks(d.N, 32), stage ? 1 : d.WB), dim3(256), 0, s, d, stage);
     else {
         // 64 KB of dynamic LDS plus the static hand-off words: above the default 64 KB cap
         static const bool lds_ok = hipFuncSetAttribute((const void*)k_match512,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        MT512_TILE * 64) == hipSuccess;
         (void)lds_ok;
-        hipLaunchKernelGGL(k_match512, dim3(match_blocks(d.N, 512), stage ? 1 : d.B), dim3(256),
+        hipLaunchKernelGGL(k_match512, dim3(match_blocks(d.N, 512), stage ? 1 : d.WB), dim3(256),
                            (size_t)MT512_TILE * 64, s, d, stage);
     }
 }
@@ -2951,7 +2974,7 @@ void launch_match(const VoDev& d, int stage, hipStream_t s)
 // are enough hypotheses to fill the chip, so no wave repeats another's 8-point fit.
 void launch_ransac(const VoDev& d, int stage, hipStream_t s)
 {
-    const int nhyp = d.max_hyp, nb = stage ? 1 : d.B;
+    const int nhyp = d.max_hyp, nb = stage ? 1 : d.WB;
     const int cut[3] = {std::min(nhyp, VO_HYP_CHUNK0), std::min(nhyp, VO_HYP_CHUNK1), nhyp};
     int k0 = 0;
     for (int c = 0; c < 3; ++c) {
@@ -2966,11 +2989,11 @@ void launch_ransac(const VoDev& d, int stage, hipStream_t s)
 }
 void launch_refit(const VoDev& d, int with_pose, int stage, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_refit, dim3(stage ? 1 : d.B), dim3(RF_T), 0, s, d, with_pose, stage);
+    hipLaunchKernelGGL(k_refit, dim3(stage ? 1 : d.WB), dim3(RF_T), 0, s, d, with_pose, stage);
 }
 void launch_triangulate(const VoDev& d, int stage, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_triangulate, dim3((4 * d.N + TRI_BLOCK - 1) / TRI_BLOCK, stage ? 1 : d.B), dim3(TRI_BLOCK), 0,
+    hipLaunchKernelGGL(k_triangulate, dim3((4 * d.N + TRI_BLOCK - 1) / TRI_BLOCK, stage ? 1 : d.WB), dim3(TRI_BLOCK), 0,
                        s, d, stage);
 }
 void launch_finalize(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s)
