@@ -606,7 +606,8 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     c->event_wait = !(getenv("VO_EVENT_WAIT") && atoi(getenv("VO_EVENT_WAIT")) == 0);
     d.xcd_map = getenv("VO_XCD") ? atoi(getenv("VO_XCD")) : 1;
     c->slack = getenv("VO_SLACK") ? std::max(0, std::min(64, atoi(getenv("VO_SLACK")))) : VO_SLACK_DEFAULT;
-    d.repair_win = getenv("VO_REPAIR_WIN") ? std::max(1, std::min(d.WB, atoi(getenv("VO_REPAIR_WIN")))) : std::min(d.WB, VO_REPAIR_WIN_DEFAULT);
+    // repair windows hold two work records per frame (k_finalize): at most WB / 2 frames
+    d.repair_win = std::max(1, std::min(d.WB / 2, getenv("VO_REPAIR_WIN") ? atoi(getenv("VO_REPAIR_WIN")) : VO_REPAIR_WIN_DEFAULT));
     if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
     for (hipStream_t& q : c->se)
         if (hip_ok(hipStreamCreateWithFlags(&q, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);

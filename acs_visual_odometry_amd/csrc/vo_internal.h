@@ -65,7 +65,7 @@ inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_T
 #define VO_MAX_WIN 128       // pose window capacity: up to two extract batches (k_finalize LDS)
 #define VO_MAX_SEQ_STARTS 4096     // vo_set_sequence_starts capacity
 #define VO_DEFAULT_BATCH 64
-#define VO_REPAIR_WIN_DEFAULT 4   // pose window after a speculation miss (frames; 4 / 8 / 64 measured 162k / 160k / 158k KITTI frames/s)
+#define VO_REPAIR_WIN_DEFAULT 8   // pose window after a speculation miss (frames; dual records: 4 / 8 / 16 measured 174k / 180k / 177k KITTI frames/s)
 #define VO_SLACK_DEFAULT 4        // extra passes per chunk of >= 4 batches (VO_SLACK)
 // ctr words: cross-queue counters on lines of their own
 #define VO_EXT_QUEUES 1        // extract queues (batch j on queue j % n, own scratch); 2 measured no faster
@@ -121,6 +121,8 @@ struct VoState {
     int32_t model_degenerate;
     int32_t pose_status;  // stage vo_pose result
     int32_t win;          // frames in the next pass's window: B, or repair_win after a pass that stopped early
+    int32_t dual;         // the next pass is a repair window: each frame also matched against desc1 (prev_slot)
+    int32_t pad;
     double model_F[9];
     double model_R[9], model_t[3];   // getPose(model) before scaling: det-fixed R, signed unit t
     double Tcurr[16];

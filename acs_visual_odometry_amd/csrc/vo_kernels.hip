@@ -1349,6 +1349,17 @@ __device__ __forceinline__ int win_count(const VoDev& d, int stage)
     const int lo = d.st->lo, w = d.st->win;
     return min(min(d.st->end, d.gmax) - lo, w > 0 && w < d.WB ? w : d.WB);
 }
+// Work records of a pass: one per window frame, and in a repair window (st->dual) a second
+// set [n, 2n): frame wf matched against desc1 as it was before the window (st->prev_slot)
+// instead of frame f - 1.  When frame f - 1 does not advance desc1 and no frame of the window
+// before it did, that is the match the sequential loop makes, so a run of frames without a
+// model (a new sequence's first frames) commits in one repair pass (k_finalize picks the
+// record per frame).  repair_win <= WB / 2.
+__device__ __forceinline__ int vwin_count(const VoDev& d, int stage)
+{
+    const int n = win_count(d, stage);
+    return (!stage && d.st->dual) ? 2 * n : n;
+}
 
 __device__ __forceinline__ uint64_t frame_seed_of(const VoDev& d, int f)
 {
@@ -1383,9 +1394,10 @@ __device__ __forceinline__ bool match_header(const VoDev& d, int stage, int wf, 
     if (stage) {
         f = -1; prev = VO_STAGE_SLOT; cur = VO_STAGE_SLOT + 1;
     } else {
-        f = d.st->lo + wf;
+        const int n = win_count(d, 0), df = wf < n ? wf : wf - n;   // record wf >= n: the dual match
+        f = d.st->lo + df;
         cur = f % VO_RING;
-        prev = wf == 0 ? d.st->prev_slot : (f - 1) % VO_RING;
+        prev = df == 0 || wf >= n ? d.st->prev_slot : (f - 1) % VO_RING;
         const int es = d.ext_st[cur];
         fl = f - seq_base(d, f);
         if (fl == 0) status = VO_STATUS_FIRST;                 // VisualOdometry.cpp:58,64-66
@@ -1486,7 +1498,7 @@ __device__ __forceinline__ void top2_merge(uint32_t& m1, uint32_t& m2, uint32_t 
 __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
 {
     const int wf = blockIdx.y;
-    if (wf >= win_count(d, stage)) return;
+    if (wf >= vwin_count(d, stage)) return;
     MatchFrame m;
     if (!match_header(d, stage, wf, m)) return;
     __shared__ unsigned s_last;
@@ -1581,7 +1593,7 @@ __device__ __forceinline__ uint32_t dist512(const uint32_t (&qw)[16], const uint
 __global__ void __launch_bounds__(256) k_match512(VoDev d, int stage)
 {
     const int wf = blockIdx.y;
-    if (wf >= win_count(d, stage)) return;
+    if (wf >= vwin_count(d, stage)) return;
     MatchFrame m;
     if (!match_header(d, stage, wf, m)) return;
     __shared__ unsigned s_last;
@@ -1937,7 +1949,7 @@ template <int WPH, int HPB>
 __global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, int k1, int nhyp, int stage, int reps)
 {
     const int wf = blockIdx.y;                     // window frame
-    if (wf >= win_count(d, stage)) return;
+    if (wf >= vwin_count(d, stage)) return;
     VoWork* w = d.work + wf;
     if (w->status != VO_STATUS_OK) return;
     if (k0 > 0 && !w->need_more) return;           // the replay of [0, k0) already stopped
@@ -2295,7 +2307,7 @@ __device__ __forceinline__ void refit_pt(const double2* s_p, const double* pts, 
 __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose, int stage)
 {
     const int wf = blockIdx.x;                     // window frame
-    if (wf >= win_count(d, stage)) return;
+    if (wf >= vwin_count(d, stage)) return;
     VoWork* w = d.work + wf;
     if (w->status != VO_STATUS_OK) return;
     const double* pts = d.pts + (size_t)wf * 4 * d.N;
@@ -2531,7 +2543,7 @@ __device__ __forceinline__ void nullvec4(const double* A, double* x)
 __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d, int stage)
 {
     const int wf = blockIdx.y;
-    if (wf >= win_count(d, stage)) return;
+    if (wf >= vwin_count(d, stage)) return;
     VoWork* w = d.work + wf;
     if (w->status != VO_STATUS_OK || !w->fitted || w->degenerate) return;
     const int n = w->n_fit;
@@ -2626,9 +2638,12 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
     __shared__ double s_Trel[MW + 2][16];             // + 2: step 3 reads two frames ahead
     __shared__ double s_row[MW][12];
     __shared__ double s_T[16];
+    __shared__ int s_rec[MW];                         // the work record each window frame uses
+    __shared__ int s_dual_nc, s_dual_lend;
     const int tid = threadIdx.x;
     VO_STAMP(d, 1996, 7);
     VoState* st = d.st;
+    const bool dual = st->dual != 0;
     if (tid == 0) {
         const int lo = st->lo;
         const int n = win_count(d, 0);
@@ -2636,6 +2651,29 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
         s_n = n;
         s_copy = -1;
         s_model_wf = -1;
+        if (dual && n > 0) {
+            // repair window: frame wf > 0 uses the match against f - 1 if f - 1 advanced desc1,
+            // the match against desc1 before the window if no frame before it did, else it was
+            // matched against neither (the commit ends before it).  The same rules as step 1,
+            // sequentially over the few frames of the window.
+            bool model = st->model_n >= 8, any = false, padv = true;
+            int nc = n, lend = -1;
+            for (int wf = 0; wf < n; ++wf) {
+                if (wf > 0 && !padv && any) { nc = wf; break; }
+                const int r = (wf == 0 || padv) ? wf : n + wf;
+                const VoWork* w = d.work + r;
+                const bool first = w->status == VO_STATUS_FIRST, ok = w->status == VO_STATUS_OK;
+                if (first) model = false;
+                if (ok && w->fitted) model = true;
+                const bool adv = first || (ok && model);
+                s_rec[wf] = r;
+                if (adv) lend = wf;
+                any = any || adv;
+                padv = adv;
+            }
+            s_dual_nc = nc;
+            s_dual_lend = lend;
+        }
     }
     __syncthreads();
     VO_STAMP(d, 1996, 0);
@@ -2643,7 +2681,7 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
     if (n <= 0) return;
     // 0
     if (tid < n) {
-        const VoWork* w = d.work + tid;
+        const VoWork* w = d.work + (dual ? s_rec[tid] : tid);
         s_status[tid] = w->status;
         s_cur[tid] = w->cur;
         const int fit = w->status == VO_STATUS_OK && w->fitted;
@@ -2710,13 +2748,14 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
             if (Madv) cadv = c0 + hibit(Madv);
             if (nc < n) break;                          // later chunks are not committed
         }
-        if (lane == 0) s_ncommit = nc;
+        if (lane == 0) s_ncommit = dual ? s_dual_nc : nc;
     }
     __syncthreads();
     if (tid == 0) {
-        // every frame before nc - 1 advanced: the last advance is nc - 1 or nc - 2
+        // every frame before nc - 1 advanced: the last advance is nc - 1 or nc - 2 (a repair
+        // window: the selection's last advance)
         const int nc = s_ncommit, prev0 = st->prev_slot, lv0 = st->last_valid;
-        const int lend = s_adv[nc - 1] ? nc - 1 : nc - 2;
+        const int lend = dual ? s_dual_lend : (s_adv[nc - 1] ? nc - 1 : nc - 2);
         const int msrc_end = s_src[nc - 1];
         int lv = lend >= 0 ? lo + lend : lv0, prev = lend >= 0 ? s_cur[lend] : prev0;
         if (msrc_end >= 0 && msrc_end < MW) s_model_wf = msrc_end;
@@ -2795,7 +2834,7 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
     VO_STAMP(d, 1996, 4);
     // 4
     if (tid < nc) {
-        const VoWork* w = d.work + tid;
+        const VoWork* w = d.work + (dual ? s_rec[tid] : tid);
         const int s = s_status[tid];
         VoFrameOut* o = out + (lo + tid - out_base);
         for (int r = 0; r < 12; ++r) o->pose[r] = s_row[tid][r];
@@ -2810,12 +2849,13 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
     } else if (tid == 255) {
         st->lo = lo + nc;
         st->win = nc < n ? d.repair_win : d.WB;
+        st->dual = nc < n && 2 * d.repair_win <= d.WB;
         st->last_valid = s_newlv;
         st->prev_slot = s_newprev;
         for (int i = 0; i < 16; ++i) st->Tcurr[i] = s_T[i];
         const int m = s_model_wf;
         if (m >= 0) {
-            const VoWork* w = d.work + m;
+            const VoWork* w = d.work + (dual ? s_rec[m] : m);
             st->model_n = w->n_fit;
             st->model_degenerate = s_degen[m];
             for (int i = 0; i < 9; ++i) st->model_F[i] = w->F[i];
@@ -2849,7 +2889,7 @@ __global__ void __launch_bounds__(256) k_reset(VoDev d)
     const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
     if (tid == 0) {
         VoState* st = d.st;
-        st->lo = 0; st->end = 0; st->prev_slot = 0; st->last_valid = 0; st->win = d.WB;
+        st->lo = 0; st->end = 0; st->prev_slot = 0; st->last_valid = 0; st->win = d.WB; st->dual = 0;
         st->model_n = 0; st->model_degenerate = 0; st->pose_status = 0;
         for (int i = 0; i < 9; ++i) { st->model_F[i] = 0.0; st->model_R[i] = 0.0; st->pose_R[i] = 0.0; }
         for (int i = 0; i < 3; ++i) { st->model_t[i] = 0.0; st->pose_t[i] = 0.0; }
