@@ -19,16 +19,10 @@ namespace vo {
 // ---------------------------------------------------------------------------
 // constant tables
 // ---------------------------------------------------------------------------
-__constant__ int8_t c_pt_x[VO_FREAK_NPOINTS];
-__constant__ int8_t c_pt_y[VO_FREAK_NPOINTS];
-__constant__ uint8_t c_pair_p[VO_FREAK_NPAIRS];
-__constant__ uint8_t c_pair_q[VO_FREAK_NPAIRS];
-__constant__ int16_t c_patch[VO_FREAK_NTESTS];
-// per pair: p | q << 8 | (int8)dx << 16 | (int8)dy << 24, and 1/|d| (f64).  (ic*d)/|d| in f32 ==
-// (float)((double)(ic*d) * (1/|d|)) for every ic in [-255,255] and every pair
-// (tests/test_describe_division.py, exhaustive)
-__constant__ uint32_t c_pairpk[VO_FREAK_NPAIRS];
-__constant__ double c_prn[VO_FREAK_NPAIRS];
+// per pair t: dx, dy (f32) and 1/|d| split into rh = f32(1/|d|), rl = f32(1/|d| - rh).
+// (ic*d)/|d| in f32 == fmaf(ic*d, rh, (ic*d) * rl) for every ic in [-255,255], every pair and
+// both components (tests/test_describe_division.py, exhaustive; up to the sign of a zero term)
+__constant__ float4 c_orient[VO_FREAK_NPAIRS];
 
 static bool g_tables_ready = false;
 static void ensure_tables()
@@ -40,23 +34,15 @@ static void ensure_tables()
     int e = 0;
     for (int p = 0; p < VO_FREAK_NPOINTS; ++p)
         for (int q = p + 1; q < VO_FREAK_NPOINTS; ++q) { pp[e] = (uint8_t)p; pq[e] = (uint8_t)q; ++e; }
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pt_x), px, sizeof(px));
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pt_y), py, sizeof(py));
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pair_p), pp, sizeof(pp));
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pair_q), pq, sizeof(pq));
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_patch), vo_freak_patch, sizeof(vo_freak_patch));
-    uint32_t pk[VO_FREAK_NPAIRS];
-    double prn[VO_FREAK_NPAIRS];
+    float4 orient[VO_FREAK_NPAIRS];
     for (int t = 0; t < VO_FREAK_NPAIRS; ++t) {
-        const int ix = px[pp[t]] - px[pq[t]], iy = py[pp[t]] - py[pq[t]];     // |.| <= 70: int8
-        float dx = (float)ix, dy = (float)iy;
-        float nrm = sqrtf(dx * dx + dy * dy);          // host sqrtf: correctly rounded
-        pk[t] = (uint32_t)pp[t] | ((uint32_t)pq[t] << 8) | ((uint32_t)(uint8_t)(int8_t)ix << 16) |
-                ((uint32_t)(uint8_t)(int8_t)iy << 24);
-        prn[t] = 1.0 / (double)nrm;
+        const float dx = (float)(px[pp[t]] - px[pq[t]]), dy = (float)(py[pp[t]] - py[pq[t]]);
+        const float nrm = sqrtf(dx * dx + dy * dy);    // host sqrtf: correctly rounded
+        const double rn = 1.0 / (double)nrm;
+        const float rh = (float)rn, rl = (float)(rn - (double)rh);
+        orient[t] = make_float4(dx, dy, rh, rl);
     }
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pairpk), pk, sizeof(pk));
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_prn), prn, sizeof(prn));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_orient), orient, sizeof(orient));
     g_tables_ready = true;
 }
 
@@ -1145,123 +1131,139 @@ __global__ void k_ext_missing(VoDev d, int slot)
 // describe: orientation (903-term sequential f32 sums) + rotation + 512 tests.
 // FREAK_feature_descriptor_parallel_GPU.cpp:10-210, kernels .c:124-225, orientation order
 // FREAK_feature_descriptor_parallel.cpp:16-44.
-// One wave per DS_KPW = 32 keypoints: lane = keypoint k + 32 * component (0: O_x, 1: O_y),
-// so each lane runs one 903-term sum itself, in order, with the pair table read by scalar
-// loads (the pair index is wave-uniform) and the samples from LDS.  No cross-lane reduction,
-// ~7 KB of LDS per wave.
+// One wave per DS_KPW = 64 keypoints, lane = keypoint: a lane runs both 903-term sums of its
+// keypoint itself, in order (one sample difference serves both components), reading its
+// samples from its own LDS column; pair p's sample stays in a register over the pairs (p, q),
+// the pair table arrives by scalar loads (the pair index is wave-uniform).  The term
+// (ic*d)/|d| is fmaf(x, rh, x * rl) with the reciprocal split into two f32 (equal to the f32
+// division for every reachable ic and pair, tests/test_describe_division.py), so the sums use
+// no f64.  The rotated samples stay in registers and the 512 tests, unrolled with the pattern's
+// pair indices as compile-time constants, are register compares shifted into 32-bit words.
+// No cross-lane traffic, no barrier.
 // ---------------------------------------------------------------------------
-#define DS_KPW 32
+#define DS_KPW 64
 #ifndef DS_WAVES
 #define DS_WAVES 4
 #endif
 #define DS_KPB (DS_KPW * DS_WAVES)
-#define DS_I1W 44                 // s_I1 row bytes: 11 dwords, odd, so 32 rows hit 32 banks
+
+// the FREAK lists of include/vo_freak_tables.h as compile-time tables; pair e is the e-th
+// (p, q), p < q, row-major (ensure_tables enumerates the same order)
+struct DsTables {
+    int px[VO_FREAK_NPOINTS], py[VO_FREAK_NPOINTS];
+    int patch[VO_FREAK_NTESTS];
+    int pp[VO_FREAK_NPAIRS], pq[VO_FREAK_NPAIRS];
+};
+constexpr DsTables ds_make_tables()
+{
+    DsTables t{};
+    constexpr int pts[VO_FREAK_NPOINTS][2] = {VO_FREAK_POINTS_LIST};
+    constexpr short patch[VO_FREAK_NTESTS] = {VO_FREAK_PATCH_LIST};
+    for (int i = 0; i < VO_FREAK_NPOINTS; ++i) { t.px[i] = pts[i][0]; t.py[i] = pts[i][1]; }
+    for (int i = 0; i < VO_FREAK_NTESTS; ++i) t.patch[i] = patch[i];
+    int e = 0;
+    for (int p = 0; p < VO_FREAK_NPOINTS; ++p)
+        for (int q = p + 1; q < VO_FREAK_NPOINTS; ++q) { t.pp[e] = p; t.pq[e] = q; ++e; }
+    return t;
+}
+constexpr DsTables kDs = ds_make_tables();
+
+// one orientation term of both components: (ic*dx)/|d|, (ic*dy)/|d| (c = dx, dy, rh, rl)
+__device__ __forceinline__ void orient_term(float ic, const float4& c, float& ox, float& oy)
+{
+    const float x0 = ic * c.x, x1 = ic * c.y;                       // exact: |ic*d| < 2^15
+    ox = ox + __builtin_fmaf(x0, c.z, x0 * c.w);
+    oy = oy + __builtin_fmaf(x1, c.z, x1 * c.w);
+}
+
+// the 32 tests 32 W .. 32 W + 31 of a keypoint's rotated samples r: bit i = test 32 W + i
+template <int W>
+__device__ __forceinline__ uint32_t ds_word(const uint32_t (&r)[VO_FREAK_NPOINTS])
+{
+    uint32_t word = 0u;
+    st_for([&](auto J) {
+        constexpr int t = 32 * W + 31 - decltype(J)::value;          // highest test first
+        constexpr int e = kDs.patch[t];
+        word = (word << 1) | (r[kDs.pp[e]] > r[kDs.pq[e]] ? 1u : 0u);
+    }, std::make_integer_sequence<int, 32>{});
+    return word;
+}
 
 __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __restrict__ img, int cur, int n,
-                                              int base, float (*s_I0)[VO_FREAK_NPOINTS],
-                                              uint8_t (*s_I1)[DS_I1W])
+                                              int base, float (*s_I0)[DS_KPW])
 {
-    constexpr int NP = VO_FREAK_NPOINTS, HALF = (NP + 1) / 2;     // points per component lane
-    const int lane = threadIdx.x & 63, k = lane & 31, comp = lane >> 5;
+    constexpr int NP = VO_FREAK_NPOINTS;
+    const int lane = threadIdx.x & 63;
     const int W = d.W, H = d.H, Wb = d.bstride;   // blurred plane: row stride Wb
-    const bool valid = base + k < n;
+    [[maybe_unused]] const int stamp_slot = 1000 + (int)((blockIdx.x * DS_WAVES + (threadIdx.x >> 6)) % 900);
+    VO_STAMP(d, stamp_slot, 0);
+    const bool valid = base + lane < n;
     // lanes past n sample around a keypoint inside the margin: every address stays in bounds
     // and the gathers need no branches (their values are never used)
-    const int2 kp = valid ? d.kps[(size_t)cur * d.N + base + k] : make_int2(d.bcol, d.brow);
-    // point u of this lane's half (the second half's last slot repeats point NP - 1)
-    auto pt = [&](int u, int& px, int& py) {
-        const int pa = u, pb = HALF + u < NP ? HALF + u : NP - 1;   // both wave-uniform
-        px = comp ? c_pt_x[pb] : c_pt_x[pa];
-        py = comp ? c_pt_y[pb] : c_pt_y[pa];
-    };
-    // 1. pattern samples of keypoint k: component 0 lanes points [0, HALF), 1 the rest; all
-    //    loads in flight before the LDS stores
+    const int2 kp = valid ? d.kps[(size_t)cur * d.N + base + lane] : make_int2(d.bcol, d.brow);
+    // 1. the 43 pattern samples -> this lane's LDS column (all loads in flight first)
     {
-        uint8_t v[HALF];
-#pragma unroll
-        for (int u = 0; u < HALF; ++u) {
-            int px, py;
-            pt(u, px, py);
-            v[u] = img[(size_t)(kp.y + py) * Wb + (kp.x + px)];
-        }
-#pragma unroll
-        for (int u = 0; u < HALF; ++u)
-            if (!comp || HALF + u < NP) s_I0[k][comp ? HALF + u : u] = (float)v[u];
+        uint32_t v[NP];
+        st_for([&](auto U) {
+            constexpr int u = decltype(U)::value;
+            v[u] = img[(size_t)(kp.y + kDs.py[u]) * Wb + (kp.x + kDs.px[u])];
+        }, std::make_integer_sequence<int, NP>{});
+        st_for([&](auto U) { s_I0[U][lane] = (float)v[U]; }, std::make_integer_sequence<int, NP>{});
     }
-    __syncthreads();
-    // 2. O_comp = sum over pairs t = 0..902 of (ic * d_comp) / |d|, in order in f32.  The
-    //    terms of DS_U consecutive pairs are independent: computed first (their conversions
-    //    and f64 products overlap), then added in order.
-    float acc = 0.0f;
+    VO_STAMP(d, stamp_slot, 1);
+    // 2. O = sum over pairs t = 0..902 of (ic * d) / |d|, each component in order in f32
+    float ox = 0.0f, oy = 0.0f;
     {
-        constexpr int DS_U = 8;
-        const float* I0k = s_I0[k];
-        const int shift = comp ? 24 : 16;
+        const float* col = &s_I0[0][lane];
         int t = 0;
-        for (; t + DS_U <= VO_FREAK_NPAIRS; t += DS_U) {
-            float tm[DS_U];
-#pragma unroll
-            for (int u = 0; u < DS_U; ++u) {
-                const uint32_t pk = c_pairpk[t + u];
-                const float ic = I0k[pk & 0xFF] - I0k[(pk >> 8) & 0xFF];
-                const float dd = (float)(int8_t)(pk >> shift);
-                tm[u] = (float)((double)(ic * dd) * c_prn[t + u]);
+        for (int p = 0; p < NP - 1; ++p) {
+            const float ip = col[p * DS_KPW];
+            const float* cq = col + (p + 1) * DS_KPW;
+            int q = p + 1;
+            for (; q + 4 <= NP; q += 4, t += 4, cq += 4 * DS_KPW) {
+                const float i0 = cq[0], i1 = cq[DS_KPW], i2 = cq[2 * DS_KPW], i3 = cq[3 * DS_KPW];
+                orient_term(ip - i0, c_orient[t], ox, oy);
+                orient_term(ip - i1, c_orient[t + 1], ox, oy);
+                orient_term(ip - i2, c_orient[t + 2], ox, oy);
+                orient_term(ip - i3, c_orient[t + 3], ox, oy);
             }
-#pragma unroll
-            for (int u = 0; u < DS_U; ++u) acc = acc + tm[u];
-        }
-        for (; t < VO_FREAK_NPAIRS; ++t) {
-            const uint32_t pk = c_pairpk[t];
-            const float ic = I0k[pk & 0xFF] - I0k[(pk >> 8) & 0xFF];
-            acc = acc + (float)((double)(ic * (float)(int8_t)(pk >> shift)) * c_prn[t]);
+            for (; q < NP; ++q, ++t, cq += DS_KPW) orient_term(ip - cq[0], c_orient[t], ox, oy);
         }
     }
-    // 3. angle and rotation (both lanes of keypoint k)
-    const float Ox = __shfl(acc, k), Oy = __shfl(acc, k + 32);
+    VO_STAMP(d, stamp_slot, 2);
+    // 3. angle and rotation
     float angle = 0.0f;
-    if (!(isnan(Ox) || isnan(Oy))) angle = (float)det_atan2((double)Oy, (double)Ox);
+    if (!(isnan(ox) || isnan(oy))) angle = (float)det_atan2((double)oy, (double)ox);
     double sd, cd;
     det_sincos((double)angle, &sd, &cd);
     const float c = (float)cd, s = (float)sd, ms = -1.0f * s;
-    // 4. rotated samples (quirk 4: A = [[c, s], [s, c]], (int) truncation)
-    {
-        uint8_t v[HALF];
-#pragma unroll
-        for (int u = 0; u < HALF; ++u) {
-            int px, py;
-            pt(u, px, py);
-            int x = (int)(((float)kp.x + (float)px * c) + (float)py * s);
-            int y = (int)(((float)kp.y + (float)(-1 * px) * ms) + (float)py * c);
-            x = min(max(x, 0), W - 1);   // in range for every keypoint inside the margin
-            y = min(max(y, 0), H - 1);
-            v[u] = img[(size_t)y * Wb + x];
-        }
-#pragma unroll
-        for (int u = 0; u < HALF; ++u)
-            if (!comp || HALF + u < NP) s_I1[k][comp ? HALF + u : u] = v[u];
+    VO_STAMP(d, stamp_slot, 3);
+    // 4. rotated samples (quirk 4: A = [[c, s], [s, c]], (int) truncation), in registers
+    uint32_t r[NP];
+    st_for([&](auto U) {
+        constexpr int u = decltype(U)::value, px = kDs.px[u], py = kDs.py[u];
+        int x = (int)(((float)kp.x + (float)px * c) + (float)py * s);
+        int y = (int)(((float)kp.y + (float)(-1 * px) * ms) + (float)py * c);
+        x = min(max(x, 0), W - 1);   // in range for every keypoint inside the margin
+        y = min(max(y, 0), H - 1);
+        r[u] = img[(size_t)y * Wb + x];
+    }, std::make_integer_sequence<int, NP>{});
+    VO_STAMP(d, stamp_slot, 4);
+    // 5. the 512 tests: 16 words of 32, stored as the 8 u64 of the packed descriptor
+    uint32_t w[16];
+    w[0] = ds_word<0>(r);   w[1] = ds_word<1>(r);   w[2] = ds_word<2>(r);   w[3] = ds_word<3>(r);
+    w[4] = ds_word<4>(r);   w[5] = ds_word<5>(r);   w[6] = ds_word<6>(r);   w[7] = ds_word<7>(r);
+    w[8] = ds_word<8>(r);   w[9] = ds_word<9>(r);   w[10] = ds_word<10>(r); w[11] = ds_word<11>(r);
+    w[12] = ds_word<12>(r); w[13] = ds_word<13>(r); w[14] = ds_word<14>(r); w[15] = ds_word<15>(r);
+    if (valid) {
+        uint4* dst = reinterpret_cast<uint4*>(d.desc + ((size_t)cur * d.N + base + lane) * 8);
+        dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+        dst[2] = make_uint4(w[8], w[9], w[10], w[11]);
+        dst[3] = make_uint4(w[12], w[13], w[14], w[15]);
+        d.pre[(size_t)cur * d.N + base + lane] = w[0];
     }
-    __syncthreads();
-    // 5. the 512 tests: lane l owns test w * 64 + l of word w; one ballot per (keypoint, word)
-    uint32_t tpq[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-        const int e = c_patch[w * 64 + lane];
-        tpq[w] = (uint32_t)c_pair_p[e] | ((uint32_t)c_pair_q[e] << 8);
-    }
-    const int nk = min(DS_KPW, n - base);
-    uint64_t* desc = d.desc + ((size_t)cur * d.N + base) * 8;
-    uint32_t* pre = d.pre + (size_t)cur * d.N + base;
-    for (int kk = 0; kk < nk; ++kk) {
-        unsigned long long mine = 0ull;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) {
-            const bool bit = s_I1[kk][tpq[w] & 0xFF] > s_I1[kk][tpq[w] >> 8];
-            const unsigned long long word = ballot64(bit);
-            mine = lane == w ? word : mine;
-        }
-        if (lane < 8) desc[(size_t)kk * 8 + lane] = mine;
-        if (lane == 0) pre[kk] = (uint32_t)mine;
-    }
+    VO_STAMP(d, stamp_slot, 5);
 }
 
 // grid xcd_grid(N / DS_KPB, nb) (frame z of the batch, workgroup bx of the frame, xcd_frame).
@@ -1270,16 +1272,15 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
 __global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int slot_override, unsigned publish,
                                                             int nb)
 {
-    __shared__ float s_I0[DS_WAVES][DS_KPW][VO_FREAK_NPOINTS];
-    __shared__ uint8_t s_I1[DS_WAVES][DS_KPW][DS_I1W];
+    __shared__ float s_I0[DS_WAVES][VO_FREAK_NPOINTS][DS_KPW];
     int z, bx;
     if (xcd_frame(d, (d.N + DS_KPB - 1) / DS_KPB, nb, z, bx)) {
         const int cur = ext_slot(d, f0, z, slot_override);
         const int n = d.ext_n[cur];
-        const int wave = threadIdx.x >> 6;
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const int base = bx * DS_KPB + wave * DS_KPW;
-        if (bx * DS_KPB < n)             // workgroup-uniform: the barriers inside are met by all
-            describe_wave(d, d.blurred + (size_t)z * d.bplane, cur, n, base, s_I0[wave], s_I1[wave]);
+        if (base < n)                    // wave-uniform; no barrier inside
+            describe_wave(d, d.blurred + (size_t)z * d.bplane, cur, n, base, s_I0[wave]);
     }
     if (!publish) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2658,6 +2659,7 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
             // sequentially over the few frames of the window.
             bool model = st->model_n >= 8, any = false, padv = true;
             int nc = n, lend = -1;
+            for (int wf = 0; wf < n; ++wf) s_rec[wf] = wf;   // frames past the commit: loaded, unused
             for (int wf = 0; wf < n; ++wf) {
                 if (wf > 0 && !padv && any) { nc = wf; break; }
                 const int r = (wf == 0 || padv) ? wf : n + wf;

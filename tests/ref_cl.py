@@ -34,11 +34,11 @@ SZ = C.c_size_t
 def freak_tables():
     """(test_cases int32[903,4], patch uint64[512]) from include/vo_freak_tables.h."""
     src = open(os.path.join(ROOT, "include", "vo_freak_tables.h")).read()
-    pts_blk = src[src.index("vo_freak_points"):src.index("};", src.index("vo_freak_points"))]
+    pts_blk = src.split("#define VO_FREAK_POINTS_LIST")[1].split("#define")[0]
     pts = [(int(a), int(b)) for a, b in re.findall(r"\{\s*(-?\d+),\s*(-?\d+)\s*\}", pts_blk)]
     assert len(pts) == 43
-    pat_blk = src[src.index("vo_freak_patch["):src.index("};", src.index("vo_freak_patch["))]
-    patch = [int(v) for v in re.findall(r"\b(\d+)\b", pat_blk.split("=", 1)[1])]
+    pat_blk = src.split("#define VO_FREAK_PATCH_LIST")[1].split("static const")[0]
+    patch = [int(v) for v in re.findall(r"\b(\d+)\b", pat_blk)]
     assert len(patch) == 512
     tc = [(pts[i][0], pts[i][1], pts[j][0], pts[j][1]) for i in range(43) for j in range(i + 1, 43)]
     return np.array(tc, np.int32), np.array(patch, np.uint64)

@@ -84,10 +84,11 @@ PTS = None
 def freak_tables():
     import re, os
     src = open(os.path.join(os.path.dirname(__file__), "..", "include", "vo_freak_tables.h")).read()
-    pts_txt = src.split("vo_freak_points[VO_FREAK_NPOINTS][2] = {")[1].split("};")[0]
+    pts_txt = src.split("#define VO_FREAK_POINTS_LIST")[1].split("#define")[0]
     pts = [tuple(map(int, p)) for p in re.findall(r"\{(-?\d+), (-?\d+)\}", pts_txt)]
-    patch_txt = src.split("vo_freak_patch[VO_FREAK_NTESTS] = {")[1].split("};")[0]
+    patch_txt = src.split("#define VO_FREAK_PATCH_LIST")[1].split("static const")[0]
     patch = [int(v) for v in re.findall(r"-?\d+", patch_txt)]
+    assert len(pts) == 43 and len(patch) == 512
     pairs = [(p, q) for p in range(43) for q in range(p + 1, 43)]
     return pts, patch, pairs
 
