@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
+#include <cstdio>
 
 #include "vo_internal.h"
 #include "../../include/vo_freak_tables.h"
@@ -22,7 +23,13 @@ namespace vo {
 // per pair t: dx, dy (f32) and 1/|d| split into rh = f32(1/|d|), rl = f32(1/|d| - rh).
 // (ic*d)/|d| in f32 == fmaf(ic*d, rh, (ic*d) * rl) for every ic in [-255,255], every pair and
 // both components (tests/test_describe_division.py, exhaustive; up to the sign of a zero term)
-__constant__ float4 c_orient[VO_FREAK_NPAIRS];
+// Rows p of the pair order padded to whole groups of DS_OG terms with zero terms (dx = dy = 0:
+// the term is a zero, which leaves a sum that is never -0 unchanged), so the describe loop has
+// no remainder iterations.
+#define DS_OG 8
+#define DS_OROWS (VO_FREAK_NPOINTS + DS_OG - 1)     // sample rows incl. the zero padding rows
+#define DS_ONPAD 1056                               // sum over p of ceil((42 - p) / 8) * 8
+__constant__ float4 c_orient[DS_ONPAD];
 
 static bool g_tables_ready = false;
 static void ensure_tables()
@@ -34,14 +41,18 @@ static void ensure_tables()
     int e = 0;
     for (int p = 0; p < VO_FREAK_NPOINTS; ++p)
         for (int q = p + 1; q < VO_FREAK_NPOINTS; ++q) { pp[e] = (uint8_t)p; pq[e] = (uint8_t)q; ++e; }
-    float4 orient[VO_FREAK_NPAIRS];
+    static float4 orient[DS_ONPAD];
+    int o = 0;
     for (int t = 0; t < VO_FREAK_NPAIRS; ++t) {
         const float dx = (float)(px[pp[t]] - px[pq[t]]), dy = (float)(py[pp[t]] - py[pq[t]]);
         const float nrm = sqrtf(dx * dx + dy * dy);    // host sqrtf: correctly rounded
         const double rn = 1.0 / (double)nrm;
         const float rh = (float)rn, rl = (float)(rn - (double)rh);
-        orient[t] = make_float4(dx, dy, rh, rl);
+        orient[o++] = make_float4(dx, dy, rh, rl);
+        if (pq[t] == VO_FREAK_NPOINTS - 1)             // end of row p: pad to a whole group
+            while (o % DS_OG) orient[o++] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
+    if (o != DS_ONPAD) fprintf(stderr, "[vo_mi355x] orientation table size %d != %d\n", o, DS_ONPAD);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_orient), orient, sizeof(orient));
     g_tables_ready = true;
 }
@@ -1209,9 +1220,13 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
             v[u] = img[(size_t)(kp.y + kDs.py[u]) * Wb + (kp.x + kDs.px[u])];
         }, std::make_integer_sequence<int, NP>{});
         st_for([&](auto U) { s_I0[U][lane] = (float)v[U]; }, std::make_integer_sequence<int, NP>{});
+#pragma unroll
+        for (int u = NP; u < DS_OROWS; ++u) s_I0[u][lane] = 0.0f;     // the padding terms' samples
     }
     VO_STAMP(d, stamp_slot, 1);
-    // 2. O = sum over pairs t = 0..902 of (ic * d) / |d|, each component in order in f32
+    // 2. O = sum over pairs t = 0..902 of (ic * d) / |d|, each component in order in f32; row p
+    //    (pairs (p, q), q > p) in groups of DS_OG, the last one padded with zero terms that read
+    //    the zero rows past the samples
     float ox = 0.0f, oy = 0.0f;
     {
         const float* col = &s_I0[0][lane];
@@ -1219,15 +1234,13 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
         for (int p = 0; p < NP - 1; ++p) {
             const float ip = col[p * DS_KPW];
             const float* cq = col + (p + 1) * DS_KPW;
-            int q = p + 1;
-            for (; q + 4 <= NP; q += 4, t += 4, cq += 4 * DS_KPW) {
-                const float i0 = cq[0], i1 = cq[DS_KPW], i2 = cq[2 * DS_KPW], i3 = cq[3 * DS_KPW];
-                orient_term(ip - i0, c_orient[t], ox, oy);
-                orient_term(ip - i1, c_orient[t + 1], ox, oy);
-                orient_term(ip - i2, c_orient[t + 2], ox, oy);
-                orient_term(ip - i3, c_orient[t + 3], ox, oy);
+            for (int g = (NP - 1 - p + DS_OG - 1) / DS_OG; g > 0; --g, t += DS_OG, cq += DS_OG * DS_KPW) {
+                float iq[DS_OG];
+#pragma unroll
+                for (int u = 0; u < DS_OG; ++u) iq[u] = cq[u * DS_KPW];
+#pragma unroll
+                for (int u = 0; u < DS_OG; ++u) orient_term(ip - iq[u], c_orient[t + u], ox, oy);
             }
-            for (; q < NP; ++q, ++t, cq += DS_KPW) orient_term(ip - cq[0], c_orient[t], ox, oy);
         }
     }
     VO_STAMP(d, stamp_slot, 2);
@@ -1272,7 +1285,7 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
 __global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int slot_override, unsigned publish,
                                                             int nb)
 {
-    __shared__ float s_I0[DS_WAVES][VO_FREAK_NPOINTS][DS_KPW];
+    __shared__ float s_I0[DS_WAVES][DS_OROWS][DS_KPW];
     int z, bx;
     if (xcd_frame(d, (d.N + DS_KPB - 1) / DS_KPB, nb, z, bx)) {
         const int cur = ext_slot(d, f0, z, slot_override);
