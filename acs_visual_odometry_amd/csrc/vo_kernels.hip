@@ -1226,21 +1226,41 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
     VO_STAMP(d, stamp_slot, 1);
     // 2. O = sum over pairs t = 0..902 of (ic * d) / |d|, each component in order in f32; row p
     //    (pairs (p, q), q > p) in groups of DS_OG, the last one padded with zero terms that read
-    //    the zero rows past the samples
+    //    the zero rows past the samples.  Software-pipelined: the samples and table entries of
+    //    group g + 1 are requested before group g is summed.
     float ox = 0.0f, oy = 0.0f;
     {
+        constexpr int NG = DS_ONPAD / DS_OG;
         const float* col = &s_I0[0][lane];
-        int t = 0;
-        for (int p = 0; p < NP - 1; ++p) {
-            const float ip = col[p * DS_KPW];
-            const float* cq = col + (p + 1) * DS_KPW;
-            for (int g = (NP - 1 - p + DS_OG - 1) / DS_OG; g > 0; --g, t += DS_OG, cq += DS_OG * DS_KPW) {
-                float iq[DS_OG];
+        int p = 0, qs = 1;                              // group g: row p, samples qs .. qs + 7
+        float ip = col[0], iq[DS_OG];
+        float4 tb[DS_OG];
 #pragma unroll
-                for (int u = 0; u < DS_OG; ++u) iq[u] = cq[u * DS_KPW];
+        for (int u = 0; u < DS_OG; ++u) { iq[u] = col[(qs + u) * DS_KPW]; tb[u] = c_orient[u]; }
+#pragma unroll 2
+        for (int g = 0; g < NG; ++g) {
+            // the next group (the last one re-reads itself)
+            int pn = p, qn = qs + DS_OG;
+            if (qn >= VO_FREAK_NPOINTS) { pn = p + 1; qn = p + 2; }
+            const int gn = g + 1 < NG ? g + 1 : g;
+            if (g + 1 >= NG) { pn = p; qn = qs; }
+            // group g's samples and table entries (requested during group g - 1) have arrived:
+            // wait here, before the next requests, since a scalar load in flight makes any
+            // LDS wait a wait for everything
+            __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0)
+            __builtin_amdgcn_sched_barrier(0);
+            const float ipn = col[pn * DS_KPW];
+            float iqn[DS_OG];
+            float4 tbn[DS_OG];
 #pragma unroll
-                for (int u = 0; u < DS_OG; ++u) orient_term(ip - iq[u], c_orient[t + u], ox, oy);
-            }
+            for (int u = 0; u < DS_OG; ++u) { iqn[u] = col[(qn + u) * DS_KPW]; tbn[u] = c_orient[gn * DS_OG + u]; }
+            __builtin_amdgcn_sched_barrier(0);          // the requests stay ahead of the sums
+#pragma unroll
+            for (int u = 0; u < DS_OG; ++u) orient_term(ip - iq[u], tb[u], ox, oy);
+            __builtin_amdgcn_sched_barrier(0);
+            p = pn; qs = qn; ip = ipn;
+#pragma unroll
+            for (int u = 0; u < DS_OG; ++u) { iq[u] = iqn[u]; tb[u] = tbn[u]; }
         }
     }
     VO_STAMP(d, stamp_slot, 2);
