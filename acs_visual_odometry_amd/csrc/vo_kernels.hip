@@ -1714,12 +1714,65 @@ __device__ __forceinline__ double rdlane(double v, int l)
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// computeFundamentalMatrix on a minimal sample (ransac.cpp:63-93), one wavefront.
-// Gauss-Jordan with complete pivoting exactly as oracle nullvec_8x9: lane l = 8r + c holds
-// A[r][c] (r, c < 8) and every lane of row r holds A[r][8]; pivot = max |a| over unused
-// rows/cols, ties to the first in row-major order (max value, then min flat index).
-__device__ void fit_F8_wave(const VoDev& d, const double* __restrict__ pts, const int s8[8], int lane, double F[9],
-                            int slot)
+// Sampson inlier test (computeSampsonError < thr, ransac.cpp:12-23,163-166).  For thr == 1
+// the division is skipped: with den >= 1e-12, RN(num/den) < 1  <=>  num < den (exact; NaN
+// and inf cases agree), tests/test_sampson_no_div.py.
+__device__ __forceinline__ bool sampson_inlier(const double* F, double x, double y, double xp, double yp,
+                                               double thr, bool thr_is_one)
+{
+    double Fx0 = (F[0] * x + F[1] * y) + F[2] * 1.0;
+    double Fx1 = (F[3] * x + F[4] * y) + F[5] * 1.0;
+    double Ft0 = (F[0] * xp + F[3] * yp) + F[6] * 1.0;
+    double Ft1 = (F[1] * xp + F[4] * yp) + F[7] * 1.0;
+    double Ft2 = (F[2] * xp + F[5] * yp) + F[8] * 1.0;
+    double v = (Ft0 * x + Ft1 * y) + Ft2 * 1.0;
+    double num = v * v;
+    double den = ((Fx0 * Fx0 + Fx1 * Fx1) + Ft0 * Ft0) + Ft1 * Ft1;
+    if (den < 1e-12) return 1.7976931348623157e308 < thr;
+    return thr_is_one ? (num < den) : (num / den < thr);
+}
+
+// ---- eight hypotheses per wave: lane = 8 h + r, hypothesis h, design-matrix row r ----
+// The sample, the normalisation, the 3x3 algebra (denormalize, rank 2) and the 8x9 rows are
+// per lane group; one instruction serves eight hypotheses (the single-hypothesis wave spent
+// most of its instructions on work that is uniform across the wave).
+
+// DPP within 8-lane groups: lane ^ 1, lane ^ 2 (quad_perm), the other quad (row_half_mirror)
+__device__ __forceinline__ int dpp_g8(int v, int step)
+{
+    switch (step) {
+    case 0: return __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);
+    case 1: return __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);
+    default: return __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false);
+    }
+}
+// lane q of each 8-lane group -> every lane of the group (ds_swizzle bitmask mode:
+// and_mask 0x18, or_mask q)
+template <int Q>
+__device__ __forceinline__ int g8_bcast(int v)
+{
+    return __builtin_amdgcn_ds_swizzle(v, 0x18 | (Q << 5));
+}
+template <int Q>
+__device__ __forceinline__ double g8_bcast_d(double v)
+{
+    const long long x = __double_as_longlong(v);
+    const int lo = g8_bcast<Q>((int)(x & 0xFFFFFFFFll)), hi = g8_bcast<Q>((int)(x >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// a[c] for a group-uniform runtime column c (9-way select)
+__device__ __forceinline__ double sel9(const double (&a)[9], int c)
+{
+    double v = a[0];
+#pragma unroll
+    for (int j = 1; j < 9; ++j) v = c == j ? a[j] : v;
+    return v;
+}
+
+// computeFundamentalMatrix on a minimal sample (ransac.cpp:63-93) for the lane group's
+// hypothesis: Gauss-Jordan with complete pivoting exactly as oracle nullvec_8x9 (pivot = max
+// |a| over unused rows/cols, ties to the first in row-major order), lane r holding row r.
+__device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], int r, int gbase, double F[9])
 {
     double P[8][4];
 #pragma unroll
@@ -1741,130 +1794,115 @@ __device__ void fit_F8_wave(const VoDev& d, const double* __restrict__ pts, cons
     }
     sc1 = sqrt(2.0) / sqrt(sc1 / 8.0);
     sc2 = sqrt(2.0) / sqrt(sc2 / 8.0);
-    double o1x = -(sc1 * mx1), o1y = -(sc1 * my1), o2x = -(sc2 * mx2), o2y = -(sc2 * my2);
-    VO_STAMP(d, slot, 2);
-    const int r = lane >> 3, c = lane & 7;
+    const double o1x = -(sc1 * mx1), o1y = -(sc1 * my1), o2x = -(sc2 * mx2), o2y = -(sc2 * my2);
     double x1 = 0, y1 = 0, x2 = 0, y2 = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
         if (i == r) { x1 = P[i][0]; y1 = P[i][1]; x2 = P[i][2]; y2 = P[i][3]; }
-    double row[9];
-    design_row(sc1 * x1 + o1x, sc1 * y1 + o1y, sc2 * x2 + o2x, sc2 * y2 + o2y, row);
-    double arc = 0.0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) if (j == c) arc = row[j];
-    double ar8 = row[8];
+    double a[9];
+    design_row(sc1 * x1 + o1x, sc1 * y1 + o1y, sc2 * x2 + o2x, sc2 * y2 + o2y, a);
     uint32_t used_c = 0, used_r = 0;
-    int prs[8], pcs[8];
-    int steps = 0;
+    int my_pc = -1;                                 // the column this row pivoted (if it did)
+    bool live = true;                               // the group's elimination still runs
 #pragma unroll
     for (int step = 0; step < 8; ++step) {
-        const bool row_free = !((used_r >> r) & 1u);
-        double v1 = (row_free && !((used_c >> c) & 1u)) ? fabs(arc) : 0.0;
-        double v2 = (row_free && c == 0 && !((used_c >> 8) & 1u)) ? fabs(ar8) : 0.0;
-        if (!(v1 > 0.0)) v1 = -1.0;
-        if (!(v2 > 0.0)) v2 = -1.0;
-        // pivot: max value (DPP), ties to the first flat index r*9+col (ballot, scalar)
-        const double gmax = wave_max_f64(fmax(v1, v2));
-        if (!(gmax > 0.0)) break;                     // rank deficient: remaining columns free
-        const unsigned long long b1 = ballot64(v1 == gmax);
-        const unsigned long long b2 = ballot64(v2 == gmax);
+        // lane-local candidate: first max |a| over the unused columns of an unused row
+        double bv = -1.0;
         int bi = 1 << 30;
-        if (b1) { int L = __ffsll((long long)b1) - 1; bi = (L >> 3) * 9 + (L & 7); }
-        if (b2) { int L = __ffsll((long long)b2) - 1; int i2 = (L >> 3) * 9 + 8; bi = i2 < bi ? i2 : bi; }
-        bi = __builtin_amdgcn_readfirstlane(bi);
-        const int pr = bi / 9, pc = bi - pr * 9;
-        used_r |= 1u << pr; used_c |= 1u << pc;
-        prs[step] = pr; pcs[step] = pc; steps = step + 1;
-        const double piv = pc < 8 ? rdlane(arc, pr * 8 + pc) : rdlane(ar8, pr * 8);
-        const double arpc = pc < 8 ? shfl_d(arc, r * 8 + pc) : ar8;      // A[r][pc]
-        const double aprc = shfl_d(arc, pr * 8 + c);                     // A[pr][c]
-        const double apr8 = rdlane(ar8, pr * 8);                         // A[pr][8]
-        if (r != pr) {
-            const double fct = arpc / piv;
-            arc = arc - fct * aprc;
-            ar8 = ar8 - fct * apr8;
+        if (!((used_r >> r) & 1u)) {
+#pragma unroll
+            for (int c = 0; c < 9; ++c) {
+                const double v = fabs(a[c]);
+                if (!((used_c >> c) & 1u) && v > 0.0 && v > bv) { bv = v; bi = r * 9 + c; }
+            }
+        }
+        // group maximum, ties to the smaller flat index
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const double ov = dpp_f64(bv, t);
+            const int oi = dpp_g8(bi, t);
+            const bool take = ov > bv || (ov == bv && oi < bi);
+            bv = take ? ov : bv;
+            bi = take ? oi : bi;
+        }
+        live = live && bv > 0.0;                    // rank deficient: remaining columns free
+        const int pr = bi / 9, pc = bi - (bi / 9) * 9;
+        const double arpc = sel9(a, live ? pc : 0);   // A[r][pc]
+        const int src = gbase + (live ? pr : 0);
+        const double piv = __shfl(arpc, src);
+        double prow[9];
+#pragma unroll
+        for (int c = 0; c < 9; ++c) prow[c] = __shfl(a[c], src);
+        if (live) {
+            used_r |= 1u << pr; used_c |= 1u << pc;
+            if (r == pr) my_pc = pc;
+            if (r != pr) {
+                const double fct = arpc / piv;
+#pragma unroll
+                for (int c = 0; c < 9; ++c) a[c] = a[c] - fct * prow[c];
+            }
         }
     }
     int fc = 0;
 #pragma unroll
     for (int j = 8; j >= 0; --j) if (!((used_c >> j) & 1u)) fc = j;
+    // back substitution: x_fc = 1, x_pc = -a[pr][fc] / a[pr][pc] from each pivot row
+    const double val = my_pc >= 0 ? -(sel9(a, fc) / sel9(a, my_pc)) : 0.0;
     double f[9];
 #pragma unroll
     for (int j = 0; j < 9; ++j) f[j] = (j == fc) ? 1.0 : 0.0;
+    auto take_row = [&](int cq, double vq) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-        if (s < steps) {
-            const int pr = prs[s], pc = pcs[s];
-            const double afc = fc < 8 ? rdlane(arc, pr * 8 + fc) : rdlane(ar8, pr * 8);
-            const double apc = pc < 8 ? rdlane(arc, pr * 8 + pc) : rdlane(ar8, pr * 8);
-            const double v = -(afc / apc);
-#pragma unroll
-            for (int j = 0; j < 9; ++j) if (j == pc) f[j] = v;
-        }
-    }
+        for (int j = 0; j < 9; ++j) f[j] = cq == j ? vq : f[j];
+    };
+    take_row(g8_bcast<0>(my_pc), g8_bcast_d<0>(val));
+    take_row(g8_bcast<1>(my_pc), g8_bcast_d<1>(val));
+    take_row(g8_bcast<2>(my_pc), g8_bcast_d<2>(val));
+    take_row(g8_bcast<3>(my_pc), g8_bcast_d<3>(val));
+    take_row(g8_bcast<4>(my_pc), g8_bcast_d<4>(val));
+    take_row(g8_bcast<5>(my_pc), g8_bcast_d<5>(val));
+    take_row(g8_bcast<6>(my_pc), g8_bcast_d<6>(val));
+    take_row(g8_bcast<7>(my_pc), g8_bcast_d<7>(val));
     double nn = 0.0;
 #pragma unroll
     for (int j = 0; j < 9; ++j) nn = nn + f[j] * f[j];
     nn = sqrt(nn);
 #pragma unroll
     for (int j = 0; j < 9; ++j) f[j] = f[j] / nn;
-    VO_STAMP(d, slot, 3);
     denormalize(f, sc1, mx1, my1, sc2, mx2, my2, F);
     rank2(F);
-    VO_STAMP(d, slot, 4);
 }
 
-// Sampson inlier test (computeSampsonError < thr, ransac.cpp:12-23,163-166).  For thr == 1
-// the division is skipped: with den >= 1e-12, RN(num/den) < 1  <=>  num < den (exact; NaN
-// and inf cases agree), tests/test_sampson_no_div.py.
-__device__ __forceinline__ bool sampson_inlier(const double* F, double x, double y, double xp, double yp,
-                                               double thr, bool thr_is_one)
-{
-    double Fx0 = (F[0] * x + F[1] * y) + F[2] * 1.0;
-    double Fx1 = (F[3] * x + F[4] * y) + F[5] * 1.0;
-    double Ft0 = (F[0] * xp + F[3] * yp) + F[6] * 1.0;
-    double Ft1 = (F[1] * xp + F[4] * yp) + F[7] * 1.0;
-    double Ft2 = (F[2] * xp + F[5] * yp) + F[8] * 1.0;
-    double v = (Ft0 * x + Ft1 * y) + Ft2 * 1.0;
-    double num = v * v;
-    double den = ((Fx0 * Fx0 + Fx1 * Fx1) + Ft0 * Ft0) + Ft1 * Ft1;
-    if (den < 1e-12) return 1.7976931348623157e308 < thr;
-    return thr_is_one ? (num < den) : (num / den < thr);
-}
-
-// inliers of F among the first `scored` matches, counted by ballot; loads 4 words ahead.
-// WPH waves share a hypothesis: sub-wave sw takes the 64-match words w = sw (mod WPH).  The
-// ballots go to `mask` (bit i = match i), from which k_refit compacts the best set.
-template <int WPH>
-__device__ __forceinline__ int count_inliers(const double* __restrict__ pts, int scored, const double* F,
-                                             double thr, int lane, int sw, uint64_t* __restrict__ mask)
+// inliers of the group's F among the first `scored` matches: lane r tests matches 8 j + r of
+// each 64-match word, the group's byte of each ballot is shifted into the word (bit i = match
+// i); the words go to `mask` (k_refit compacts the best set from it)
+__device__ int count_inliers_group(const double* __restrict__ pts, int scored, const double* F, double thr,
+                                   int h, int r, bool store, uint64_t* __restrict__ mask)
 {
     const bool one = thr == 1.0;
     const int nw = (scored + 63) >> 6;
-    int cnt = 0, j = 0;
-    unsigned long long myword = 0ull;            // lane j keeps word sw + WPH * j (scored <= 4096)
-    for (int w0 = sw; w0 < nw; w0 += 4 * WPH) {
-        double2 a[4], c[4];
+    int cnt = 0;
+    for (int w = 0; w < nw; ++w) {
+        double2 a[8], c[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = (w0 + u * WPH) * 64 + lane;
+        for (int j = 0; j < 8; ++j) {
+            const int i = w * 64 + j * 8 + r;
             if (i < scored) {
                 const double2* p = reinterpret_cast<const double2*>(pts + 4 * (size_t)i);
-                a[u] = p[0]; c[u] = p[1];
+                a[j] = p[0]; c[j] = p[1];
             }
         }
+        uint64_t word = 0ull;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = (w0 + u * WPH) * 64 + lane;
-            const bool in = i < scored && sampson_inlier(F, a[u].x, a[u].y, c[u].x, c[u].y, thr, one);
+        for (int j = 0; j < 8; ++j) {
+            const int i = w * 64 + j * 8 + r;
+            const bool in = i < scored && sampson_inlier(F, a[j].x, a[j].y, c[j].x, c[j].y, thr, one);
             const unsigned long long bal = ballot64(in);
-            myword = lane == j + u ? bal : myword;
-            cnt += __popcll(bal);
+            word |= ((bal >> (8 * h)) & 0xFFull) << (8 * j);
         }
-        j += 4;
+        cnt += __popcll(word);
+        if (store && r == (w & 7)) mask[w] = word;
     }
-    if (sw + WPH * lane < nw) mask[sw + WPH * lane] = myword;
     return cnt;
 }
 
@@ -1977,10 +2015,11 @@ __device__ void inv4(const double* M, double* Inv)
 // 4-wave workgroup (each wave fits the same F, the four split the Sampson count: the latency
 // path); second chunk: four single-wave hypotheses per workgroup, since it usually exits at
 // once (fewer workgroups to dispatch).
-template <int WPH, int HPB>
-// reps: hypotheses per wave (strided by the grid), so a later chunk, which usually exits at
-// once, dispatches reps times fewer workgroups
-__global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, int k1, int nhyp, int stage, int reps)
+// HPB waves per workgroup, eight hypotheses per wave (lane 8 h + r: hypothesis h, row r).
+// reps: hypothesis blocks per workgroup (strided by the grid), so a later chunk, which usually
+// exits at once, dispatches reps times fewer workgroups
+template <int HPB>
+__global__ void __launch_bounds__(64 * HPB) k_ransac_hyp(VoDev d, int k0, int k1, int nhyp, int stage, int reps)
 {
     const int wf = blockIdx.y;                     // window frame
     if (wf >= vwin_count(d, stage)) return;
@@ -1988,59 +2027,45 @@ __global__ void __launch_bounds__(64 * WPH * HPB) k_ransac_hyp(VoDev d, int k0, 
     if (w->status != VO_STATUS_OK) return;
     if (k0 > 0 && !w->need_more) return;           // the replay of [0, k0) already stopped
     __shared__ unsigned s_last;
-    __shared__ int s_cnt[HPB][WPH];
-    const int wave = threadIdx.x >> 6, h = wave / WPH, sw = wave - h * WPH;
-    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 3, r = lane & 7;
     const int M = w->M, scored = w->scored;
     const double* pts = d.pts + (size_t)wf * 4 * d.N;
     int32_t* counts = d.counts + (size_t)wf * d.max_hyp;
-    int k = k0 + blockIdx.x * HPB + h;                 // (WPH > 1 only with reps == 1: s_cnt below)
+    int k = k0 + (blockIdx.x * HPB + wave) * 8 + h;
     // Hypotheses at or past the previous replay's bound are never evaluated by the sequential
     // loop: once an improvement updated maxIterations (best > 0 and its table entry is not the
     // 'denom == 0: no update' mark) and the loop went on past k0 (maxit > 100), the inlier ratio
     // is in the band where maxIterations only falls as best rises (below it the x86 INT_MIN clamp
     // gives 100, quirk 8), so maxit bounds every later hypothesis.  Otherwise maxit is still the
-    // initial 1176 and the next improvement may raise it to 2000.  Waves past the bound skip
-    // straight to the arrival.
+    // initial 1176 and the next improvement may raise it to 2000.  Hypotheses past the bound are
+    // marked -1 and cost nothing.
     int kbound = k1;
     if (k0 > 0 && w->best > 0 && d.maxit_tab[(size_t)M * (M + 1) / 2 + w->best] != 0xFFFFu)
         kbound = min(w->maxit, k1);
-    for (int rep = 0; rep < reps; ++rep, k += gridDim.x * HPB) {
-    if (k < kbound) {
-        VO_STAMP(d, k, 0);
-        int s8[8];
-        sample8(w->frame_seed, k, M, s8);
-        VO_STAMP(d, k, 1);
-        double F[9];
-        fit_F8_wave(d, pts, s8, lane, F, k);
-        VO_STAMP(d, k, 5);
-        if (sw == 0 && lane < 9) {
-            double v = 0.0;
+    for (int rep = 0; rep < reps; ++rep, k += gridDim.x * HPB * 8) {
+        const int kb = k - h;                      // the wave's first hypothesis
+        if (kb >= k1) break;                       // wave-uniform
+        const bool mine = k < kbound;
+        if (__builtin_amdgcn_readfirstlane(kb) < kbound) {   // some group of the wave has work
+            VO_STAMP(d, k, 0);
+            int s8[8];
+            sample8(w->frame_seed, min(k, nhyp - 1), M, s8);
+            VO_STAMP(d, k, 1);
+            double F[9];
+            fit_F8_group(pts, s8, r, lane & ~7, F);
+            VO_STAMP(d, k, 5);
+            if (mine) {
+                double* hf = d.hypF + ((size_t)wf * d.max_hyp + k) * 9;
 #pragma unroll
-            for (int c = 0; c < 9; ++c) if (c == lane) v = F[c];
-            d.hypF[((size_t)wf * d.max_hyp + k) * 9 + lane] = v;
+                for (int j = 0; j < 9; ++j)
+                    if (j == r || (j == 8 && r == 0)) hf[j] = F[j];   // lane r: F[r]; lane 0 also F[8]
+            }
+            const int cnt = count_inliers_group(pts, scored, F, d.sampson_thr, h, r, mine,
+                                                d.inlmask + ((size_t)wf * d.max_hyp + min(k, nhyp - 1)) * d.mask_words);
+            if (mine && r == 0) st_sc1(counts + k, cnt);
+            VO_STAMP(d, k, 6);
         }
-        const int cnt =
-            count_inliers<WPH>(pts, scored, F, d.sampson_thr, lane, sw,
-                               d.inlmask + ((size_t)wf * d.max_hyp + k) * d.mask_words);
-        if (WPH == 1) {
-            if (lane == 0) st_sc1(counts + k, cnt);
-        } else if (lane == 0) {
-            s_cnt[h][sw] = cnt;
-        }
-        VO_STAMP(d, k, 6);
-    } else if (k < k1 && sw == 0 && lane == 0) {
-        st_sc1(counts + k, -1);                    // skipped: the replay never takes it
-    }
-    }
-    if (WPH > 1) {
-        __syncthreads();
-        if (k < kbound && sw == 0 && lane == 0) {
-            int t = 0;
-#pragma unroll
-            for (int w = 0; w < WPH; ++w) t += s_cnt[h][w];
-            st_sc1(counts + k, t);
-        }
+        if (!mine && k < k1 && r == 0) st_sc1(counts + k, -1);   // skipped: the replay never takes it
     }
     unsigned* ctr = &w->ctr[k0 == 0 ? 1 : (k0 < VO_HYP_CHUNK1 ? 2 : 3)];   // one arrival counter per chunk
     if (!arrive_last(ctr, gridDim.x, &s_last)) return;
@@ -3057,8 +3082,8 @@ void launch_ransac(const VoDev& d, int stage, hipStream_t s)
         if (k1 <= k0) continue;
         static const int r2 = getenv("VO_RREPS") ? std::max(1, atoi(getenv("VO_RREPS"))) : VO_HYP_REPS;
         const int reps = c == 0 ? 1 : (c == 1 ? std::max(1, r2 / 2) : r2);
-        const int blocks = ((k1 - k0 + 3) / 4 + reps - 1) / reps;
-        hipLaunchKernelGGL((k_ransac_hyp<1, 4>), dim3(blocks, nb), dim3(256), 0, s, d, k0, k1, nhyp, stage, reps);
+        const int blocks = ((k1 - k0 + 31) / 32 + reps - 1) / reps;      // 32 hypotheses per workgroup
+        hipLaunchKernelGGL((k_ransac_hyp<4>), dim3(blocks, nb), dim3(256), 0, s, d, k0, k1, nhyp, stage, reps);
         k0 = k1;
     }
 }
