@@ -1360,8 +1360,9 @@ __device__ __forceinline__ int ratio_accept(uint32_t m1, uint32_t m2, float rati
     return ((float)d1 < ratio * (float)d2) ? (int)(m1 & 0xFFFF) : -1;
 }
 
-// 32-bit prefix mode: 64 queries per workgroup (k_match)
-#define MT_QPB 64
+// 32-bit prefix mode: MT_QPL queries per lane, 64 MT_QPL per workgroup (k_match)
+#define MT_QPL 4
+#define MT_QPB (64 * MT_QPL)
 #define MT512_QPB 256                 // 512-test matcher: queries per workgroup (one per thread)
 __host__ __device__ inline int match_blocks(int N, int match_bits)
 {
@@ -1457,56 +1458,64 @@ __device__ __forceinline__ bool match_header(const VoDev& d, int stage, int wf, 
 // the < 8 matches status (VisualOdometry.cpp:108-123).
 __device__ void match_compact(const VoDev& d, int wf, const MatchFrame& m, int* s_wsum)
 {
+    // rounds of 256 queries (thread t: query 256 u + t), in order: a match's position is the
+    // matches of the earlier rounds, of the earlier waves of its round, and of the lower lanes
+    // of its wave (ballot counts, one barrier per 8 rounds)
+    constexpr int RC = 8;                         // rounds per pass (s_wsum holds RC x 4 counts)
     const int N = d.N, n1 = m.n1, lane = threadIdx.x & 63;
     const int tid = threadIdx.x, wave = tid >> 6;
     const int2* kp1 = d.kps + (size_t)m.prev * N;
     const int2* kp2 = d.kps + (size_t)m.cur * N;
     int2* match_pairs = d.match_pairs + (size_t)wf * N;
     double* pts = d.pts + (size_t)wf * 4 * N;
-    const int per = (n1 + 255) / 256;            // <= 16 (N <= 4096)
-    const int q0 = tid * per;
     VO_STAMP(d, 1993, 2);
-    int js[16];
-    int2 ka[16], kb[16];
-    int cnt = 0;
+    int pos0 = 0;                                 // matches of the earlier passes
+    for (int r0 = 0; r0 * 256 < n1; r0 += RC) {
+        int js[RC];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        int i = q0 + u;
-        js[u] = (u < per && i < n1) ? ld_sc1(m.match_j + i) : -1;
-        cnt += js[u] >= 0;
-    }
-    // all keypoint gathers in flight before the scan (no load-use chain per match)
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        ka[u] = make_int2(0, 0); kb[u] = make_int2(0, 0);
-        if (js[u] >= 0) { ka[u] = kp1[q0 + u]; kb[u] = kp2[js[u]]; }
-    }
-    // block exclusive scan of cnt (wave inclusive scan + wave totals)
-    int incl = cnt;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        int v = __shfl_up(incl, off);
-        if (lane >= off) incl += v;
-    }
-    if (lane == 63) s_wsum[wave] = incl;
-    __syncthreads();
-    int pos = incl - cnt;
-    for (int w = 0; w < wave; ++w) pos += s_wsum[w];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        if (js[u] >= 0) {
-            int i = q0 + u, j = js[u];
-            match_pairs[pos] = make_int2(i, j);
-            const int2 a = ka[u], b = kb[u];
-            double2* p = reinterpret_cast<double2*>(pts + 4 * (size_t)pos);
-            p[0] = make_double2((double)a.x, (double)a.y);
-            p[1] = make_double2((double)b.x, (double)b.y);
-            ++pos;
+        for (int u = 0; u < RC; ++u) {
+            const int i = (r0 + u) * 256 + tid;
+            js[u] = i < n1 ? ld_sc1(m.match_j + i) : -1;
         }
+        int2 ka[RC], kb[RC];
+#pragma unroll
+        for (int u = 0; u < RC; ++u) {
+            ka[u] = make_int2(0, 0); kb[u] = make_int2(0, 0);
+            if (js[u] >= 0) { ka[u] = kp1[(r0 + u) * 256 + tid]; kb[u] = kp2[js[u]]; }
+        }
+        unsigned long long bal[RC];
+#pragma unroll
+        for (int u = 0; u < RC; ++u) {
+            bal[u] = ballot64(js[u] >= 0);
+            if (lane == 0) s_wsum[u * 4 + wave] = __popcll(bal[u]);
+        }
+        __syncthreads();
+        int pos = pos0;
+#pragma unroll
+        for (int u = 0; u < RC; ++u) {
+            int before = 0, total = 0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const int c = s_wsum[u * 4 + w];
+                before += w < wave ? c : 0;
+                total += c;
+            }
+            if (js[u] >= 0) {
+                const int p = pos + before + __popcll(bal[u] & ((1ull << lane) - 1ull));
+                match_pairs[p] = make_int2((r0 + u) * 256 + tid, js[u]);
+                const int2 a = ka[u], b = kb[u];
+                double2* pp = reinterpret_cast<double2*>(pts + 4 * (size_t)p);
+                pp[0] = make_double2((double)a.x, (double)a.y);
+                pp[1] = make_double2((double)b.x, (double)b.y);
+            }
+            pos += total;
+        }
+        pos0 = pos;
+        __syncthreads();                          // s_wsum is rewritten by the next pass
     }
     if (tid == 0) {
         VoWork* w = m.w;
-        int M = ((s_wsum[0] + s_wsum[1]) + s_wsum[2]) + s_wsum[3];
+        const int M = pos0;
         w->M = M;
         w->scored = (M / d.T) * d.T;
         w->status = M < 8 ? VO_STATUS_FEW_MATCHES : VO_STATUS_OK;   // VisualOdometry.cpp:108-115
@@ -1536,9 +1545,9 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
     MatchFrame m;
     if (!match_header(d, stage, wf, m)) return;
     __shared__ unsigned s_last;
-    __shared__ int s_wsum[4];
+    __shared__ int s_wsum[32];
     __shared__ uint4 s_cand4[1024];                  // 4096 prefixes
-    __shared__ uint2 s_top[3][64];
+    __shared__ uint2 s_top[3][MT_QPL][64];
     uint32_t* s_cand = reinterpret_cast<uint32_t*>(s_cand4);
     const int N = d.N, n1 = m.n1, n2 = m.n2;
     // wave-uniform candidate range: scalar loop counter, key index an SGPR operand
@@ -1553,33 +1562,53 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
             for (int u = 0; u < 4; ++u)
                 if (j0 + u * 256 < n2) s_cand[j0 + u * 256] = v[u];
         }
-        const int q = blockIdx.x * MT_QPB + lane;
-        const uint32_t qv = q < n1 ? d.pre[(size_t)m.prev * N + q] : 0u;
+        // lane's queries: blockIdx.x * MT_QPB + 64 u + lane
+        uint32_t qv[MT_QPL];
+#pragma unroll
+        for (int u = 0; u < MT_QPL; ++u) {
+            const int q = blockIdx.x * MT_QPB + 64 * u + lane;
+            qv[u] = q < n1 ? d.pre[(size_t)m.prev * N + q] : 0u;
+        }
         // quarter of the candidates: [j0, j1), j0 a multiple of 4
         const int qs = ((n2 + 15) >> 4) << 2;
         const int j0 = min(wave * qs, n2), j1 = min(j0 + qs, n2);
-        uint32_t a1 = 0xFFFFFFFFu, a2 = 0xFFFFFFFFu, b1 = 0xFFFFFFFFu, b2 = 0xFFFFFFFFu;
+        uint32_t a1[MT_QPL], a2[MT_QPL], b1[MT_QPL], b2[MT_QPL];
+#pragma unroll
+        for (int u = 0; u < MT_QPL; ++u) a1[u] = a2[u] = b1[u] = b2[u] = 0xFFFFFFFFu;
         __syncthreads();
         int j = j0;
-#pragma unroll 2
         for (; j + 4 <= j1; j += 4) {
             const uint4 c = s_cand4[j >> 2];
-            top2_insert(((uint32_t)__popc(qv ^ c.x) << 16) | (uint32_t)j, a1, a2);
-            top2_insert(((uint32_t)__popc(qv ^ c.y) << 16) | (uint32_t)(j + 1), b1, b2);
-            top2_insert(((uint32_t)__popc(qv ^ c.z) << 16) | (uint32_t)(j + 2), a1, a2);
-            top2_insert(((uint32_t)__popc(qv ^ c.w) << 16) | (uint32_t)(j + 3), b1, b2);
+#pragma unroll
+            for (int u = 0; u < MT_QPL; ++u) {
+                top2_insert(((uint32_t)__popc(qv[u] ^ c.x) << 16) | (uint32_t)j, a1[u], a2[u]);
+                top2_insert(((uint32_t)__popc(qv[u] ^ c.y) << 16) | (uint32_t)(j + 1), b1[u], b2[u]);
+                top2_insert(((uint32_t)__popc(qv[u] ^ c.z) << 16) | (uint32_t)(j + 2), a1[u], a2[u]);
+                top2_insert(((uint32_t)__popc(qv[u] ^ c.w) << 16) | (uint32_t)(j + 3), b1[u], b2[u]);
+            }
         }
-        for (; j < j1; ++j) top2_insert(((uint32_t)__popc(qv ^ s_cand[j]) << 16) | (uint32_t)j, a1, a2);
-        top2_merge(a1, a2, b1, b2);
-        if (wave > 0) s_top[wave - 1][lane] = make_uint2(a1, a2);
+        for (; j < j1; ++j) {
+            const uint32_t cj = s_cand[j];
+#pragma unroll
+            for (int u = 0; u < MT_QPL; ++u) top2_insert(((uint32_t)__popc(qv[u] ^ cj) << 16) | (uint32_t)j, a1[u], a2[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < MT_QPL; ++u) {
+            top2_merge(a1[u], a2[u], b1[u], b2[u]);
+            if (wave > 0) s_top[wave - 1][u][lane] = make_uint2(a1[u], a2[u]);
+        }
         __syncthreads();
         if (wave == 0) {
 #pragma unroll
-            for (int w = 0; w < 3; ++w) {
-                const uint2 o = s_top[w][lane];
-                top2_merge(a1, a2, o.x, o.y);
+            for (int u = 0; u < MT_QPL; ++u) {
+#pragma unroll
+                for (int w = 0; w < 3; ++w) {
+                    const uint2 o = s_top[w][u][lane];
+                    top2_merge(a1[u], a2[u], o.x, o.y);
+                }
+                const int q = blockIdx.x * MT_QPB + 64 * u + lane;
+                if (q < n1) st_sc1(m.match_j + q, ratio_accept(a1[u], a2[u], d.ratio));
             }
-            if (q < n1) st_sc1(m.match_j + q, ratio_accept(a1, a2, d.ratio));
         }
     }
     if (blockIdx.x == 0) VO_STAMP(d, 1993, 1);
@@ -1631,7 +1660,7 @@ __global__ void __launch_bounds__(256) k_match512(VoDev d, int stage)
     MatchFrame m;
     if (!match_header(d, stage, wf, m)) return;
     __shared__ unsigned s_last;
-    __shared__ int s_wsum[4];
+    __shared__ int s_wsum[32];                      // match_compact: 8 rounds x 4 waves
     extern __shared__ uint4 s_tile[];        // MT512_TILE x 64 B
     const int N = d.N, n1 = m.n1, n2 = m.n2;
     const int q = blockIdx.x * MT512_QPB + threadIdx.x;

@@ -1,0 +1,8 @@
+# 4 queries per lane matcher + round-wise compaction: GPU parity tests, bench
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r2z; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+bash tools/gpu_ab_env.sh r2z/ab "VO_X=0"
