@@ -41,9 +41,12 @@ struct vo_ctx {
     bool serial = false;              // VO_SERIAL=1: every kernel on one queue, no cross-queue
                                       // waits (for profilers that serialize dispatches: PMC passes)
     bool event_wait = true;           // pose queue waits for extract batches on events (default)
-    int slack = 0;                    // VO_SLACK: extra passes enqueued per chunk (misses re-run without a host round trip)
                                       // or on the stream-wait-value packet (VO_EVENT_WAIT=0; events
                                       // again after the runtime refused a wait-value packet)
+    int slack = 0;                    // VO_SLACK: extra passes enqueued per chunk (misses re-run without a host round trip)
+    hipStream_t st = nullptr;         // trajectory queue: k_traj of each pass (T_curr chain, pose rows)
+    hipEvent_t ev_fin = nullptr;      // a pass's k_finalize done (the trajectory queue waits on it)
+    int npass = 0;                    // pose passes enqueued (their pass-log entries)
     // per-batch event pools of a chunk: [VO_EV_WAIT] extract done (event_wait mode),
     // [VO_EV_COPY] H2D copy done, [VO_EV_STENCIL] stencil done (host streaming)
     std::vector<hipEvent_t> ev_batch[3];
@@ -130,6 +133,7 @@ int sync_all(vo_ctx* c)
     for (hipStream_t q : c->se)
         if (q) HIPCHK(hipStreamSynchronize(q));
     if (c->s) HIPCHK(hipStreamSynchronize(c->s));
+    if (c->st) HIPCHK(hipStreamSynchronize(c->st));
     return VO_OK;
 }
 #define SYNC_ALL(c)                        \
@@ -326,11 +330,19 @@ void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax)
     hipStream_t s = c->s;
     VoDev d = c->d;
     d.gmax = gmax;
+    d.pass = c->npass++;
     timed(c, ev, 3, s, [&] { vo::launch_match(d, 0, s); });
     timed(c, ev, 4, s, [&] { vo::launch_ransac(d, 0, s); });
     timed(c, ev, 5, s, [&] { vo::launch_refit(d, 1, 0, s); });
     timed(c, ev, 6, s, [&] { vo::launch_triangulate(d, 0, s); });
     timed(c, ev, 7, s, [&] { vo::launch_finalize(d, out, out_base, s); });
+    // the T_curr chain and the pose rows on the trajectory queue (serial mode: the pose queue)
+    hipStream_t q = c->serial ? s : c->st;
+    if (q != s) {
+        (void)hipEventRecord(c->ev_fin, s);
+        (void)hipStreamWaitEvent(q, c->ev_fin, 0);
+    }
+    timed(c, ev, 8, q, [&] { vo::launch_traj(d, out, out_base, q); });
 }
 
 // Batch sizes of a chunk: B frames per extract batch and per pass window (the last one
@@ -460,11 +472,14 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     // every pass commits at least its first frame, so nf re-pass rounds bound the loop
     for (int round = 0, prev_lo = base;; ++round) {
         HIPCHK(hipGetLastError());
-        // the chunk's output rows and the commit point in one round trip
+        // the chunk's output rows (complete once the trajectory queue's last k_traj ran, which
+        // waited for the last k_finalize) and the commit point
+        hipStream_t tq = c->serial ? s : c->st;
         HIPCHK(hipMemcpyAsync(c->out_host + (base - out_base), out + (base - out_base), sizeof(VoFrameOut) * nf,
-                              hipMemcpyDeviceToHost, s));
+                              hipMemcpyDeviceToHost, tq));
         HIPCHK(hipMemcpyAsync(c->lo_host, &c->d.st->lo, sizeof(int32_t), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipStreamSynchronize(tq));
         const int lo = *c->lo_host;
         if (lo >= end) break;
         if (lo < base || lo > end || round > nf || (round > 0 && lo <= prev_lo)) {
@@ -609,6 +624,9 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     // repair windows hold two work records per frame (k_finalize): at most WB / 2 frames
     d.repair_win = std::max(1, std::min(d.WB / 2, getenv("VO_REPAIR_WIN") ? atoi(getenv("VO_REPAIR_WIN")) : VO_REPAIR_WIN_DEFAULT));
     if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK)
+        return bail(VO_ERR_HIP);
     for (hipStream_t& q : c->se)
         if (hip_ok(hipStreamCreateWithFlags(&q, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming)) != VO_OK) return bail(VO_ERR_HIP);
@@ -644,6 +662,8 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc(&d.ext_st, VO_SLOTS);
     rc |= dalloc(&d.seq_starts, VO_MAX_SEQ_STARTS);
     rc |= dalloc(&d.ctr, VO_CTR_WORDS);
+    rc |= dalloc(&d.trec, VO_SLOTS);
+    rc |= dalloc(&d.plog, VO_PLOG);
 #ifdef VO_STAMPS
     rc |= dalloc(&d.dbg, (size_t)d.max_hyp * 16);
 #endif
@@ -676,10 +696,11 @@ void vo_destroy(vo_ctx* c)
     for (hipStream_t q : c->se)
         if (q) (void)hipStreamSynchronize(q);
     if (c->s) (void)hipStreamSynchronize(c->s);
+    if (c->st) (void)hipStreamSynchronize(c->st);
     VoDev& d = c->d;
     void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.tilerows, d.ckeys, d.selbits, d.hist, d.ext_n, d.ext_st, (void*)d.seq_starts,
                     d.kps, d.desc, d.pre, d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.inlmask,
-                    d.model_p, d.work, d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr, d.dbg};
+                    d.model_p, d.work, d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr, d.trec, d.plog, d.dbg};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->out_host) (void)hipHostFree(c->out_host);
@@ -695,6 +716,8 @@ void vo_destroy(vo_ctx* c)
     for (hipStream_t q : c->se)
         if (q) (void)hipStreamDestroy(q);
     if (c->s) (void)hipStreamDestroy(c->s);
+    if (c->st) (void)hipStreamDestroy(c->st);
+    if (c->ev_fin) (void)hipEventDestroy(c->ev_fin);
     delete c;
 }
 

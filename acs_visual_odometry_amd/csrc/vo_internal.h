@@ -66,7 +66,7 @@ inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_T
 #define VO_MAX_SEQ_STARTS 4096     // vo_set_sequence_starts capacity
 #define VO_DEFAULT_BATCH 64
 #define VO_REPAIR_WIN_DEFAULT 8   // pose window after a speculation miss (frames; dual records: 4 / 8 / 16 measured 174k / 180k / 177k KITTI frames/s)
-#define VO_SLACK_DEFAULT 4        // extra passes per chunk of >= 4 batches (VO_SLACK)
+#define VO_SLACK_DEFAULT 1        // extra passes per chunk of >= 4 batches (VO_SLACK; 0 / 1 / 4 measured within noise)
 // ctr words: cross-queue counters on lines of their own
 #define VO_EXT_QUEUES 1        // extract queues (batch j on queue j % n, own scratch); 2 measured no faster
 #define VO_CTR_DESCRIBE 0      // + 16 * queue: describe's in-launch arrival counter
@@ -111,7 +111,20 @@ struct VoWork {
     double R1[9], R2[9], t[3];
 };
 
-// Trajectory state (VisualOdometry::run's locals), read and written by k_finalize only.
+// A committed frame's input to the trajectory (written by k_finalize, read by k_traj on the
+// trajectory queue): the relative motion's model (R, unit t before the GT scale) and the
+// frame's kind.  Ring of d.ring records, frame f at f % ring.
+struct VoTrajRec {
+    double R[9], t[3];
+    int32_t kind;         // 1: T_curr = T_curr * T_rel (a posed frame); 0: T_curr unchanged
+    int32_t first;        // FIRST: T_curr = eye(4) (VisualOdometry.cpp:57)
+    int32_t flip;         // the row is flipZ * T_curr (all but FIRST / MISSING)
+    int32_t lvb;          // last valid frame before it (the GT scale's reference)
+};
+#define VO_PLOG 4096       // pass log ring: (lo, committed frames) of pass p at p % VO_PLOG
+
+// Trajectory state (VisualOdometry::run's locals), read and written by k_finalize only
+// (T_curr: by k_traj only).
 struct VoState {
     int32_t lo;           // frames committed since vo_reset (the next pass starts here)
     int32_t end;          // end of the frames enqueued so far
@@ -186,6 +199,9 @@ struct VoDev {
     const int32_t* seq_starts;   // sorted frame indices (since vo_reset) where a new sequence begins
     int n_seq_starts;
     unsigned* ctr;
+    VoTrajRec* trec;      // x ring: committed frames' trajectory inputs (k_finalize -> k_traj)
+    int2* plog;           // x VO_PLOG: (lo, committed) per pose pass
+    int pass;             // pose pass number (its plog entry)
     unsigned long long* dbg;   // diagnostic s_memtime stamps (VO_STAMPS builds only)
 };
 
@@ -206,6 +222,7 @@ void launch_ransac(const VoDev& d, int stage, hipStream_t s);       // all hypot
 void launch_refit(const VoDev& d, int with_pose, int stage, hipStream_t s);
 void launch_triangulate(const VoDev& d, int stage, hipStream_t s);
 void launch_finalize(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s);
+void launch_traj(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s);   // T_curr chain + pose rows of pass d.pass
 void launch_pose_stage(const VoDev& d, int phase, hipStream_t s);   // vo_pose: 0 prepare, 1 choose
 void launch_reset(const VoDev& d, hipStream_t s);                   // vo_reset's device state
 void launch_selftest_arith(const float* fa, const float* fb, float* fo, const double* da,

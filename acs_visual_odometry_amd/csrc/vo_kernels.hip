@@ -380,16 +380,23 @@ __device__ __forceinline__ int refl101(int i, int n)
 // read of a lane that is off in EXEC returns 0, so the shift must run with the whole wave on:
 // the empty volatile asm pins it where it is written (the compiler otherwise sank a shift into
 // the masked arm of a select, and border lanes read 0 from their masked neighbours).
+#ifndef VO_DPP_PIN
+#define VO_DPP_PIN 1
+#endif
 __device__ __forceinline__ int from_left(int v)
 {
     int r = __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true);   // bound_ctrl: edge lanes read 0, no old operand
+#if VO_DPP_PIN
     asm volatile("" : "+v"(r));
+#endif
     return r;
 }
 __device__ __forceinline__ int from_right(int v)
 {
     int r = __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true);   // bound_ctrl: edge lanes read 0, no old operand
+#if VO_DPP_PIN
     asm volatile("" : "+v"(r));
+#endif
     return r;
 }
 
@@ -2711,10 +2718,11 @@ __device__ __forceinline__ double dpp_quad_bcast(double v, int k)
 //      desc1 / last_valid advance (quirk 10) -- and the commit point: the first frame after
 //      a frame that did not advance desc1 was matched against the wrong previous frame, so
 //      it and everything after it go to the next pass
-//   2  per committed frame: GT scale (VisualOdometry.cpp:161-162) and T_rel
-//   3  wave 0, lane = entry: T_curr = T_curr * T_rel in frame order (mm4's operation order)
-//   4  per committed frame: the output row; thread 0: the trajectory state; all: the carry
-//      copy of desc1 when the window ends in a skip (its ring slot will be rewritten)
+//   2  per committed frame: the trajectory record (model R, t, kind) for k_traj, the output
+//      row's counts; thread 255: the loop state and the pass log entry; all: the carry copy of
+//      desc1 when the window ends in a skip (its ring slot will be rewritten)
+// The T_curr chain and the pose rows run in k_traj on the trajectory queue: the next pass
+// needs none of them, so they overlap it.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int out_base)
 {
@@ -2723,9 +2731,6 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
     __shared__ int s_status[MW], s_kind[MW], s_src[MW], s_lvb[MW];
     __shared__ int s_flip[MW], s_fitted[MW], s_degen[MW], s_cur[MW], s_adv[MW];
     __shared__ double s_R[MW + 1][9], s_t[MW + 1][3];
-    __shared__ double s_Trel[MW + 2][16];             // + 2: step 3 reads two frames ahead
-    __shared__ double s_row[MW][12];
-    __shared__ double s_T[16];
     __shared__ int s_rec[MW];                         // the work record each window frame uses
     __shared__ int s_dual_nc, s_dual_lend;
     const int tid = threadIdx.x;
@@ -2767,7 +2772,10 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
     __syncthreads();
     VO_STAMP(d, 1996, 0);
     const int n = s_n, lo = s_lo;
-    if (n <= 0) return;
+    if (n <= 0) {
+        if (tid == 0) d.plog[d.pass % VO_PLOG] = make_int2(lo, 0);   // k_traj: nothing committed
+        return;
+    }
     // 0
     if (tid < n) {
         const VoWork* w = d.work + (dual ? s_rec[tid] : tid);
@@ -2784,8 +2792,6 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
     } else if (tid == 255) {
         for (int i = 0; i < 9; ++i) s_R[MW][i] = st->model_R[i];
         for (int i = 0; i < 3; ++i) s_t[MW][i] = st->model_t[i];
-    } else if (tid == 254) {
-        for (int i = 0; i < 16; ++i) s_T[i] = st->Tcurr[i];
     }
     __syncthreads();
     VO_STAMP(d, 1996, 1);
@@ -2856,77 +2862,20 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
     VO_STAMP(d, 1996, 2);
     const int nc = s_ncommit;
     // 2
-    if (tid < nc && s_kind[tid] == 1) {
-        const int f = lo + tid, lvb = s_lvb[tid], src = s_src[tid];
-        double scale = 1.0;
-        if (d.gt_n > 0 && f < d.gt_n && lvb < d.gt_n) {
-            double Gi[16], Gl[16], Ii[16], Tr[16];
-            for (int r = 0; r < 16; ++r) {
-                Gi[r] = r < 12 ? d.gt[12 * (size_t)f + r] : (r == 15 ? 1.0 : 0.0);
-                Gl[r] = r < 12 ? d.gt[12 * (size_t)lvb + r] : (r == 15 ? 1.0 : 0.0);
-            }
-            inv4(Gi, Ii);
-            mm4(Ii, Gl, Tr);
-            scale = sqrt((Tr[3] * Tr[3] + Tr[7] * Tr[7]) + Tr[11] * Tr[11]);
-        }
-        const double* R = s_R[src];
-        double tf[3] = {s_t[src][0], s_t[src][1], s_t[src][2]};
-        scale_t(tf, scale);
-        double* T = s_Trel[tid];
-        T[0] = R[0]; T[1] = R[1]; T[2] = R[2]; T[3] = tf[0];
-        T[4] = R[3]; T[5] = R[4]; T[6] = R[5]; T[7] = tf[1];
-        T[8] = R[6]; T[9] = R[7]; T[10] = R[8]; T[11] = tf[2];
-        T[12] = 0.0; T[13] = 0.0; T[14] = 0.0; T[15] = 1.0;
-    }
-    __syncthreads();
-    VO_STAMP(d, 1996, 3);
-    // 3 (wave 0): the frame kinds as wave-uniform bit masks, T_rel columns read from LDS two
-    //   frames ahead, so each step's critical path is the quad broadcasts and the four products
-    if (tid < 64) {
-        const int e = tid & 15, i = e >> 2, j = e & 3;
-        // frame kinds of window frames tid (chunk 0) and 64 + tid (chunk 1)
-        const bool inc = tid < nc, inc1 = 64 + tid < nc;
-        const unsigned long long Mkind0 = ballot64(inc && s_kind[tid] == 1);
-        const unsigned long long Mfirst0 = ballot64(inc && s_status[tid] == VO_STATUS_FIRST);
-        const unsigned long long Mflip0 = ballot64(inc && s_flip[tid] != 0);
-        const unsigned long long Mkind1 = ballot64(inc1 && s_kind[64 + tid] == 1);
-        const unsigned long long Mfirst1 = ballot64(inc1 && s_status[64 + tid] == VO_STATUS_FIRST);
-        const unsigned long long Mflip1 = ballot64(inc1 && s_flip[64 + tid] != 0);
-        double Tv = s_T[e];
-        const double ident = (e % 5 == 0) ? 1.0 : 0.0;  // VisualOdometry.cpp:57 T_curr = eye(4)
-        double b[3][4];
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) b[u][k] = s_Trel[u][k * 4 + j];
-        // branch-free: every step computes the product and selects (s_Trel rows past nc are
-        // never used); the loads of frame wf + 2 are unconditional
-        for (int wf = 0; wf < nc; ++wf) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) b[2][k] = s_Trel[wf + 2][k * 4 + j];
-            // row i of T_curr: entry k from lane 4i + k of the quad (DPP quad broadcast)
-            const double a0 = dpp_quad_bcast(Tv, 0), a1 = dpp_quad_bcast(Tv, 1);
-            const double a2 = dpp_quad_bcast(Tv, 2), a3 = dpp_quad_bcast(Tv, 3);
-            const double pv = ((a0 * b[0][0] + a1 * b[0][1]) + a2 * b[0][2]) + a3 * b[0][3];
-            const int sh = wf & 63;
-            const bool kind = ((wf < 64 ? Mkind0 : Mkind1) >> sh) & 1ull;
-            const bool firstf = ((wf < 64 ? Mfirst0 : Mfirst1) >> sh) & 1ull;
-            const bool flip = ((wf < 64 ? Mflip0 : Mflip1) >> sh) & 1ull;
-            Tv = kind ? pv : (firstf ? ident : Tv);
-            if (tid < 12) s_row[wf][tid] = (flip && i == 2) ? -Tv : Tv;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) { b[0][k] = b[1][k]; b[1][k] = b[2][k]; }
-        }
-        if (tid < 16) s_T[tid] = Tv;
-    }
-    __syncthreads();
-    VO_STAMP(d, 1996, 4);
-    // 4
     if (tid < nc) {
         const VoWork* w = d.work + (dual ? s_rec[tid] : tid);
         const int s = s_status[tid];
+        VoTrajRec* tr = d.trec + (lo + tid) % VO_RING;
+        if (s_kind[tid] == 1) {
+            const int src = s_src[tid];
+            for (int i = 0; i < 9; ++i) tr->R[i] = s_R[src][i];
+            for (int i = 0; i < 3; ++i) tr->t[i] = s_t[src][i];
+        }
+        tr->kind = s_kind[tid];
+        tr->first = s == VO_STATUS_FIRST;
+        tr->flip = s_flip[tid];
+        tr->lvb = s_lvb[tid];
         VoFrameOut* o = out + (lo + tid - out_base);
-        for (int r = 0; r < 12; ++r) o->pose[r] = s_row[tid][r];
         o->status = s;
         o->n_kps = s == VO_STATUS_MISSING ? 0 : d.ext_n[s_cur[tid]];
         o->n_matches = w->M;
@@ -2936,12 +2885,12 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
         o->fitted = s_fitted[tid];
         o->frame = lo + tid;
     } else if (tid == 255) {
+        d.plog[d.pass % VO_PLOG] = make_int2(lo, nc);
         st->lo = lo + nc;
         st->win = nc < n ? d.repair_win : d.WB;
         st->dual = nc < n && 2 * d.repair_win <= d.WB;
         st->last_valid = s_newlv;
         st->prev_slot = s_newprev;
-        for (int i = 0; i < 16; ++i) st->Tcurr[i] = s_T[i];
         const int m = s_model_wf;
         if (m >= 0) {
             const VoWork* w = d.work + (dual ? s_rec[m] : m);
@@ -2968,6 +2917,111 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
             d.ext_n[VO_CARRY_SLOT] = nk;
             d.ext_st[VO_CARRY_SLOT] = VO_STATUS_OK;
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// trajectory (trajectory queue, after pass d.pass's k_finalize): the committed frames' GT scale
+// and T_rel (VisualOdometry.cpp:161-166), T_curr = T_curr * T_rel in frame order (mm4's
+// operation order) and the pose rows (:175-181).  One workgroup:
+//   1  per committed frame: GT scale and T_rel from its trajectory record
+//   2  wave 0, lane = entry: the chain, the frame kinds as wave-uniform bit masks, T_rel columns
+//      read from LDS two frames ahead, so each step's critical path is the quad broadcasts and
+//      the four products
+//   3  per committed frame: the pose row; thread 255: T_curr
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_traj(VoDev d, VoFrameOut* out, int out_base)
+{
+    constexpr int MW = VO_MAX_WIN;
+    __shared__ double s_Trel[MW + 2][16];             // + 2: step 2 reads two frames ahead
+    __shared__ double s_row[MW][12];
+    __shared__ double s_T[16];
+    __shared__ int s_kind[MW], s_first[MW], s_flip[MW];
+    const int tid = threadIdx.x;
+    const int2 lg = d.plog[d.pass % VO_PLOG];
+    const int lo = lg.x, nc = lg.y;
+    if (nc <= 0) return;
+    VoState* st = d.st;
+    // 1
+    if (tid < nc) {
+        const int f = lo + tid;
+        const VoTrajRec* tr = d.trec + f % VO_RING;
+        const int kind = tr->kind;
+        s_kind[tid] = kind;
+        s_first[tid] = tr->first;
+        s_flip[tid] = tr->flip;
+        if (kind == 1) {
+            const int lvb = tr->lvb;
+            double scale = 1.0;
+            if (d.gt_n > 0 && f < d.gt_n && lvb < d.gt_n) {
+                double Gi[16], Gl[16], Ii[16], Tr[16];
+                for (int r = 0; r < 16; ++r) {
+                    Gi[r] = r < 12 ? d.gt[12 * (size_t)f + r] : (r == 15 ? 1.0 : 0.0);
+                    Gl[r] = r < 12 ? d.gt[12 * (size_t)lvb + r] : (r == 15 ? 1.0 : 0.0);
+                }
+                inv4(Gi, Ii);
+                mm4(Ii, Gl, Tr);
+                scale = sqrt((Tr[3] * Tr[3] + Tr[7] * Tr[7]) + Tr[11] * Tr[11]);
+            }
+            double R[9], tf[3];
+            for (int i = 0; i < 9; ++i) R[i] = tr->R[i];
+            for (int i = 0; i < 3; ++i) tf[i] = tr->t[i];
+            scale_t(tf, scale);
+            double* T = s_Trel[tid];
+            T[0] = R[0]; T[1] = R[1]; T[2] = R[2]; T[3] = tf[0];
+            T[4] = R[3]; T[5] = R[4]; T[6] = R[5]; T[7] = tf[1];
+            T[8] = R[6]; T[9] = R[7]; T[10] = R[8]; T[11] = tf[2];
+            T[12] = 0.0; T[13] = 0.0; T[14] = 0.0; T[15] = 1.0;
+        }
+    } else if (tid == 255) {
+        for (int i = 0; i < 16; ++i) s_T[i] = st->Tcurr[i];
+    }
+    __syncthreads();
+    // 2
+    if (tid < 64) {
+        const int e = tid & 15, i = e >> 2, j = e & 3;
+        // frame kinds of window frames tid (chunk 0) and 64 + tid (chunk 1)
+        const bool inc = tid < nc, inc1 = 64 + tid < nc;
+        const unsigned long long Mkind0 = ballot64(inc && s_kind[tid] == 1);
+        const unsigned long long Mfirst0 = ballot64(inc && s_first[tid] != 0);
+        const unsigned long long Mflip0 = ballot64(inc && s_flip[tid] != 0);
+        const unsigned long long Mkind1 = ballot64(inc1 && s_kind[64 + tid] == 1);
+        const unsigned long long Mfirst1 = ballot64(inc1 && s_first[64 + tid] != 0);
+        const unsigned long long Mflip1 = ballot64(inc1 && s_flip[64 + tid] != 0);
+        double Tv = s_T[e];
+        const double ident = (e % 5 == 0) ? 1.0 : 0.0;  // VisualOdometry.cpp:57 T_curr = eye(4)
+        double b[3][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) b[u][k] = s_Trel[u][k * 4 + j];
+        // branch-free: every step computes the product and selects (s_Trel rows of other
+        // kinds are never used); the loads of frame wf + 2 are unconditional
+        for (int wf = 0; wf < nc; ++wf) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) b[2][k] = s_Trel[wf + 2][k * 4 + j];
+            // row i of T_curr: entry k from lane 4i + k of the quad (DPP quad broadcast)
+            const double a0 = dpp_quad_bcast(Tv, 0), a1 = dpp_quad_bcast(Tv, 1);
+            const double a2 = dpp_quad_bcast(Tv, 2), a3 = dpp_quad_bcast(Tv, 3);
+            const double pv = ((a0 * b[0][0] + a1 * b[0][1]) + a2 * b[0][2]) + a3 * b[0][3];
+            const int sh = wf & 63;
+            const bool kind = ((wf < 64 ? Mkind0 : Mkind1) >> sh) & 1ull;
+            const bool firstf = ((wf < 64 ? Mfirst0 : Mfirst1) >> sh) & 1ull;
+            const bool flip = ((wf < 64 ? Mflip0 : Mflip1) >> sh) & 1ull;
+            Tv = kind ? pv : (firstf ? ident : Tv);
+            if (tid < 12) s_row[wf][tid] = (flip && i == 2) ? -Tv : Tv;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { b[0][k] = b[1][k]; b[1][k] = b[2][k]; }
+        }
+        if (tid < 16) s_T[tid] = Tv;
+    }
+    __syncthreads();
+    // 3
+    if (tid < nc) {
+        VoFrameOut* o = out + (lo + tid - out_base);
+        for (int r = 0; r < 12; ++r) o->pose[r] = s_row[tid][r];
+    } else if (tid == 255) {
+        for (int i = 0; i < 16; ++i) st->Tcurr[i] = s_T[i];
     }
 }
 
@@ -3033,7 +3087,7 @@ __global__ void k_selftest_arith(const float* fa, const float* fb, float* fo, co
 // launch wrappers
 // ---------------------------------------------------------------------------
 static const char* g_names[] = {"stencil", "select", "describe", "match", "ransac", "refit", "triangulate",
-                                "finalize"};
+                                "finalize", "trajectory"};
 int kernel_count() { return (int)(sizeof(g_names) / sizeof(g_names[0])); }
 const char* kernel_name(int i) { return g_names[i]; }
 
@@ -3128,6 +3182,10 @@ void launch_triangulate(const VoDev& d, int stage, hipStream_t s)
 void launch_finalize(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s)
 {
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, d, out, out_base);
+}
+void launch_traj(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_traj, dim3(1), dim3(256), 0, s, d, out, out_base);
 }
 void launch_reset(const VoDev& d, hipStream_t s)
 {

@@ -49,11 +49,11 @@ METRIC = "VO frames/sec (extract+match+pose), 1241×376 mono, 2000 kpts/frame"
 HBM_PEAK_GBS = 8000.0
 # VALU issue peak: 256 CUs x 4 SIMD-32, a wave64 VALU instruction every 2 cycles per SIMD
 VALU_SIMDS = 1024
-KERNELS = ["stencil", "select", "describe", "match", "ransac", "refit", "triangulate", "finalize"]
-POSE_QUEUE = ["match", "ransac", "refit", "triangulate", "finalize"]
+KERNELS = ["stencil", "select", "describe", "match", "ransac", "refit", "triangulate", "finalize", "trajectory"]
+POSE_QUEUE = ["match", "ransac", "refit", "triangulate", "finalize"]     # the trajectory queue overlaps them
 ROCPROF_NAME = {"stencil": "k_stencil", "select": "k_select", "describe": "k_describe", "match": "k_match",
                 "ransac": "k_ransac_hyp", "refit": "k_refit", "triangulate": "k_triangulate",
-                "finalize": "k_finalize"}
+                "finalize": "k_finalize", "trajectory": "k_traj"}
 # committed rocprofv3 summaries (tools/profile.sh -> tools/rocprof_summary.py --json): kernel
 # durations, PMC HBM bytes and VALU counters per launch
 PROFILES = {(1241, 376, 32): "r2_kitti_kernels.json", (1920, 1080, 32): "r2_1080_kernels.json",
@@ -65,13 +65,13 @@ def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray) -> float:
     kernel that moves each term (n = keypoints, M = matches, I = inliers, averaged over info):
     the image read (stencil), 8n keypoints written (select), 64n descriptors written (describe),
     8n prefixes read + 8M matches written (match), 16M match coordinates read (RANSAC), 96 B of
-    R, t (finalize).  Refit and triangulate have no term of their own in 8(d); they are given
+    R, t (the trajectory kernel, which writes the pose row).  Refit and triangulate have no term of their own in 8(d); they are given
     their 16I inlier coordinates read."""
     n = float(info[:, 0].mean())
     M = float(info[:, 1].mean())
     I = float(info[:, 2].mean())
     return {"stencil": W * H, "select": 8 * n, "describe": 64 * n, "match": 8 * n + 8 * M, "ransac": 16 * M,
-            "refit": 16 * I, "triangulate": 16 * I, "finalize": 96.0,
+            "refit": 16 * I, "triangulate": 16 * I, "finalize": 0.0, "trajectory": 96.0,
             "path": W * H + 80 * n + 24 * M + 96}[kernel]
 
 
@@ -95,7 +95,7 @@ def profile_row(prof, kernel: str):
     rows = [r for k, r in prof.items() if k.split("<")[0] == ROCPROF_NAME[kernel]]
     if not rows:
         return None
-    ref = "k_match" if kernel in POSE_QUEUE else "k_stencil"
+    ref = "k_match" if kernel in POSE_QUEUE or kernel == "trajectory" else "k_stencil"
     ref_calls = [r["calls"] for k, r in prof.items() if k.split("<")[0] == ref]
     launches = max(ref_calls) if ref_calls else max(r["calls"] for r in rows)
 

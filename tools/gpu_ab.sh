@@ -13,7 +13,7 @@ done
 for rep in 1 2; do
 for lib in $LIBS; do
   VO_LIB_PATH=acs_visual_odometry_amd/$lib timeout -k 10 200 python -u bench.py --no-cpu --no-variants "$@" > $O/b_$lib.json 2> $O/b_$lib.err || { echo "$lib BENCH_FAIL"; tail -5 $O/b_$lib.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/b_$lib.json')); print('$lib', round(d['value']), {k: round(v*1e3,1) for k, v in d['kernels_ms_per_launch'].items()})"
+  python3 -c "import json; d=json.load(open('$O/b_$lib.json')); print('$lib', round(d['value']), {k: v['us_per_frame'] for k, v in d['kernels'].items()})"
 done
 done
 echo DONE
