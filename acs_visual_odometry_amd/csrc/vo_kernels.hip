@@ -439,8 +439,9 @@ __device__ __forceinline__ float st_response(int sx, int sy, int ss)
     const float jx2 = (float)sx, jy2 = (float)sy, sxy = (float)ss;
     const float det = (jx2 * jy2) - (sxy * sxy);
     const float tr = jx2 + jy2;
-    // tr / 2 == tr * 0.5 exactly (both the correctly rounded halving)
-    return (tr * 0.5f) - (0.5f * sqrt_cr_intval(tr * tr - 4.0f * det));
+    // (tr * 0.5) - (0.5 * s) == 0.5 * (tr - s) exactly: both halvings are exact (tr and s are 0,
+    // >= 1 or NaN) and rounding commutes with scaling by 2 in the normal range (tr / 2 == tr * 0.5)
+    return 0.5f * (tr - sqrt_cr_intval(tr * tr - 4.0f * det));
 }
 
 typedef unsigned short st_u16x2 __attribute__((ext_vector_type(2)));
@@ -468,8 +469,11 @@ __device__ __forceinline__ void st_for(F&& f, std::integer_sequence<int, I...>)
 #define ST_BUF_DW3 0x00020000      // gfx9 buffer descriptor word 3 (raw bytes, no format)
 
 // grid xcd_grid(ceil(waves / 4), nb): 4 waves per workgroup, one (strip, segment) per wave
+#ifndef ST_WAVES_PER_EU
+#define ST_WAVES_PER_EU 4
+#endif
 template <int SEGT, bool DBG>
-__global__ void __launch_bounds__(256) k_stencil(VoDev d, const uint8_t* __restrict__ img0, size_t frame_bytes,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAVES_PER_EU))) k_stencil(VoDev d, const uint8_t* __restrict__ img0, size_t frame_bytes,
                                                   int write_response, int nb)
 {
     constexpr int SEG = ST_TH * SEGT;
