@@ -68,7 +68,9 @@ inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_T
 #define VO_REPAIR_WIN_DEFAULT 8   // pose window after a speculation miss (frames; dual records: 4 / 8 / 16 measured 174k / 180k / 177k KITTI frames/s)
 #define VO_SLACK_DEFAULT 1        // extra passes per chunk of >= 4 batches (VO_SLACK; 0 / 1 / 4 measured within noise)
 // ctr words: cross-queue counters on lines of their own
+#ifndef VO_EXT_QUEUES
 #define VO_EXT_QUEUES 1        // extract queues (batch j on queue j % n, own scratch); 2 measured no faster
+#endif
 #define VO_CTR_DESCRIBE 0      // + 16 * queue: describe's in-launch arrival counter
 #define VO_SYNC_EXT 32         // + 16 * queue: frames extracted since vo_reset by that queue
                                // (its batches complete in order; the pose queue waits on it)
