@@ -767,8 +767,8 @@ __host__ __device__ inline SelLayout sel_layout(int ntiles, int lds_bytes)
     L.segw = L.tpre + al((ntiles + 1) * 4);
     const int segb = al(nseg > BND_CAP * 8 ? nseg : BND_CAP * 8);     // u8 counts, aliased by boundary keys
     L.bits = L.segw + segb;
-    L.chunk = L.bits + SEL_LDS_BITS / 8;
-    L.keys = L.chunk + 1024 * 4;
+    L.chunk = L.bits + SEL_LDS_BITS / 8;                      // u16 prefix per 4 segments
+    L.keys = L.chunk + al(((nseg + 3) / 4) * 2);
     L.key_cap = (lds_bytes - L.keys) / 8;
     L.total = lds_bytes;
     return L;
@@ -818,10 +818,9 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     uint4* s_rows = reinterpret_cast<uint4*>(smem + L.rows);
     int* s_tpre = reinterpret_cast<int*>(smem + L.tpre);
     uint32_t* s_segw = reinterpret_cast<uint32_t*>(smem + L.segw);
-    const uint8_t* s_segb = smem + L.segw;
     uint64_t* s_bnd = reinterpret_cast<uint64_t*>(smem + L.segw);        // phase C only
     uint64_t* s_bitsl = reinterpret_cast<uint64_t*>(smem + L.bits);
-    int* s_chunk = reinterpret_cast<int*>(smem + L.chunk);
+    uint16_t* s_wpre = reinterpret_cast<uint16_t*>(smem + L.chunk);   // selected keys before 4-segment word w
     uint64_t* s_keys = reinterpret_cast<uint64_t*>(smem + L.keys);
     const size_t TCAP = ST_TW * ST_TH / 4;
     if (tid == 0) {
@@ -1015,26 +1014,17 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
         }
     }
     __syncthreads();
-    // E: thread tid owns segments [tid*cs, tid*cs+cs)
-    const int cs = (nseg + 1023) / 1024;
-    auto bytesum = [&](int s0, int s1) -> int {         // sum of u8 counts in [s0, s1)
-        int acc = 0;
-        for (int s = s0; s < s1;) {
-            if ((s & 3) == 0 && s + 4 <= s1) {
-                const uint32_t w = s_segw[s >> 2];
-                const uint32_t p = (w & 0x00FF00FFu) + ((w >> 8) & 0x00FF00FFu);
-                acc += (int)((p & 0xFFFF) + (p >> 16));
-                s += 4;
-            } else {
-                acc += s_segb[s];
-                ++s;
-            }
-        }
-        return acc;
+    // E: exclusive prefix of the selected counts per 4-segment word; thread tid owns words
+    //    [tid*cw, tid*cw+cw) (segment counts are u8, four to a word)
+    auto wordsum = [](uint32_t w) -> int {
+        const uint32_t p = (w & 0x00FF00FFu) + ((w >> 8) & 0x00FF00FFu);
+        return (int)((p & 0xFFFF) + (p >> 16));
     };
     {
-        const int s0 = min(tid * cs, nseg), s1 = min(s0 + cs, nseg);
-        const int mine = bytesum(s0, s1);
+        const int nw = (nseg + 3) / 4, cw = (nw + 1023) / 1024;
+        const int w0 = min(tid * cw, nw), w1 = min(w0 + cw, nw);
+        int mine = 0;
+        for (int w = w0; w < w1; ++w) mine += wordsum(s_segw[w]);
         int inc2 = mine;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
@@ -1045,7 +1035,10 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
         __syncthreads();
         int pre = inc2 - mine;
         for (int w = 0; w < wave; ++w) pre += s_wsum[w];
-        s_chunk[tid] = pre;
+        for (int w = w0; w < w1; ++w) {
+            s_wpre[w] = (uint16_t)pre;                  // <= N <= 4096 selected keys
+            pre += wordsum(s_segw[w]);
+        }
     }
     __syncthreads();
     VO_STAMP(d, 1990, 5);
@@ -1082,9 +1075,10 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
                 if (wi == (g >> 6)) m &= (g & 63) ? (~0ull >> (64 - (g & 63))) : 0ull;
                 within += __popcll(m);
             }
-            const int ch = seg / cs;
-            const int pos = s_chunk[ch] + bytesum(ch * cs, seg) + within;
-            out[pos] = make_int2(col, row);
+            // the segment's start: its word's prefix plus the counts of the word's lower segments
+            const uint32_t sw = s_segw[seg >> 2] & ((1u << (8 * (seg & 3))) - 1u);
+            const int pos = (int)s_wpre[seg >> 2] + wordsum(sw) + within;
+            if (pos < N) out[pos] = make_int2(col, row);  // < N by construction (corrupt input: no stray store)
         }
     }
     VO_STAMP(d, 1990, 6);
