@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""k_select anatomy from s_memtime stamps (diagnostic VO_STAMPS build): cycles per phase of the
-last frame's select in a 64-frame batched run (slot 1990), median over runs.
+"""k_select anatomy from s_memtime stamps (diagnostic VO_STAMPS build): cycles per phase of one
+frame's select (the stage API: one workgroup writes slot 1990), median over frames.
 usage: VO_LIB_PATH=acs_visual_odometry_amd/libvo_mi355x_stamps.so python tools/stamps_select.py"""
 import ctypes as C
 import os
@@ -21,11 +21,8 @@ L.vo_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
 names = ["A+B tile counts, scan, key staging", "C histogram boundary bin", "C boundary keys gathered",
          "C rank (threshold key) + clear", "D bitmap + segment counts, E scan", "F keypoint emission"]
 rows = []
-for rep in range(10):
-    df = ctx.device_frames(fr)
-    ctx.reset()
-    ctx.process_frames_device(df)
-    df.free()
+for rep in range(20):
+    ctx.extract(fr[rep % len(fr)])
     buf = np.zeros(2000 * 16, np.uint64)
     L.vo_debug_stamps(ctx.h, buf.ctypes.data_as(C.c_void_p), buf.size)
     t = buf[1990 * 16:1990 * 16 + 7].astype(np.int64)
