@@ -47,7 +47,9 @@ import numpy as np  # noqa: E402
 
 METRIC = "VO frames/sec (extract+match+pose), 1241×376 mono, 2000 kpts/frame"
 HBM_PEAK_GBS = 8000.0
-# VALU issue peak: 256 CUs x 4 SIMD-32, a wave64 VALU instruction every 2 cycles per SIMD
+# VALU issue peak: 256 CUs x 4 SIMDs, a wave64 VALU instruction every 4 cycles per SIMD
+# (profiles/r2_valu_calibration.md: tools/valu_rate.hip measures 4-4.5 cycles for f32, int, f64, DPP)
+VALU_CYCLES = 4
 VALU_SIMDS = 1024
 KERNELS = ["stencil", "select", "describe", "match", "ransac", "refit", "triangulate", "finalize", "trajectory"]
 POSE_QUEUE = ["match", "ransac", "refit", "triangulate", "finalize"]     # the trajectory queue overlaps them
@@ -105,7 +107,7 @@ def profile_row(prof, kernel: str):
         return sum(r[key] * r["calls"] for r in rows) / launches
     vi, gc = per("valu_insts"), per("grbm_cycles")
     return {"avg_us": per("avg_us"), "hbm_bytes": per("hbm_bytes_per_launch"), "valu_insts": vi,
-            "valu_issue_frac": vi * 2 / (VALU_SIMDS * gc / 8) if vi is not None and gc else None}
+            "valu_issue_frac": vi * VALU_CYCLES / (VALU_SIMDS * gc / 8) if vi is not None and gc else None}
 
 
 # -- multi-GPU harness (config 5) --------------------------------------------------------
@@ -477,7 +479,7 @@ def main():
                 "choice": "largest per-frame time among the pose-queue kernels (the serial critical path)",
                 "valu": None if not prow else {
                     "insts_per_launch": prow["valu_insts"], "issue_frac": prow["valu_issue_frac"],
-                    "peak": f"{VALU_SIMDS} SIMDs x 1 wave64 VALU instruction / 2 cycles (PMC: SQ_INSTS_VALU, "
+                    "peak": f"{VALU_SIMDS} SIMDs x 1 wave64 VALU instruction / {VALU_CYCLES} cycles (PMC: SQ_INSTS_VALU, "
                             f"GRBM_GUI_ACTIVE)"}}
         path_bytes = algorithmic_bytes("path", W, H, info_all)
         kern = {}

@@ -8,7 +8,7 @@ read, MI355X_MICROARCH.md 'HBM'; tools/fetch_calib.hip measures the factor for t
 1-byte-per-lane reads the VO kernels issue, profiles/r2_fetch_calibration.md) + WRITE_SIZE*1024
 (exact for 16-, 4- and 1-byte stores).
 VALU (a third pass, "valu*": SQ_INSTS_VALU, SQ_WAVES, GRBM_GUI_ACTIVE): issue fraction =
-SQ_INSTS_VALU x 2 cycles (a wave64 instruction on a SIMD-32) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8
+SQ_INSTS_VALU x 4 cycles (a wave64 instruction per SIMD, profiles/r2_valu_calibration.md) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8
 XCDs), i.e. the share of the dispatch's SIMD cycles spent issuing VALU at the f32/integer rate
 (f64 FMAs and transcendentals take longer, so f64 kernels read low).
 """
@@ -47,7 +47,7 @@ def main():
     table = {}
     print(f"# {title}\n")
     print("rocprofv3 --kernel-trace --stats (durations) and separate --pmc passes: FETCH_SIZE, WRITE_SIZE, and "
-          "SQ_INSTS_VALU + SQ_WAVES + GRBM_GUI_ACTIVE.  VALU issue = SQ_INSTS_VALU x 2 / (1024 x "
+          "SQ_INSTS_VALU + SQ_WAVES + GRBM_GUI_ACTIVE.  VALU issue = SQ_INSTS_VALU x 4 / (1024 x "
           "GRBM_GUI_ACTIVE / 8).\n")
     print("| kernel | calls | avg us | share % | FETCH_SIZE KB/launch | WRITE_SIZE KB/launch | HBM bytes/launch | "
           "VALU insts/launch | waves/launch | VALU issue |")
@@ -56,7 +56,7 @@ def main():
         k = short(r["Name"])
         f, w = fetch.get(k), write.get(k)
         vi, wv, gc = vinst.get(k), waves.get(k), grbm.get(k)
-        issue = vi * 2 / (1024 * gc / 8) if vi is not None and gc else None
+        issue = vi * 4 / (1024 * gc / 8) if vi is not None and gc else None
         hb = "" if f is None or w is None else f"{(f * (2 if x2 else 1) + w) * 1024:,.0f}"
         table[k] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
                     "fetch_kb": f, "write_kb": w,
