@@ -328,7 +328,7 @@ __device__ __forceinline__ double sampson(const double* F, double x, double y, d
     return num / den;
 }
 
-__device__ __forceinline__ unsigned long long ballot64(bool p) { return __ballot(p); }
+__device__ __forceinline__ unsigned long long ballot64(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
 // diagnostic stamps (separate VO_STAMPS build; never in the product library)
 #ifdef VO_STAMPS
@@ -420,30 +420,6 @@ __device__ __forceinline__ bool xcd_frame(const VoDev& d, int nx, int nb, int& z
 }
 __host__ inline int xcd_grid(int nx, int nb) { return nx * ((nb + 7) / 8) * 8; }
 
-// correctly rounded sqrtf for the response's argument: integer-valued (0 or |x| >= 1: every
-// term of tr * tr - 4 det is an integer-valued f32) or negative (NaN).  v_sqrt_f32 is within
-// 1 ulp; one residual test on each neighbour rounds it (the compiler's own sqrtf expansion
-// without its denormal scaling and its 0 / inf class test, which this range never needs).
-__device__ __forceinline__ float sqrt_cr_intval(float x)
-{
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const float sm = __int_as_float(__float_as_int(s) - 1), sp = __int_as_float(__float_as_int(s) + 1);
-    const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
-    float r = rm <= 0.0f ? sm : s;
-    r = rp > 0.0f ? sp : r;
-    return r;
-}
-// kernel .c:108-114 (f32, in the reference's order)
-__device__ __forceinline__ float st_response(int sx, int sy, int ss)
-{
-    const float jx2 = (float)sx, jy2 = (float)sy, sxy = (float)ss;
-    const float det = (jx2 * jy2) - (sxy * sxy);
-    const float tr = jx2 + jy2;
-    // (tr * 0.5) - (0.5 * s) == 0.5 * (tr - s) exactly: both halvings are exact (tr and s are 0,
-    // >= 1 or NaN) and rounding commutes with scaling by 2 in the normal range (tr / 2 == tr * 0.5)
-    return 0.5f * (tr - sqrt_cr_intval(tr * tr - 4.0f * det));
-}
-
 typedef unsigned short st_u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ st_u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(st_u16x2, v); }
 __device__ __forceinline__ uint32_t as_u32(st_u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -459,6 +435,43 @@ __device__ __forceinline__ int from_right16(int v)
     const int r = from_right(v);
     __builtin_assume((unsigned)r < 65536u);
     return r;
+}
+// column pairs in f32 from the blurred plane on: every value up to the response is an integer
+// below 2^24 (|J| <= 512 after the blur, a sum of 25 squares < 2^24), so f32 sums are exact and
+// their order is free; the pair runs as one packed-FP32 instruction (v_pk_add/mul/fma_f32:
+// two lanes' worth per issue, tools/valu_rate.hip)
+typedef float st_f2 __attribute__((ext_vector_type(2)));
+typedef unsigned short st_w2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float from_leftf(float v) { return __int_as_float(from_left(__float_as_int(v))); }
+__device__ __forceinline__ float from_rightf(float v) { return __int_as_float(from_right(__float_as_int(v))); }
+// (a.x - b.y, b.x - a.y) in one v_pk_add_f32: cross halves through op_sel, signs through neg
+__device__ __forceinline__ st_f2 st_xsub(st_f2 a, st_f2 b)
+{
+    st_f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ st_f2 st_fma(st_f2 a, st_f2 b, st_f2 c) { return __builtin_elementwise_fma(a, b, c); }
+// the pair's response, kernel .c:108-114 (f32, in the reference's order): det = (jx2 jy2) -
+// (sxy sxy); (tr tr) - 4 det as one fma (4 det is exact); (tr * 0.5) - (0.5 * s) == 0.5 * (tr - s)
+// exactly (both halvings are exact: tr and s are 0, >= 1 or NaN).  sqrtf correctly rounded for
+// this argument, integer-valued (0 or |x| >= 1: every term is an integer-valued f32) or negative
+// (NaN): v_sqrt_f32 is within 1 ulp, and one residual test on each neighbour rounds it (the
+// compiler's own expansion without its denormal scaling and 0 / inf class test); the two
+// residuals of the pair in one packed fma each
+__device__ __forceinline__ st_f2 st_response2(st_f2 jx2, st_f2 jy2, st_f2 sxy)
+{
+    const st_f2 det = (jx2 * jy2) - (sxy * sxy);
+    const st_f2 tr = jx2 + jy2;
+    const st_f2 x = st_fma(det, st_f2{-4.0f, -4.0f}, tr * tr);
+    const st_f2 s = {__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+    const st_f2 sm = {__int_as_float(__float_as_int(s.x) - 1), __int_as_float(__float_as_int(s.y) - 1)};
+    const st_f2 sp = {__int_as_float(__float_as_int(s.x) + 1), __int_as_float(__float_as_int(s.y) + 1)};
+    const st_f2 rm = st_fma(-sm, s, x), rp = st_fma(-sp, s, x);
+    st_f2 r;
+    r.x = rp.x > 0.0f ? sp.x : (rm.x <= 0.0f ? sm.x : s.x);
+    r.y = rp.y > 0.0f ? sp.y : (rm.y <= 0.0f ? sm.y : s.y);
+    return 0.5f * (tr - r);
 }
 // f(integral_constant<int, I>) for I = 0 .. N-1, unrolled at compile time
 template <typename F, int... I>
@@ -526,10 +539,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
 
     // register histories (index 0 oldest); source rows packed: column c0 low half, c0 + 1 high
     uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0;
-    int ba0 = 0, bm0 = 0, be0 = 0, ba1 = 0, bm1 = 0, be1 = 0;               // blurred rows
-    int qx0[5] = {0, 0, 0, 0, 0}, qx1[5] = {0, 0, 0, 0, 0}, vx0 = 0, vx1 = 0;   // Jx^2 rows, vertical sums
-    int qy0[5] = {0, 0, 0, 0, 0}, qy1[5] = {0, 0, 0, 0, 0}, vy0 = 0, vy1 = 0;   // Jy^2
-    int qs0[5] = {0, 0, 0, 0, 0}, qs1[5] = {0, 0, 0, 0, 0}, vs0 = 0, vs1 = 0;   // Jxy
+    const st_f2 z2 = {0.0f, 0.0f};
+    st_f2 BA = z2, BM = z2, BE = z2;                                          // blurred rows
+    st_f2 QX[5] = {z2, z2, z2, z2, z2}, VX = z2;                              // Jx^2 rows, vertical sums
+    st_f2 QY[5] = {z2, z2, z2, z2, z2}, VY = z2;                              // Jy^2
+    st_f2 QS[5] = {z2, z2, z2, z2, z2}, VS = z2;                              // Jxy
     int ru0 = 0, rm0 = 0, rd0 = 0, ru1 = 0, rm1 = 0, rd1 = 0;               // response rows (f32 bits)
     int toffA = 0, toffB = 0;                                                // candidates so far per tile
     int trows = 0;                                                           // lane r (16 + r): tile A (B) row r count
@@ -553,24 +567,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         s0 = s1; s1 = s2; s2 = s3; s3 = s4; s4 = s5; s5 = s6; s6 = src;
         if constexpr (P >= 1) {
             // 1. 7x7 blur (cv::GaussianBlur 8U fixed point, A.1): vertical taps on both columns
-            //    in 16-bit halves (<= 65280), horizontal taps from the pair and its neighbours,
-            //    one rounding: (sum k_i k_j I + 2^15) >> 16
+            //    in 16-bit halves (<= 65280); the horizontal taps as dot products of 16-bit pairs
+            //    (v_dot2_u32_u16) of the lane's pair and its neighbours' (wave shifts of the packed
+            //    word move both columns), the rounding bias as the first addend:
+            //    (sum k_i k_j I + 2^15) >> 16 is byte 2 of the sum (< 2^24)
             const st_u16x2 v = (as_u16x2(s0) + as_u16x2(s6)) * (unsigned short)8 +
                                (as_u16x2(s1) + as_u16x2(s5)) * (unsigned short)28 +
                                (as_u16x2(s2) + as_u16x2(s4)) * (unsigned short)56 + as_u16x2(s3) * (unsigned short)72;
-            const int va = (int)(as_u32(v) & 0xFFFFu), vb = (int)(as_u32(v) >> 16);
-            const int aL1 = from_left16(va), bL1 = from_left16(vb), aR1 = from_right16(va), bR1 = from_right16(vb);
-            const int bL2 = from_left16(bL1), aR2 = from_right16(aR1);
-            const int ha = 8 * (bL2 + bR1) + 28 * (aL1 + aR1) + 56 * (bL1 + vb) + 72 * va;   // < 2^24
-            const int hb = 8 * (aL1 + aR2) + 28 * (bL1 + bR1) + 56 * (va + aR1) + 72 * vb;
-            const int b0 = (ha + 32768) >> 16, b1 = (hb + 32768) >> 16;
-            ba0 = bm0; bm0 = be0; be0 = b0;
-            ba1 = bm1; bm1 = be1; be1 = b1;
+            const uint32_t V = as_u32(v);
+            const uint32_t VL = (uint32_t)from_left((int)V), VR = (uint32_t)from_right((int)V);
+            const uint32_t VL2 = (uint32_t)from_left((int)VL), VR2 = (uint32_t)from_right((int)VR);
+            auto dot = [](uint32_t a, st_w2 w, uint32_t c) { return __builtin_amdgcn_udot2(as_u16x2(a), w, c, false); };
+            // column c0: 72 I(c0) + 56 (I(c0-1) + I(c0+1)) + 28 (I(c0-2) + I(c0+2)) + 8 (I(c0-3) + I(c0+3))
+            const uint32_t ha = dot(VR, st_w2{28, 8}, dot(VL2, st_w2{0, 8}, dot(VL, st_w2{28, 56}, dot(V, st_w2{72, 56}, 32768u))));
+            const uint32_t hb = dot(VR2, st_w2{8, 0}, dot(VR, st_w2{56, 28}, dot(VL, st_w2{8, 28}, dot(V, st_w2{56, 72}, 32768u))));
+            BA = BM; BM = BE;
+            BE = st_f2{(float)((ha >> 16) & 255u), (float)((hb >> 16) & 255u)};
             if constexpr (P >= 3) {
                 // blurred row ys - 10 + k: the plane is padded to whole strips and 4 rows past the
                 // last tile, so every output lane stores (rows past the segment are the next
                 // segment's, the same values)
-                __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(b0 | (b1 << 8)), rblur, boff,
+                __builtin_amdgcn_raw_buffer_store_b16((unsigned short)__builtin_amdgcn_perm(hb, ha, 0x0c0c0602u), rblur, boff,
                                                       (ys - 10 + k) * Wb, 0);
             }
         }
@@ -578,55 +595,53 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             // 2. gradients of row yg (kernel .c:59-76), 0 outside 1 <= i <= H-2, 1 <= j <= W-2;
             //    the reference's f32 values are these integers (all below 2^11)
             const int yg = ys - 11 + k;
-            const int dv0 = ba0 - be0, sv0 = (ba0 + 2 * bm0) + be0;
-            const int dv1 = ba1 - be1, sv1 = (ba1 + 2 * bm1) + be1;
-            const int dL = from_left(dv1), dR = from_right(dv0), sL = from_left(sv1), sR = from_right(sv0);
-            int jx0 = (dL + 2 * dv0) + dv1, jy0 = sL - sv1, jxy0 = dL - dv1;
-            int jx1 = (dv0 + 2 * dv1) + dR, jy1 = sv0 - sR, jxy1 = dv0 - dR;
+            const st_f2 DV = BA - BE, SV = st_fma(BM, st_f2{2.0f, 2.0f}, BA + BE);
+            const st_f2 Y = {from_leftf(DV.y), from_rightf(DV.x)};   // dv of columns c0 - 1, c0 + 2
+            const st_f2 Z = {from_leftf(SV.y), from_rightf(SV.x)};
+            st_f2 JX = st_fma(DV, st_f2{2.0f, 2.0f}, Y + DV.yx);      // (dL + 2 dv0 + dv1, dv0 + 2 dv1 + dR)
+            st_f2 JY = st_xsub(Z, SV);                                // (sL - sv1, sv0 - sR)
+            st_f2 JXY = st_xsub(Y, DV);                               // (dL - dv1, dv0 - dR)
+            // both conditions are wave-uniform and rare (the image's outer columns and rows): the
+            // empty volatile asm keeps them branches (if-converted, they cost 12 selects a row)
             if (colfix) {
-                if (!g0) jx0 = jy0 = jxy0 = 0;
-                if (!g1) jx1 = jy1 = jxy1 = 0;
+                asm volatile("");
+                if (!g0) JX.x = JY.x = JXY.x = 0.0f;
+                if (!g1) JX.y = JY.y = JXY.y = 0.0f;
             }
-            if ((unsigned)(yg - 1) > (unsigned)(H - 3)) jx0 = jy0 = jxy0 = jx1 = jy1 = jxy1 = 0;
-            // 3. 5x5 window sums (kernel .c:97-107): |J| <= 512 after the blur, so a sum of 25
-            //    squares is below 2^24 and the in-order f32 sum is this integer sum
-            const int x20 = __mul24(jx0, jx0), y20 = __mul24(jy0, jy0);
-            const int x21 = __mul24(jx1, jx1), y21 = __mul24(jy1, jy1);
-            vx0 += x20 - qx0[0]; vy0 += y20 - qy0[0]; vs0 += jxy0 - qs0[0];
-            vx1 += x21 - qx1[0]; vy1 += y21 - qy1[0]; vs1 += jxy1 - qs1[0];
+            if ((unsigned)(yg - 1) > (unsigned)(H - 3)) {
+                asm volatile("");
+                JX = JY = JXY = z2;
+            }
+            // 3. 5x5 window sums (kernel .c:97-107): vertical running sums, then horizontal
+            const st_f2 X2 = JX * JX, Y2 = JY * JY;
+            VX = VX + (X2 - QX[0]); VY = VY + (Y2 - QY[0]); VS = VS + (JXY - QS[0]);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                qx0[i] = qx0[i + 1]; qy0[i] = qy0[i + 1]; qs0[i] = qs0[i + 1];
-                qx1[i] = qx1[i + 1]; qy1[i] = qy1[i + 1]; qs1[i] = qs1[i + 1];
-            }
-            qx0[4] = x20; qy0[4] = y20; qs0[4] = jxy0;
-            qx1[4] = x21; qy1[4] = y21; qs1[4] = jxy1;
+            for (int i = 0; i < 4; ++i) { QX[i] = QX[i + 1]; QY[i] = QY[i + 1]; QS[i] = QS[i + 1]; }
+            QX[4] = X2; QY[4] = Y2; QS[4] = JXY;
         }
         if constexpr (P >= 4) {
             // horizontal 5-sums: column c0 takes c0-2 .. c0+2 = the left pair, its own pair and
             // the right lane's c0; column c0 + 1 the left lane's c0 + 1, its pair, the right pair
-            auto box = [](int a, int b, int& sa, int& sb) {
-                const int p = a + b;
-                sa = (from_left(p) + p) + from_right(a);
-                sb = (from_left(b) + p) + from_right(p);
+            auto box = [](st_f2 a) {
+                const st_f2 p = a + a.yx;                              // (a0 + a1, a0 + a1)
+                const st_f2 l = {from_leftf(p.x), from_leftf(a.y)};
+                const st_f2 r = {from_rightf(a.x), from_rightf(p.x)};
+                return (l + p) + r;
             };
-            int sxa, sxb, sya, syb, ssa, ssb;
-            box(vx0, vx1, sxa, sxb);
-            box(vy0, vy1, sya, syb);
-            box(vs0, vs1, ssa, ssb);
+            const st_f2 SX = box(VX), SY = box(VY), SS = box(VS);
             // 4. response of row yr (kernel .c:108-114), 0 outside 2 <= i <= H-3, 2 <= j <= W-3
             const int yr = ys - 13 + k;
             const bool rrow = (unsigned)(yr - 2) <= (unsigned)(H - 5);
-            const float rv0 = st_response(sxa, sya, ssa), rv1 = st_response(sxb, syb, ssb);
-            const int o0 = ((rv0 > thr0) & rrow) ? __float_as_int(rv0) : 0;
-            const int o1 = ((rv1 > thr1) & rrow) ? __float_as_int(rv1) : 0;
+            const st_f2 rv = st_response2(SX, SY, SS);
+            const int o0 = ((rv.x > thr0) & rrow) ? __float_as_int(rv.x) : 0;
+            const int o1 = ((rv.y > thr1) & rrow) ? __float_as_int(rv.y) : 0;
             if constexpr (DBG) {
                 if (write_response && yr >= ys && yr < min(ys + SEG, H) && out_lane) {
                     float* R = d.response + (size_t)yr * W;
-                    const float w0 = write_response == 2 ? (float)sxa : write_response == 3 ? (float)sya
-                                   : write_response == 4 ? (float)ssa : __int_as_float(o0);
-                    const float w1 = write_response == 2 ? (float)sxb : write_response == 3 ? (float)syb
-                                   : write_response == 4 ? (float)ssb : __int_as_float(o1);
+                    const float w0 = write_response == 2 ? SX.x : write_response == 3 ? SY.x
+                                   : write_response == 4 ? SS.x : __int_as_float(o0);
+                    const float w1 = write_response == 2 ? SX.y : write_response == 3 ? SY.y
+                                   : write_response == 4 ? SS.y : __int_as_float(o1);
                     if (c0 < W) R[c0] = w0;
                     if (c0 + 1 < W) R[c0 + 1] = w1;
                 }
@@ -645,8 +660,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             const int nb0 = max(max(cL, cm1), max(max(ru0, rd0), nmsk0));
             const int nb1 = max(max(cm0, cR), max(max(ru1, rd1), nmsk1));
             const bool rok = (unsigned)(yn - nlo) < (unsigned)(nhi - nlo);
-            const bool mx0 = (nb0 < rm0) & rok, mx1 = (nb1 < rm1) & rok;
-            const unsigned long long b0 = ballot64(mx0), b1 = ballot64(mx1);
+            // the maxima's lane masks straight from the compares (a ballot of a compare ANDed with
+            // rok materialised the lane bools and compared them again, 4 VALU a row); rok is
+            // wave-uniform and masks them as scalars, and inside the branch it holds
+            auto lt_mask = [](int a, int b) {
+                unsigned long long m;
+                asm("v_cmp_lt_i32_e64 %0, %1, %2" : "=s"(m) : "v"(a), "v"(b));
+                return m;
+            };
+            const unsigned long long b0 = rok ? lt_mask(nb0, rm0) : 0ull, b1 = rok ? lt_mask(nb1, rm1) : 0ull;
+            const bool mx0 = nb0 < rm0, mx1 = nb1 < rm1;
             const int cA = __popcll(b0 & mA) + __popcll(b1 & mA);
             const int cB = __popcll(b0 & mB) + __popcll(b1 & mB);
             asm("v_writelane_b32 %0, %1, %2" : "+v"(trows) : "s"(cA), "n"(r));
@@ -1184,12 +1207,15 @@ constexpr DsTables ds_make_tables()
 }
 constexpr DsTables kDs = ds_make_tables();
 
-// one orientation term of both components: (ic*dx)/|d|, (ic*dy)/|d| (c = dx, dy, rh, rl)
-__device__ __forceinline__ void orient_term(float ic, const float4& c, float& ox, float& oy)
+// one orientation term of both components: (ic*dx)/|d|, (ic*dy)/|d| (c = dx, dy, rh, rl), the
+// two components as one packed-FP32 pair (v_pk_mul/fma/add_f32: two lanes' worth per
+// instruction, tools/valu_rate.hip; IEEE per element, so the sums are those of the scalar form)
+typedef float ds_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void orient_term(float ic, const float4& c, ds_f2& o)
 {
-    const float x0 = ic * c.x, x1 = ic * c.y;                       // exact: |ic*d| < 2^15
-    ox = ox + __builtin_fmaf(x0, c.z, x0 * c.w);
-    oy = oy + __builtin_fmaf(x1, c.z, x1 * c.w);
+    const ds_f2 d = {c.x, c.y};
+    const ds_f2 x = ic * d;                                          // exact: |ic*d| < 2^15
+    o = o + __builtin_elementwise_fma(x, ds_f2{c.z, c.z}, x * ds_f2{c.w, c.w});
 }
 
 // the 32 tests 32 W .. 32 W + 31 of a keypoint's rotated samples r: bit i = test 32 W + i
@@ -1233,7 +1259,7 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
     //    (pairs (p, q), q > p) in groups of DS_OG, the last one padded with zero terms that read
     //    the zero rows past the samples.  Software-pipelined: the samples and table entries of
     //    group g + 1 are requested before group g is summed.
-    float ox = 0.0f, oy = 0.0f;
+    ds_f2 oxy = {0.0f, 0.0f};
     {
         constexpr int NG = DS_ONPAD / DS_OG;
         const float* col = &s_I0[0][lane];
@@ -1261,7 +1287,7 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
             for (int u = 0; u < DS_OG; ++u) { iqn[u] = col[(qn + u) * DS_KPW]; tbn[u] = c_orient[gn * DS_OG + u]; }
             __builtin_amdgcn_sched_barrier(0);          // the requests stay ahead of the sums
 #pragma unroll
-            for (int u = 0; u < DS_OG; ++u) orient_term(ip - iq[u], tb[u], ox, oy);
+            for (int u = 0; u < DS_OG; ++u) orient_term(ip - iq[u], tb[u], oxy);
             __builtin_amdgcn_sched_barrier(0);
             p = pn; qs = qn; ip = ipn;
 #pragma unroll
@@ -1269,6 +1295,7 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
         }
     }
     VO_STAMP(d, stamp_slot, 2);
+    const float ox = oxy.x, oy = oxy.y;
     // 3. angle and rotation
     float angle = 0.0f;
     if (!(isnan(ox) || isnan(oy))) angle = (float)det_atan2((double)oy, (double)ox);
