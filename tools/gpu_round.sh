@@ -16,7 +16,4 @@ python3 -c "import json;d=json.load(open('$O/bench.json'));print('VALUE',round(d
 bash tools/profile.sh $O/prof_kitti > $O/prof_kitti.log 2>&1 || { echo PROF_FAIL; tail $O/prof_kitti.log; exit 1; }
 bash tools/profile.sh $O/prof_1080 --width 1920 --height 1080 --max-kpts 4096 --frames 64 > $O/prof_1080.log 2>&1 || { echo PROF1080_FAIL; tail $O/prof_1080.log; exit 1; }
 bash tools/profile.sh $O/prof_1080_512 --width 1920 --height 1080 --max-kpts 4096 --frames 64 --match-bits 512 > $O/prof_1080_512.log 2>&1 || { echo PROF512_FAIL; tail $O/prof_1080_512.log; exit 1; }
-mkdir -p $O/calib
-timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/calib -o fetch -- ./tools/fetch_calib > $O/calib/fetch.log 2>&1 || { echo CALIB_FAIL; exit 1; }
-timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/calib -o write -- ./tools/fetch_calib > $O/calib/write.log 2>&1 || { echo CALIB_FAIL; exit 1; }
 echo DONE

@@ -10,7 +10,9 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$ROOT"
-B="--steps 3 --warmup 1 --no-cpu --no-variants --sequences 1"
+# the headline workload (8 sequences as one stream), without the after-timing check runs, so the
+# average launch of every kernel is the bench's own launch
+B="--steps 3 --warmup 1 --no-cpu --no-variants --no-check"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o stats -- \
     python3 bench.py $B "$@" > "$OUT/bench_stats.json"
 # PMC collection serializes dispatches, so the frame pipeline's cross-queue waits would spin
@@ -18,9 +20,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT"
 # bytes; VO_SERIAL=1)
 export VO_SERIAL=1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT" -o fetch -- \
-    python3 bench.py --steps 1 --warmup 1 --no-cpu --no-variants --sequences 1 "$@" > "$OUT/bench_fetch.json"
+    python3 bench.py --steps 1 --warmup 1 --no-cpu --no-variants --no-check "$@" > "$OUT/bench_fetch.json"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT" -o write -- \
-    python3 bench.py --steps 1 --warmup 1 --no-cpu --no-variants --sequences 1 "$@" > "$OUT/bench_write.json"
+    python3 bench.py --steps 1 --warmup 1 --no-cpu --no-variants --no-check "$@" > "$OUT/bench_write.json"
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d "$OUT" -o valu -- \
-    python3 bench.py --steps 1 --warmup 1 --no-cpu --no-variants --sequences 1 "$@" > "$OUT/bench_valu.json"
+    python3 bench.py --steps 1 --warmup 1 --no-cpu --no-variants --no-check "$@" > "$OUT/bench_valu.json"
 echo "profile written to $OUT"
