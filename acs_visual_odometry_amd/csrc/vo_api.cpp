@@ -681,6 +681,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     (void)hipMemset(d.desc, 0, sizeof(uint64_t) * 8 * N * VO_SLOTS);
     (void)hipMemset(d.pre, 0, sizeof(uint32_t) * N * VO_SLOTS);
     d.n_seq_starts = 0;
+    d.origin = 0;
     if (ensure_out(c, 16) != VO_OK) return bail(VO_ERR_HIP);
     c->klaunch.assign(vo::kernel_count(), 0);
     if (vo_reset(c) != VO_OK) return bail(VO_ERR_HIP);
@@ -744,6 +745,44 @@ int vo_set_sequence_starts(vo_ctx* c, const int32_t* starts, int n)
     SYNC_ALL(c);
     if (n) HIPCHK(hipMemcpy((void*)c->d.seq_starts, starts, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice));
     c->d.n_seq_starts = n;
+    return VO_OK;
+}
+
+int vo_set_frame_origin(vo_ctx* c, int origin)
+{
+    if (!c || origin < 0) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    SYNC_ALL(c);
+    c->d.origin = origin;
+    return VO_OK;
+}
+
+int vo_trajectory_state(vo_ctx* c, double Tcurr[16])
+{
+    if (!c || !Tcurr) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    SYNC_ALL(c);
+    HIPCHK(hipMemcpy(Tcurr, c->d.st->Tcurr, sizeof(double) * 16, hipMemcpyDeviceToHost));
+    return VO_OK;
+}
+
+// the chain of committed frames [f0, f0 + n) from T_in, in windows of VO_MAX_WIN frames on the
+// trajectory queue (k_traj_range); their trajectory records must still be in the ring
+int vo_rechain(vo_ctx* c, const double T_in[16], int f0, int n, double* poses_out)
+{
+    if (!c || !T_in || f0 < 0 || n < 0) return VO_ERR_ARG;
+    if (f0 + n > c->fidx || f0 < c->fidx - c->d.ring) return VO_ERR_STATE;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    SYNC_ALL(c);
+    int rc = ensure_out(c, std::max(n, 1));
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(c->d.st->Tcurr, T_in, sizeof(double) * 16, hipMemcpyHostToDevice));
+    for (int lo = f0; lo < f0 + n; lo += VO_MAX_WIN)
+        vo::launch_traj_range(c->d, c->out_dev, f0, lo, std::min(VO_MAX_WIN, f0 + n - lo), c->st);
+    HIPCHK(hipGetLastError());
+    if (n) HIPCHK(hipMemcpyAsync(c->out_host, c->out_dev, sizeof(VoFrameOut) * (size_t)n, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    for (int f = 0; f < n && poses_out; ++f) std::memcpy(poses_out + 12 * (size_t)f, c->out_host[f].pose, sizeof(double) * 12);
     return VO_OK;
 }
 

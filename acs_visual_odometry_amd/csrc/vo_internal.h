@@ -200,6 +200,7 @@ struct VoDev {
     int32_t* ext_st;      // x SLOTS: VO_STATUS_OK, VO_STATUS_OVERFLOW (select capacity), VO_STATUS_MISSING
     const int32_t* seq_starts;   // sorted frame indices (since vo_reset) where a new sequence begins
     int n_seq_starts;
+    int origin;           // in-sequence index of frame 0 of the stream's first sequence (a shard of one sequence)
     unsigned* ctr;
     VoTrajRec* trec;      // x ring: committed frames' trajectory inputs (k_finalize -> k_traj)
     int2* plog;           // x VO_PLOG: (lo, committed) per pose pass
@@ -225,6 +226,7 @@ void launch_refit(const VoDev& d, int with_pose, int stage, hipStream_t s);
 void launch_triangulate(const VoDev& d, int stage, hipStream_t s);
 void launch_finalize(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s);
 void launch_traj(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s);   // T_curr chain + pose rows of pass d.pass
+void launch_traj_range(const VoDev& d, VoFrameOut* out, int out_base, int lo, int nc, hipStream_t s);   // vo_rechain
 void launch_pose_stage(const VoDev& d, int phase, hipStream_t s);   // vo_pose: 0 prepare, 1 choose
 void launch_reset(const VoDev& d, hipStream_t s);                   // vo_reset's device state
 void launch_selftest_arith(const float* fa, const float* fb, float* fo, const double* da,

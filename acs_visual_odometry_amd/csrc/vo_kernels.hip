@@ -1466,9 +1466,11 @@ __device__ __forceinline__ bool match_header(const VoDev& d, int stage, int wf, 
         cur = f % VO_RING;
         prev = df == 0 || wf >= n ? d.st->prev_slot : (f - 1) % VO_RING;
         const int es = d.ext_st[cur];
-        fl = f - seq_base(d, f);
+        const int base = seq_base(d, f);
+        fl = f - base;
         if (fl == 0) status = VO_STATUS_FIRST;                 // VisualOdometry.cpp:58,64-66
         else if (es != VO_STATUS_OK) status = es;              // MISSING / OVERFLOW
+        if (base == 0) fl += d.origin;                         // a sequence shard: the sampler's frame index
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         w->frame = f; w->cur = cur; w->prev = prev;
@@ -2955,7 +2957,7 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
 //      the four products
 //   3  per committed frame: the pose row; thread 255: T_curr
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_traj(VoDev d, VoFrameOut* out, int out_base)
+__device__ __forceinline__ void traj_chain(const VoDev& d, VoFrameOut* out, int out_base, int lo, int nc)
 {
     constexpr int MW = VO_MAX_WIN;
     __shared__ double s_Trel[MW + 2][16];             // + 2: step 2 reads two frames ahead
@@ -2963,9 +2965,6 @@ __global__ void __launch_bounds__(256) k_traj(VoDev d, VoFrameOut* out, int out_
     __shared__ double s_T[16];
     __shared__ int s_kind[MW], s_first[MW], s_flip[MW];
     const int tid = threadIdx.x;
-    const int2 lg = d.plog[d.pass % VO_PLOG];
-    const int lo = lg.x, nc = lg.y;
-    if (nc <= 0) return;
     VoState* st = d.st;
     // 1
     if (tid < nc) {
@@ -3048,6 +3047,21 @@ __global__ void __launch_bounds__(256) k_traj(VoDev d, VoFrameOut* out, int out_
     } else if (tid == 255) {
         for (int i = 0; i < 16; ++i) st->Tcurr[i] = s_T[i];
     }
+}
+
+__global__ void __launch_bounds__(256) k_traj(VoDev d, VoFrameOut* out, int out_base)
+{
+    const int2 lg = d.plog[d.pass % VO_PLOG];
+    if (lg.y <= 0) return;
+    traj_chain(d, out, out_base, lg.x, lg.y);
+}
+
+// vo_rechain: the chain over committed frames [lo, lo + nc) (nc <= VO_MAX_WIN) from st->Tcurr,
+// their trajectory records still in the ring (a sequence shard's rows from its predecessor's T_curr)
+__global__ void __launch_bounds__(256) k_traj_range(VoDev d, VoFrameOut* out, int out_base, int lo, int nc)
+{
+    if (nc <= 0) return;
+    traj_chain(d, out, out_base, lo, nc);
 }
 
 // vo_reset on the device (VisualOdometry.cpp:50-62 initial state): trajectory state, slot
@@ -3211,6 +3225,11 @@ void launch_finalize(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t 
 void launch_traj(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s)
 {
     hipLaunchKernelGGL(k_traj, dim3(1), dim3(256), 0, s, d, out, out_base);
+}
+
+void launch_traj_range(const VoDev& d, VoFrameOut* out, int out_base, int lo, int nc, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_traj_range, dim3(1), dim3(256), 0, s, d, out, out_base, lo, nc);
 }
 void launch_reset(const VoDev& d, hipStream_t s)
 {

@@ -114,6 +114,24 @@ class Context:
         a = np.ascontiguousarray(np.asarray(starts, dtype=np.int32).reshape(-1))
         check(self.lib.vo_set_sequence_starts(self.h, _p(a) if a.size else None, a.size), "vo_set_sequence_starts")
 
+    def set_frame_origin(self, origin: int):
+        """The stream's first frame is frame `origin` of its sequence (a sequence shard,
+        vo_set_frame_origin): RANSAC draws the hypotheses of the unsplit run."""
+        check(self.lib.vo_set_frame_origin(self.h, int(origin)), "vo_set_frame_origin")
+
+    def trajectory_state(self) -> np.ndarray:
+        """T_curr after the last committed frame (4x4)."""
+        T = np.zeros(16)
+        check(self.lib.vo_trajectory_state(self.h, _p(T)), "vo_trajectory_state")
+        return T.reshape(4, 4)
+
+    def rechain(self, T_in: np.ndarray, f0: int, n: int) -> np.ndarray:
+        """Rows of committed frames [f0, f0 + n) chained from T_curr = T_in (vo_rechain)."""
+        T = np.ascontiguousarray(T_in, dtype=np.float64).reshape(16)
+        poses = np.zeros((max(n, 0), 12))
+        check(self.lib.vo_rechain(self.h, _p(T), int(f0), int(n), _p(poses)), "vo_rechain")
+        return poses.reshape(-1, 3, 4)
+
     def reset(self):
         check(self.lib.vo_reset(self.h), "vo_reset")
 

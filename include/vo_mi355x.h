@@ -126,6 +126,21 @@ int  vo_set_ground_truth(vo_ctx* ctx, const double* poses12, int n);
  * sequence.  Kept across vo_reset. */
 int  vo_set_sequence_starts(vo_ctx* ctx, const int32_t* starts, int n);
 
+/* Sequence shards (one sequence split over GPUs; acs_visual_odometry_amd/shard.py).  A shard's
+ * stream starts at frame `origin` of its sequence: its first frame starts the trajectory as
+ * VisualOdometry.cpp:57-66 do (the halo of the shard: identity pose, no model), and the RANSAC
+ * sampler of the stream's first sequence counts frames from origin, so every frame draws the
+ * hypotheses it draws in the unsplit run.  Kept across vo_reset; 0 = an ordinary stream. */
+int  vo_set_frame_origin(vo_ctx* ctx, int origin);
+/* T_curr after the last committed frame (VisualOdometry.cpp:184, 4x4 row-major). */
+int  vo_trajectory_state(vo_ctx* ctx, double Tcurr[16]);
+/* The trajectory chain (VisualOdometry.cpp:161-186) of committed frames [f0, f0 + n) (counted since
+ * vo_reset) again, from T_curr = T_in instead of the chain the stream ran: the rows a shard's frames
+ * get in the unsplit run once its predecessor's T_curr is known.  The frames' trajectory records
+ * must still be in the ring (f0 >= frames - ring slots); T_curr is left at the chain's end.
+ * poses_out: n x 12 (host, optional). */
+int  vo_rechain(vo_ctx* ctx, const double T_in[16], int f0, int n, double* poses_out);
+
 /* One iteration of VisualOdometry::run's loop (VisualOdometry.cpp:68-189): frame in,
  * pose out.  gray == NULL marks a missing image.  pose_out: 12 doubles, the row the
  * reference appends to estimated_poses.  info (optional, 8 ints): n_kpts, n_matches,

@@ -11,7 +11,7 @@ import pytest
 from PIL import Image
 
 import oracle as O
-from acs_visual_odometry_amd import Context, VisualOdometry
+from acs_visual_odometry_amd import Context, VisualOdometry, shard
 from acs_visual_odometry_amd.synth import SceneSequence
 
 pytestmark = pytest.mark.gpu
@@ -289,3 +289,79 @@ def test_sequence_starts(batch, host):
     assert [out[1][s] for s in [0] + starts] == [1] * (len(starts) + 1)
     _check(refs, *out)
     ctx.close()
+
+
+# -- one sequence split over shards (acs_visual_odometry_amd/shard.py) -------------
+def _shard_run(seq, frames, G, **ctx_kw):
+    ctxs = [Context(seq.W, seq.H, K=seq.K, **ctx_kw) for _ in range(G)]
+    try:
+        res = shard.run_local([shard.ContextEngine(c, frames, seq.gt()) for c in ctxs], len(frames))
+    finally:
+        for c in ctxs:
+            c.close()
+    poses = np.concatenate([r.poses for r in res])
+    st = np.concatenate([r.status for r in res])
+    info = np.concatenate([r.info for r in res])
+    return res, poses, st, info
+
+
+@pytest.mark.parametrize("G", [2, 3, 7])
+def test_sequence_shards_match_unsplit(leak_case, G):
+    """Shards of the leak sequence (FEW_INLIERS before the first fit, model leaks next to the
+    shard boundaries): halo streams with the sequence's sampler indices, the T_curr chain
+    carried over the shards (vo_rechain) -- every row equals the oracle's unsplit run."""
+    seq, frames, ref = leak_case
+    res, poses, st, info = _shard_run(seq, frames, G, frame_batch=16)
+    assert [(r.a, r.b) for r in res] == shard.partition(80, G)
+    _check(ref, poses, st, info)
+
+
+def test_sequence_shard_second_run():
+    """A blank frame right before the boundary (FEW_MATCHES: desc1 stays on frame 38) and a
+    far frame after it (no fit of its own): the halo run cannot reach the unsplit state, so
+    shard 1 runs again from the restart point -- and still equals the oracle."""
+    from acs_visual_odometry_amd.synth import noise_frames
+    seq, frames = _leak_sequence()
+    frames[39] = 128                      # a blank frame: no keypoints, no matches
+    ref = _oracle_rows(seq, frames)
+    assert ref[39][1] == 3
+    res, poses, st, info = _shard_run(seq, frames, 2)
+    assert res[1].runs == 2 and res[1].start < 38
+    _check(ref, poses, st, info)
+
+
+def _shard_rank(rank, world, port, q, nframes):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    seq, frames = _leak_sequence()
+    frames = frames[:nframes]
+    ctx = Context(seq.W, seq.H, K=seq.K, frame_batch=16)       # every rank on the box's one GPU
+    r = shard.run_shard(shard.ContextEngine(ctx, frames, seq.gt()), shard.TorchComm(dist), nframes)
+    ctx.close()
+    q.put((rank, r.a, r.b, r.poses, r.status, r.info, r.runs))
+    dist.destroy_process_group()
+
+
+def test_sequence_shards_two_processes(leak_case):
+    """run_shard in two processes (one context each, gloo carrying the flags and T_curr; RCCL on a
+    multi-GPU node): the concatenated rows equal the oracle's unsplit run."""
+    import socket
+    import torch.multiprocessing as mp
+    seq, frames, ref = leak_case
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    procs = [mpc.Process(target=_shard_rank, args=(r, 2, port, q, 80)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in procs), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [(x[1], x[2]) for x in res] == shard.partition(80, 2)
+    _check(ref, np.concatenate([x[3] for x in res]), np.concatenate([x[4] for x in res]),
+           np.concatenate([x[5] for x in res]))
