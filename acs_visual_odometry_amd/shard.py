@@ -18,7 +18,8 @@ RANSAC inliers; `fitted`), both runs leave x with the same state (last_valid = d
 model = x's fit), and every later frame is computed identically -- except T_curr, which the
 halo run started from the identity.  So:
   1. every shard runs its halo stream in parallel (one all_gather of per-frame status and
-     fitted flags afterwards);
+     fitted flags afterwards); the halo grows (2, 4, 8, ... frames) until the halo run itself
+     holds such an x, so step 2 rarely fails;
   2. shards are checked in rank order against the (final) flags of the frames before them;
      a shard whose halo shows no such x runs again from the latest frame x' < a_r of the
      unsplit run that advanced after an advancing predecessor (x' - 1 becomes the stream's
@@ -74,6 +75,31 @@ def entry_holds(true_adv: np.ndarray, s: int, a: int, halo_status: np.ndarray, h
     return False
 
 
+def halo_reaches(s: int, a: int, status: np.ndarray, fit: np.ndarray) -> bool:
+    """The halo side of entry_holds over the halo frames alone (x < a): some x in (s, a) follows
+    an advancing frame of the halo run and fits its own model."""
+    hadv = advanced(status)
+    return any(hadv[x - 1 - s] and fit[x - s] for x in range(s + 1, a))
+
+
+def halo_run(engine, a: int, b: int, halo: int):
+    """Phase 1 of a shard: the halo frames [a - h, a) first, h doubling until the halo run holds a
+    frame that makes it reach the unsplit state (or h reaches the sequence start) -- at the survey's
+    1.0 m/frame only a quarter of the frames fit a model of their own, so two halo frames would
+    often fail the check -- then the shard's own frames continue the same stream."""
+    if a == 0:
+        return 0, engine.run(0, b)
+    h = max(1, halo)
+    while True:
+        s = max(0, a - h)
+        o1 = engine.run(s, a)
+        if s == 0 or halo_reaches(s, a, o1[1], o1[2][:, 5]):
+            break
+        h *= 2
+    o2 = engine.extend(a, b)
+    return s, tuple(np.concatenate([x, y]) for x, y in zip(o1, o2))
+
+
 def restart_point(true_adv: np.ndarray, true_fit: np.ndarray, a: int) -> int:
     """First frame of a shard's second run: x' - 1 for the latest x' < a that fitted its own model
     after an advancing predecessor in the unsplit run, else 0 (the sequence start)."""
@@ -117,8 +143,7 @@ def run_shard(engine, comm, nframes: int, halo: int = DEFAULT_HALO) -> ShardResu
     r, G = comm.rank, comm.world
     parts = partition(nframes, G)
     a, b = parts[r]
-    s = max(0, a - halo)
-    out = engine.run(s, b) if b > a else None
+    s, out = halo_run(engine, a, b, halo) if b > a else (max(0, a - halo), None)
     mine = (s, out[1], out[2][:, 5]) if out is not None else (s, np.zeros(0, np.int32), np.zeros(0, np.int32))
     flags = comm.allgather(mine)
     runs = [1]
@@ -157,8 +182,7 @@ def run_local(engines: Sequence, nframes: int, halo: int = DEFAULT_HALO) -> List
     parts = partition(nframes, G)
     outs, flags = [], []
     for r, (a, b) in enumerate(parts):
-        s = max(0, a - halo)
-        o = engines[r].run(s, b) if b > a else None
+        s, o = halo_run(engines[r], a, b, halo) if b > a else (max(0, a - halo), None)
         outs.append(o)
         flags.append((s, o[1], o[2][:, 5]) if o is not None else (s, np.zeros(0, np.int32), np.zeros(0, np.int32)))
     runs = [1] * G
@@ -183,19 +207,37 @@ def run_local(engines: Sequence, nframes: int, halo: int = DEFAULT_HALO) -> List
 
 
 class ContextEngine:
-    """A shard's engine over a Context: the sequence's frames (host, F x H x W u8) and GT rows."""
+    """A shard's engine over a Context: the sequence's frames and GT rows.  frames: host
+    (F x H x W u8, uploaded per run) or a DeviceFrames batch of the whole sequence, or of the
+    frames from `base` on (resident in HBM; a run uses a view of it)."""
 
-    def __init__(self, ctx, frames: np.ndarray, gt: Optional[np.ndarray] = None):
-        self.ctx, self.frames, self.gt = ctx, frames, gt
+    def __init__(self, ctx, frames, gt: Optional[np.ndarray] = None, base: int = 0):
+        self.ctx, self.frames, self.gt, self.base = ctx, frames, gt, base
 
     def run(self, s: int, b: int):
         ctx = self.ctx
-        df = ctx.device_frames(np.ascontiguousarray(self.frames[s:b]))
+        if not isinstance(self.frames, np.ndarray):
+            if s < self.base:
+                raise ValueError(f"frames before {self.base} are not resident on this shard (run from {s})")
+            df = self.frames.view(s - self.base, b - self.base)
+        else:
+            df = ctx.device_frames(np.ascontiguousarray(self.frames[s:b]))
         try:
             ctx.reset()
             ctx.set_sequence_starts([])
             ctx.set_frame_origin(s)
             ctx.set_ground_truth(None if self.gt is None else self.gt[s:])
+            return ctx.process_frames_device(df)
+        finally:
+            df.free()
+
+    def extend(self, a: int, b: int):
+        """Frames [a, b) continuing the stream of the last run (which ended at frame a)."""
+        ctx = self.ctx
+        if not isinstance(self.frames, np.ndarray):
+            return ctx.process_frames_device(self.frames.view(a - self.base, b - self.base))
+        df = ctx.device_frames(np.ascontiguousarray(self.frames[a:b]))
+        try:
             return ctx.process_frames_device(df)
         finally:
             df.free()

@@ -218,6 +218,11 @@ class DeviceFrames:
         self.ptr = p
         check(ctx.lib.vo_device_upload(ctx.h, p, _p(f), f.nbytes), "vo_device_upload")
 
+    def view(self, f0: int, f1: int) -> "DeviceFrameView":
+        """Frames [f0, f1) of the batch, without a copy."""
+        assert 0 <= f0 <= f1 <= self.n
+        return DeviceFrameView(C.c_void_p(self.ptr.value + f0 * self.frame_bytes), f1 - f0, self.frame_bytes)
+
     def free(self):
         if self.ptr:
             self.ctx.lib.vo_device_free(self.ctx.h, self.ptr)
@@ -228,6 +233,16 @@ class DeviceFrames:
             self.free()
         except Exception:
             pass
+
+
+class DeviceFrameView:
+    """Frames of a DeviceFrames batch (process_frames_device accepts either)."""
+
+    def __init__(self, ptr, n: int, frame_bytes: int):
+        self.ptr, self.n, self.frame_bytes = ptr, n, frame_bytes
+
+    def free(self):
+        pass
 
 
 class HostFrames:

@@ -335,6 +335,87 @@ def run_variants(args, ctx, W, H, frames0, gt0, extra, Context) -> dict:
     return out
 
 
+def shard_main(args, world: int, rank: int, local: int):
+    """--shard-sequence: ONE sequence of sequences x frames frames split into G contiguous shards
+    (acs_visual_odometry_amd/shard.py).  Each rank holds the frames up to the end of
+    its shard in HBM, runs its halo stream, the flag exchange, a second run where needed and the
+    T_curr hand-over (RCCL send/recv of 16 doubles).  value = the sequence's frames / the slowest
+    rank's time; rank 0 checks the gathered rows against the unsplit run on its own GPU."""
+    from acs_visual_odometry_amd import shard
+    from acs_visual_odometry_amd.synth import SceneSequence, render_sequences
+    W, H = args.width, args.height
+    F = args.frames * args.sequences
+    a, b = shard.partition(F, world)[rank]
+    workers = max(1, min(16, (os.cpu_count() or 4) // max(world, 1)))
+    seq = SceneSequence(W, H, nframes=F, seq=0, step=args.motion)
+    need = F if rank == 0 else b                      # rank 0 also runs the unsplit check
+    frames = render_sequences([(W, H, F, 0, args.motion)], workers)[0][:need]
+    dev = local if args.device < 0 else args.device
+    dist = dist_init(world, dev, backend=args.backend)
+    from acs_visual_odometry_amd import Context
+    ctx = Context(W, H, K=seq.K, max_kpts=args.max_kpts, device=dev, frame_batch=args.batch,
+                  match_bits=args.match_bits)
+    dall = ctx.device_frames(frames)
+    gt = seq.gt()
+    eng = shard.ContextEngine(ctx, dall, gt)
+
+    class One:
+        rank, world = 0, 1
+
+    comm = (shard.TorchComm(dist, device=f"cuda:{dev}" if args.backend == "nccl" else "cpu") if dist is not None
+            else One())
+
+    def step():
+        return shard.run_shard(eng, comm, F) if dist is not None else shard.run_local([eng], F)[0]
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(max(args.warmup, 1)):
+        res = step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    dt = time.perf_counter() - t0
+    barrier()
+    dt, _ = aggregate(dist, dt, 0, world, backend=args.backend, local=dev)
+    value = F * args.steps / dt
+    rows = np.concatenate([res.poses.reshape(-1, 12), res.status.reshape(-1, 1).astype(np.float64)], axis=1)
+    if dist is not None:
+        allrows = [None] * world
+        dist.all_gather_object(allrows, (rows, res.runs, res.a - res.start))
+    else:
+        allrows = [(rows, res.runs, res.a - res.start)]
+    if rank == 0:
+        ctx.reset()
+        ctx.set_sequence_starts([])
+        ctx.set_frame_origin(0)
+        ctx.set_ground_truth(gt)
+        p, st, info = ctx.process_frames_device(dall)
+        unsplit = np.concatenate([p.reshape(F, 12), st.reshape(F, 1).astype(np.float64)], axis=1)
+        ok = bool(np.array_equal(np.concatenate([r[0] for r in allrows]), unsplit))
+        line = {
+            "metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u8/f32/u32/f64", "data": "synthetic",
+            "config": {"workload": f"{W}x{H}_{args.max_kpts}kpts_one_sequence_sharded", "frames": F,
+                       "width": W, "height": H, "max_kpts": args.max_kpts, "match_bits": args.match_bits,
+                       "motion": f"+{args.motion} m/frame along z, 0.1 deg/frame yaw",
+                       "parallelism": f"one sequence in {world} contiguous shards, halo {shard.DEFAULT_HALO} frames, "
+                                      f"T_curr handed over rank to rank",
+                       "inputs": "device-resident (HBM) before timing", "shard_runs": [r[1] for r in allrows],
+                       "halo_frames": [r[2] for r in allrows]},
+            "determinism": {"shard_rows_equal_unsplit_run": ok},
+        }
+        print(json.dumps(line))
+    dall.free()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -353,6 +434,10 @@ def main():
     ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the per-sequence separate runs after timing (profiles: every launch is then a bench launch)")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for CPU/one-GPU rehearsal)")
+    ap.add_argument("--device", type=int, default=-1, help="GPU of every rank (default: LOCAL_RANK; one-GPU rehearsal: 0)")
+    ap.add_argument("--shard-sequence", action="store_true",
+                    help="one sequence (sequences x frames frames) split over the ranks (within-sequence sharding)")
     ap.add_argument("--breakdown", action="store_true", help="print the per-kernel table to stderr")
     args = ap.parse_args()
 
@@ -361,6 +446,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     if world != args.gpus:
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if args.shard_sequence:
+        return shard_main(args, world, rank, local)
     W, H, F = args.width, args.height, args.frames
     S = max(args.sequences, world)          # every rank gets at least one sequence
     my_seqs = rank_sequences(S, rank, world)

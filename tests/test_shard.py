@@ -70,18 +70,21 @@ class ToyEngine:
         self.T = np.eye(4)
 
     def run(self, s, b):
-        w = self.w
-        n = b - s
+        self.rec, self.T, self.L, self.model, self.s, self.end = [], np.eye(4), s, None, s, s
+        return self.extend(s, b)
+
+    def extend(self, a, b):
+        assert a == self.end
+        w, s = self.w, self.s
+        n = b - a
         poses = np.zeros((n, 3, 4))
         status = np.zeros(n, np.int32)
         info = np.zeros((n, 8), np.int32)
-        self.rec = []
-        T = np.eye(4)
-        L, model = s, None
+        T, L, model = self.T, self.L, self.model
         for k in range(n):
-            i = s + k
+            i = a + k
             kind, Trel = 0, None
-            if k == 0:
+            if i == s:
                 status[k], row = shard.ST_FIRST, T.copy()
             elif w.missing(i):
                 status[k], row = shard.ST_MISSING, T.copy()
@@ -103,7 +106,7 @@ class ToyEngine:
                     status[k], row = shard.ST_OK, FLIPZ @ T
             self.rec.append((kind, Trel, status[k] in (shard.ST_FIRST, shard.ST_MISSING)))
             poses[k] = row[:3]
-        self.T = T
+        self.T, self.L, self.model, self.end = T, L, model, b
         return poses, status, info
 
     def rechain(self, T_in, f0, n):
