@@ -43,13 +43,14 @@ struct vo_ctx {
     bool event_wait = true;           // pose queue waits for extract batches on events (default)
                                       // or on the stream-wait-value packet (VO_EVENT_WAIT=0; events
                                       // again after the runtime refused a wait-value packet)
+    bool split = false;               // VO_SPLIT: stencil and select/describe of a batch on two extract queues
     int slack = 0;                    // VO_SLACK: extra passes enqueued per chunk (misses re-run without a host round trip)
     hipStream_t st = nullptr;         // trajectory queue: k_traj of each pass (T_curr chain, pose rows)
     hipEvent_t ev_fin = nullptr;      // a pass's k_finalize done (the trajectory queue waits on it)
     int npass = 0;                    // pose passes enqueued (their pass-log entries)
     // per-batch event pools of a chunk: [VO_EV_WAIT] extract done (event_wait mode),
     // [VO_EV_COPY] H2D copy done, [VO_EV_STENCIL] stencil done (host streaming)
-    std::vector<hipEvent_t> ev_batch[3];
+    std::vector<hipEvent_t> ev_batch[VO_EV_POOLS];
     hipStream_t sc = nullptr;         // host streaming: H2D copies of frame batches
     uint8_t* dring = nullptr;         // host streaming: VO_HRING device slots of B frames
     uint8_t* hstage = nullptr;        // host streaming: pinned staging ring for pageable sources
@@ -257,8 +258,10 @@ void timed(vo_ctx* c, EvRec* ev, int k, hipStream_t st, F&& launch)
 // the pose queue may wait for frames < f0 + nb
 // eq: extract queue index (its scratch copy and counters)
 // ev_stencil (optional): recorded on q once the stencil (the only reader of the images) is enqueued
+// q2 (optional): select and describe on a second queue after the stencil (event e_s)
 int enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, int nb, bool publish,
-                    hipStream_t q, EvRec* ev, int eq, hipEvent_t ev_stencil = nullptr)
+                    hipStream_t q, EvRec* ev, int eq, hipEvent_t ev_stencil = nullptr, hipStream_t q2 = nullptr,
+                    hipEvent_t e_s = nullptr)
 {
     VoDev d = c->d;
     const size_t B = (size_t)c->B;
@@ -271,6 +274,11 @@ int enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, 
     d.hist += (size_t)VO_HIST_BINS * B * eq;
     timed(c, ev, 0, q, [&] { vo::launch_stencil(d, img0, frame_bytes, nb, 0, q); });
     if (ev_stencil) HIPCHK(hipEventRecord(ev_stencil, q));
+    if (q2) {
+        HIPCHK(hipEventRecord(e_s, q));
+        HIPCHK(hipStreamWaitEvent(q2, e_s, 0));
+        q = q2;
+    }
     timed(c, ev, 1, q, [&] { vo::launch_select(d, f0, nb, -1, q); });
     timed(c, ev, 2, q, [&] { vo::launch_describe(d, f0, nb, -1, publish ? (unsigned)(f0 + nb) : 0u, q); });
     return VO_OK;
@@ -376,7 +384,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     const int base = c->fidx, end = base + nf, B = c->B;
     hipStream_t s = c->s;
     const bool multi = hs || !(c->serial || host_frame || !img0);   // extract on its own queues
-    static const int nq = getenv("VO_EXTQ") ? std::max(1, std::min(VO_EXT_QUEUES, atoi(getenv("VO_EXTQ")))) : VO_EXT_QUEUES;
+    static const int nq = getenv("VO_EXTQ") ? std::max(1, std::min(VO_EXT_QUEUES, atoi(getenv("VO_EXTQ")))) : 1;
     if (multi && c->reset_pending) {
         for (hipStream_t q : c->se) HIPCHK(hipStreamWaitEvent(q, c->ev_reset, 0));
         c->reset_pending = false;
@@ -390,8 +398,21 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         const int f0 = f0s[j], cnt = sched[j];
         // describe publishes the extracted-frame count only for the wait-value packet
         const bool publish = multi && !c->event_wait;
-        const int eq = multi ? j % nq : 0;
-        hipStream_t q = multi ? c->se[eq] : s;
+        const bool split = multi && c->split;
+        const int eq = split ? j % 2 : (multi ? j % nq : 0);
+        hipStream_t q = split ? c->se[0] : (multi ? c->se[eq] : s);
+        hipStream_t q2 = split ? c->se[1] : nullptr;      // the queue whose last kernel is describe
+        hipEvent_t e_s = nullptr, e_d = nullptr;
+        if (split) {
+            int rc = batch_event(c, VO_EV_SPLIT_S, (size_t)j, &e_s);
+            if (rc == VO_OK) rc = batch_event(c, VO_EV_SPLIT_D, (size_t)j, &e_d);
+            if (rc) return rc;
+            if (j >= 2) {                                 // scratch copy eq: describe of batch j - 2 read it last
+                hipEvent_t e_prev;
+                if ((rc = batch_event(c, VO_EV_SPLIT_D, (size_t)(j - 2), &e_prev)) != VO_OK) return rc;
+                HIPCHK(hipStreamWaitEvent(q, e_prev, 0));
+            }
+        }
         if (hs) {
             uint8_t* dimg = nullptr;
             hipEvent_t e_cp, e_st;
@@ -401,18 +422,20 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
             if (rc) return rc;
             HIPCHK(hipStreamWaitEvent(q, e_cp, 0));
             rc = enqueue_extract(c, dimg, (size_t)c->cfg.width * c->cfg.height, base + f0, cnt, publish, q, ev, eq,
-                                 e_st);
+                                 e_st, q2, e_s);
             if (rc) return rc;
         } else {
             int rc = enqueue_extract(c, img0 + (size_t)f0 * frame_bytes, frame_bytes, base + f0, cnt, publish, q, ev,
-                                     eq);
+                                     eq, nullptr, q2, e_s);
             if (rc) return rc;
         }
+        hipStream_t qd = q2 ? q2 : q;
+        if (split) HIPCHK(hipEventRecord(e_d, qd));
         if (multi && c->event_wait) {
             hipEvent_t e;
             int rc = batch_event(c, VO_EV_WAIT, (size_t)j, &e);
             if (rc) return rc;
-            HIPCHK(hipEventRecord(e, c->se[eq]));
+            HIPCHK(hipEventRecord(e, qd));
         }
         return VO_OK;
     };
@@ -420,7 +443,8 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     // k-1, which precedes pass k on the pose queue
     auto pass = [&](int k) -> int {
         if (multi) {
-            const int eq = k % nq;
+            const int eq = c->split ? k % 2 : k % nq;          // describe's counter copy (d.eq)
+            hipStream_t qd = c->split ? c->se[1] : c->se[eq];  // the queue describe ran on
             hipEvent_t e;
             if (!c->event_wait) {
                 const hipError_t we = hipStreamWaitValue32(s, c->d.ctr + VO_SYNC_EXT + 16 * eq,
@@ -436,7 +460,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
                     c->event_wait = true;
                     int rc = batch_event(c, VO_EV_WAIT, (size_t)k, &e);
                     if (rc) return rc;
-                    HIPCHK(hipEventRecord(e, c->se[eq]));
+                    HIPCHK(hipEventRecord(e, qd));
                     HIPCHK(hipStreamWaitEvent(s, e, 0));
                 }
             } else {
@@ -620,15 +644,22 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     // counter, which ROCm runs as a polling blit kernel (measured equal or slightly slower)
     c->event_wait = !(getenv("VO_EVENT_WAIT") && atoi(getenv("VO_EVENT_WAIT")) == 0);
     d.xcd_map = getenv("VO_XCD") ? atoi(getenv("VO_XCD")) : 1;
+    c->split = VO_EXT_QUEUES >= 2 && (getenv("VO_SPLIT") ? atoi(getenv("VO_SPLIT")) != 0 : VO_SPLIT_DEFAULT != 0);
     c->slack = getenv("VO_SLACK") ? std::max(0, std::min(64, atoi(getenv("VO_SLACK")))) : VO_SLACK_DEFAULT;
     // repair windows hold two work records per frame (k_finalize): at most WB / 2 frames
     d.repair_win = std::max(1, std::min(d.WB / 2, getenv("VO_REPAIR_WIN") ? atoi(getenv("VO_REPAIR_WIN")) : VO_REPAIR_WIN_DEFAULT));
-    if (hip_ok(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
-    if (hip_ok(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
+    // queue priorities (VO_PRIO): 0 none; 1 the pose and trajectory queues high (the pose queue is the
+    // serial critical path; the extract queue has slack); -1 the extract queues high
+    const int prio = getenv("VO_PRIO") ? atoi(getenv("VO_PRIO")) : VO_PRIO_DEFAULT;
+    int p_lo = 0, p_hi = 0;
+    if (prio) (void)hipDeviceGetStreamPriorityRange(&p_lo, &p_hi);
+    const int p_pose = prio > 0 ? p_hi : p_lo, p_ext = prio < 0 ? p_hi : p_lo;
+    if (hip_ok(hipStreamCreateWithPriority(&c->s, hipStreamNonBlocking, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK)
         return bail(VO_ERR_HIP);
     for (hipStream_t& q : c->se)
-        if (hip_ok(hipStreamCreateWithFlags(&q, hipStreamNonBlocking)) != VO_OK) return bail(VO_ERR_HIP);
+        if (hip_ok(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, p_ext)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming)) != VO_OK) return bail(VO_ERR_HIP);
     d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
     if (d.sel_lds < 0) return bail(VO_ERR_HIP);

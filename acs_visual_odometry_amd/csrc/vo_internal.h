@@ -69,7 +69,13 @@ inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_T
 #define VO_SLACK_DEFAULT 1        // extra passes per chunk of >= 4 batches (VO_SLACK; 0 / 1 / 4 measured within noise)
 // ctr words: cross-queue counters on lines of their own
 #ifndef VO_EXT_QUEUES
-#define VO_EXT_QUEUES 1        // extract queues (batch j on queue j % n, own scratch); 2 measured no faster
+#define VO_EXT_QUEUES 2        // extract queues and scratch copies (VO_EXTQ: batch j on queue j % n; 2 measured no faster)
+#endif
+#ifndef VO_PRIO_DEFAULT
+#define VO_PRIO_DEFAULT 0      // VO_PRIO: 1 pose / trajectory queues at high priority, -1 extract queues
+#endif
+#ifndef VO_SPLIT_DEFAULT
+#define VO_SPLIT_DEFAULT 0     // VO_SPLIT=1: stencils on extract queue 0, select + describe on queue 1 (batch j in scratch j % 2)
 #endif
 #define VO_CTR_DESCRIBE 0      // + 16 * queue: describe's in-launch arrival counter
 #define VO_SYNC_EXT 32         // + 16 * queue: frames extracted since vo_reset by that queue
@@ -81,6 +87,9 @@ inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_T
 #define VO_EV_WAIT 0           // per-batch event pools of a chunk (vo_api.cpp)
 #define VO_EV_COPY 1
 #define VO_EV_STENCIL 2
+#define VO_EV_SPLIT_S 3        // split extract: stencil of batch j done (select / describe queue waits)
+#define VO_EV_SPLIT_D 4        // split extract: describe of batch j done (its scratch copy is free again)
+#define VO_EV_POOLS 5
 #define VO_MAX_HYP 2000
 #define VO_HYP_CHUNK0 100     // RANSAC launch chunks (vo_kernels.hip launch_ransac); 100 = the clamp
 #define VO_HYP_CHUNK1 512

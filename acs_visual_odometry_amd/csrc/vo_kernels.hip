@@ -366,7 +366,8 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #define ST_HALO 7                      // blur 3 + gradient 1 + window 2 + nms 1
 #define ST_TCAP (ST_TW * ST_TH / 4)    // candidates per tile (strict maxima: at most 1 in 4)
 #ifndef ST_SEGT_DEFAULT
-#define ST_SEGT_DEFAULT 4              // tiles per wave segment (VO_STSEG picks 2 / 4 / 6 / 8)
+#define ST_SEGT_DEFAULT 8              // tiles per wave segment (VO_STSEG picks 2 / 4 / 6 / 8 / 12; KITTI: 8 measured
+                                       // 260k vs 246k frames/s for 4 -- 14 halo rows per 128 instead of per 64 --, 12 257k, 24 231k)
 #endif
 static_assert(ST_SW + 2 * ST_HALO + 1 <= 128, "strip + halo within one wave of column pairs");
 
@@ -3135,11 +3136,13 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
     ensure_tables();
     const int ntx = (d.W + ST_TW - 1) / ST_TW, nsx = (ntx + 1) / 2, nty = (d.H + ST_TH - 1) / ST_TH;
     static const int segt = getenv("VO_STSEG") ? atoi(getenv("VO_STSEG")) : ST_SEGT_DEFAULT;
-    const int st = write_response ? 4 : segt == 2 || segt == 6 || segt == 8 ? segt : 4;
+    const int st = write_response ? 4 : segt == 2 || segt == 6 || segt == 8 || segt == 12 ? segt : ST_SEGT_DEFAULT;
     const int waves = nsx * ((nty + st - 1) / st);                 // one (strip, segment) per wave
     dim3 g(xcd_grid((waves + 3) / 4, nb));
     if (write_response)
         hipLaunchKernelGGL((k_stencil<4, true>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response, nb);
+    else if (st == 12)
+        hipLaunchKernelGGL((k_stencil<12, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
     else if (st == 8)
         hipLaunchKernelGGL((k_stencil<8, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
     else if (st == 6)
