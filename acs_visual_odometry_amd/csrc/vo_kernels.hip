@@ -2663,6 +2663,9 @@ __device__ __forceinline__ void nullvec4(const double* A, double* x)
 // grid (4N / TRI_BLOCK, B): frame wf = blockIdx.y; only frames whose own refit ran (a frame
 // whose model leaked reuses the pose of the model's frame, k_finalize).
 #define TRI_BLOCK 128
+#ifndef TRI_BPF_DEFAULT
+#define TRI_BPF_DEFAULT 16     // KITTI 1.0 m/frame: 266k vs 253k frames/s for one block per 128 (point, candidate) pairs (0); 0.05 m/frame within noise
+#endif
 __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d, int stage)
 {
     const int wf = blockIdx.y;
@@ -2675,7 +2678,10 @@ __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d, int stage)
     __shared__ int s_cnt[4];
     if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
     __syncthreads();
-    const int g = blockIdx.x * TRI_BLOCK + threadIdx.x;   // (point, candidate) = (g >> 2, g & 3)
+    int mycnt = 0;
+    // (point, candidate) = (g >> 2, g & 3); a grid of fewer blocks than 4n / TRI_BLOCK strides
+    for (int g = blockIdx.x * TRI_BLOCK + threadIdx.x; g < ((4 * n + TRI_BLOCK - 1) / TRI_BLOCK) * TRI_BLOCK;
+         g += gridDim.x * TRI_BLOCK) {
     const int i = g >> 2, cnd = g & 3;
     bool pos = false;
     if (i < n) {
@@ -2712,11 +2718,9 @@ __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d, int stage)
     }
     unsigned long long bal = ballot64(pos);
     const int lane = threadIdx.x & 63;
-    if (lane < 4) {
-        const unsigned long long mask = 0x1111111111111111ull << lane;
-        int c = __popcll(bal & mask);
-        if (c) atomicAdd(&s_cnt[lane], c);
+    if (lane < 4) mycnt += __popcll(bal & (0x1111111111111111ull << lane));
     }
+    if ((threadIdx.x & 63) < 4 && mycnt) atomicAdd(&s_cnt[threadIdx.x & 63], mycnt);
     __syncthreads();
     if (threadIdx.x < 4 && s_cnt[threadIdx.x])
         __hip_atomic_fetch_add((gi32*)&w->counts4[threadIdx.x], s_cnt[threadIdx.x], __ATOMIC_RELAXED,
@@ -3218,8 +3222,11 @@ void launch_refit(const VoDev& d, int with_pose, int stage, hipStream_t s)
 }
 void launch_triangulate(const VoDev& d, int stage, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_triangulate, dim3((4 * d.N + TRI_BLOCK - 1) / TRI_BLOCK, stage ? 1 : d.WB), dim3(TRI_BLOCK), 0,
-                       s, d, stage);
+    // blocks per frame (VO_TRI_BPF; 0 = one (point, candidate) per thread, 4N / TRI_BLOCK blocks)
+    static const int bpf_env = getenv("VO_TRI_BPF") ? atoi(getenv("VO_TRI_BPF")) : TRI_BPF_DEFAULT;
+    const int full = (4 * d.N + TRI_BLOCK - 1) / TRI_BLOCK;
+    const int bpf = bpf_env > 0 ? std::min(bpf_env, full) : full;
+    hipLaunchKernelGGL(k_triangulate, dim3(bpf, stage ? 1 : d.WB), dim3(TRI_BLOCK), 0, s, d, stage);
 }
 void launch_finalize(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s)
 {
