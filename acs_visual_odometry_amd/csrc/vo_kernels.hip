@@ -1375,6 +1375,16 @@ __device__ __forceinline__ void top2_insert(uint32_t key, uint32_t& m1, uint32_t
     m2 = med3_u32(key, m1, m2);
     m1 = min(m1, key);
 }
+// two keys at once (m1 <= m2): the smallest of the four is min3(m1, k1, k2); the second
+// smallest is the median of {m1, k1, k2} unless m2 is below it -- three VALU for two keys
+// (v_med3_u32, v_min_u32, v_min3_u32) instead of four
+__device__ __forceinline__ void top2_insert2(uint32_t k1, uint32_t k2, uint32_t& m1, uint32_t& m2)
+{
+    m2 = min(med3_u32(m1, k1, k2), m2);
+    uint32_t r;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(m1), "v"(k1), "v"(k2));   // left alone, LLVM emits two v_min_u32
+    m1 = r;
+}
 __device__ __forceinline__ void top2_wave(uint32_t& m1, uint32_t& m2)
 {
 #pragma unroll
@@ -1616,10 +1626,10 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
             const uint4 c = s_cand4[j >> 2];
 #pragma unroll
             for (int u = 0; u < MT_QPL; ++u) {
-                top2_insert(((uint32_t)__popc(qv[u] ^ c.x) << 16) | (uint32_t)j, a1[u], a2[u]);
-                top2_insert(((uint32_t)__popc(qv[u] ^ c.y) << 16) | (uint32_t)(j + 1), b1[u], b2[u]);
-                top2_insert(((uint32_t)__popc(qv[u] ^ c.z) << 16) | (uint32_t)(j + 2), a1[u], a2[u]);
-                top2_insert(((uint32_t)__popc(qv[u] ^ c.w) << 16) | (uint32_t)(j + 3), b1[u], b2[u]);
+                top2_insert2(((uint32_t)__popc(qv[u] ^ c.x) << 16) | (uint32_t)j,
+                             ((uint32_t)__popc(qv[u] ^ c.y) << 16) | (uint32_t)(j + 1), a1[u], a2[u]);
+                top2_insert2(((uint32_t)__popc(qv[u] ^ c.z) << 16) | (uint32_t)(j + 2),
+                             ((uint32_t)__popc(qv[u] ^ c.w) << 16) | (uint32_t)(j + 3), b1[u], b2[u]);
             }
         }
         for (; j < j1; ++j) {
