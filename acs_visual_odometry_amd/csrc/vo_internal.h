@@ -17,9 +17,9 @@
 //   blurred     u8  Wb*Hb    x B   7x7 Gaussian output (read back by describe); rows of
 //                                  Wb = whole stencil strips, Hb = whole tiles + 4 rows
 //   response    f32 W*H            optional dense R map (debug / parity only)
-//   cand        u64 192/tile x B   NMS survivors per 48x16 tile, key = Rbits<<32 | row<<16 | col
+//   cand        u64 224/tile x B   NMS survivors per 56x16 tile, key = Rbits<<32 | row<<16 | col
 //   tilerows    u8  16/tile  x B   survivors per tile row (select emits raster order from them)
-//   ckeys       u64 192/tile x B   compact survivors (only when they overflow select's LDS)
+//   ckeys       u64 224/tile x B   compact survivors (only when they overflow select's LDS)
 //   selbits     u64 4/tile   x B   selected-survivor bitmap (only when it overflows LDS)
 //   hist        u32 4096     x B   coarse histogram of candidate R (top-N boundary)
 //   kps         int2 N  x SLOTS    raster-ordered keypoints: ring slot f % VO_RING, carry, stage
@@ -41,9 +41,12 @@
 #include <stdint.h>
 
 #define VO_HIST_BINS 4096
-#define VO_TILE_W 48       // stencil tile = one wave's strip width x 16 rows (k_stencil ST_TW, ST_TH)
+#ifndef VO_TILE_W
+#define VO_TILE_W 56       // stencil tile = half a wave's strip x 16 rows (k_stencil ST_TW, ST_TH)
+#endif
 #define VO_TILE_H 16
-#define VO_STRIP_W 96      // stencil strip = one wave: two tiles side by side
+#define VO_STRIP_W (2 * VO_TILE_W)   // stencil strip = one wave: two tiles side by side (<= 112: 64 lanes
+                                     // of column pairs hold the strip and 7 halo columns each side)
 // blurred plane of a W x H frame: row stride and rows (every stencil wave stores whole rows of
 // its strip, up to 4 rows past its segment)
 inline int vo_blur_stride(int W) { return ((W + 2 * VO_TILE_W - 1) / (2 * VO_TILE_W)) * VO_STRIP_W; }

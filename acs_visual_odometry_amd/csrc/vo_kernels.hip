@@ -347,10 +347,10 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // stencil: blur7x7 -> gradients -> 5x5 response -> strict 3x3 NMS candidates
 // kernels/feature_extraction_kernel_functions.c:43-120, corner_detection_parallel_GPU.cpp:146-180
 //
-// Column-streaming form: one wave owns a strip of ST_SW = 96 output columns (two 48-column
+// Column-streaming form: one wave owns a strip of ST_SW = 112 output columns (two 56-column
 // tiles) and walks down a segment of 16 SEGT output rows.  Lane L holds the column PAIR
 // c0 = xs - 8 + 2L, c0 + 1 in every stage (128 columns: the strip, 7 halo columns on each
-// side, 18 spare).  Vertical neighbours are register histories (one new source row per step);
+// side, 2 spare).  Vertical neighbours are register histories (one new source row per step);
 // horizontal neighbours are the lane's other column or a DPP wave shift (v_mov_b32_dpp
 // wave_shr:1 / wave_shl:1), so a shift serves two columns.  No LDS, no barrier.
 // Source row k of the segment (y = ys - 7 + k) completes blurred row ys - 10 + k, gradient
@@ -360,9 +360,9 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // The wave's row and column conditions are uniform branches or lane masks, so the scalar
 // unit (one per CU, shared by its four SIMDs) stays well below the VALU's issue rate.
 // ---------------------------------------------------------------------------
-#define ST_TW VO_TILE_W                // tile width: 48
+#define ST_TW VO_TILE_W                // tile width: 56 (48 measured: KITTI within noise, 1080p -3 %)
 #define ST_TH VO_TILE_H                // tile height (select reads 16 row counts per tile)
-#define ST_SW VO_STRIP_W               // strip width = two tiles: 96 output columns per wave
+#define ST_SW VO_STRIP_W               // strip width = two tiles: 112 output columns per wave
 #define ST_HALO 7                      // blur 3 + gradient 1 + window 2 + nms 1
 #define ST_TCAP (ST_TW * ST_TH / 4)    // candidates per tile (strict maxima: at most 1 in 4)
 #ifndef ST_SEGT_DEFAULT
@@ -516,7 +516,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
     const int xs = sxi * ST_SW, ys = seg * SEG;
     const int c0 = xs - 8 + 2 * lane;                          // this lane's columns: c0, c0 + 1
     const int xl0 = refl101(c0, W), xl1 = refl101(c0 + 1, W);  // BORDER_REFLECT_101
-    const bool out_lane = lane >= 4 && lane < 4 + ST_SW / 2;  // columns xs .. xs + 95
+    const bool out_lane = lane >= 4 && lane < 4 + ST_SW / 2;  // columns xs .. xs + ST_SW - 1
     const int boff = out_lane ? c0 : 0x40000000;               // blurred store: out of range off the strip
     const bool isB = lane >= 4 + ST_TW / 2;                   // the strip's second tile
     const bool hasB = 2 * sxi + 1 < ntx;
@@ -535,8 +535,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
     const int nmsk0 = ncol(c0) ? 0 : 0x7FFFFFFF, nmsk1 = ncol(c0 + 1) ? 0 : 0x7FFFFFFF;
     const int nlo = max(hk, d.brow), nhi = max(nlo, min(H - hk, H - d.brow + 1));   // NMS rows [nlo, nhi)
     const uint32_t thr_bits = d.thr_bits;
-    constexpr unsigned long long mA = 0x000000000FFFFFF0ull;   // lanes 4..27: tile 2 sxi
-    constexpr unsigned long long mB = 0x000FFFFFF0000000ull;   // lanes 28..51: tile 2 sxi + 1
+    constexpr unsigned long long mT = (1ull << (ST_TW / 2)) - 1ull;
+    constexpr unsigned long long mA = mT << 4;                 // lanes 4 .. 3 + TW/2: tile 2 sxi
+    constexpr unsigned long long mB = mT << (4 + ST_TW / 2);   // the next TW/2 lanes: tile 2 sxi + 1
 
     // register histories (index 0 oldest); source rows packed: column c0 low half, c0 + 1 high
     uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0;
