@@ -30,6 +30,21 @@ def h2d_bandwidth():
             e1.record()
         e1.synchronize()
         out[f"{mb}MB"] = round(n * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+    # the same bytes split over two / four copy streams at once (several SDMA engines)
+    for ns in (2, 4):
+        n = int(30e6)
+        h = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        d = torch.empty(n, dtype=torch.uint8, device="cuda")
+        ss = [torch.cuda.Stream() for _ in range(ns)]
+        part = n // ns
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(10):
+            for i, s in enumerate(ss):
+                with torch.cuda.stream(s):
+                    d[i * part:(i + 1) * part].copy_(h[i * part:(i + 1) * part], non_blocking=True)
+        torch.cuda.synchronize()
+        out[f"30MB_x{ns}streams"] = round(n * 10 / (time.perf_counter() - t0) / 1e9, 1)
     return out
 
 
