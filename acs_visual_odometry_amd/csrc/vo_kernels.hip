@@ -3215,7 +3215,9 @@ void launch_match(const VoDev& d, int stage, hipStream_t s)
 void launch_ransac(const VoDev& d, int stage, hipStream_t s)
 {
     const int nhyp = d.max_hyp, nb = stage ? 1 : d.WB;
-    const int cut[3] = {std::min(nhyp, VO_HYP_CHUNK0), std::min(nhyp, VO_HYP_CHUNK1), nhyp};
+    // VO_HYP_CUT1: the second cut (VO_HYP_CHUNK1; >= max_hyp merges the last two chunks)
+    static const int cut1 = getenv("VO_HYP_CUT1") ? std::max(VO_HYP_CHUNK0, atoi(getenv("VO_HYP_CUT1"))) : VO_HYP_CHUNK1;
+    const int cut[3] = {std::min(nhyp, VO_HYP_CHUNK0), std::min(nhyp, cut1), nhyp};
     int k0 = 0;
     for (int c = 0; c < 3; ++c) {
         const int k1 = cut[c];
