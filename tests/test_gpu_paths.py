@@ -364,3 +364,47 @@ def test_sequence_shards_two_processes(leak_case):
     assert [(x[1], x[2]) for x in res] == shard.partition(80, 2)
     _check(ref, np.concatenate([x[3] for x in res]), np.concatenate([x[4] for x in res]),
            np.concatenate([x[5] for x in res]))
+
+
+# -- execution knobs: every measured-and-kept-off alternative still gives the oracle's rows ------
+@pytest.mark.parametrize("env", ["VO_SPLIT=1", "VO_PRIO=1", "VO_PRIO=-1"])
+def test_queue_knobs_match_oracle(leak_case, monkeypatch, env):
+    """Per-context queue layouts (read by vo_create): select + describe on a second extract queue
+    (VO_SPLIT), pose or extract queues at high priority (VO_PRIO)."""
+    seq, frames, ref = leak_case
+    k, v = env.split("=")
+    monkeypatch.setenv(k, v)
+    _device_run(seq, frames, ref=ref, frame_batch=16)
+
+
+_KNOB_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from acs_visual_odometry_amd import Context
+d = np.load(sys.argv[2])
+ctx = Context(int(d["W"]), int(d["H"]), K=d["K"], frame_batch=int(sys.argv[3]))
+ctx.set_ground_truth(d["gt"])
+df = ctx.device_frames(d["frames"])
+poses, st, info = ctx.process_frames_device(df)
+df.free(); ctx.close()
+ok = np.array_equal(st, d["st"]) and np.array_equal(poses, d["poses"]) and np.array_equal(info[:, :6], d["info"])
+print("KNOB_OK" if ok else "KNOB_DIFF")
+"""
+
+
+@pytest.mark.parametrize("env,batch", [("VO_STSEG=4", 16), ("VO_STSEG=2", 64), ("VO_STSEG=12", 64), ("VO_HYP_CUT1=512", 16),
+                                       ("VO_TRI_BPF=0", 64), ("VO_RREPS=4", 16), ("VO_EXTQ=2", 8), ("VO_XCD=0", 64)])
+def test_process_knobs_match_oracle(leak_case, tmp_path, env, batch):
+    """Knobs the library reads once per process (stencil segment height, RANSAC cut and loop,
+    triangulation grid, alternating extract queues, XCD placement), each in a child process on the
+    leak sequence: rows, statuses and counts equal the oracle's."""
+    import sys
+    seq, frames, ref = leak_case
+    npz = tmp_path / "case.npz"
+    np.savez(npz, W=seq.W, H=seq.H, K=seq.K, gt=seq.gt(), frames=frames,
+             st=np.array([r[1] for r in ref]), poses=np.stack([r[0] for r in ref]),
+             info=np.stack([r[2][:6] for r in ref]))
+    k, v = env.split("=")
+    out = subprocess.run([sys.executable, "-c", _KNOB_SCRIPT, ROOT, str(npz), str(batch)], capture_output=True,
+                         text=True, timeout=240, env={**os.environ, k: v})
+    assert "KNOB_OK" in out.stdout, (out.stdout[-2000:], out.stderr[-2000:])
