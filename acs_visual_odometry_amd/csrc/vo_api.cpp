@@ -43,6 +43,8 @@ struct vo_ctx {
     bool event_wait = true;           // pose queue waits for extract batches on events (default)
                                       // or on the stream-wait-value packet (VO_EVENT_WAIT=0; events
                                       // again after the runtime refused a wait-value packet)
+    bool fuse_fin = false;            // VO_FUSE_FIN=1: the pass's finalize in k_triangulate's last workgroup
+                                      // (measured slower: 246-259k vs 257-272k frames/s KITTI)
     bool split = false;               // VO_SPLIT: stencil and select/describe of a batch on two extract queues
     int slack = 0;                    // VO_SLACK: extra passes enqueued per chunk (misses re-run without a host round trip)
     hipStream_t st = nullptr;         // trajectory queue: k_traj of each pass (T_curr chain, pose rows)
@@ -342,8 +344,12 @@ void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax)
     timed(c, ev, 3, s, [&] { vo::launch_match(d, 0, s); });
     timed(c, ev, 4, s, [&] { vo::launch_ransac(d, 0, s); });
     timed(c, ev, 5, s, [&] { vo::launch_refit(d, 1, 0, s); });
-    timed(c, ev, 6, s, [&] { vo::launch_triangulate(d, 0, s); });
-    timed(c, ev, 7, s, [&] { vo::launch_finalize(d, out, out_base, s); });
+    if (c->fuse_fin) {
+        timed(c, ev, 6, s, [&] { vo::launch_triangulate(d, 0, s, out, out_base, 1); });
+    } else {
+        timed(c, ev, 6, s, [&] { vo::launch_triangulate(d, 0, s); });
+        timed(c, ev, 7, s, [&] { vo::launch_finalize(d, out, out_base, s); });
+    }
     // the T_curr chain and the pose rows on the trajectory queue (serial mode: the pose queue)
     hipStream_t q = c->serial ? s : c->st;
     if (q != s) {
@@ -644,6 +650,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     // counter, which ROCm runs as a polling blit kernel (measured equal or slightly slower)
     c->event_wait = !(getenv("VO_EVENT_WAIT") && atoi(getenv("VO_EVENT_WAIT")) == 0);
     d.xcd_map = getenv("VO_XCD") ? atoi(getenv("VO_XCD")) : 1;
+    c->fuse_fin = getenv("VO_FUSE_FIN") && atoi(getenv("VO_FUSE_FIN")) != 0;
     c->split = VO_EXT_QUEUES >= 2 && (getenv("VO_SPLIT") ? atoi(getenv("VO_SPLIT")) != 0 : VO_SPLIT_DEFAULT != 0);
     c->slack = getenv("VO_SLACK") ? std::max(0, std::min(64, atoi(getenv("VO_SLACK")))) : VO_SLACK_DEFAULT;
     // repair windows hold two work records per frame (k_finalize): at most WB / 2 frames

@@ -83,7 +83,8 @@ inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_T
 #define VO_CTR_DESCRIBE 0      // + 16 * queue: describe's in-launch arrival counter
 #define VO_SYNC_EXT 32         // + 16 * queue: frames extracted since vo_reset by that queue
                                // (its batches complete in order; the pose queue waits on it)
-#define VO_CTR_WORDS 64
+#define VO_CTR_FIN 64          // fused triangulate + finalize: workgroups arrived (the last one finalizes)
+#define VO_CTR_WORDS 80
 // host-frame streaming (vo_process_frames_host): device ring of VO_HRING slots of B frames
 #define VO_HRING 3
 #define VO_HOST_FIRST_BATCH 16 // host streaming: frames in a chunk's first batch (shorter pipeline fill)
@@ -235,7 +236,8 @@ void launch_ext_missing(const VoDev& d, int slot, hipStream_t s);   // extract s
 void launch_match(const VoDev& d, int stage, hipStream_t s);        // + ordered compaction per frame
 void launch_ransac(const VoDev& d, int stage, hipStream_t s);       // all hypotheses + replay per frame
 void launch_refit(const VoDev& d, int with_pose, int stage, hipStream_t s);
-void launch_triangulate(const VoDev& d, int stage, hipStream_t s);
+// fin: the pass's finalize in the last workgroup of the launch (out / out_base as launch_finalize)
+void launch_triangulate(const VoDev& d, int stage, hipStream_t s, VoFrameOut* out = nullptr, int out_base = 0, int fin = 0);
 void launch_finalize(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s);
 void launch_traj(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s);   // T_curr chain + pose rows of pass d.pass
 void launch_traj_range(const VoDev& d, VoFrameOut* out, int out_base, int lo, int nc, hipStream_t s);   // vo_rechain

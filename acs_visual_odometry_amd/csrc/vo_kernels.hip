@@ -2673,20 +2673,27 @@ __device__ __forceinline__ void nullvec4(const double* A, double* x)
 // (cv::undistortPoints + cv::triangulatePoints + depth test, PoseUpdate.hpp:101-147).
 // grid (4N / TRI_BLOCK, B): frame wf = blockIdx.y; only frames whose own refit ran (a frame
 // whose model leaked reuses the pose of the model's frame, k_finalize).
-#define TRI_BLOCK 128
+#define TRI_BLOCK 256
 #ifndef TRI_BPF_DEFAULT
-#define TRI_BPF_DEFAULT 16     // KITTI 1.0 m/frame: 266k vs 253k frames/s for one block per 128 (point, candidate) pairs (0); 0.05 m/frame within noise
+#define TRI_BPF_DEFAULT 8      // workgroups per frame (x 256 threads; KITTI 1.0 m/frame: 266k vs 253k frames/s for one per
+                               // 128 (point, candidate) pairs; 0.05 m/frame within noise)
 #endif
-__global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d, int stage)
+__device__ void finalize_body(const VoDev& d, VoFrameOut* out, int out_base);
+// fin: the pass's k_finalize runs in the workgroup that arrives last (every workgroup arrives,
+// with or without work; the cheirality counts are agent-scope atomics, read back with agent-scope
+// loads), saving the pass a launch and a queue gap
+__global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d, int stage, VoFrameOut* out, int out_base, int fin)
 {
     const int wf = blockIdx.y;
-    if (wf >= vwin_count(d, stage)) return;
     VoWork* w = d.work + wf;
-    if (w->status != VO_STATUS_OK || !w->fitted || w->degenerate) return;
-    const int n = w->n_fit;
-    const unsigned active = (unsigned)((4 * n + TRI_BLOCK - 1) / TRI_BLOCK);
-    if (blockIdx.x >= active) return;
     __shared__ int s_cnt[4];
+    __shared__ unsigned s_last;
+    bool go = wf < vwin_count(d, stage);
+    if (go) go = w->status == VO_STATUS_OK && w->fitted && !w->degenerate;
+    const int n = go ? w->n_fit : 0;
+    const unsigned active = (unsigned)((4 * n + TRI_BLOCK - 1) / TRI_BLOCK);
+    go = go && blockIdx.x < active;
+    if (go) {
     if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
     __syncthreads();
     int mycnt = 0;
@@ -2736,6 +2743,11 @@ __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d, int stage)
     if (threadIdx.x < 4 && s_cnt[threadIdx.x])
         __hip_atomic_fetch_add((gi32*)&w->counts4[threadIdx.x], s_cnt[threadIdx.x], __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!fin) return;
+    if (!arrive_last(d.ctr + VO_CTR_FIN, gridDim.x * gridDim.y, &s_last)) return;
+    if (threadIdx.x == 0) d.ctr[VO_CTR_FIN] = 0u;      // the next pass's launch (kernel boundary orders it)
+    finalize_body(d, out, out_base);
 }
 
 // lane 4q + k of each quad -> every lane of the quad (DPP quad_perm [k, k, k, k])
@@ -2768,6 +2780,11 @@ __device__ __forceinline__ double dpp_quad_bcast(double v, int k)
 // needs none of them, so they overlap it.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int out_base)
+{
+    finalize_body(d, out, out_base);
+}
+
+__device__ void finalize_body(const VoDev& d, VoFrameOut* out, int out_base)
 {
     constexpr int MW = VO_MAX_WIN;                    // s_R / s_t [MW]: the model before the window
     __shared__ int s_n, s_ncommit, s_lo, s_copy, s_model_wf, s_model_clear, s_newlv, s_newprev;
@@ -2829,7 +2846,7 @@ __global__ void __launch_bounds__(256) k_finalize(VoDev d, VoFrameOut* out, int 
         s_degen[tid] = w->degenerate;
         if (fit && !w->degenerate) {
             int c4[4];
-            for (int c = 0; c < 4; ++c) c4[c] = w->counts4[c];
+            for (int c = 0; c < 4; ++c) c4[c] = ld_sc1(&w->counts4[c]);   // k_triangulate's atomics (fused: this launch)
             choose_pose(c4, w->R1, w->R2, w->t, s_R[tid], s_t[tid]);
         }
     } else if (tid == 255) {
@@ -3233,13 +3250,13 @@ void launch_refit(const VoDev& d, int with_pose, int stage, hipStream_t s)
 {
     hipLaunchKernelGGL(k_refit, dim3(stage ? 1 : d.WB), dim3(RF_T), 0, s, d, with_pose, stage);
 }
-void launch_triangulate(const VoDev& d, int stage, hipStream_t s)
+void launch_triangulate(const VoDev& d, int stage, hipStream_t s, VoFrameOut* out, int out_base, int fin)
 {
     // blocks per frame (VO_TRI_BPF; 0 = one (point, candidate) per thread, 4N / TRI_BLOCK blocks)
     static const int bpf_env = getenv("VO_TRI_BPF") ? atoi(getenv("VO_TRI_BPF")) : TRI_BPF_DEFAULT;
     const int full = (4 * d.N + TRI_BLOCK - 1) / TRI_BLOCK;
     const int bpf = bpf_env > 0 ? std::min(bpf_env, full) : full;
-    hipLaunchKernelGGL(k_triangulate, dim3(bpf, stage ? 1 : d.WB), dim3(TRI_BLOCK), 0, s, d, stage);
+    hipLaunchKernelGGL(k_triangulate, dim3(bpf, stage ? 1 : d.WB), dim3(TRI_BLOCK), 0, s, d, stage, out, out_base, fin);
 }
 void launch_finalize(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s)
 {
