@@ -65,7 +65,10 @@ inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_T
 // (frame f's slot is rewritten by frame f + VO_RING; passes read frames >= lo - 1)
 #define VO_CHUNK (d.ring - 1)
 #define VO_MAX_BATCH 64
-#define VO_MAX_WIN 128       // pose window capacity: up to two extract batches (k_finalize LDS)
+#ifndef VO_MAX_WIN
+#define VO_MAX_WIN 128       // pose window capacity (k_finalize / k_traj LDS; < 255: thread 255 keeps the loop state).
+                             // Windows measured: 64 227k, 96 258k, 128 268k, 160 / 192 within noise of 128
+#endif
 #define VO_MAX_SEQ_STARTS 4096     // vo_set_sequence_starts capacity
 #define VO_DEFAULT_BATCH 64
 #define VO_REPAIR_WIN_DEFAULT 8   // pose window after a speculation miss (frames; dual records: 4 / 8 / 16 measured 174k / 180k / 177k KITTI frames/s)

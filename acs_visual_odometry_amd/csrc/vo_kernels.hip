@@ -3037,14 +3037,16 @@ __device__ __forceinline__ void traj_chain(const VoDev& d, VoFrameOut* out, int 
     // 2
     if (tid < 64) {
         const int e = tid & 15, i = e >> 2, j = e & 3;
-        // frame kinds of window frames tid (chunk 0) and 64 + tid (chunk 1)
-        const bool inc = tid < nc, inc1 = 64 + tid < nc;
-        const unsigned long long Mkind0 = ballot64(inc && s_kind[tid] == 1);
-        const unsigned long long Mfirst0 = ballot64(inc && s_first[tid] != 0);
-        const unsigned long long Mflip0 = ballot64(inc && s_flip[tid] != 0);
-        const unsigned long long Mkind1 = ballot64(inc1 && s_kind[64 + tid] == 1);
-        const unsigned long long Mfirst1 = ballot64(inc1 && s_first[64 + tid] != 0);
-        const unsigned long long Mflip1 = ballot64(inc1 && s_flip[64 + tid] != 0);
+        // frame kinds of window frames 64 c + tid (chunk c) as wave-uniform masks
+        constexpr int NCH = (MW + 63) / 64;
+        unsigned long long Mkind[NCH], Mfirst[NCH], Mflip[NCH];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const bool inc = 64 * c + tid < nc;
+            Mkind[c] = ballot64(inc && s_kind[64 * c + tid] == 1);
+            Mfirst[c] = ballot64(inc && s_first[64 * c + tid] != 0);
+            Mflip[c] = ballot64(inc && s_flip[64 * c + tid] != 0);
+        }
         double Tv = s_T[e];
         const double ident = (e % 5 == 0) ? 1.0 : 0.0;  // VisualOdometry.cpp:57 T_curr = eye(4)
         double b[3][4];
@@ -3061,10 +3063,14 @@ __device__ __forceinline__ void traj_chain(const VoDev& d, VoFrameOut* out, int 
             const double a0 = dpp_quad_bcast(Tv, 0), a1 = dpp_quad_bcast(Tv, 1);
             const double a2 = dpp_quad_bcast(Tv, 2), a3 = dpp_quad_bcast(Tv, 3);
             const double pv = ((a0 * b[0][0] + a1 * b[0][1]) + a2 * b[0][2]) + a3 * b[0][3];
-            const int sh = wf & 63;
-            const bool kind = ((wf < 64 ? Mkind0 : Mkind1) >> sh) & 1ull;
-            const bool firstf = ((wf < 64 ? Mfirst0 : Mfirst1) >> sh) & 1ull;
-            const bool flip = ((wf < 64 ? Mflip0 : Mflip1) >> sh) & 1ull;
+            const int sh = wf & 63, ch = wf >> 6;
+            unsigned long long mk = Mkind[0], mf = Mfirst[0], ml = Mflip[0];
+#pragma unroll
+            for (int c = 1; c < NCH; ++c)
+                if (ch == c) { mk = Mkind[c]; mf = Mfirst[c]; ml = Mflip[c]; }
+            const bool kind = (mk >> sh) & 1ull;
+            const bool firstf = (mf >> sh) & 1ull;
+            const bool flip = (ml >> sh) & 1ull;
             Tv = kind ? pv : (firstf ? ident : Tv);
             if (tid < 12) s_row[wf][tid] = (flip && i == 2) ? -Tv : Tv;
 #pragma unroll
