@@ -94,11 +94,12 @@ def profile_row(prof, kernel: str):
     normalised by the passes (k_match calls) and the extract kernels by the batches (k_stencil)."""
     if not prof:
         return None
-    rows = [r for k, r in prof.items() if k.split("<")[0] == ROCPROF_NAME[kernel]]
+    names = {ROCPROF_NAME[kernel]} | ({"k_match512"} if kernel == "match" else set())   # 512-test mode
+    rows = [r for k, r in prof.items() if k.split("<")[0] in names]
     if not rows:
         return None
-    ref = "k_match" if kernel in POSE_QUEUE or kernel == "trajectory" else "k_stencil"
-    ref_calls = [r["calls"] for k, r in prof.items() if k.split("<")[0] == ref]
+    ref = {"k_match", "k_match512"} if kernel in POSE_QUEUE or kernel == "trajectory" else {"k_stencil"}
+    ref_calls = [r["calls"] for k, r in prof.items() if k.split("<")[0] in ref]
     launches = max(ref_calls) if ref_calls else max(r["calls"] for r in rows)
 
     def per(key):
@@ -328,7 +329,8 @@ def run_variants(args, ctx, W, H, frames0, gt0, extra, Context) -> dict:
                 "frames_ok": int((st == 0).sum()), "mean_matches": float(info[1:, 1].mean()),
                 "match_us_per_launch": ks.get("match", (float("nan"), 0))[0] * 1e3,
                 "match_frames_per_launch": ks.get("match", (0, 0))[1],
-                "match_rocprof_avg_us": prow["avg_us"] if prow else None, "profile": src,
+                "match_rocprof_avg_us": prow["avg_us"] if prow else None,
+                "match_valu_issue_frac": prow["valu_issue_frac"] if prow else None, "profile": src,
                 "kernels_us_per_frame": {k: round(v[0] / v[1] * 1e3, 3) for k, v in ks.items() if v[1] > 0}}
             dx.free()
             cx.close()
