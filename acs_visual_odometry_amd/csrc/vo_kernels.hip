@@ -896,25 +896,18 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     // B
     const bool staged = C <= L.key_cap;
     uint64_t* keys = staged ? s_keys : d.ckeys + (size_t)z * d.cand_cap;
-    {
-        auto slot_of = [&](int g) -> size_t {
-            int lo = 0, hi = ntiles - 1;
-            while (lo < hi) {
-                int mid = (lo + hi + 1) >> 1;
-                if (s_tpre[mid] <= g) lo = mid; else hi = mid - 1;
-            }
-            return (size_t)lo * TCAP + (size_t)(g - s_tpre[lo]);
-        };
-        for (int g0 = tid; g0 < C; g0 += 4 * 1024) {
+    // a thread per tile copies the tile's keys to their compact positions (the keys of a tile
+    // are contiguous in both; a binary search of the tile per key cost ten dependent LDS reads)
+    for (int t = tid; t < ntiles; t += 1024) {
+        const int b = s_tpre[t], n = s_tpre[t + 1] - b;
+        const uint64_t* src = cand + (size_t)t * TCAP;
+        for (int i = 0; i < n; i += 4) {
             uint64_t v[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int g = g0 + u * 1024;
-                v[u] = g < C ? cand[slot_of(g)] : 0ull;
-            }
+            for (int u = 0; u < 4; ++u) v[u] = i + u < n ? src[i + u] : 0ull;
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                if (g0 + u * 1024 < C) keys[g0 + u * 1024] = v[u];
+                if (i + u < n) keys[b + i + u] = v[u];
         }
     }
     __syncthreads();
