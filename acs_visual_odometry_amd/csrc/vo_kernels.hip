@@ -363,6 +363,9 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #define ST_TW VO_TILE_W                // tile width: 56 (48 measured: KITTI within noise, 1080p -3 %)
 #define ST_TH VO_TILE_H                // tile height (select reads 16 row counts per tile)
 #define ST_SW VO_STRIP_W               // strip width = two tiles: 112 output columns per wave
+#ifndef ST_DPP_ADD
+#define ST_DPP_ADD 1                   // box sums with v_add_f32_dpp (0: v_mov_b32_dpp + packed adds)
+#endif
 #define ST_HALO 7                      // blur 3 + gradient 1 + window 2 + nms 1
 #define ST_TCAP (ST_TW * ST_TH / 4)    // candidates per tile (strict maxima: at most 1 in 4)
 #ifndef ST_SEGT_DEFAULT
@@ -443,6 +446,24 @@ __device__ __forceinline__ int from_right16(int v)
 // two lanes' worth per issue, tools/valu_rate.hip)
 typedef float st_f2 __attribute__((ext_vector_type(2)));
 typedef unsigned short st_w2 __attribute__((ext_vector_type(2)));
+// v + (the left / right lane's s): one v_add_f32_dpp (the wave shift on src0) instead of a
+// v_mov_b32_dpp and an add.  By hand: the build disables LLVM's DPP combine (it mis-folded a
+// wave shift into v_subrev_u32_dpp on gfx950, Makefile), and inline asm is opaque to the hazard
+// recognizer, so the two wait states a DPP read of a just-written VGPR needs are in the asm
+__device__ __forceinline__ float add_from_left(float s, float v)
+{
+    float r;
+    asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+                 : "=v"(r) : "v"(s), "v"(v));
+    return r;
+}
+__device__ __forceinline__ float add_from_right(float s, float v)
+{
+    float r;
+    asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+                 : "=v"(r) : "v"(s), "v"(v));
+    return r;
+}
 __device__ __forceinline__ float from_leftf(float v) { return __int_as_float(from_left(__float_as_int(v))); }
 __device__ __forceinline__ float from_rightf(float v) { return __int_as_float(from_right(__float_as_int(v))); }
 // (a.x - b.y, b.x - a.y) in one v_pk_add_f32: cross halves through op_sel, signs through neg
@@ -624,12 +645,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         if constexpr (P >= 4) {
             // horizontal 5-sums: column c0 takes c0-2 .. c0+2 = the left pair, its own pair and
             // the right lane's c0; column c0 + 1 the left lane's c0 + 1, its pair, the right pair
+#if ST_DPP_ADD
+            // (exact integer sums below 2^24: the order is free) four DPP adds and one add
+            auto box = [](st_f2 a) {
+                const float p = a.x + a.y;
+                const float x = add_from_left(p, p), y = add_from_left(a.y, p);
+                return st_f2{add_from_right(a.x, x), add_from_right(p, y)};
+            };
+#else
             auto box = [](st_f2 a) {
                 const st_f2 p = a + a.yx;                              // (a0 + a1, a0 + a1)
                 const st_f2 l = {from_leftf(p.x), from_leftf(a.y)};
                 const st_f2 r = {from_rightf(a.x), from_rightf(p.x)};
                 return (l + p) + r;
             };
+#endif
             const st_f2 SX = box(VX), SY = box(VY), SS = box(VS);
             // 4. response of row yr (kernel .c:108-114), 0 outside 2 <= i <= H-3, 2 <= j <= W-3
             const int yr = ys - 13 + k;
