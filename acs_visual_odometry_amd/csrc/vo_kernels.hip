@@ -446,24 +446,8 @@ __device__ __forceinline__ int from_right16(int v)
 // two lanes' worth per issue, tools/valu_rate.hip)
 typedef float st_f2 __attribute__((ext_vector_type(2)));
 typedef unsigned short st_w2 __attribute__((ext_vector_type(2)));
-// v + (the left / right lane's s): one v_add_f32_dpp (the wave shift on src0) instead of a
-// v_mov_b32_dpp and an add.  By hand: the build disables LLVM's DPP combine (it mis-folded a
-// wave shift into v_subrev_u32_dpp on gfx950, Makefile), and inline asm is opaque to the hazard
-// recognizer, so the two wait states a DPP read of a just-written VGPR needs are in the asm
-__device__ __forceinline__ float add_from_left(float s, float v)
-{
-    float r;
-    asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
-                 : "=v"(r) : "v"(s), "v"(v));
-    return r;
-}
-__device__ __forceinline__ float add_from_right(float s, float v)
-{
-    float r;
-    asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
-                 : "=v"(r) : "v"(s), "v"(v));
-    return r;
-}
+// (the box sums add across lanes with hand-written v_add_f32_dpp in k_stencil: the build disables
+// LLVM's DPP combine -- it mis-folded a wave shift into v_subrev_u32_dpp on gfx950, Makefile)
 __device__ __forceinline__ float from_leftf(float v) { return __int_as_float(from_left(__float_as_int(v))); }
 __device__ __forceinline__ float from_rightf(float v) { return __int_as_float(from_right(__float_as_int(v))); }
 // (a.x - b.y, b.x - a.y) in one v_pk_add_f32: cross halves through op_sel, signs through neg
@@ -646,12 +630,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             // horizontal 5-sums: column c0 takes c0-2 .. c0+2 = the left pair, its own pair and
             // the right lane's c0; column c0 + 1 the left lane's c0 + 1, its pair, the right pair
 #if ST_DPP_ADD
-            // (exact integer sums below 2^24: the order is free) four DPP adds and one add
-            auto box = [](st_f2 a) {
-                const float p = a.x + a.y;
-                const float x = add_from_left(p, p), y = add_from_left(a.y, p);
-                return st_f2{add_from_right(a.x, x), add_from_right(p, y)};
-            };
+            // (exact integer sums below 2^24: the order is free) per plane four DPP adds and one add,
+            // the three planes in one block ordered so that every DPP source was written at least
+            // two VALU instructions earlier (the wait states a DPP read of a fresh VGPR needs; the
+            // inputs come from before the block): no s_nop
+            float sx0, sx1, sy0, sy1, ss0, ss1;
+            {
+                float pX, pY, pS, xX, yX, xY, yY, xS, yS;
+                asm volatile(
+                    "v_add_f32 %[pX], %[ax], %[ay]\n\t"
+                    "v_add_f32 %[pY], %[bx], %[by]\n\t"
+                    "v_add_f32 %[pS], %[cx], %[cy]\n\t"
+                    "v_add_f32_dpp %[xX], %[pX], %[pX] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                    "v_add_f32_dpp %[yX], %[ay], %[pX] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                    "v_add_f32_dpp %[xY], %[pY], %[pY] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                    "v_add_f32_dpp %[yY], %[by], %[pY] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                    "v_add_f32_dpp %[xS], %[pS], %[pS] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                    "v_add_f32_dpp %[yS], %[cy], %[pS] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                    "v_add_f32_dpp %[sx0], %[ax], %[xX] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                    "v_add_f32_dpp %[sx1], %[pX], %[yX] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                    "v_add_f32_dpp %[sy0], %[bx], %[xY] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                    "v_add_f32_dpp %[sy1], %[pY], %[yY] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                    "v_add_f32_dpp %[ss0], %[cx], %[xS] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                    "v_add_f32_dpp %[ss1], %[pS], %[yS] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+                    : [pX] "=&v"(pX), [pY] "=&v"(pY), [pS] "=&v"(pS), [xX] "=&v"(xX), [yX] "=&v"(yX),
+                      [xY] "=&v"(xY), [yY] "=&v"(yY), [xS] "=&v"(xS), [yS] "=&v"(yS),
+                      [sx0] "=&v"(sx0), [sx1] "=&v"(sx1), [sy0] "=&v"(sy0), [sy1] "=&v"(sy1),
+                      [ss0] "=&v"(ss0), [ss1] "=&v"(ss1)
+                    : [ax] "v"(VX.x), [ay] "v"(VX.y), [bx] "v"(VY.x), [by] "v"(VY.y), [cx] "v"(VS.x), [cy] "v"(VS.y));
+            }
+            const st_f2 SX = {sx0, sx1}, SY = {sy0, sy1}, SS = {ss0, ss1};
 #else
             auto box = [](st_f2 a) {
                 const st_f2 p = a + a.yx;                              // (a0 + a1, a0 + a1)
@@ -659,8 +667,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                 const st_f2 r = {from_rightf(a.x), from_rightf(p.x)};
                 return (l + p) + r;
             };
-#endif
             const st_f2 SX = box(VX), SY = box(VY), SS = box(VS);
+#endif
             // 4. response of row yr (kernel .c:108-114), 0 outside 2 <= i <= H-3, 2 <= j <= W-3
             const int yr = ys - 13 + k;
             const bool rrow = (unsigned)(yr - 2) <= (unsigned)(H - 5);
