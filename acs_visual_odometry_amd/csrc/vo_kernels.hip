@@ -363,6 +363,9 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #define ST_TW VO_TILE_W                // tile width: 56 (48 measured: KITTI within noise, 1080p -3 %)
 #define ST_TH VO_TILE_H                // tile height (select reads 16 row counts per tile)
 #define ST_SW VO_STRIP_W               // strip width = two tiles: 112 output columns per wave
+#ifndef ST_SOFF_HOIST
+#define ST_SOFF_HOIST 1                // a row group's source-row offsets read into SGPRs before its rows
+#endif
 #ifndef ST_DPP_ADD
 #define ST_DPP_ADD 1                   // box sums with v_add_f32_dpp (0: v_mov_b32_dpp + packed adds)
 #endif
@@ -776,9 +779,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         const int k0 = 14 + ST_TH * i;
         const int rows = row_offsets(k0 + LA);
         toffA = 0; toffB = 0;
+        // the group's 16 row offsets to SGPRs up front: a v_readlane right before the buffer load
+        // whose offset it feeds costs the wave five wait states (s_nop 4) per row
+        int soff[ST_TH];
+#if ST_SOFF_HOIST
+        st_for([&](auto U) { soff[U] = __builtin_amdgcn_readlane(rows, U); }, std::make_integer_sequence<int, ST_TH>{});
+#endif
         st_for([&](auto U) {
             const uint32_t cur = ahead[U % LA];
+#if ST_SOFF_HOIST
+            ahead[U % LA] = load(soff[U]);
+#else
+            (void)soff;
             ahead[U % LA] = load(__builtin_amdgcn_readlane(rows, U));
+#endif
             step(P5{}, k0 + U, cur, U);
         }, std::make_integer_sequence<int, ST_TH>{});
         // the 16 row counts of tile A (lanes 0..15) and B (16..31) are contiguous
