@@ -363,6 +363,9 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #define ST_TW VO_TILE_W                // tile width: 56 (48 measured: KITTI within noise, 1080p -3 %)
 #define ST_TH VO_TILE_H                // tile height (select reads 16 row counts per tile)
 #define ST_SW VO_STRIP_W               // strip width = two tiles: 112 output columns per wave
+#ifndef ST_RSEL_ASM
+#define ST_RSEL_ASM 1                  // the response's rounding selects ordered by hand (no s_nop)
+#endif
 #ifndef ST_SOFF_HOIST
 #define ST_SOFF_HOIST 1                // a row group's source-row offsets read into SGPRs before its rows
 #endif
@@ -478,8 +481,31 @@ __device__ __forceinline__ st_f2 st_response2(st_f2 jx2, st_f2 jy2, st_f2 sxy)
     const st_f2 sp = {__int_as_float(__float_as_int(s.x) + 1), __int_as_float(__float_as_int(s.y) + 1)};
     const st_f2 rm = st_fma(-sm, s, x), rp = st_fma(-sp, s, x);
     st_f2 r;
+#if ST_RSEL_ASM
+    // r = rp > 0 ? sp : (rm <= 0 ? sm : s) per component (NaN: s), the four compares into SGPR
+    // pairs first, so every select reads a mask written two or more instructions earlier (left to
+    // itself LLVM pairs each compare with its select through VCC and pads it with s_nop 1)
+    {
+        unsigned long long ma, mb, mc, md;
+        float tx, ty;
+        asm volatile(
+            "v_cmp_ge_f32_e64 %[mc], 0, %[rmx]\n\t"
+            "v_cmp_ge_f32_e64 %[md], 0, %[rmy]\n\t"
+            "v_cmp_lt_f32_e64 %[ma], 0, %[rpx]\n\t"
+            "v_cmp_lt_f32_e64 %[mb], 0, %[rpy]\n\t"
+            "v_cndmask_b32_e64 %[tx], %[sx], %[smx], %[mc]\n\t"
+            "v_cndmask_b32_e64 %[ty], %[sy], %[smy], %[md]\n\t"
+            "v_cndmask_b32_e64 %[rx], %[tx], %[spx], %[ma]\n\t"
+            "v_cndmask_b32_e64 %[ry], %[ty], %[spy], %[mb]"
+            : [ma] "=&s"(ma), [mb] "=&s"(mb), [mc] "=&s"(mc), [md] "=&s"(md), [tx] "=&v"(tx), [ty] "=&v"(ty),
+              [rx] "=&v"(r.x), [ry] "=&v"(r.y)
+            : [rmx] "v"(rm.x), [rmy] "v"(rm.y), [rpx] "v"(rp.x), [rpy] "v"(rp.y), [sx] "v"(s.x), [sy] "v"(s.y),
+              [smx] "v"(sm.x), [smy] "v"(sm.y), [spx] "v"(sp.x), [spy] "v"(sp.y));
+    }
+#else
     r.x = rp.x > 0.0f ? sp.x : (rm.x <= 0.0f ? sm.x : s.x);
     r.y = rp.y > 0.0f ? sp.y : (rm.y <= 0.0f ? sm.y : s.y);
+#endif
     return 0.5f * (tr - r);
 }
 // f(integral_constant<int, I>) for I = 0 .. N-1, unrolled at compile time
