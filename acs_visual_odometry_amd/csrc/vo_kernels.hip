@@ -1254,6 +1254,9 @@ __global__ void k_ext_missing(VoDev d, int slot)
 // No cross-lane traffic, no barrier.
 // ---------------------------------------------------------------------------
 #define DS_KPW 64
+#ifndef DS_ALIGNBIT
+#define DS_ALIGNBIT 1
+#endif
 #ifndef DS_WAVES
 #define DS_WAVES 4
 #endif
@@ -1299,7 +1302,13 @@ __device__ __forceinline__ uint32_t ds_word(const uint32_t (&r)[VO_FREAK_NPOINTS
     st_for([&](auto J) {
         constexpr int t = 32 * W + 31 - decltype(J)::value;          // highest test first
         constexpr int e = kDs.patch[t];
+#if DS_ALIGNBIT
+        // (word << 1) | (I(q) - I(p) < 0): v_sub + v_alignbit_b32 (funnel shift of word:diff by 31),
+        // no compare, no VCC select and its wait states (samples are bytes: no overflow)
+        word = __builtin_amdgcn_alignbit(word, r[kDs.pq[e]] - r[kDs.pp[e]], 31u);
+#else
         word = (word << 1) | (r[kDs.pp[e]] > r[kDs.pq[e]] ? 1u : 0u);
+#endif
     }, std::make_integer_sequence<int, 32>{});
     return word;
 }
