@@ -26,9 +26,17 @@ namespace vo {
 // Rows p of the pair order padded to whole groups of DS_OG terms with zero terms (dx = dy = 0:
 // the term is a zero, which leaves a sum that is never -0 unchanged), so the describe loop has
 // no remainder iterations.
+#ifndef DS_OG
 #define DS_OG 8
+#endif
 #define DS_OROWS (VO_FREAK_NPOINTS + DS_OG - 1)     // sample rows incl. the zero padding rows
-#define DS_ONPAD 1056                               // sum over p of ceil((42 - p) / 8) * 8
+constexpr int ds_onpad()                            // sum over p of ceil((42 - p) / OG) * OG (1056 at 8)
+{
+    int n = 0;
+    for (int k = 1; k < VO_FREAK_NPOINTS; ++k) n += (k + DS_OG - 1) / DS_OG * DS_OG;
+    return n;
+}
+#define DS_ONPAD (ds_onpad())
 __constant__ float4 c_orient[DS_ONPAD];
 
 static bool g_tables_ready = false;
@@ -1350,7 +1358,10 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
         float4 tb[DS_OG];
 #pragma unroll
         for (int u = 0; u < DS_OG; ++u) { iq[u] = col[(qs + u) * DS_KPW]; tb[u] = c_orient[u]; }
-#pragma unroll 2
+#ifndef DS_GUNROLL
+#define DS_GUNROLL 4          // orientation groups unrolled (2: 269k vs 277k frames/s in alternating A/B)
+#endif
+#pragma unroll DS_GUNROLL
         for (int g = 0; g < NG; ++g) {
             // the next group (the last one re-reads itself)
             int pn = p, qn = qs + DS_OG;
