@@ -1496,7 +1496,9 @@ __device__ __forceinline__ int ratio_accept(uint32_t m1, uint32_t m2, float rati
 }
 
 // 32-bit prefix mode: MT_QPL queries per lane, 64 MT_QPL per workgroup (k_match)
+#ifndef MT_QPL
 #define MT_QPL 4
+#endif
 #define MT_QPB (64 * MT_QPL)
 #define MT512_QPB 256                 // 512-test matcher: queries per workgroup (one per thread)
 __host__ __device__ inline int match_blocks(int N, int match_bits)
