@@ -1929,12 +1929,25 @@ __device__ __forceinline__ double g8_bcast_d(double v)
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 // a[c] for a group-uniform runtime column c (9-way select)
+#ifndef RS_FASTSEL
+#define RS_FASTSEL 1
+#endif
+#define RS_GROUPS_MAX 32       // lane groups of eight per workgroup (k_ransac_hyp<4>: 256 threads)
 __device__ __forceinline__ double sel9(const double (&a)[9], int c)
 {
+#if RS_FASTSEL
+    // a[c], c in [0, 8], as a select tree on the bits of c: four masks, each reused
+    const bool b0 = (c & 1) != 0, b1 = (c & 2) != 0, b2 = (c & 4) != 0, b3 = (c & 8) != 0;
+    const double v01 = b0 ? a[1] : a[0], v23 = b0 ? a[3] : a[2], v45 = b0 ? a[5] : a[4], v67 = b0 ? a[7] : a[6];
+    const double v03 = b1 ? v23 : v01, v47 = b1 ? v67 : v45;
+    const double v07 = b2 ? v47 : v03;
+    return b3 ? a[8] : v07;
+#else
     double v = a[0];
 #pragma unroll
     for (int j = 1; j < 9; ++j) v = c == j ? a[j] : v;
     return v;
+#endif
 }
 
 // computeFundamentalMatrix on a minimal sample (ransac.cpp:63-93) for the lane group's
@@ -2017,6 +2030,29 @@ __device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], in
     // back substitution: x_fc = 1, x_pc = -a[pr][fc] / a[pr][pc] from each pivot row
     const double val = my_pc >= 0 ? -(sel9(a, fc) / sel9(a, my_pc)) : 0.0;
     double f[9];
+#if RS_FASTSEL
+    // the group's solution vector through LDS: each pivot row stores its x_pc at column pc, the
+    // free column holds 1, the rest 0 -- the same vector as eight broadcast rows selected into
+    // nine registers (72 compare / select pairs, each padded for its VCC read), in three LDS
+    // steps.  One wave's lanes only, ordered by wave barriers.
+    {
+        __shared__ double s_fb[RS_GROUPS_MAX][9];
+        double* fb = s_fb[threadIdx.x >> 3];
+        fb[r] = 0.0;
+        if (r == 0) fb[8] = 0.0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (my_pc >= 0) fb[my_pc] = val;
+        if (r == 0) fb[fc] = 1.0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int j = 0; j < 9; ++j) f[j] = fb[j];
+        __builtin_amdgcn_wave_barrier();              // the next hypothesis' fit rewrites fb
+    }
+#else
 #pragma unroll
     for (int j = 0; j < 9; ++j) f[j] = (j == fc) ? 1.0 : 0.0;
     auto take_row = [&](int cq, double vq) {
@@ -2031,6 +2067,7 @@ __device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], in
     take_row(g8_bcast<5>(my_pc), g8_bcast_d<5>(val));
     take_row(g8_bcast<6>(my_pc), g8_bcast_d<6>(val));
     take_row(g8_bcast<7>(my_pc), g8_bcast_d<7>(val));
+#endif
     double nn = 0.0;
 #pragma unroll
     for (int j = 0; j < 9; ++j) nn = nn + f[j] * f[j];
