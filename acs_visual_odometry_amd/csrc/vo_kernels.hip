@@ -842,6 +842,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
 // (feature_extraction_parallel_GPU.cpp:259-265).
 // ---------------------------------------------------------------------------
 #define SEL_MAX 4096
+#ifndef SEL_DOT4
+#define SEL_DOT4 1
+#endif
 #define BND_CAP 2048
 #define SEL_MAX_TILES 3072
 #define SEL_LDS_BITS 65536
@@ -1167,9 +1170,21 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
             const uint4 rc = s_rows[t];
             const uint32_t w4[4] = {rc.x, rc.y, rc.z, rc.w};
             int start = 0;
+#if SEL_DOT4
+            // the row counts below r (bytes of the four words): each word masked to its bytes below
+            // r (a 64-bit shift covers the whole-word and empty cases) and summed by v_dot4_u32_u8
+            // -- no compare / select per row
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int sh = 8 * min(max(r - 4 * k, 0), 4);
+                const uint32_t m = (uint32_t)(0xFFFFFFFFull >> (32 - sh));
+                start = (int)__builtin_amdgcn_udot4(w4[k] & m, 0x01010101u, (uint32_t)start, false);
+            }
+#else
 #pragma unroll
             for (int q = 0; q < ST_TH; ++q)
                 if (q < r) start += (int)((w4[q >> 2] >> (8 * (q & 3))) & 0xFF);
+#endif
             const int gs = s_tpre[t] + start;
             // selected keys before g inside the segment
             int within = 0;
