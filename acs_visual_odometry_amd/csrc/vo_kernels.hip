@@ -2005,6 +2005,31 @@ __device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], in
         // lane-local candidate: first max |a| over the unused columns of an unused row
         double bv = -1.0;
         int bi = 1 << 30;
+#if RS_FASTSEL
+        // the same first maximum as a tournament (depth 4 instead of a 9-step compare / select
+        // chain): candidates are |a| over unused columns, > 0, else -1; a later one wins only if
+        // strictly greater, so ties go to the smaller column
+        {
+            double mv[9];
+#pragma unroll
+            for (int c = 0; c < 9; ++c) {
+                const double v = fabs(a[c]);
+                mv[c] = (!((used_c >> c) & 1u) && v > 0.0) ? v : -1.0;
+            }
+            auto win = [](double& va, int& ia, double vb, int ib) {
+                const bool t = vb > va;
+                va = t ? vb : va;
+                ia = t ? ib : ia;
+            };
+            double w0 = mv[0], w1 = mv[2], w2 = mv[4], w3 = mv[6];
+            int i0 = 0, i1 = 2, i2 = 4, i3 = 6;
+            win(w0, i0, mv[1], 1); win(w1, i1, mv[3], 3); win(w2, i2, mv[5], 5); win(w3, i3, mv[7], 7);
+            win(w0, i0, w1, i1); win(w2, i2, w3, i3);
+            win(w0, i0, w2, i2);
+            win(w0, i0, mv[8], 8);
+            if (!((used_r >> r) & 1u) && w0 > 0.0) { bv = w0; bi = r * 9 + i0; }
+        }
+#else
         if (!((used_r >> r) & 1u)) {
 #pragma unroll
             for (int c = 0; c < 9; ++c) {
@@ -2012,6 +2037,7 @@ __device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], in
                 if (!((used_c >> c) & 1u) && v > 0.0 && v > bv) { bv = v; bi = r * 9 + c; }
             }
         }
+#endif
         // group maximum, ties to the smaller flat index
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
