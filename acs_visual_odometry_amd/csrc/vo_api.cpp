@@ -43,6 +43,8 @@ struct vo_ctx {
     bool event_wait = true;           // pose queue waits for extract batches on events (default)
                                       // or on the stream-wait-value packet (VO_EVENT_WAIT=0; events
                                       // again after the runtime refused a wait-value packet)
+    bool force_wait_refusal = false;  // VO_FORCE_WAIT_REFUSAL=1 (tests): treat the first wait-value packet as
+                                      // refused, so the event fallback path runs
     bool fuse_fin = false;            // VO_FUSE_FIN=1: the pass's finalize in k_triangulate's last workgroup
                                       // (measured slower: 246-259k vs 257-272k frames/s KITTI)
     bool split = false;               // VO_SPLIT: stencil and select/describe of a batch on two extract queues
@@ -437,7 +439,10 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         }
         hipStream_t qd = q2 ? q2 : q;
         if (split) HIPCHK(hipEventRecord(e_d, qd));
-        if (multi && c->event_wait) {
+        if (multi) {
+            // recorded in both wait modes: if the runtime refuses a wait-value packet, the passes
+            // fall back to these events, and every batch enqueued so far -- on any extract queue --
+            // already has its own
             hipEvent_t e;
             int rc = batch_event(c, VO_EV_WAIT, (size_t)j, &e);
             if (rc) return rc;
@@ -450,23 +455,20 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     auto pass = [&](int k) -> int {
         if (multi) {
             const int eq = c->split ? k % 2 : k % nq;          // describe's counter copy (d.eq)
-            hipStream_t qd = c->split ? c->se[1] : c->se[eq];  // the queue describe ran on
             hipEvent_t e;
             if (!c->event_wait) {
                 const hipError_t we = hipStreamWaitValue32(s, c->d.ctr + VO_SYNC_EXT + 16 * eq,
                                                            (uint32_t)(base + f0s[k + 1]), hipStreamWaitValueGte,
                                                            0xFFFFFFFFu);
-                if (we != hipSuccess) {
-                    // the packet was refused: events from now on.  The fallback event, recorded
-                    // now, covers every batch of queue eq enqueued so far (correct, less overlap);
-                    // later batches record one event each
+                if (we != hipSuccess || c->force_wait_refusal) {
+                    // the packet was refused: events from now on -- batch k's own event, recorded
+                    // on the queue its describe ran on when the batch was enqueued
                     fprintf(stderr, "[vo_mi355x] hipStreamWaitValue32 failed (%s): event waits\n",
-                            hipGetErrorString(we));
+                            we != hipSuccess ? hipGetErrorString(we) : "refusal forced by VO_FORCE_WAIT_REFUSAL");
                     (void)hipGetLastError();
                     c->event_wait = true;
                     int rc = batch_event(c, VO_EV_WAIT, (size_t)k, &e);
                     if (rc) return rc;
-                    HIPCHK(hipEventRecord(e, qd));
                     HIPCHK(hipStreamWaitEvent(s, e, 0));
                 }
             } else {
@@ -651,6 +653,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     c->event_wait = !(getenv("VO_EVENT_WAIT") && atoi(getenv("VO_EVENT_WAIT")) == 0);
     d.xcd_map = getenv("VO_XCD") ? atoi(getenv("VO_XCD")) : 1;
     c->fuse_fin = getenv("VO_FUSE_FIN") && atoi(getenv("VO_FUSE_FIN")) != 0;
+    c->force_wait_refusal = getenv("VO_FORCE_WAIT_REFUSAL") && atoi(getenv("VO_FORCE_WAIT_REFUSAL")) != 0;
     c->split = VO_EXT_QUEUES >= 2 && (getenv("VO_SPLIT") ? atoi(getenv("VO_SPLIT")) != 0 : VO_SPLIT_DEFAULT != 0);
     c->slack = getenv("VO_SLACK") ? std::max(0, std::min(64, atoi(getenv("VO_SLACK")))) : VO_SLACK_DEFAULT;
     // repair windows hold two work records per frame (k_finalize): at most WB / 2 frames

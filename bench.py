@@ -59,7 +59,7 @@ ROCPROF_NAME = {"stencil": "k_stencil", "select": "k_select", "describe": "k_des
 # committed rocprofv3 summaries (tools/profile.sh -> tools/rocprof_summary.py --json): kernel
 # durations, PMC HBM bytes and VALU counters per launch
 PROFILES = {(1241, 376, 32): "r2_kitti_kernels.json", (1920, 1080, 32): "r2_1080_kernels.json",
-            (1920, 1080, 512): "r2_1080_512_kernels.json"}
+            (1920, 1080, 512): "r2_1080_512_kernels.json", (1241, 376, 32, 0.12): "r3_kitti_012_kernels.json"}
 
 
 def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray) -> float:
@@ -77,8 +77,8 @@ def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray) -> float:
             "path": W * H + 80 * n + 24 * M + 96}[kernel]
 
 
-def load_profile(W: int, H: int, bits: int):
-    name = PROFILES.get((W, H, bits))
+def load_profile(W: int, H: int, bits: int, motion: float = 1.0):
+    name = PROFILES.get((W, H, bits)) if motion == 1.0 else PROFILES.get((W, H, bits, motion))
     if not name:
         return None, None
     path = os.path.join(ROOT, "profiles", name)
@@ -109,6 +109,29 @@ def profile_row(prof, kernel: str):
     vi, gc = per("valu_insts"), per("grbm_cycles")
     return {"avg_us": per("avg_us"), "hbm_bytes": per("hbm_bytes_per_launch"), "valu_insts": vi,
             "valu_issue_frac": vi * VALU_CYCLES / (VALU_SIMDS * gc / 8) if vi is not None and gc else None}
+
+
+def roofline_entry(kernel: str, live: list, info: np.ndarray, W: int, H: int, prof, psrc) -> dict:
+    """roofline object of `kernel`: SURVEY 8(d)'s algorithmic bytes per launch over its average
+    launch time, the launches timed live with HIP events on its own stream (`live`: kernel_stats()
+    of the timed calls); traffic and VALU issue from the committed PMC profile."""
+    ms = [b[kernel][0] for b in live if kernel in b]
+    fpl = [b[kernel][1] for b in live if kernel in b]
+    dom_ms = float(np.mean(ms)) if ms else float("nan")
+    dom_fpl = float(np.mean(fpl)) if fpl else float("nan")
+    abytes = algorithmic_bytes(kernel, W, H, info) * dom_fpl
+    achieved = abytes / (dom_ms * 1e-3) / 1e9
+    prow = profile_row(prof, kernel)
+    return {"bound": "hbm", "kernel": kernel, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": prow["hbm_bytes"] if prow else None, "traffic_source": psrc,
+            "avg_launch_ms": dom_ms, "frames_per_launch": dom_fpl, "algorithmic_bytes_per_launch": abytes,
+            "rocprof_avg_launch_us": prow["avg_us"] if prow else None,
+            "choice": "largest per-frame time among the pose-queue kernels (the serial critical path)",
+            "valu": None if not prow else {
+                "insts_per_launch": prow["valu_insts"], "issue_frac": prow["valu_issue_frac"],
+                "peak": f"{VALU_SIMDS} SIMDs x 1 wave64 VALU instruction / {VALU_CYCLES} cycles (PMC: SQ_INSTS_VALU, "
+                        f"GRBM_GUI_ACTIVE)"}}
 
 
 # -- multi-GPU harness (config 5) --------------------------------------------------------
@@ -166,23 +189,31 @@ def gather_poses(dist, local_rows: dict, n_seq: int, nframes: int, backend: str 
 _CPU = {}
 
 
-def _cpu_worker(budget_s: float):
+def _cpu_worker(budget_s: float, keep_rows: bool = False):
+    """The oracle over the sequence, restarted at frame 0 after each pass, for ~budget_s.
+    keep_rows: also return the first complete pass's rows (pose, status) -- the bench checks the
+    GPU's rows of the same sequence against them."""
     import oracle as O
     frames, W, H, K, gt, N = (_CPU[k] for k in ("frames", "W", "H", "K", "gt", "N"))
     cfg = O.config(W, H, K=K.reshape(9), max_kpts=N)
     t0 = time.perf_counter()
     done = 0
+    rows = None
     while True:
         vo = O.VO(cfg, gt=gt)
+        pas = []
         for f in range(frames.shape[0]):
-            vo.process(frames[f])
+            p, st, _ = vo.process(frames[f])
+            pas.append((p, st))
             done += 1
             if time.perf_counter() - t0 > budget_s and done >= 2:
                 break
         vo.close()
-        if time.perf_counter() - t0 > budget_s:
+        if keep_rows and rows is None and len(pas) == frames.shape[0]:
+            rows = pas
+        if time.perf_counter() - t0 > budget_s and (rows is not None or not keep_rows):
             break
-    return done, time.perf_counter() - t0
+    return (done, time.perf_counter() - t0, rows) if keep_rows else (done, time.perf_counter() - t0)
 
 
 def cpu_model() -> str:
@@ -195,18 +226,19 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(frames, seq, budget_s: float, max_kpts: int, procs: int) -> dict:
+def cpu_baseline(frames, seq, budget_s: float, max_kpts: int, procs: int):
     """The CPU oracle over the bench sequence (restarted at frame 0 after each pass) for about
     budget_s seconds: `procs` forked processes, one per host core, each running the sequence
     (throughput = all frames / the slowest process), and one process alone.  Runs before the
-    process touches the GPU."""
+    process touches the GPU.  Returns (the JSON object, the single process's first complete pass
+    as [(pose 3x4, status)] -- the oracle's rows of the sequence, checked against the GPU's)."""
     _CPU.update(frames=frames, W=seq.W, H=seq.H, K=seq.K, gt=seq.gt(), N=max_kpts)
-    one_done, one_dt = _cpu_worker(budget_s)
+    one_done, one_dt, rows = _cpu_worker(budget_s, keep_rows=True)
     single = {"value": one_done / one_dt, "unit": "frames/s", "cores": 1, "kind": "port",
               "sample": f"{one_done} frames of the {frames.shape[0]}-frame sequence (restarted at frame 0 after "
                         f"each pass), oracle/vo_oracle.c in one process, {one_dt:.1f} s"}
     if procs <= 1:
-        return dict(single, cpu_model=cpu_model())
+        return dict(single, cpu_model=cpu_model()), rows
     pool = mp.get_context("fork").Pool(procs)
     try:
         res = pool.map(_cpu_worker, [budget_s] * procs)
@@ -218,7 +250,7 @@ def cpu_baseline(frames, seq, budget_s: float, max_kpts: int, procs: int) -> dic
     return {"value": done / dt, "unit": "frames/s", "cores": procs, "kind": "port",
             "sample": f"{procs} processes (one per host core), each running oracle/vo_oracle.c over the same "
                       f"{frames.shape[0]}-frame sequence for ~{budget_s:.0f} s: {done} frames in {dt:.1f} s",
-            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "single_thread": single}
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "single_thread": single}, rows
 
 
 # -- GPU measurement helpers ---------------------------------------------------------------
@@ -256,8 +288,20 @@ def run_variants(args, ctx, W, H, frames0, gt0, extra, Context) -> dict:
         ks = breakdown(ctx, go)
         out[tag] = {"fps": rate, "motion_m_per_frame": seq.step, "frames": fr.shape[0],
                     "mean_hypotheses": float(info[1:, 4].mean()), "mean_matches": float(info[1:, 1].mean()),
-                    "mean_inliers": float(info[1:, 2].mean()), "frames_ok": int((st == 0).sum()),
+                    "mean_inliers": float(info[1:, 2].mean()), "fitted_fraction": float(info[1:, 5].mean()),
+                    "frames_ok": int((st == 0).sum()),
                     "kernels_us_per_frame": {k: round(v[0] / v[1] * 1e3, 3) for k, v in ks.items() if v[1] > 0}}
+        if tag.startswith("low_inlier"):
+            # its own roofline entry: the critical-path kernel of this regime (RANSAC runs hundreds
+            # of hypotheses per frame here), timed live over `steps` calls like the headline's
+            per_frame = {k: v[0] / v[1] for k, v in ks.items() if v[1] > 0}
+            dom = max((k for k in POSE_QUEUE if k in per_frame), key=lambda k: per_frame[k])
+            live = []
+            for _ in range(steps):
+                go(timing=100 + KERNELS.index(dom))
+                live.append(ctx.kernel_stats())
+            prof, psrc = load_profile(W, H, 32, motion=seq.step)
+            out[tag]["roofline"] = roofline_entry(dom, live, info, W, H, prof, psrc)
         df.free()
     # extract only (config 2), device-resident frames of sequence 0
     df = ctx.device_frames(frames0)
@@ -470,10 +514,10 @@ def main():
             for i, sp in enumerate(specs)}
     extra = {tag: (rendered[len(specs) + i], SceneSequence(sp[0], sp[1], nframes=sp[2], seq=sp[3], step=sp[4]))
              for i, (tag, sp) in enumerate(extra_specs.items())}
-    cpu = None
+    cpu, oracle_rows = None, None
     if lead and not args.no_cpu:
         s0, fr0 = seqs[my_seqs[0]]
-        cpu = cpu_baseline(fr0, s0, args.cpu_seconds, args.max_kpts, workers)
+        cpu, oracle_rows = cpu_baseline(fr0, s0, args.cpu_seconds, args.max_kpts, workers)
 
     dist = dist_init(world, local)
     from acs_visual_odometry_amd import Context
@@ -546,6 +590,14 @@ def main():
     gather_ok = None
     if rank == 0 and not args.no_check:
         gather_ok = all(bool(np.array_equal(separate(s, seqs[s][1]), gathered[s])) for s in range(S))
+    # the CPU oracle's rows of the first sequence (the cpu_baseline leg's first complete pass)
+    # against the GPU's rows of that sequence in the timed stream, bit for bit
+    oracle_ok = None
+    if oracle_rows is not None:
+        s0 = my_seqs[0]
+        oracle_ok = bool(len(oracle_rows) == F and
+                         all(np.array_equal(last[s0][0][f], oracle_rows[f][0]) and int(last[s0][1][f]) == oracle_rows[f][1]
+                             for f in range(F)))
 
     variants = None
     if lead and not args.no_variants:
@@ -554,24 +606,8 @@ def main():
         variants = run_variants(args, ctx, W, H, seqs[s0][1], gts[s0], extra, Context)
 
     if rank == 0:
-        live_ms = [b[dominant][0] for b in live if dominant in b]
-        live_fpl = [b[dominant][1] for b in live if dominant in b]
-        dom_ms = float(np.mean(live_ms)) if live_ms else float("nan")
-        dom_fpl = float(np.mean(live_fpl)) if live_fpl else float("nan")
         prof, psrc = load_profile(W, H, args.match_bits)
-        abytes = algorithmic_bytes(dominant, W, H, info_all) * dom_fpl
-        achieved = abytes / (dom_ms * 1e-3) / 1e9
-        prow = profile_row(prof, dominant)
-        roof = {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": prow["hbm_bytes"] if prow else None, "traffic_source": psrc,
-                "avg_launch_ms": dom_ms, "frames_per_launch": dom_fpl, "algorithmic_bytes_per_launch": abytes,
-                "rocprof_avg_launch_us": prow["avg_us"] if prow else None,
-                "choice": "largest per-frame time among the pose-queue kernels (the serial critical path)",
-                "valu": None if not prow else {
-                    "insts_per_launch": prow["valu_insts"], "issue_frac": prow["valu_issue_frac"],
-                    "peak": f"{VALU_SIMDS} SIMDs x 1 wave64 VALU instruction / {VALU_CYCLES} cycles (PMC: SQ_INSTS_VALU, "
-                            f"GRBM_GUI_ACTIVE)"}}
+        roof = roofline_entry(dominant, live, info_all, W, H, prof, psrc)
         path_bytes = algorithmic_bytes("path", W, H, info_all)
         kern = {}
         for k in KERNELS:
@@ -599,14 +635,24 @@ def main():
                        "mean_kpts": float(info_all[:, 0].mean()), "mean_matches": float(info_all[:, 1].mean()),
                        "mean_inliers": float(info_all[:, 2].mean()),
                        "mean_hypotheses": float(info_all[:, 4].mean()),
+                       "fitted_fraction": float(info_all[np.concatenate([last[s][1] for s in my_seqs]) != 1, 5].mean()),
                        "frames_ok": int((st_all == 0).sum()), "frames": int(st_all.size)},
             "roofline": roof,
+            # SURVEY 8(d) times "from frame H2D to pose D2H": the same path with the frames streamed
+            # from pinned host memory (a 1000-frame sequence, vo_process_frames_host); never `value`
+            "h2d_inclusive": None if not variants or "host_stream" not in variants else {
+                "value": variants["host_stream"]["fps"], "unit": "frames/s",
+                "source": "variants.host_stream (pinned host frames, H2D on a copy queue inside the timing)"},
             "path_roofline": {"algorithmic_bytes_per_frame": path_bytes,
                               "achieved_GBs": path_bytes * value / world / 1e9,
                               "frac": path_bytes * value / world / 1e9 / HBM_PEAK_GBS},
             "kernels": kern,
             "determinism": {"timed_rows_equal_warmup_rows": bool(repeat_equal),
-                            "gathered_rows_equal_separate_runs": gather_ok},
+                            "gathered_rows_equal_separate_runs": gather_ok,
+                            "oracle_rows_equal": oracle_ok,
+                            "oracle_rows_checked": f"sequence {my_seqs[0]}: {F} frames (pose rows + statuses) against "
+                                                   f"the CPU oracle's run in the cpu_baseline leg" if oracle_ok is not None
+                            else None},
             "variants": variants,
             "cpu_baseline": cpu,
         }

@@ -394,18 +394,23 @@ print("KNOB_OK" if ok else "KNOB_DIFF")
 
 
 @pytest.mark.parametrize("env,batch", [("VO_STSEG=4", 16), ("VO_STSEG=2", 64), ("VO_STSEG=12", 64), ("VO_HYP_CUT1=512", 16),
-                                       ("VO_TRI_BPF=0", 64), ("VO_RREPS=4", 16), ("VO_EXTQ=2", 8), ("VO_XCD=0", 64)])
+                                       ("VO_TRI_BPF=0", 64), ("VO_RREPS=4", 16), ("VO_EXTQ=2", 8), ("VO_XCD=0", 64),
+                                       ("VO_EVENT_WAIT=0,VO_FORCE_WAIT_REFUSAL=1,VO_EXTQ=2", 8)])
 def test_process_knobs_match_oracle(leak_case, tmp_path, env, batch):
     """Knobs the library reads once per process (stencil segment height, RANSAC cut and loop,
     triangulation grid, alternating extract queues, XCD placement), each in a child process on the
-    leak sequence: rows, statuses and counts equal the oracle's."""
+    leak sequence: rows, statuses and counts equal the oracle's.  The last case makes the first
+    stream-wait-value packet count as refused with batches alternating over two extract queues: the
+    passes fall back to each batch's own event, recorded on the queue that batch ran on."""
     import sys
     seq, frames, ref = leak_case
     npz = tmp_path / "case.npz"
     np.savez(npz, W=seq.W, H=seq.H, K=seq.K, gt=seq.gt(), frames=frames,
              st=np.array([r[1] for r in ref]), poses=np.stack([r[0] for r in ref]),
              info=np.stack([r[2][:6] for r in ref]))
-    k, v = env.split("=")
+    kv = dict(e.split("=") for e in env.split(","))
     out = subprocess.run([sys.executable, "-c", _KNOB_SCRIPT, ROOT, str(npz), str(batch)], capture_output=True,
-                         text=True, timeout=240, env={**os.environ, k: v})
+                         text=True, timeout=240, env={**os.environ, **kv})
     assert "KNOB_OK" in out.stdout, (out.stdout[-2000:], out.stderr[-2000:])
+    if "VO_FORCE_WAIT_REFUSAL" in kv:
+        assert "event waits" in out.stderr
