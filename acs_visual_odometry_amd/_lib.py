@@ -19,8 +19,8 @@ STATUS = {0: "OK", 1: "FIRST", 2: "MISSING", 3: "FEW_MATCHES", 4: "FEW_INLIERS",
 # every symbol include/vo_mi355x.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "vo_config_default", "vo_create", "vo_destroy", "vo_strerror", "vo_abi_version", "vo_extract",
-    "vo_response", "vo_match", "vo_ransac_F", "vo_pose", "vo_set_ground_truth", "vo_set_sequence_starts", "vo_set_frame_origin",
-    "vo_trajectory_state", "vo_rechain", "vo_process_frame",
+    "vo_response", "vo_match", "vo_ransac_F", "vo_ransac_run", "vo_fit_F", "vo_pose", "vo_set_ground_truth", "vo_set_sequence_starts", "vo_set_frame_origin",
+    "vo_trajectory_state", "vo_ring_slots", "vo_rechain", "vo_process_frame",
     "vo_process_frames_device", "vo_process_frames_host", "vo_extract_frames_device", "vo_host_alloc", "vo_host_free", "vo_imread_gray", "vo_device_alloc", "vo_device_free", "vo_device_upload", "vo_reset",
     "vo_last_kernel_times", "vo_last_kernel_stats", "vo_enable_kernel_timing", "vo_unpack_descriptor",
 ]
@@ -62,10 +62,14 @@ def load():
     L.vo_ransac_F.argtypes = [P, P, I, C.c_uint64, P, C.POINTER(I), P, C.POINTER(I), C.POINTER(I),
                               C.POINTER(I), P]
     L.vo_pose.argtypes = [P, P, P, P, I, C.c_double, P, P, P]
+    L.vo_ransac_run.argtypes = [P, P, I, C.c_double, C.c_double, I, C.c_uint64, P, C.POINTER(I), P,
+                                C.POINTER(I), C.POINTER(I)]
+    L.vo_fit_F.argtypes = [P, P, I, P]
     L.vo_set_ground_truth.argtypes = [P, P, I]
     L.vo_set_sequence_starts.argtypes = [P, P, I]
     L.vo_set_frame_origin.argtypes = [P, I]
     L.vo_trajectory_state.argtypes = [P, P]
+    L.vo_ring_slots.argtypes = [P]
     L.vo_rechain.argtypes = [P, P, I, I, P]
     L.vo_process_frame.argtypes = [P, P, C.c_size_t, P, C.POINTER(I), P]
     L.vo_process_frames_device.argtypes = [P, P, C.c_size_t, I, P, P, P]
@@ -84,6 +88,7 @@ def load():
     L.vo_unpack_descriptor.argtypes = [P, P]
     L.vo_unpack_descriptor.restype = None
     L.vo_selftest_arith.argtypes = [P, P, P, P, P, P, I, I]
+    L.vo_selftest_nullvec9.argtypes = [P, P, P, P, I, I]
     _lib = L
     return L
 

@@ -68,6 +68,7 @@ struct vo_ctx {
     uint8_t* stage_host = nullptr;    // pinned frame staging
     uint16_t* tab_dev = nullptr;
     double stage_F[9] = {0};          // vo_ransac_F's FundamentalMatrix (persists across calls)
+    std::map<double, uint16_t*> tab_by_p;   // vo_ransac_run: maxIterations tables of other probabilities
     int timing = 0;                   // 0 off, 1 all kernels, 100+k only kernel k
     std::vector<hipEvent_t> ev_pool;
     std::vector<float> ktime_ms;
@@ -755,6 +756,7 @@ void vo_destroy(vo_ctx* c)
     if (c->hstage) (void)hipHostFree(c->hstage);
     if (c->sc) (void)hipStreamDestroy(c->sc);
     if (c->ev_reset) (void)hipEventDestroy(c->ev_reset);
+    for (auto& kv : c->tab_by_p) (void)hipFree(kv.second);
     for (hipStream_t q : c->se)
         if (q) (void)hipStreamDestroy(q);
     if (c->s) (void)hipStreamDestroy(c->s);
@@ -796,6 +798,12 @@ int vo_set_frame_origin(vo_ctx* c, int origin)
     SYNC_ALL(c);
     c->d.origin = origin;
     return VO_OK;
+}
+
+int vo_ring_slots(vo_ctx* c)
+{
+    if (!c) return VO_ERR_ARG;
+    return c->d.ring;
 }
 
 int vo_trajectory_state(vo_ctx* c, double Tcurr[16])
@@ -947,6 +955,79 @@ int vo_ransac_F(vo_ctx* c, const double* pts, int m, uint64_t seed, double F[9],
         HIPCHK(hipMemcpy(inlier_idx, c->d.inl, sizeof(int32_t) * w.n_inl, hipMemcpyDeviceToHost));
     if (counts && w.n_eval > 0)
         HIPCHK(hipMemcpy(counts, c->d.counts, sizeof(int32_t) * std::min(w.n_eval, VO_MAX_HYP), hipMemcpyDeviceToHost));
+    return VO_OK;
+}
+
+int vo_ransac_run(vo_ctx* c, const double* pts, int m, double probability, double sampson_thr, int num_threads,
+                  uint64_t seed, double F[9], int* fitted, int32_t* inlier_idx, int* n_inl, int* n_evaluated)
+{
+    if (!c || !pts || m < 8 || m > c->cfg.max_kpts || num_threads < 1) return VO_ERR_ARG;
+    if (!(probability > 0.0 && probability < 1.0) || !(sampson_thr >= 0.0)) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    // ransac.cpp:129-131: the initial bound for this probability; the hypothesis buffers hold max_hyp
+    VoDev d = c->d;
+    d.maxit_initial = to_int_x86(std::log(1.0 - probability) / std::log(1.0 - std::pow(1.0 - 0.5, 8.0)));
+    if (d.maxit_initial > d.max_hyp) return VO_ERR_CAPACITY;
+    d.sampson_thr = sampson_thr;
+    d.T = num_threads;
+    if (probability != c->cfg.ransac_p) {
+        auto it = c->tab_by_p.find(probability);
+        if (it == c->tab_by_p.end()) {
+            const std::vector<uint16_t>& tab = maxit_table(c->cfg.max_kpts, probability);
+            uint16_t* t = nullptr;
+            HIPCHK(hipMalloc((void**)&t, tab.size() * sizeof(uint16_t)));
+            HIPCHK(hipMemcpy(t, tab.data(), tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+            it = c->tab_by_p.emplace(probability, t).first;
+        }
+        d.maxit_tab = it->second;
+    }
+    SYNC_ALL(c);
+    HIPCHK(hipMemcpy(d.pts, pts, sizeof(double) * 4 * (size_t)m, hipMemcpyHostToDevice));
+    VoWork w;
+    stage_work(&w, d.ring);
+    w.M = m;
+    w.scored = (m / num_threads) * num_threads;        // ransac.cpp:152-157 (quirk 7)
+    w.frame_seed = seed;
+    int rc = write_work0(c, &w);
+    if (rc) return rc;
+    vo::launch_ransac(d, 1, c->s);
+    vo::launch_refit(d, 0, 1, c->s);
+    HIPCHK(hipGetLastError());
+    rc = read_work0(c, &w);
+    if (rc) return rc;
+    if (fitted) *fitted = w.fitted;
+    if (F && w.fitted) std::memcpy(F, w.F, sizeof(w.F));
+    if (n_inl) *n_inl = w.n_inl;
+    if (n_evaluated) *n_evaluated = w.n_eval;
+    if (inlier_idx && w.bestk >= 0 && w.n_inl > 0)
+        HIPCHK(hipMemcpy(inlier_idx, c->d.inl, sizeof(int32_t) * w.n_inl, hipMemcpyDeviceToHost));
+    return VO_OK;
+}
+
+int vo_fit_F(vo_ctx* c, const double* pts, int n, double F[9])
+{
+    if (!c || !pts || !F || n < 8 || n > c->cfg.max_kpts) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    SYNC_ALL(c);
+    HIPCHK(hipMemcpy(c->d.pts, pts, sizeof(double) * 4 * (size_t)n, hipMemcpyHostToDevice));
+    // every point is an inlier of "hypothesis 0" (k_refit compacts the refit set from its mask)
+    std::vector<uint64_t> mask((size_t)c->d.mask_words, 0ull);
+    for (int i = 0; i < n; ++i) mask[(size_t)i >> 6] |= 1ull << (i & 63);
+    HIPCHK(hipMemcpy(c->d.inlmask, mask.data(), sizeof(uint64_t) * mask.size(), hipMemcpyHostToDevice));
+    VoWork w;
+    stage_work(&w, c->d.ring);
+    w.M = n;
+    w.scored = n;
+    w.bestk = 0;
+    w.cold = 1;
+    int rc = write_work0(c, &w);
+    if (rc) return rc;
+    vo::launch_refit(c->d, 0, 1, c->s);
+    HIPCHK(hipGetLastError());
+    rc = read_work0(c, &w);
+    if (rc) return rc;
+    if (!w.fitted) return VO_ERR_STATE;
+    std::memcpy(F, w.F, sizeof(w.F));
     return VO_OK;
 }
 
@@ -1242,6 +1323,28 @@ int vo_device_upload(vo_ctx* c, void* dptr, const void* src, size_t bytes)
     if (!c || !dptr || !src) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
     HIPCHK(hipMemcpy(dptr, src, bytes, hipMemcpyHostToDevice));
+    return VO_OK;
+}
+
+// test hook: the refit's null-vector solver (k_refit's ls_nullvec9_par) on n 9x9 matrices
+int vo_selftest_nullvec9(const double* S, const double* x0, double* f, int32_t* status, int n, int device)
+{
+    if (n <= 0 || !S || !x0 || !f || !status) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(device));
+    double *dS, *dx, *df;
+    int* dst;
+    HIPCHK(hipMalloc((void**)&dS, sizeof(double) * 81 * n));
+    HIPCHK(hipMalloc((void**)&dx, sizeof(double) * 9 * n));
+    HIPCHK(hipMalloc((void**)&df, sizeof(double) * 9 * n));
+    HIPCHK(hipMalloc((void**)&dst, sizeof(int) * n));
+    HIPCHK(hipMemcpy(dS, S, sizeof(double) * 81 * n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dx, x0, sizeof(double) * 9 * n, hipMemcpyHostToDevice));
+    vo::launch_selftest_nullvec9(dS, dx, df, dst, n, nullptr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(f, df, sizeof(double) * 9 * n, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(status, dst, sizeof(int) * n, hipMemcpyDeviceToHost));
+    (void)hipFree(dS); (void)hipFree(dx); (void)hipFree(df); (void)hipFree(dst);
     return VO_OK;
 }
 

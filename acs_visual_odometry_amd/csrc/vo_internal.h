@@ -122,6 +122,8 @@ struct VoWork {
     int32_t fitted;       // refit ran (>= 8 inliers); else the model leaks (quirk 9)
     int32_t n_fit;        // refit inliers (== n_inl when fitted)
     int32_t degenerate;   // getPose would throw on this frame's F (PoseUpdate.hpp:71-73)
+    int32_t nv_status;    // refit null-vector solver: 0 converged, 1 certified after the cap, 2 Jacobi fallback
+    int32_t cold;         // refit from x0 = ones instead of the best hypothesis (vo_fit_F, stage only)
     int32_t counts4[4];   // positive-depth counts per (R, t) candidate
     uint32_t ctr[4];      // in-launch arrival counters: [0] match, [1] ransac chunk 1, [2] chunk 2
     uint64_t frame_seed;
@@ -246,6 +248,7 @@ void launch_traj(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s); 
 void launch_traj_range(const VoDev& d, VoFrameOut* out, int out_base, int lo, int nc, hipStream_t s);   // vo_rechain
 void launch_pose_stage(const VoDev& d, int phase, hipStream_t s);   // vo_pose: 0 prepare, 1 choose
 void launch_reset(const VoDev& d, hipStream_t s);                   // vo_reset's device state
+void launch_selftest_nullvec9(const double* S, const double* x0, double* f, int* status, int n, hipStream_t s);
 void launch_selftest_arith(const float* fa, const float* fb, float* fo, const double* da,
                            const double* db, double* dout, int n, hipStream_t s);
 int kernel_count();

@@ -118,8 +118,13 @@ inline uint8_t to_gray(const uint8_t* row, int x, const PngInfo& p)
     default:   // RGB (2) / RGBA (6)
         r = sample(row, x, 0, p); g = sample(row, x, 1, p); b = sample(row, x, 2, p);
     }
-    // png_do_rgb_to_gray (no gamma): equal channels pass through, else the fixed-point sum
-    uint32_t v = (r == g && g == b) ? r : (9797u * r + 19234u * g + 3737u * b + 16384u) >> 15;
+    // png_do_rgb_to_gray without a gamma table (libpng 1.6 pngrtran.c): equal channels pass
+    // through, else the 15-bit fixed-point sum -- truncated for 8-bit samples ("the historical
+    // approach which simply truncates"), rounded for 16-bit ones, which png_set_strip_16 then
+    // truncates to 8 bits.  A PNG whose gAMA / sRGB chunk makes libpng build gamma tables is
+    // converted through those tables by libpng; that path is not modelled here.
+    const uint32_t sum = 9797u * r + 19234u * g + 3737u * b;
+    const uint32_t v = (r == g && g == b) ? r : (p.depth == 16 ? (sum + 16384u) >> 15 : sum >> 15);
     return (uint8_t)(p.depth == 16 ? v >> 8 : v);
 }
 

@@ -2419,7 +2419,8 @@ __device__ __forceinline__ void scale_t(double* tf, double scale)
 // iteration from the warm start x0.  Called by the whole k_refit workgroup; each wave runs it
 // (wave 1 duplicates wave 0), lanes 0..8 own rows / columns, lanes 0..44 own the upper-
 // triangle entries of the squarings, and every sum runs in the oracle's ascending order.
-// Returns the number of power steps; f (unit) is valid in every lane.
+// Returns the status (0 converged, 1 certified in the null space after the 32-step cap, 2 cyclic-
+// Jacobi fallback; oracle voo_dbg_nullvec_status); f (unit) is valid in every lane.
 __constant__ unsigned char c_tri9[45][2] = {
     {0, 0}, {0, 1}, {0, 2}, {0, 3}, {0, 4}, {0, 5}, {0, 6}, {0, 7}, {0, 8}, {1, 1}, {1, 2}, {1, 3},
     {1, 4}, {1, 5}, {1, 6}, {1, 7}, {1, 8}, {2, 2}, {2, 3}, {2, 4}, {2, 5}, {2, 6}, {2, 7}, {2, 8},
@@ -2449,6 +2450,53 @@ __device__ __forceinline__ void sym_square9(const double* A, double* B, int lane
     for (int k = 0; k < 9; ++k) v = v + (A[i * 9 + k] * r) * (A[k * 9 + j] * r);
     if (lane < 45) { B[i * 9 + j] = v; B[j * 9 + i] = v; }
     __syncthreads();
+}
+
+// smallest eigenvector of the 9x9 symmetric S by cyclic Jacobi (mirror of oracle
+// jacobi_min_eigvec9): one thread, a and v in LDS (a, v: 81 doubles each), f (9) to LDS.  The
+// fallback of ls_nullvec9_par when its power iteration neither converges nor is certified.
+__device__ __noinline__ void jacobi_min_eigvec9(const double* S, const double* x0, double* a, double* v, double* f)
+{
+    for (int i = 0; i < 81; ++i) { a[i] = S[i]; v[i] = (i % 10 == 0) ? 1.0 : 0.0; }
+    for (int sweep = 0; sweep < 64; ++sweep) {
+        int rot = 0;
+        for (int p = 0; p < 8; ++p)
+            for (int q = p + 1; q < 9; ++q) {
+                const double apq = a[p * 9 + q];
+                if (apq == 0.0) continue;
+                if (fabs(apq) <= 1e-18 * (fabs(a[p * 9 + p]) + fabs(a[q * 9 + q]))) {
+                    a[p * 9 + q] = 0.0; a[q * 9 + p] = 0.0;
+                    continue;
+                }
+                ++rot;
+                const double th = (a[q * 9 + q] - a[p * 9 + p]) / (2.0 * apq);
+                double t = 1.0 / (fabs(th) + sqrt(th * th + 1.0));
+                if (th < 0.0) t = -t;
+                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < 9; ++k) {
+                    const double akp = a[k * 9 + p], akq = a[k * 9 + q];
+                    a[k * 9 + p] = c * akp - s * akq;
+                    a[k * 9 + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < 9; ++k) {
+                    const double apk = a[p * 9 + k], aqk = a[q * 9 + k];
+                    a[p * 9 + k] = c * apk - s * aqk;
+                    a[q * 9 + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < 9; ++k) {
+                    const double vkp = v[k * 9 + p], vkq = v[k * 9 + q];
+                    v[k * 9 + p] = c * vkp - s * vkq;
+                    v[k * 9 + q] = s * vkp + c * vkq;
+                }
+            }
+        if (!rot) break;
+    }
+    int k = 0;
+    for (int i = 1; i < 9; ++i) if (a[i * 9 + i] < a[k * 9 + k]) k = i;
+    double dot = 0.0;
+    for (int i = 0; i < 9; ++i) dot = dot + v[i * 9 + k] * x0[i];
+    const double sg = dot < 0.0 ? -1.0 : 1.0;
+    for (int i = 0; i < 9; ++i) f[i] = v[i * 9 + k] * sg;
 }
 
 __device__ int ls_nullvec9_par(const VoDev& d, const double* S, const double* x0, double* f, double* s_L,
@@ -2531,6 +2579,7 @@ __device__ int ls_nullvec9_par(const VoDev& d, const double* S, const double* x0
         for (int i = 0; i < 9; ++i) x[i] = 1.0 / 3.0;
     }
     int it = 0;
+    bool conv = false;
     for (; it < 32; ++it) {
         double zi = 0.0;
 #pragma unroll
@@ -2551,12 +2600,34 @@ __device__ int ls_nullvec9_par(const VoDev& d, const double* S, const double* x0
             if (dd > diff) diff = dd;
             x[i] = xn;
         }
-        if (diff <= 4e-16) { ++it; break; }
+        if (diff <= 4e-16) { ++it; conv = true; break; }
+    }
+    // no convergence in 32 steps (uniform over the workgroup: every lane holds the same iterate):
+    // keep the iterate if its Rayleigh quotient certifies it in S's numerical null space, else
+    // cyclic Jacobi on S by thread 0 in LDS (the oracle's NV_CERTIFIED / NV_JACOBI)
+    int status = 0;
+    if (!conv) {
+        double rq = 0.0;
+        for (int i = 0; i < 9; ++i) {
+            double si = 0.0;
+            for (int j = 0; j < 9; ++j) si = si + S[i * 9 + j] * x[j];
+            rq = rq + x[i] * si;
+        }
+        if (rq <= 64.0 * fl) {
+            status = 1;
+        } else {
+            status = 2;
+            __syncthreads();                    // s_W / s_W2 / s_L are free: W^64 and L were read above
+            if (threadIdx.x == 0) jacobi_min_eigvec9(S, x0, s_W, s_W2, s_L);
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 9; ++i) x[i] = s_L[i];
+        }
     }
 #pragma unroll
     for (int i = 0; i < 9; ++i) f[i] = x[i];
     VO_STAMP(d, 1994, 4);
-    return it;
+    return status;
 }
 
 __device__ __forceinline__ void warm_start(const double* Fb, double s1, double mx1, double my1, double s2,
@@ -2715,16 +2786,20 @@ __global__ void __launch_bounds__(RF_T) k_refit(VoDev d, int with_pose, int stag
         }
         __syncthreads();
         double Fb[9], f0[9], f[9];
-        for (int i = 0; i < 9; ++i) Fb[i] = d.hypF[((size_t)wf * d.max_hyp + bestk) * 9 + i];
         VO_STAMP(d, 1995, 5);
-        warm_start(Fb, sc1, mean[0], mean[1], sc2, mean[2], mean[3], f0);
-        const int its = ls_nullvec9_par(d, s_A, f0, f, &s_part[0][0], &s_part[9][0], &s_part[18][0]);
+        if (w->cold) {             // vo_fit_F: a plain fit, no hypothesis (oracle voo_fit_F's x0)
+#pragma unroll
+            for (int i = 0; i < 9; ++i) f0[i] = 1.0;
+        } else {
+            for (int i = 0; i < 9; ++i) Fb[i] = d.hypF[((size_t)wf * d.max_hyp + bestk) * 9 + i];
+            warm_start(Fb, sc1, mean[0], mean[1], sc2, mean[2], mean[3], f0);
+        }
+        const int nv_status = ls_nullvec9_par(d, s_A, f0, f, &s_part[0][0], &s_part[9][0], &s_part[18][0]);
         if (tid == 0) {
             VO_STAMP(d, 1995, 6);
+            w->nv_status = nv_status;
 #ifdef VO_STAMPS
-            if (d.dbg) { d.dbg[1995 * 16 + 14] = (unsigned long long)its; d.dbg[1995 * 16 + 15] = (unsigned long long)n; }
-#else
-            (void)its;
+            if (d.dbg) d.dbg[1995 * 16 + 15] = (unsigned long long)n;
 #endif
             double Fn[9];
             denormalize(f, sc1, mean[0], mean[1], sc2, mean[2], mean[3], Fn);
@@ -3332,6 +3407,26 @@ __global__ void k_selftest_arith(const float* fa, const float* fb, float* fo, co
     dout[4 * i + 3] = c;
 }
 
+// null-vector solver self-test: ls_nullvec9_par on matrix b of S (one workgroup of RF_T each), as
+// k_refit calls it
+__global__ void __launch_bounds__(RF_T) k_selftest_nullvec9(const double* S, const double* x0, double* f, int* status)
+{
+    __shared__ double s_S[81], s_a[81], s_b[81], s_c[81];
+    const int b = blockIdx.x;
+    for (int i = threadIdx.x; i < 81; i += RF_T) s_S[i] = S[81 * b + i];
+    __syncthreads();
+    double x[9], out[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) x[i] = x0[9 * b + i];
+    VoDev d;
+    d.dbg = nullptr;
+    const int st = ls_nullvec9_par(d, s_S, x, out, s_a, s_b, s_c);
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < 9; ++i) f[9 * b + i] = out[i];
+        status[b] = st;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // launch wrappers
 // ---------------------------------------------------------------------------
@@ -3455,6 +3550,10 @@ void launch_reset(const VoDev& d, hipStream_t s)
 void launch_pose_stage(const VoDev& d, int phase, hipStream_t s)
 {
     hipLaunchKernelGGL(k_pose_stage, dim3(1), dim3(64), 0, s, d, phase);
+}
+void launch_selftest_nullvec9(const double* S, const double* x0, double* f, int* status, int n, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_selftest_nullvec9, dim3(n), dim3(RF_T), 0, s, S, x0, f, status);
 }
 void launch_selftest_arith(const float* fa, const float* fb, float* fo, const double* da, const double* db,
                            double* dout, int n, hipStream_t s)

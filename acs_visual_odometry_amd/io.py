@@ -35,8 +35,12 @@ def write_pgm(path: str, img: np.ndarray) -> None:
         f.write(img.tobytes())
 
 
-# what libstdc++'s num_get accepts for a double (istream >> double)
-_NUM = re.compile(r"[+-]?(?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?")
+# the characters libstdc++'s num_get accumulates for a double (istream >> double): a sign, the
+# mantissa, and -- once the mantissa has a digit -- 'e' / 'E' with an optional sign and digits.  The
+# accumulated token is then converted whole: one that is not a complete number ("1e", "1e+", ".")
+# stores 0 and fails the stream.
+_MANT = re.compile(r"[+-]?(?:\d+\.?\d*|\.\d+)")
+_EXP = re.compile(r"[eE][+-]?(\d*)")
 _EYE34 = (1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0)
 
 
@@ -51,12 +55,19 @@ def read_gt_line(line: str) -> np.ndarray:
             pos += 1
         if pos >= n:
             break
-        m = _NUM.match(line, pos)
+        m = _MANT.match(line, pos)
         if not m:
             T[i] = 0.0
             break
-        T[i] = float(m.group(0))
-        pos = m.end()
+        end = m.end()
+        e = _EXP.match(line, end)
+        if e:
+            if not e.group(1):                # "1e", "1e+": the whole token is not a number
+                T[i] = 0.0
+                break
+            end = e.end()
+        T[i] = float(line[pos:end])
+        pos = end
     return np.array(T, dtype=np.float64)
 
 
@@ -64,8 +75,14 @@ def read_kitti_poses(path: str) -> np.ndarray:
     """One 3x4 row-major pose per getline, blank or short lines included, exactly as
     VisualOdometry.cpp:50-52 pushes readGTLine(line) for every line (so the GT index of frame i
     stays line i)."""
-    with open(path, newline=None) as f:
-        rows = [read_gt_line(line.rstrip("\n")) for line in f]
+    # std::getline splits on '\n' only (a lone '\r' stays in the line, where >> skips it as space);
+    # text after the last '\n' is one more line, an empty remainder is none
+    with open(path, "r", newline="") as f:
+        text = f.read()
+    lines = text.split("\n")
+    if lines and lines[-1] == "":
+        lines.pop()
+    rows = [read_gt_line(line) for line in lines]
     return np.array(rows, dtype=np.float64).reshape(-1, 12)
 
 

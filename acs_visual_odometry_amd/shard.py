@@ -138,38 +138,89 @@ def _resolve(parts, flags, nframes, rerun):
     return starts
 
 
+class ShardError(RuntimeError):
+    """Raised on every rank when one rank's engine failed (or a shard cannot be chained), so no
+    rank is left blocked in a collective or a recv."""
+
+
+def _capacity(engine) -> Optional[int]:
+    cap = getattr(engine, "capacity", None)
+    return cap() if cap is not None else None
+
+
+def check_capacity(parts, caps) -> None:
+    """vo_rechain chains a shard's frames from trajectory records that must still be resident:
+    a shard longer than its engine's record ring cannot be handed its T_curr."""
+    for q, ((a, b), cap) in enumerate(zip(parts, caps)):
+        if cap is not None and b - a > cap:
+            raise ShardError(f"shard {q} holds {b - a} frames, more than its engine keeps for vo_rechain ({cap}); "
+                             f"use more shards or a larger ring (VO_RING_SLOTS)")
+
+
+def _poison_T():
+    T = np.full((4, 4), np.nan)
+    return T
+
+
 def run_shard(engine, comm, nframes: int, halo: int = DEFAULT_HALO) -> ShardResult:
-    """This rank's shard of one sequence (comm: rank, world, allgather, broadcast, send, recv)."""
+    """This rank's shard of one sequence (comm: rank, world, allgather, broadcast, send, recv).
+    A failure on any rank -- a capacity check, an engine error in the halo run, the second run or
+    the re-chain -- raises ShardError on every rank: the failing rank's error travels in the flag
+    exchange, the second-run broadcast or (as a NaN T_curr) the hand-over."""
     r, G = comm.rank, comm.world
     parts = partition(nframes, G)
     a, b = parts[r]
-    s, out = halo_run(engine, a, b, halo) if b > a else (max(0, a - halo), None)
+    check_capacity(parts, comm.allgather(_capacity(engine)))      # every rank raises together
+    err = None
+    try:
+        s, out = halo_run(engine, a, b, halo) if b > a else (max(0, a - halo), None)
+    except Exception as e:                                        # noqa: BLE001 -- re-raised on every rank
+        s, out, err = max(0, a - halo), None, f"rank {r}: halo run failed: {e!r}"
     mine = (s, out[1], out[2][:, 5]) if out is not None else (s, np.zeros(0, np.int32), np.zeros(0, np.int32))
-    flags = comm.allgather(mine)
+    flags = comm.allgather(mine + (err,))
+    errs = [f[3] for f in flags if f[3]]
+    if errs:
+        raise ShardError("; ".join(errs))
+    flags = [f[:3] for f in flags]
     runs = [1]
 
     def rerun(q, s2):
         nonlocal out
         payload = None
         if q == r:
-            out = engine.run(s2, b)
-            runs[0] = 2
-            payload = (s2, out[1], out[2][:, 5])
-        return comm.broadcast(payload, q)
+            try:
+                out = engine.run(s2, b)
+                runs[0] = 2
+                payload = (s2, out[1], out[2][:, 5], None)
+            except Exception as e:                                # noqa: BLE001
+                payload = (s2, None, None, f"rank {r}: second run from frame {s2} failed: {e!r}")
+        got = comm.broadcast(payload, q)
+        if got[3]:
+            raise ShardError(got[3])
+        return got[:3]
 
     starts = _resolve(parts, flags, nframes, rerun)
     s = starts[r]
-    # step 3: T_curr in rank order
+    # step 3: T_curr in rank order; a rank that cannot chain passes a NaN T_curr on, so every later
+    # rank raises instead of waiting
     T = None
+    failed = None
     if r > 0:
         T = comm.recv(r - 1)
-    if b > a:
+        if not np.isfinite(np.asarray(T, np.float64)).all():
+            failed = "an earlier rank failed to chain its shard"
+    if b > a and failed is None:
         poses = out[0][a - s:]
-        if r > 0:
-            poses = engine.rechain(T, a - s, b - a)
-        T = engine.trajectory_state()
+        try:
+            if r > 0:
+                poses = engine.rechain(T, a - s, b - a)
+            T = engine.trajectory_state()
+        except Exception as e:                                    # noqa: BLE001
+            failed = f"rank {r}: re-chain failed: {e!r}"
     if r < G - 1:
-        comm.send(T, r + 1)
+        comm.send(_poison_T() if failed else T, r + 1)
+    if failed:
+        raise ShardError(failed)
     if b <= a:
         return ShardResult(a, b, np.zeros((0, 3, 4)), np.zeros(0, np.int32), np.zeros((0, 8), np.int32), s, runs[0])
     return ShardResult(a, b, poses, out[1][a - s:], out[2][a - s:], s, runs[0])
@@ -180,6 +231,7 @@ def run_local(engines: Sequence, nframes: int, halo: int = DEFAULT_HALO) -> List
     contexts on one GPU): the same steps in the order the ranks would reach them."""
     G = len(engines)
     parts = partition(nframes, G)
+    check_capacity(parts, [_capacity(e) for e in engines])
     outs, flags = [], []
     for r, (a, b) in enumerate(parts):
         s, o = halo_run(engines[r], a, b, halo) if b > a else (max(0, a - halo), None)
@@ -244,6 +296,10 @@ class ContextEngine:
 
     def rechain(self, T_in, f0: int, n: int):
         return self.ctx.rechain(T_in, f0, n)
+
+    def capacity(self) -> int:
+        """Frames whose trajectory records stay resident for rechain (the context's ring)."""
+        return self.ctx.ring_slots()
 
     def trajectory_state(self):
         return self.ctx.trajectory_state()

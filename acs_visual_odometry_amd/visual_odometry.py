@@ -90,6 +90,27 @@ class Context:
                     n_evaluated=ne, counts=counts[:min(ne, 2000)].copy(),
                     inliers=inl[:n_inl.value].copy() if best_k.value >= 0 else np.zeros(0, np.int32))
 
+    def ransac_run(self, pts: np.ndarray, probability: float = 0.99, sampson_thr: float = 1.0,
+                   num_threads: int = 8, seed: int = 0):
+        """Ransac::run with the call's own parameters (vo_ransac_run): F is None when the model was
+        not refit (fewer than 8 inliers: the caller's previous model stays, quirk 9)."""
+        pts = np.ascontiguousarray(pts, dtype=np.float64).reshape(-1, 4)
+        m = pts.shape[0]
+        F = np.zeros(9)
+        inl = np.zeros(max(m, 1), np.int32)
+        fitted, n_inl, n_eval = C.c_int(), C.c_int(), C.c_int()
+        check(self.lib.vo_ransac_run(self.h, _p(pts), m, probability, sampson_thr, num_threads, seed, _p(F),
+                                     C.byref(fitted), _p(inl), C.byref(n_inl), C.byref(n_eval)), "vo_ransac_run")
+        return dict(F=F.reshape(3, 3) if fitted.value else None, fitted=fitted.value, n_inl=n_inl.value,
+                    n_evaluated=n_eval.value, inliers=inl[:n_inl.value].copy())
+
+    def fit_F(self, pts: np.ndarray) -> np.ndarray:
+        """FundamentalMatrix::fit / computeFundamentalMatrix on all n >= 8 correspondences (vo_fit_F)."""
+        pts = np.ascontiguousarray(pts, dtype=np.float64).reshape(-1, 4)
+        F = np.zeros(9)
+        check(self.lib.vo_fit_F(self.h, _p(pts), pts.shape[0], _p(F)), "vo_fit_F")
+        return F.reshape(3, 3)
+
     def pose(self, F, p1, p2, scale: float = 1.0):
         F = np.ascontiguousarray(F, dtype=np.float64).reshape(9)
         p1 = np.ascontiguousarray(p1, dtype=np.float32).reshape(-1, 2)
@@ -134,6 +155,10 @@ class Context:
 
     def reset(self):
         check(self.lib.vo_reset(self.h), "vo_reset")
+
+    def ring_slots(self) -> int:
+        """Frames whose keypoints, descriptors and trajectory records stay resident (vo_ring_slots)."""
+        return check(self.lib.vo_ring_slots(self.h), "vo_ring_slots")
 
     def process_frame(self, gray: Optional[np.ndarray]):
         pose = np.zeros(12)
@@ -360,6 +385,8 @@ class VisualOdometry:
                         raise RuntimeError(f"image size differs from frame 0: {path(i0 + e)}")
                     e += 1
                 poses, st, _ = self.ctx.process_frames_host(np.stack(imgs[z:e]))
+                for k in np.flatnonzero(st == 3):          # VisualOdometry.cpp:108-109
+                    print(f"Too few matches at frame {i0 + z + int(k)}", file=sys.stderr)
                 if (st == 5).any():
                     raise RuntimeError("Degenerate essential matrix")
                 rows.extend(poses)

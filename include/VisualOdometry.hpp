@@ -8,11 +8,13 @@
 #pragma once
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <fstream>
 #include <iomanip>
 #include <iostream>
+#include <mutex>
 #include <sstream>
 #include <stdexcept>
 #include <string>
@@ -40,6 +42,166 @@ inline void check(int rc, const char* what)
     if (rc < 0) throw std::runtime_error(std::string(what) + ": " + vo_strerror(rc));
 }
 
+// -- the reference's stage types, OpenCV / Eigen replaced by plain ones -------------------------
+struct Point { double x, y; };                     // ransac.hpp:14-16
+struct Point2f { float x, y; };                    // cv::Point2f (PoseUpdate::getPose's points)
+struct Matrix3d {                                  // Eigen::Matrix3d / cv::Mat 3x3 CV_64F, row-major
+    double a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    double& operator()(int r, int c) { return a[3 * r + c]; }
+    double operator()(int r, int c) const { return a[3 * r + c]; }
+};
+struct Vec3d {                                     // cv::Mat 3x1 CV_64F (getPose's t)
+    double a[3] = {0, 0, 0};
+    double& operator()(int r) { return a[r]; }
+    double operator()(int r) const { return a[r]; }
+};
+
+// The execution resource of the stage calls: the reference's thread_pool VO_pool
+// (VisualOdometry.h:17), which Ransac::run takes, becomes the GPU context.  It also draws the
+// RANSAC sampler seed of each Ransac::run call, which replaces std::random_device
+// (ransac.cpp:137): call k uses frame_seed(seed, k), the seed frame k of a trajectory uses.
+class DevicePool {
+public:
+    explicit DevicePool(vo_ctx* ctx = nullptr, uint64_t seed = 0xACE0ULL) : seed(seed), ctx_(ctx) {}
+    vo_ctx* handle() const { return ctx_; }
+    void bind(vo_ctx* ctx) { ctx_ = ctx; }
+    uint64_t next_seed() { return frame_seed(seed, calls++); }
+    static uint64_t frame_seed(uint64_t s, int64_t k)       // splitmix64 finaliser (oracle voo_frame_seed)
+    {
+        uint64_t z = s + 0x632BE59BD9B4E019ULL * (uint64_t)(k + 1);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        return z ^ (z >> 31);
+    }
+    uint64_t seed;
+    int64_t calls = 0;
+
+private:
+    vo_ctx* ctx_;
+};
+using thread_pool = DevicePool;
+
+namespace detail {
+// a process-wide context for stage objects built without one (FundamentalMatrix::fit and a
+// default-constructed PoseUpdate, as the reference constructs them); created on first use
+inline vo_ctx* default_ctx()
+{
+    static std::mutex mu;
+    static vo_ctx* ctx = nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!ctx) {
+        vo_config c;
+        vo_config_default(&c, 1241, 376);
+        c.max_kpts = 4096;
+        check(vo_create(&c, &ctx), "vo_create");
+    }
+    return ctx;
+}
+inline std::vector<double> xyxy(const std::vector<std::pair<Point, Point>>& d)
+{
+    std::vector<double> v(d.size() * 4);
+    for (size_t i = 0; i < d.size(); ++i) {
+        v[4 * i] = d[i].first.x; v[4 * i + 1] = d[i].first.y;
+        v[4 * i + 2] = d[i].second.x; v[4 * i + 3] = d[i].second.y;
+    }
+    return v;
+}
+}  // namespace detail
+
+// FundamentalMatrix (ransac.hpp:18-34): the model Ransac::run refits; it keeps its F and inliers
+// when a fit is refused (< 8 points, ransac.cpp:95-99), which is the reference's model leak across
+// frames (quirk 9).
+class FundamentalMatrix {
+public:
+    // ransac.cpp:95-99: computeFundamentalMatrix on all points (normalized least squares, rank 2)
+    void fit(const std::vector<std::pair<Point, Point>>& sample)
+    {
+        if (sample.size() < 8) return;
+        const std::vector<double> p = detail::xyxy(sample);
+        vo_ctx* ctx = ctx_ ? ctx_ : detail::default_ctx();
+        check(vo_fit_F(ctx, p.data(), (int)sample.size(), F_.a), "vo_fit_F");
+        inliers_ = sample;
+    }
+    Matrix3d getMatrix() const { return F_; }
+    const std::vector<std::pair<Point, Point>>& getInliers() const { return inliers_; }
+    // ransac.cpp:105-114 (unused by the reference's loop): |x2^T F x1| < threshold
+    int countInliers(const std::vector<std::pair<Point, Point>>& data, double threshold) const
+    {
+        int n = 0;
+        for (const auto& pr : data) {
+            const double x = pr.first.x, y = pr.first.y, xp = pr.second.x, yp = pr.second.y;
+            const double e = xp * (F_(0, 0) * x + F_(0, 1) * y + F_(0, 2)) + yp * (F_(1, 0) * x + F_(1, 1) * y + F_(1, 2)) +
+                             (F_(2, 0) * x + F_(2, 1) * y + F_(2, 2));
+            n += std::abs(e) < threshold;
+        }
+        return n;
+    }
+    void bind(vo_ctx* ctx) { ctx_ = ctx; }
+
+private:
+    friend class Ransac;
+    Matrix3d F_;
+    std::vector<std::pair<Point, Point>> inliers_;
+    vo_ctx* ctx_ = nullptr;
+};
+
+// Ransac::run (ransac.hpp:40-48, ransac.cpp:120-194) on the pool's GPU: every hypothesis, the
+// chunk drop of numThreads chunks (quirk 7), the adaptive stop (quirk 8), then model.fit on the best
+// hypothesis' inliers (in data order; the reference's order is its mutex's) -- kept from the
+// previous call when fewer than 8 (quirk 9).
+class Ransac {
+public:
+    void run(FundamentalMatrix& model, const std::vector<std::pair<Point, Point>>& data, double probability,
+             double sampsonThreshold, int numThreads, thread_pool& pool)
+    {
+        const uint64_t seed = pool.next_seed();
+        if (data.size() < 8) return;              // std::sample of < 8 points: fit() refuses every sample
+        const std::vector<double> p = detail::xyxy(data);
+        std::vector<int32_t> inl(data.size());
+        Matrix3d F;
+        int fitted = 0, n_inl = 0, n_eval = 0;
+        check(vo_ransac_run(pool.handle(), p.data(), (int)data.size(), probability, sampsonThreshold, numThreads, seed,
+                            F.a, &fitted, inl.data(), &n_inl, &n_eval),
+              "vo_ransac_run");
+        last_iterations = n_eval;
+        if (!fitted) return;
+        model.F_ = F;
+        model.inliers_.clear();
+        for (int k = 0; k < n_inl; ++k) model.inliers_.push_back(data[(size_t)inl[k]]);
+    }
+    int last_iterations = 0;                      // hypotheses evaluated by the last run
+};
+
+// PoseUpdate::getPose (PoseUpdate.hpp:61-179) on the GPU: E = K^T F K, SVD, the four (R, t)
+// candidates by triangulation and cheirality, first maximum, t scaled to GT_pos_norm.  Throws
+// std::runtime_error("Degenerate essential matrix") where the reference throws (:71-73), and prints
+// its stderr warning when fewer than 100 points have positive depth (:149-152).
+class PoseUpdate {
+public:
+    PoseUpdate() = default;
+    explicit PoseUpdate(thread_pool& pool) : ctx_(pool.handle()) {}
+    std::pair<Matrix3d, Vec3d> getPose(const Matrix3d& F, const std::vector<Point2f>& points1,
+                                       const std::vector<Point2f>& points2, double GT_pos_norm)
+    {
+        if (points1.size() != points2.size()) throw std::invalid_argument("getPose: point counts differ");
+        vo_ctx* ctx = ctx_ ? ctx_ : detail::default_ctx();
+        std::vector<float> a(2 * points1.size()), b(2 * points2.size());
+        for (size_t i = 0; i < points1.size(); ++i) {
+            a[2 * i] = points1[i].x; a[2 * i + 1] = points1[i].y;
+            b[2 * i] = points2[i].x; b[2 * i + 1] = points2[i].y;
+        }
+        std::pair<Matrix3d, Vec3d> out;
+        int32_t counts[4] = {0, 0, 0, 0};
+        check(vo_pose(ctx, F.a, a.data(), b.data(), (int)points1.size(), GT_pos_norm, out.first.a, out.second.a, counts),
+              "vo_pose");
+        if (*std::max_element(counts, counts + 4) < 100) std::cerr << "Max positive depth too small\n";
+        return out;
+    }
+
+private:
+    vo_ctx* ctx_ = nullptr;
+};
+
 class VisualOdometry {
 public:
     // VisualOdometry(kernel_filename, num_threads) (VisualOdometry.h:23).  The HIP code
@@ -54,6 +216,7 @@ public:
         cfg_.device = device;
         check(vo_create(&cfg_, &ctx_), "vo_create");
         max_kpts_ = cfg_.max_kpts;
+        VO_pool.bind(ctx_);
     }
     ~VisualOdometry() { vo_destroy(ctx_); }
     VisualOdometry(const VisualOdometry&) = delete;
@@ -146,6 +309,7 @@ public:
                 vo_destroy(ctx_);
                 ctx_ = nc;
                 cfg_ = c;
+                VO_pool.bind(ctx_);
             }
         }
         check(vo_reset(ctx_), "vo_reset");
@@ -192,8 +356,11 @@ public:
                     check(vo_process_frames_host(ctx_, buf + z * np, np, (int)(e - z), poses.data(), status.data(),
                                                  nullptr),
                           "vo_process_frames_host");
-                    for (std::size_t k = 0; k < e - z; ++k)
+                    for (std::size_t k = 0; k < e - z; ++k) {
+                        if (status[k] == VO_STATUS_FEW_MATCHES)          // VisualOdometry.cpp:108-109
+                            std::cerr << "Too few matches at frame " << (i0 + z + k) << "\n";
                         if (status[k] == VO_STATUS_DEGENERATE) throw std::runtime_error("Degenerate essential matrix");
+                    }
                     rows.insert(rows.end(), poses.begin(), poses.end());
                     z = e;
                 }
@@ -235,6 +402,9 @@ public:
     }
 
     vo_ctx* handle() { return ctx_; }
+    // the stage objects' execution resource (the reference's VO_pool, VisualOdometry.h:17)
+    thread_pool& pool() { return VO_pool; }
+    std::size_t threads() const { return number_of_threads_; }
 
 private:
     static std::vector<uint64_t> pack(const std::vector<std::vector<uint8_t>>& d)
@@ -251,6 +421,7 @@ private:
     vo_config cfg_;
     vo_ctx* ctx_ = nullptr;
     int max_kpts_ = 2000;
+    thread_pool VO_pool;
 };
 
 }  // namespace vo_mi355x

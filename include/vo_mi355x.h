@@ -107,6 +107,21 @@ int  vo_ransac_F(vo_ctx* ctx, const double* pts, int m, uint64_t seed, double F[
                  int* fitted, int32_t* inlier_idx, int* n_inl, int* best_k, int* n_evaluated,
                  int32_t* counts);
 
+/* Ransac::run(model, data, probability, sampsonThreshold, numThreads, pool)  ransac.hpp:42-47,
+ * ransac.cpp:120-194, with the call's own parameters: pts m x (x1,y1,x2,y2) (m >= 8; the reference
+ * is undefined below 8), the chunk drop of num_threads chunks (quirk 7), the sampler seed of this
+ * call.  *fitted = 1: model.fit(bestInlierSet) ran (>= 8 inliers) and F is its F; 0: the model
+ * keeps its previous F and inliers (quirk 9; F untouched).  inlier_idx (optional, m entries): the
+ * best hypothesis' inliers in data order.  VO_ERR_CAPACITY if the probability's initial
+ * iteration bound exceeds the context's 2000 hypothesis slots. */
+int  vo_ransac_run(vo_ctx* ctx, const double* pts, int m, double probability, double sampson_thr,
+                   int num_threads, uint64_t seed, double F[9], int* fitted, int32_t* inlier_idx,
+                   int* n_inl, int* n_evaluated);
+
+/* FundamentalMatrix::fit(sample) -> computeFundamentalMatrix  ransac.cpp:63-99: normalized
+ * least-squares F of all n >= 8 correspondences (pts n x (x1,y1,x2,y2)), rank 2 enforced. */
+int  vo_fit_F(vo_ctx* ctx, const double* pts, int n, double F[9]);
+
 /* PoseUpdate::getPose(F, points1, points2, scale)  PoseUpdate.hpp:61-62.
  * p1/p2: n x 2 f32.  counts4 (optional): positive-depth count per candidate
  * {R1,t},{R1,-t},{R2,t},{R2,-t}.  Returns VO_ERR_DEGENERATE_E where the reference throws. */
@@ -132,6 +147,10 @@ int  vo_set_sequence_starts(vo_ctx* ctx, const int32_t* starts, int n);
  * sampler of the stream's first sequence counts frames from origin, so every frame draws the
  * hypotheses it draws in the unsplit run.  Kept across vo_reset; 0 = an ordinary stream. */
 int  vo_set_frame_origin(vo_ctx* ctx, int origin);
+/* Frames whose keypoints, descriptors and trajectory records stay resident on the device (the
+ * ring: 4096 by default, VO_RING_SLOTS): vo_rechain reaches back this far, so a shard may hold at
+ * most this many frames.  Returns the count (> 0) or an error code. */
+int  vo_ring_slots(vo_ctx* ctx);
 /* T_curr after the last committed frame (VisualOdometry.cpp:184, 4x4 row-major). */
 int  vo_trajectory_state(vo_ctx* ctx, double Tcurr[16]);
 /* The trajectory chain (VisualOdometry.cpp:161-186) of committed frames [f0, f0 + n) (counted since

@@ -67,6 +67,8 @@ def lib():
         L.voo_match.argtypes = [P, C.c_int, P, C.c_int, C.c_int, C.c_float, P]
         L.voo_fit_F.argtypes = [P, P, C.c_int, P]
         L.voo_fit_F8.argtypes = [P, P, P]
+        L.voo_ls_nullvec9.argtypes = [P, P, P]
+        L.voo_refit_normal.argtypes = [P, P, C.c_int, P]
         L.voo_sampson.restype = C.c_double
         L.voo_sampson.argtypes = [P, P]
         L.voo_ransac.argtypes = [P, C.c_int, C.c_double, C.c_double, C.c_int, C.c_uint64, P, P,
@@ -196,6 +198,25 @@ def fit_F(pts, idx):
     rc = lib().voo_fit_F(_p(pts), _p(idx), len(idx), _p(F))
     assert rc == 0
     return F.reshape(3, 3)
+
+
+def ls_nullvec9(S, x0):
+    """The refit's null-vector solver on a 9x9 PSD S (oracle ls_nullvec9): (f, status), status 0
+    converged, 1 certified in the null space after the 32-step cap, 2 cyclic-Jacobi fallback."""
+    S = np.ascontiguousarray(S, dtype=np.float64).reshape(81)
+    x0 = np.ascontiguousarray(x0, dtype=np.float64).reshape(9)
+    f = np.empty(9)
+    st = lib().voo_ls_nullvec9(_p(S), _p(x0), _p(f))
+    return f, st
+
+
+def refit_normal(pts):
+    """The refit's normal matrix A^T A over all rows of pts (n x 4), in the refit's sum order."""
+    pts = np.ascontiguousarray(pts, dtype=np.float64).reshape(-1, 4)
+    idx = np.arange(pts.shape[0], dtype=np.int32)
+    S = np.empty(81)
+    assert lib().voo_refit_normal(_p(pts), _p(idx), pts.shape[0], _p(S)) == 0
+    return S.reshape(9, 9)
 
 
 def sampson(F, p):

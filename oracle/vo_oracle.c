@@ -188,10 +188,18 @@ static void mtm3(const double* A, const double* B, double* C);
  *      power first scaled by the power of two that brings its largest diagonal entry into
  *      [0.5, 1) (exact; eigenvectors unchanged);
  *   3. power iteration x <- W64 x / |W64 x| (sign kept towards x) from the warm start x0 until
- *      the unit iterate moves by <= 4e-16 (at most 32 steps; one step = 64 inverse iterations).
+ *      the unit iterate moves by <= 4e-16 (at most 32 steps; one step = 64 inverse iterations);
+ *   4. no convergence: keep x if its Rayleigh quotient certifies it in S's numerical null space,
+ *      else cyclic Jacobi on S (voo_dbg_nullvec_status says which).
  * Every entry's sum runs in ascending index order; k_refit computes the same entries lane-
  * parallel in that order, so the two agree bit for bit. */
 int voo_dbg_nullvec_iters;
+#define NV_CONVERGED 0      /* the power iterate moved by <= 4e-16 */
+#define NV_CERTIFIED 1      /* 32 steps, iterate's Rayleigh quotient at the Cholesky floor: in the null space */
+#define NV_JACOBI 2         /* 32 steps, above the floor: cyclic Jacobi fallback */
+int voo_dbg_nullvec_status;
+double voo_dbg_refit_f[9];
+static double* voo_dbg_capture_normal;   /* voo_refit_normal: where the refit copies A^T A */   /* test hook: the last refit's normalized null vector (before denormalization) */
 /* power of two r with max_i W_ii * r in [0.5, 1): W is symmetric PSD, so |W_ij| <= max_i W_ii,
  * and scaling by r is exact (the squarings only need it to keep clear of overflow) */
 static double pow2_scale9(const double* W)
@@ -211,6 +219,68 @@ static void sym_square9(const double* A, double r, double* B)   /* B = (rA)(rA),
             B[i * 9 + j] = v; B[j * 9 + i] = v;
         }
 }
+/* x^T S x, sums in ascending index order (x unit) */
+static double nv_rayleigh9(const double* S, const double* x)
+{
+    double rq = 0.0;
+    for (int i = 0; i < 9; ++i) {
+        double si = 0.0;
+        for (int j = 0; j < 9; ++j) si = si + S[i * 9 + j] * x[j];
+        rq = rq + x[i] * si;
+    }
+    return rq;
+}
+
+/* Smallest eigenvector of the 9x9 symmetric S by cyclic Jacobi (the classic rotation
+ * t = sgn(th) / (|th| + sqrt(th^2 + 1)), th = (a_qq - a_pp) / (2 a_pq); pairs p < q in row order;
+ * an off-diagonal entry at or below 1e-18 of the diagonal's magnitude is set to zero; at most 64
+ * sweeps, ending at the first sweep that finds every off-diagonal entry zero).  The eigenvector of
+ * the first smallest diagonal entry, signed towards x0 (the warm start). */
+static void jacobi_min_eigvec9(const double* S, const double* x0, double* f)
+{
+    double a[81], v[81];
+    for (int i = 0; i < 81; ++i) { a[i] = S[i]; v[i] = (i % 10 == 0) ? 1.0 : 0.0; }
+    for (int sweep = 0; sweep < 64; ++sweep) {
+        int rot = 0;
+        for (int p = 0; p < 8; ++p)
+            for (int q = p + 1; q < 9; ++q) {
+                double apq = a[p * 9 + q];
+                if (apq == 0.0) continue;
+                if (fabs(apq) <= 1e-18 * (fabs(a[p * 9 + p]) + fabs(a[q * 9 + q]))) {
+                    a[p * 9 + q] = 0.0; a[q * 9 + p] = 0.0;
+                    continue;
+                }
+                ++rot;
+                double th = (a[q * 9 + q] - a[p * 9 + p]) / (2.0 * apq);
+                double t = 1.0 / (fabs(th) + sqrt(th * th + 1.0));
+                if (th < 0.0) t = -t;
+                double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < 9; ++k) {            /* columns p, q */
+                    double akp = a[k * 9 + p], akq = a[k * 9 + q];
+                    a[k * 9 + p] = c * akp - s * akq;
+                    a[k * 9 + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < 9; ++k) {            /* rows p, q */
+                    double apk = a[p * 9 + k], aqk = a[q * 9 + k];
+                    a[p * 9 + k] = c * apk - s * aqk;
+                    a[q * 9 + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < 9; ++k) {
+                    double vkp = v[k * 9 + p], vkq = v[k * 9 + q];
+                    v[k * 9 + p] = c * vkp - s * vkq;
+                    v[k * 9 + q] = s * vkp + c * vkq;
+                }
+            }
+        if (!rot) break;
+    }
+    int k = 0;
+    for (int i = 1; i < 9; ++i) if (a[i * 9 + i] < a[k * 9 + k]) k = i;
+    double dot = 0.0;
+    for (int i = 0; i < 9; ++i) dot = dot + v[i * 9 + k] * x0[i];
+    double sg = dot < 0.0 ? -1.0 : 1.0;
+    for (int i = 0; i < 9; ++i) f[i] = v[i * 9 + k] * sg;
+}
+
 static void ls_nullvec9(const double* S, const double* x0, double* f)
 {
     double L[81], invd[9], Li[81], W[81], W2[81];
@@ -257,7 +327,7 @@ static void ls_nullvec9(const double* S, const double* x0, double* f)
     n0 = sqrt(n0);
     if (n0 > 0.0 && n0 < 1e300) { for (int i = 0; i < 9; ++i) x[i] = x0[i] / n0; }
     else { for (int i = 0; i < 9; ++i) x[i] = 1.0 / 3.0; }
-    int it = 0;
+    int it = 0, conv = 0;
     for (; it < 32; ++it) {
         double z[9];
         for (int i = 0; i < 9; ++i) {
@@ -276,10 +346,27 @@ static void ls_nullvec9(const double* S, const double* x0, double* f)
             if (dd > diff) diff = dd;
             x[i] = xn;
         }
-        if (diff <= 4e-16) { ++it; break; }
+        if (diff <= 4e-16) { ++it; conv = 1; break; }
     }
     voo_dbg_nullvec_iters = it;
+    voo_dbg_nullvec_status = NV_CONVERGED;
+    if (!conv) {
+        /* No convergence in 32 steps (2048 inverse iterations): the two smallest eigenvalues of S
+         * are within a factor ~1 - 1e-5.  If the iterate's Rayleigh quotient is at the Cholesky floor,
+         * it lies in S's numerical null space (several directions below the floor: a degenerate set,
+         * where any null vector is as good as JacobiSVD's pick) and is kept; otherwise the smallest
+         * eigenvector comes from cyclic Jacobi on S. */
+        if (nv_rayleigh9(S, x) <= 64.0 * fl) voo_dbg_nullvec_status = NV_CERTIFIED;
+        else { jacobi_min_eigvec9(S, x0, x); voo_dbg_nullvec_status = NV_JACOBI; }
+    }
     for (int i = 0; i < 9; ++i) f[i] = x[i];
+}
+
+/* test hook: ls_nullvec9 on a given S; returns the status (NV_*) */
+int voo_ls_nullvec9(const double* S, const double* x0, double* f)
+{
+    ls_nullvec9(S, x0, f);
+    return voo_dbg_nullvec_status;
 }
 
 /* warm start for ls_nullvec9: the best hypothesis' F mapped into the refit's normalized
@@ -845,13 +932,26 @@ int voo_fit_F_warm(const double* pts, const int32_t* idx, int n, const double* F
                 AtA[u * 9 + v] = x; AtA[v * 9 + u] = x;
             }
     }
+    if (voo_dbg_capture_normal) memcpy(voo_dbg_capture_normal, AtA, sizeof(AtA));
     double f0[9], f[9];
     if (Fb) warm_start(Fb, sc1, mean[0], mean[1], sc2, mean[2], mean[3], f0);
     else for (int i = 0; i < 9; ++i) f0[i] = 1.0;
     ls_nullvec9(AtA, f0, f);
+    memcpy(voo_dbg_refit_f, f, sizeof(f));
     denormalize(f, sc1, mean[0], mean[1], sc2, mean[2], mean[3], F);
     rank2(F);
     return 0;
+}
+
+/* test hook: the refit's normal matrix A^T A (voo_fit_F_warm's 45 sums, in its order) */
+int voo_refit_normal(const double* pts, const int32_t* idx, int n, double AtA_out[81])
+{
+    if (n < 8) return -1;
+    voo_dbg_capture_normal = AtA_out;
+    double F[9];
+    int rc = voo_fit_F_warm(pts, idx, n, NULL, F);
+    voo_dbg_capture_normal = NULL;
+    return rc;
 }
 
 /* Ransac::run, ransac.cpp:120-194, with the sampler of voo_sample8 and the chunk drop of

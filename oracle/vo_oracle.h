@@ -87,6 +87,11 @@ typedef struct {
 
 int  voo_fit_F(const double* pts, const int32_t* idx, int n, double F[9]);
 int  voo_fit_F_warm(const double* pts, const int32_t* idx, int n, const double* Fb, double F[9]);
+/* the refit's least-squares null vector of a 9x9 PSD S from warm start x0; returns 0 converged,
+ * 1 certified in the numerical null space after 32 power steps, 2 cyclic-Jacobi fallback */
+int  voo_ls_nullvec9(const double* S, const double* x0, double* f);
+/* the refit's normal matrix A^T A of inliers idx (its fixed summation order) */
+int  voo_refit_normal(const double* pts, const int32_t* idx, int n, double AtA_out[81]);
 int  voo_fit_F8(const double* pts, const int32_t idx[8], double F[9]);
 double voo_sampson(const double F[9], const double* p);
 int  voo_ransac(const double* pts /* m*4: x1,y1,x2,y2 */, int m, double prob, double thr,

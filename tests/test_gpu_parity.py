@@ -72,6 +72,23 @@ def test_device_arithmetic_matches_host():
     assert np.array_equal(fo[:4096, 3], ref_s.astype(np.float32))
 
 
+def test_refit_nullvec_solver_bit_exact():
+    """k_refit's null-vector solver (ls_nullvec9_par) against the oracle's on matrices reaching each
+    of its exits -- converged, certified in the null space after the 32-step cap (the bench
+    regimes' degenerate inlier sets), cyclic-Jacobi fallback: the same status and f bit for bit."""
+    from test_oracle_kat import nullvec_cases
+    L = load()
+    cases = [(S, x0, f, st) for st, lst in nullvec_cases().items() for S, x0, f in lst]
+    assert {c[3] for c in cases} == {0, 1, 2}
+    S = np.ascontiguousarray(np.stack([c[0] for c in cases]))
+    x0 = np.ascontiguousarray(np.stack([c[1] for c in cases]))
+    f = np.zeros((len(cases), 9))
+    st = np.zeros(len(cases), np.int32)
+    assert L.vo_selftest_nullvec9(_p(S), _p(x0), _p(f), _p(st), len(cases), 0) == 0
+    assert list(st) == [c[3] for c in cases]
+    assert np.array_equal(f, np.stack([c[2] for c in cases]))
+
+
 def test_response_map_bit_exact(ctx_kitti, scene, factory):
     seq, frames = scene
     R = ctx_kitti.response(frames[0])

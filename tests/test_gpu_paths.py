@@ -159,6 +159,7 @@ def test_run_png_sequence(tmp_path, via):
     oracle's formatted with %.9g."""
     seq = SceneSequence(nframes=14, step=0.05)
     frames = list(seq.frames())
+    frames[9] = np.full_like(frames[9], 128)          # a blank frame: < 8 matches (VisualOdometry.cpp:108-115)
     missing = (6,)
     d = str(tmp_path / "seq") + "/"
     _write_sequence(d, seq, frames, missing)
@@ -168,10 +169,18 @@ def test_run_png_sequence(tmp_path, via):
         r = subprocess.run([CLI, "4", d, str(len(frames)), d + "poses.txt", out], capture_output=True, text=True,
                            timeout=120)
         assert r.returncode == 0, r.stderr
-        assert "Failed to load image: " + d + "000006.png" in r.stderr
+        err = r.stderr
         assert "Wrote estimated poses to: " + out in r.stdout
     else:
-        VisualOdometry("", 4, seq.W, seq.H, K=seq.K).run(d, len(frames), d + "poses.txt", out)
+        import contextlib
+        import io
+        buf = io.StringIO()
+        with contextlib.redirect_stderr(buf):
+            VisualOdometry("", 4, seq.W, seq.H, K=seq.K).run(d, len(frames), d + "poses.txt", out)
+        err = buf.getvalue()
+    assert [r[1] for r in ref][9] == 3
+    # the reference's stderr lines, in frame order
+    assert err.index("Failed to load image: " + d + "000006.png") < err.index("Too few matches at frame 9")
     assert open(out).read() == _csv([r[0] for r in ref])
 
 

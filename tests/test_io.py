@@ -29,9 +29,12 @@ def test_png_gray8_fixtures_equal_pil():
         assert np.array_equal(a, b)
 
 
-def _libpng_gray(rgb):
+def _libpng_gray(rgb, depth=8):
+    """png_do_rgb_to_gray, no gamma table: 8-bit samples truncate the 15-bit fixed-point sum,
+    16-bit samples round it (libpng 1.6 pngrtran.c)."""
     r, g, b = (rgb[..., k].astype(np.uint32) for k in range(3))
-    v = (9797 * r + 19234 * g + 3737 * b + 16384) >> 15
+    s = 9797 * r + 19234 * g + 3737 * b
+    v = (s + 16384) >> 15 if depth == 16 else s >> 15
     return np.where((r == g) & (g == b), r, v)
 
 
@@ -76,6 +79,22 @@ def test_png_modes(tmp_path, mode):
 
 def _chunk(t, d):
     return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)
+
+
+def test_png_rgb16_rounds_then_strips(tmp_path):
+    """16-bit RGB: png_do_rgb_to_gray rounds the 16-bit fixed-point sum, png_set_strip_16 keeps
+    the high byte (8-bit RGB truncates instead: test_png_modes)."""
+    rng = np.random.default_rng(3)
+    H, W = 9, 13
+    rgb = rng.integers(0, 65536, (H, W, 3), dtype=np.uint16)
+    rgb[0] = rgb[0, :, :1]
+    raw = b"".join(b"\x00" + rgb[y].astype(">u2").tobytes() for y in range(H))
+    png = b"\x89PNG\r\n\x1a\n" + _chunk(b"IHDR", struct.pack(">IIBBBBB", W, H, 16, 2, 0, 0, 0))
+    png += _chunk(b"IDAT", zlib.compress(raw)) + _chunk(b"IEND", b"")
+    p = tmp_path / "rgb16.png"
+    p.write_bytes(png)
+    expect = (_libpng_gray(rgb, depth=16) >> 8).astype(np.uint8)
+    assert np.array_equal(read_gray(str(p)), expect)
 
 
 def test_png_adam7_and_every_filter(tmp_path):
@@ -176,6 +195,19 @@ def test_gt_reader_and_csv_match_libstdcxx(tmp_path, gt_tool):
     ref = subprocess.check_output([gt_tool, str(gt)]).decode()
     assert ours.read_text() == ref
     assert np.array_equal(read_gt_line(""), np.array([1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0], float))
+
+
+def test_gt_token_edge_cases_match_libstdcxx(tmp_path, gt_tool):
+    """Tokens libstdc++'s num_get accumulates past a valid prefix ("1e", "1e+", "2E-": 0 and the
+    stream fails), exponents, a lone '\r' inside a line (getline keeps it, >> skips it), CRLF."""
+    lines = ["1e 5 6", "1e+ 7", "3 2E- 8 9", "4 1e5x 6", "5 1.5e3.25 7", "6\r7 8", "9 10\r", ". 1", "+ 2", "-.5e2 .e3",
+             "1E+2 1e-0 1e09 7 8 9 10 11 12 13 14 15"]
+    gt = tmp_path / "gt.txt"
+    gt.write_bytes(("\n".join(lines) + "\r\n" + "42\n").encode())
+    rows = read_kitti_poses(str(gt))
+    ours = tmp_path / "ours.csv"
+    write_pose_csv(str(ours), rows)
+    assert ours.read_text() == subprocess.check_output([gt_tool, str(gt)]).decode()
 
 
 def test_gt_without_trailing_newline(tmp_path, gt_tool):

@@ -430,3 +430,72 @@ def test_trajectory_bookkeeping():
     assert s3 == 0
     # GT scale: camera centres 1 step apart per frame, frame 3 vs last valid frame 1 -> 2 steps
     assert abs(np.linalg.norm(p3[:, 3] - p1[:, 3] * np.array([1, 1, -1]) * np.array([1, 1, -1])) - 0.1) < 0.1
+
+
+# -- the refit's null-vector solver: convergence, certificate, Jacobi fallback -------------------
+def nullvec_cases(n_search=2000, seed=0):
+    """9x9 PSD matrices S for ls_nullvec9 covering its three exits (0 converged, 1 certified in the
+    null space after the 32-step cap, 2 cyclic-Jacobi fallback): random spectra with separated,
+    near-equal and zero smallest eigenvalues, and normal matrices A^T A of design rows of repeated
+    points (a null space of dimension > 1, as the degenerate inlier sets of the bench regimes)."""
+    import oracle as O
+    rng = np.random.default_rng(seed)
+
+    def spd(eigs):
+        Q, _ = np.linalg.qr(rng.normal(size=(9, 9)))
+        S = (Q * np.asarray(eigs, float)) @ Q.T
+        return (S + S.T) / 2
+
+    def design(P):
+        n = len(P)
+        m = P.mean(0)
+        s1 = np.sqrt(2) / np.sqrt(((P[:, :2] - m[:2]) ** 2).sum() / n)
+        s2 = np.sqrt(2) / np.sqrt(((P[:, 2:] - m[2:]) ** 2).sum() / n)
+        a, b = (P[:, :2] - m[:2]) * s1, (P[:, 2:] - m[2:]) * s2
+        return np.stack([a[:, 0] * b[:, 0], a[:, 0] * b[:, 1], a[:, 0], a[:, 1] * b[:, 0], a[:, 1] * b[:, 1],
+                         a[:, 1], b[:, 0], b[:, 1], np.ones(n)], 1)
+
+    out = {0: [], 1: [], 2: []}
+    # the bench regimes' degenerate refit sets (tools/make_degenerate_fixture.py): the certified exit
+    import os
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "degenerate_inliers.npz"))
+    for k in d.files:
+        S = O.refit_normal(d[k])
+        for x0 in (np.ones(9), rng.normal(size=9)):
+            f, st = O.ls_nullvec9(S, x0)
+            out[st].append((S, x0, f))
+    tail = [[1e-3], [1.0 + 1e-7, 1.0], [0.0, 0.0], [1e-9, 1e-9 * (1 + 1e-9)], [0.5, 0.5]]
+    for t in range(n_search):
+        if t % 2:
+            k = int(rng.integers(3, 8))
+            base = rng.uniform(0, 1000, size=(k, 4))
+            A = design(base[rng.integers(0, k, size=int(rng.integers(8, 14)))])
+            S = A.T @ A
+        else:
+            tl = tail[(t // 2) % len(tail)]
+            S = spd(list(rng.uniform(2, 100, size=9 - len(tl))) + tl)
+        x0 = rng.normal(size=9)
+        f, st = O.ls_nullvec9(S, x0)
+        if len(out[st]) < 8:
+            out[st].append((S, x0, f))
+        if all(len(v) >= 8 for v in out.values()):
+            break
+    return out
+
+
+def test_nullvec9_solver_exits(oracle_lib):
+    """Every exit of the refit's null-vector solver is reachable and returns a unit eigenvector of
+    the smallest eigenvalue: converged and Jacobi results within 1e-9 of S's eigen-equation, certified
+    ones inside S's numerical null space (Rayleigh quotient at the Cholesky floor)."""
+    cases = nullvec_cases()
+    assert all(len(v) >= 1 for v in cases.values()), {k: len(v) for k, v in cases.items()}
+    for st, lst in cases.items():
+        for S, x0, f in lst:
+            assert abs(np.linalg.norm(f) - 1.0) < 1e-12
+            lam = f @ S @ f
+            w = np.linalg.eigvalsh(S)
+            if st == 1:
+                assert lam <= 64 * 1e-15 * np.diag(S).max()
+            else:
+                assert np.linalg.norm(S @ f - lam * f) <= 1e-9 * w[-1], (st, np.linalg.norm(S @ f - lam * f))
+                assert lam <= w[0] + 1e-9 * w[-1], (st, lam, w[:2])

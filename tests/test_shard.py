@@ -213,3 +213,85 @@ def test_run_shard_gloo(world):
         assert [(p[0], p[1]) for p in parts] == shard.partition(F, world)
         assert np.array_equal(np.concatenate([p[3] for p in parts]), full[1])
         assert np.array_equal(np.concatenate([p[2] for p in parts]), full[0])
+
+
+# -- failures: every rank raises ShardError, none is left blocked ---------------------------------
+class FailingEngine(ToyEngine):
+    """mode: 'halo' raises in the halo run, 'rerun' in the second run, 'rechain' in the hand-over;
+    'capacity' reports a record ring shorter than the shard."""
+
+    def __init__(self, world, mode):
+        super().__init__(world)
+        self.mode, self.halo_done = mode, False
+
+    def run(self, s, b):
+        if self.mode == "halo" or (self.mode == "rerun" and self.halo_done):
+            raise ValueError(f"frames before {s + 1} are not resident on this shard")
+        return super().run(s, b)
+
+    def extend(self, a, b):
+        out = super().extend(a, b)
+        self.halo_done = True
+        return out
+
+    def rechain(self, T_in, f0, n):
+        if self.mode == "rechain":
+            raise RuntimeError("vo_rechain: invalid state (-5)")
+        return super().rechain(T_in, f0, n)
+
+    def capacity(self):
+        return 3 if self.mode == "capacity" else None
+
+
+def _rerun_world(world):
+    """A ToyWorld in which shard 1 of `world` needs its second run."""
+    for seed in range(300, 400):
+        w = ToyWorld(48, seed, p_skip=0.5, p_fit=0.3)
+        if shard.run_local([ToyEngine(w) for _ in range(world)], 48)[1].runs == 2:
+            return (48, seed, 0.5, 0.3)
+    raise AssertionError("no world with a second run on shard 1")
+
+
+def _fail_rank(rank, world, port, q, wspec, mode):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from acs_visual_odometry_amd import shard as S
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    F, seed, ps, pf = wspec
+    w = ToyWorld(F, seed, ps, pf)
+    eng = FailingEngine(w, mode) if rank == 1 else ToyEngine(w)
+    try:
+        S.run_shard(eng, S.TorchComm(dist), F)
+        q.put((rank, "ok"))
+    except S.ShardError as e:
+        q.put((rank, "raised: " + str(e)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["halo", "rerun", "rechain", "capacity"])
+def test_run_shard_failure_reaches_every_rank(mode):
+    world = 3
+    wspec = _rerun_world(world) if mode == "rerun" else (60, 1, 0.15, 0.6)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_rank, args=(r, world, port, q, wspec, mode)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    if mode == "rechain":
+        # rank 0 chains before rank 1 and finishes; every rank after the failing one raises
+        assert res[0] == "ok" and all(res[r].startswith("raised") for r in (1, 2)), res
+    else:
+        assert all(v.startswith("raised") for v in res.values()), res
+    assert "rank 1" in res[1] or mode == "capacity"
+
+
+def test_run_local_capacity_check():
+    w = ToyWorld(60, 1)
+    with pytest.raises(shard.ShardError):
+        shard.run_local([FailingEngine(w, "capacity") for _ in range(2)], 60)
