@@ -51,6 +51,12 @@ struct vo_ctx {
     int slack = 0;                    // VO_SLACK: extra passes enqueued per chunk (misses re-run without a host round trip)
     hipStream_t st = nullptr;         // trajectory queue: k_traj of each pass (T_curr chain, pose rows)
     hipEvent_t ev_fin = nullptr;      // a pass's k_finalize done (the trajectory queue waits on it)
+    hipStream_t sf = nullptr;         // fit queue: refit, triangulation and finalize of pipelined passes
+    static constexpr int kPassEv = 8;
+    hipEvent_t ev_rs[kPassEv] = {};   // pass p's RANSAC done (the fit queue waits on it), p % 8
+    hipEvent_t ev_fn[kPassEv] = {};   // pass p's finalize done (pass p + 2 and the trajectory queue wait on it)
+    bool pipeline = true;             // VO_PIPELINE=0: every pass on the pose queue, one after the other
+    size_t set_off[9] = {};           // element offsets of window buffer set 1 (pass p uses set p & 1)
     int npass = 0;                    // pose passes enqueued (their pass-log entries)
     // per-batch event pools of a chunk: [VO_EV_WAIT] extract done (event_wait mode),
     // [VO_EV_COPY] H2D copy done, [VO_EV_STENCIL] stencil done (host streaming)
@@ -139,6 +145,7 @@ int sync_all(vo_ctx* c)
     for (hipStream_t q : c->se)
         if (q) HIPCHK(hipStreamSynchronize(q));
     if (c->s) HIPCHK(hipStreamSynchronize(c->s));
+    if (c->sf) HIPCHK(hipStreamSynchronize(c->sf));
     if (c->st) HIPCHK(hipStreamSynchronize(c->st));
     return VO_OK;
 }
@@ -335,29 +342,54 @@ int enqueue_h2d(vo_ctx* c, const HostSrc& hs, int f0, int nb, int j, uint8_t** d
     return VO_OK;
 }
 
-// one pose pass over the window [lo, lo + n) of the frames enqueued so far, n <= WB
-// gmax: frames < gmax are extracted once the pass runs (its wait covers them); every kernel of
-// the pass sees the same VoDev
-void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax)
+// the window buffers of pass p: set p & 1 (a pipelined pass's match and RANSAC write one set while
+// the previous pass's refit, triangulation and finalize read the other)
+VoDev pass_dev(const vo_ctx* c, int p)
+{
+    VoDev d = c->d;
+    if (p & 1) {
+        const size_t* o = c->set_off;
+        d.match_j += o[0]; d.match_pairs += o[1]; d.pts += o[2]; d.hypF += o[3]; d.counts += o[4];
+        d.inl += o[5]; d.inlmask += o[6]; d.model_p += o[7]; d.work += o[8];
+    }
+    return d;
+}
+
+// one pose pass over the window of the frames enqueued so far (up to WB frames; k_match decides
+// it on the device, vo_kernels.hip pass_window).  gmax: frames < gmax are extracted once the pass
+// runs (its wait covers them).  pipelined: match and RANSAC on the pose queue, refit,
+// triangulation and finalize on the fit queue, so the next pass's match overlaps them; the pass
+// first waits for pass p - 2's finalize (its buffer set and its state snapshot).  Otherwise every
+// kernel on the pose queue and the window comes from the state (every earlier pass finalized).
+void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax, bool pipelined)
 {
     hipStream_t s = c->s;
-    VoDev d = c->d;
+    const int p = c->npass++;
+    VoDev d = pass_dev(c, p);
     d.gmax = gmax;
-    d.pass = c->npass++;
+    d.pass = p;
+    d.nospec = pipelined ? 0 : 1;
+    hipStream_t sf = pipelined ? c->sf : s;
+    if (pipelined) (void)hipStreamWaitEvent(s, c->ev_fn[(p + vo_ctx::kPassEv - 2) % vo_ctx::kPassEv], 0);
     timed(c, ev, 3, s, [&] { vo::launch_match(d, 0, s); });
     timed(c, ev, 4, s, [&] { vo::launch_ransac(d, 0, s); });
-    timed(c, ev, 5, s, [&] { vo::launch_refit(d, 1, 0, s); });
+    if (pipelined) {
+        (void)hipEventRecord(c->ev_rs[p % vo_ctx::kPassEv], s);
+        (void)hipStreamWaitEvent(sf, c->ev_rs[p % vo_ctx::kPassEv], 0);
+    }
+    timed(c, ev, 5, sf, [&] { vo::launch_refit(d, 1, 0, sf); });
     if (c->fuse_fin) {
-        timed(c, ev, 6, s, [&] { vo::launch_triangulate(d, 0, s, out, out_base, 1); });
+        timed(c, ev, 6, sf, [&] { vo::launch_triangulate(d, 0, sf, out, out_base, 1); });
     } else {
-        timed(c, ev, 6, s, [&] { vo::launch_triangulate(d, 0, s); });
-        timed(c, ev, 7, s, [&] { vo::launch_finalize(d, out, out_base, s); });
+        timed(c, ev, 6, sf, [&] { vo::launch_triangulate(d, 0, sf); });
+        timed(c, ev, 7, sf, [&] { vo::launch_finalize(d, out, out_base, sf); });
     }
     // the T_curr chain and the pose rows on the trajectory queue (serial mode: the pose queue)
     hipStream_t q = c->serial ? s : c->st;
-    if (q != s) {
-        (void)hipEventRecord(c->ev_fin, s);
-        (void)hipStreamWaitEvent(q, c->ev_fin, 0);
+    hipEvent_t ef = pipelined ? c->ev_fn[p % vo_ctx::kPassEv] : c->ev_fin;
+    if (q != sf || pipelined) {
+        (void)hipEventRecord(ef, sf);
+        if (q != sf) (void)hipStreamWaitEvent(q, ef, 0);
     }
     timed(c, ev, 8, q, [&] { vo::launch_traj(d, out, out_base, q); });
 }
@@ -478,7 +510,9 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
                 HIPCHK(hipStreamWaitEvent(s, e, 0));
             }
         }
-        enqueue_pass(c, out, out_base, ev, base + f0s[k + 1]);
+        // the chunk's first pass sees every earlier pass finalized (the last call synchronised):
+        // its window comes from the state; later passes are pipelined
+        enqueue_pass(c, out, out_base, ev, base + f0s[k + 1], multi && c->pipeline && k > 0);
         return VO_OK;
     };
     if (!img0 && !hs) {
@@ -500,7 +534,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         // slack passes: the frames left behind by speculation misses, without a host round trip
         // (a pass with nothing left to commit returns at once); long chunks only
         if (sched.size() >= 4)
-            for (int k = 0; k < c->slack; ++k) enqueue_pass(c, out, out_base, ev, end);
+            for (int k = 0; k < c->slack; ++k) enqueue_pass(c, out, out_base, ev, end, multi && c->pipeline);
     }
     // every pass commits at least its first frame, so nf re-pass rounds bound the loop
     for (int round = 0, prev_lo = base;; ++round) {
@@ -510,8 +544,10 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         hipStream_t tq = c->serial ? s : c->st;
         HIPCHK(hipMemcpyAsync(c->out_host + (base - out_base), out + (base - out_base), sizeof(VoFrameOut) * nf,
                               hipMemcpyDeviceToHost, tq));
-        HIPCHK(hipMemcpyAsync(c->lo_host, &c->d.st->lo, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        // the commit point after the last finalize (the fit queue's, which the trajectory queue waited for)
+        HIPCHK(hipMemcpyAsync(c->lo_host, &c->d.st->lo, sizeof(int32_t), hipMemcpyDeviceToHost, tq));
         HIPCHK(hipStreamSynchronize(s));
+        if (c->sf) HIPCHK(hipStreamSynchronize(c->sf));
         HIPCHK(hipStreamSynchronize(tq));
         const int lo = *c->lo_host;
         if (lo >= end) break;
@@ -522,7 +558,8 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         }
         prev_lo = lo;
         // frames after skipped ones: their windows restart at lo (extracts are complete)
-        for (int k = 0; k < (end - lo + B - 1) / B; ++k) enqueue_pass(c, out, out_base, ev, end);
+        // (the host synchronised: every pass is finalized, so these run from the state, in order)
+        for (int k = 0; k < (end - lo + B - 1) / B; ++k) enqueue_pass(c, out, out_base, ev, end, false);
     }
     return ev && ev->err ? ev->err : VO_OK;
 }
@@ -654,6 +691,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     c->event_wait = !(getenv("VO_EVENT_WAIT") && atoi(getenv("VO_EVENT_WAIT")) == 0);
     d.xcd_map = getenv("VO_XCD") ? atoi(getenv("VO_XCD")) : 1;
     c->fuse_fin = getenv("VO_FUSE_FIN") && atoi(getenv("VO_FUSE_FIN")) != 0;
+    c->pipeline = !c->serial && !(getenv("VO_PIPELINE") && atoi(getenv("VO_PIPELINE")) == 0);
     c->force_wait_refusal = getenv("VO_FORCE_WAIT_REFUSAL") && atoi(getenv("VO_FORCE_WAIT_REFUSAL")) != 0;
     c->split = VO_EXT_QUEUES >= 2 && (getenv("VO_SPLIT") ? atoi(getenv("VO_SPLIT")) != 0 : VO_SPLIT_DEFAULT != 0);
     c->slack = getenv("VO_SLACK") ? std::max(0, std::min(64, atoi(getenv("VO_SLACK")))) : VO_SLACK_DEFAULT;
@@ -669,6 +707,11 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     if (hip_ok(hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK)
         return bail(VO_ERR_HIP);
+    if (hip_ok(hipStreamCreateWithPriority(&c->sf, hipStreamNonBlocking, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
+    for (int i = 0; i < vo_ctx::kPassEv; ++i)
+        if (hip_ok(hipEventCreateWithFlags(&c->ev_rs[i], hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK ||
+            hip_ok(hipEventCreateWithFlags(&c->ev_fn[i], hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK)
+            return bail(VO_ERR_HIP);
     for (hipStream_t& q : c->se)
         if (hip_ok(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, p_ext)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming)) != VO_OK) return bail(VO_ERR_HIP);
@@ -688,17 +731,23 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc(&d.kps, (size_t)N * VO_SLOTS);
     rc |= dalloc(&d.desc, (size_t)N * 8 * VO_SLOTS);
     rc |= dalloc(&d.pre, (size_t)N * VO_SLOTS);
-    const int WB = d.WB;                                       // pose window buffers
-    rc |= dalloc(&d.match_j, (size_t)N * WB);
-    rc |= dalloc(&d.match_pairs, (size_t)N * WB);
-    rc |= dalloc(&d.pts, (size_t)N * 4 * WB);
-    rc |= dalloc(&d.hypF, (size_t)d.max_hyp * 9 * WB);
-    rc |= dalloc(&d.counts, (size_t)d.max_hyp * WB);
-    rc |= dalloc(&d.inl, (size_t)N * WB);
+    const int WB = d.WB;                                       // pose window buffers: two sets (pass p uses set p & 1)
     d.mask_words = (N + 63) / 64;
-    rc |= dalloc(&d.inlmask, (size_t)d.max_hyp * d.mask_words * WB);
-    rc |= dalloc(&d.model_p, (size_t)N * 4 * WB);
-    rc |= dalloc(&d.work, WB);
+    const size_t per[9] = {(size_t)N * WB, (size_t)N * WB, (size_t)N * 4 * WB, (size_t)d.max_hyp * 9 * WB,
+                           (size_t)d.max_hyp * WB, (size_t)N * WB, (size_t)d.max_hyp * d.mask_words * WB,
+                           (size_t)N * 4 * WB, (size_t)WB};
+    std::memcpy(c->set_off, per, sizeof(per));
+    rc |= dalloc(&d.match_j, 2 * per[0]);
+    rc |= dalloc(&d.match_pairs, 2 * per[1]);
+    rc |= dalloc(&d.pts, 2 * per[2]);
+    rc |= dalloc(&d.hypF, 2 * per[3]);
+    rc |= dalloc(&d.counts, 2 * per[4]);
+    rc |= dalloc(&d.inl, 2 * per[5]);
+    rc |= dalloc(&d.inlmask, 2 * per[6]);
+    rc |= dalloc(&d.model_p, 2 * per[7]);
+    rc |= dalloc(&d.work, 2 * per[8]);
+    rc |= dalloc(&d.plan, VO_PASS_RING);
+    rc |= dalloc(&d.snap, VO_PASS_RING);
     rc |= dalloc(&d.st, 1);
     rc |= dalloc(&d.ext_n, VO_SLOTS);
     rc |= dalloc(&d.ext_st, VO_SLOTS);
@@ -739,11 +788,13 @@ void vo_destroy(vo_ctx* c)
     for (hipStream_t q : c->se)
         if (q) (void)hipStreamSynchronize(q);
     if (c->s) (void)hipStreamSynchronize(c->s);
+    if (c->sf) (void)hipStreamSynchronize(c->sf);
     if (c->st) (void)hipStreamSynchronize(c->st);
     VoDev& d = c->d;
     void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.tilerows, d.ckeys, d.selbits, d.hist, d.ext_n, d.ext_st, (void*)d.seq_starts,
                     d.kps, d.desc, d.pre, d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.inlmask,
-                    d.model_p, d.work, d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr, d.trec, d.plog, d.dbg};
+                    d.model_p, d.work, d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr, d.trec, d.plog, d.dbg,
+                    d.plan, d.snap};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->out_host) (void)hipHostFree(c->out_host);
@@ -762,6 +813,11 @@ void vo_destroy(vo_ctx* c)
     if (c->s) (void)hipStreamDestroy(c->s);
     if (c->st) (void)hipStreamDestroy(c->st);
     if (c->ev_fin) (void)hipEventDestroy(c->ev_fin);
+    if (c->sf) (void)hipStreamDestroy(c->sf);
+    for (int i = 0; i < vo_ctx::kPassEv; ++i) {
+        if (c->ev_rs[i]) (void)hipEventDestroy(c->ev_rs[i]);
+        if (c->ev_fn[i]) (void)hipEventDestroy(c->ev_fn[i]);
+    }
     delete c;
 }
 
@@ -771,7 +827,9 @@ int vo_reset(vo_ctx* c)
 {
     if (!c) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    vo::launch_reset(c->d, c->s);
+    VoDev d = c->d;
+    d.pass = c->npass;                 // the pass rings start over at the next pass
+    vo::launch_reset(d, c->s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev_reset, c->s));
     c->reset_pending = true;

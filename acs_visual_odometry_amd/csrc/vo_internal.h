@@ -143,6 +143,25 @@ struct VoTrajRec {
 };
 #define VO_PLOG 4096       // pass log ring: (lo, committed frames) of pass p at p % VO_PLOG
 
+// Cross-pass pipelining: a pass's match and RANSAC run on the pose queue
+// while the previous pass's refit, triangulation and finalize run on the fit queue, so pass p
+// chooses its window before pass p - 1 has committed.  k_match decides it from the state after
+// pass p - 2 (its snapshot; the pose queue waited for that finalize) and pass p - 1's window:
+// if pass p - 1 starts where pass p - 2 left the trajectory (its window start and first-frame
+// desc1 slot), pass p speculates that p - 1 commits its whole window and starts after it;
+// otherwise pass p - 1 will be discarded and pass p starts from the snapshot.  k_finalize commits
+// a pass only if its window start and first-frame desc1 slot match the trajectory state then
+// (a speculation miss discards it; the next pass restarts from the state).  Rings of 4 by pass.
+#define VO_PASS_RING 4
+struct VoPlan {           // the window of pose pass p (k_match's first workgroup writes it)
+    int32_t lo, n;        // frames [lo, lo + n)
+    int32_t dual;         // a repair window with two work records per frame
+    int32_t prev0;        // desc1 slot the window's first frame was matched against
+};
+struct VoSnap {           // the trajectory state after pass p's k_finalize
+    int32_t lo, prev_slot, win, dual;
+};
+
 // Trajectory state (VisualOdometry::run's locals), read and written by k_finalize only
 // (T_curr: by k_traj only).
 struct VoState {
@@ -223,6 +242,9 @@ struct VoDev {
     VoTrajRec* trec;      // x ring: committed frames' trajectory inputs (k_finalize -> k_traj)
     int2* plog;           // x VO_PLOG: (lo, committed) per pose pass
     int pass;             // pose pass number (its plog entry)
+    int nospec;           // every earlier pass is finalized: the window comes from the state itself
+    VoPlan* plan;         // x VO_PASS_RING
+    VoSnap* snap;         // x VO_PASS_RING
     unsigned long long* dbg;   // diagnostic s_memtime stamps (VO_STAMPS builds only)
 };
 

@@ -1521,31 +1521,62 @@ __host__ __device__ inline int match_blocks(int N, int match_bits)
     return match_bits == 32 ? (N + MT_QPB - 1) / MT_QPB : (N + MT512_QPB - 1) / MT512_QPB;
 }
 
-// Window of a pose pass: frames [st->lo, st->lo + n), n = min(st->win, st->end - st->lo,
-// d.gmax - st->lo) with st->win <= d.WB: up to WB frames (2 extract batches), but only frames
-// the pass's extract wait covers (d.gmax), so the window grows when the pose queue lags behind
-// the extract queue and each pass's fixed latency is spread over more frames.  A stage call
-// works on work[0] alone.  st changes only in k_finalize, the pass's last kernel.
-// st->win is B, or d.repair_win after a pass whose commit stopped early: the frames after a
-// speculation miss (a frame that did not advance desc1) are re-run in a short window, since
-// misses come in runs (a new sequence's first frames without a model, quirk 9) and each
-// re-run window commits only up to the next miss.
+// Window of a pose pass: frames [lo, lo + n), n = min(win, st->end - lo, d.gmax - lo) with
+// win <= d.WB: up to WB frames (2 extract batches), but only frames the pass's extract wait
+// covers (d.gmax), so the window grows when the pose queue lags behind the extract queue and each
+// pass's fixed latency is spread over more frames.  win is WB, or d.repair_win after a pass whose
+// commit stopped early: the frames after a speculation miss (a frame that did not advance desc1)
+// are re-run in a short window, since misses come in runs (a new sequence's first frames without
+// a model, quirk 9) and each re-run window commits only up to the next miss.
+// k_match decides the window (pass_window, every workgroup alike) and its first workgroup
+// records it (d.plan); the pass's later kernels read the record (pass_plan).  With cross-pass
+// pipelining (vo_internal.h VoPlan) the window comes from the state after pass p - 2 and pass
+// p - 1's window; d.nospec (every earlier pass finalized) takes it from the state itself.
+__device__ __forceinline__ VoPlan pass_window(const VoDev& d)
+{
+    const VoState* st = d.st;
+    VoPlan P;
+    int win;
+    if (d.nospec) {
+        P.lo = st->lo; P.dual = st->dual; P.prev0 = st->prev_slot; win = st->win;
+    } else {
+        const VoSnap s = d.snap[(d.pass + VO_PASS_RING - 2) & (VO_PASS_RING - 1)];
+        const VoPlan q = d.plan[(d.pass + VO_PASS_RING - 1) & (VO_PASS_RING - 1)];
+        if (q.n > 0 && q.lo == s.lo && q.prev0 == s.prev_slot) {
+            // pass p - 1 starts where pass p - 2 left off: speculate that it commits its window
+            P.lo = q.lo + q.n; P.dual = 0; P.prev0 = (P.lo - 1) % VO_RING; win = d.WB;
+        } else {
+            // pass p - 1 will be discarded (or commits nothing): the state after pass p - 2 holds
+            P.lo = s.lo; P.dual = s.dual; P.prev0 = s.prev_slot; win = s.win;
+        }
+    }
+    P.n = max(0, min(min(st->end, d.gmax) - P.lo, win > 0 && win < d.WB ? win : d.WB));
+    return P;
+}
+__device__ __forceinline__ VoPlan pass_plan(const VoDev& d) { return d.plan[d.pass & (VO_PASS_RING - 1)]; }
 __device__ __forceinline__ int win_count(const VoDev& d, int stage)
 {
-    if (stage) return 1;
-    const int lo = d.st->lo, w = d.st->win;
-    return min(min(d.st->end, d.gmax) - lo, w > 0 && w < d.WB ? w : d.WB);
+    return stage ? 1 : pass_plan(d).n;
 }
-// Work records of a pass: one per window frame, and in a repair window (st->dual) a second
-// set [n, 2n): frame wf matched against desc1 as it was before the window (st->prev_slot)
+// Work records of a pass: one per window frame, and in a repair window (plan.dual) a second
+// set [n, 2n): frame wf matched against desc1 as it was before the window (plan.prev0)
 // instead of frame f - 1.  When frame f - 1 does not advance desc1 and no frame of the window
 // before it did, that is the match the sequential loop makes, so a run of frames without a
 // model (a new sequence's first frames) commits in one repair pass (k_finalize picks the
 // record per frame).  repair_win <= WB / 2.
+__device__ __forceinline__ int vwin_records(const VoPlan& P) { return P.dual ? 2 * P.n : P.n; }
 __device__ __forceinline__ int vwin_count(const VoDev& d, int stage)
 {
-    const int n = win_count(d, stage);
-    return (!stage && d.st->dual) ? 2 * n : n;
+    if (stage) return 1;
+    return vwin_records(pass_plan(d));
+}
+// k_match's window: decided here, recorded by the first workgroup for the pass's later kernels
+__device__ __forceinline__ VoPlan match_window(const VoDev& d, int stage)
+{
+    if (stage) return VoPlan{0, 1, 0, 0};
+    const VoPlan P = pass_window(d);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) d.plan[d.pass & (VO_PASS_RING - 1)] = P;
+    return P;
 }
 
 __device__ __forceinline__ uint64_t frame_seed_of(const VoDev& d, int f)
@@ -1574,17 +1605,17 @@ struct MatchFrame {
     int f, cur, prev, n1, n2;
     int32_t* match_j;
 };
-__device__ __forceinline__ bool match_header(const VoDev& d, int stage, int wf, MatchFrame& m)
+__device__ __forceinline__ bool match_header(const VoDev& d, int stage, const VoPlan& P, int wf, MatchFrame& m)
 {
     VoWork* w = d.work + wf;
     int f, fl = -1, cur, prev, status = VO_STATUS_OK;
     if (stage) {
         f = -1; prev = VO_STAGE_SLOT; cur = VO_STAGE_SLOT + 1;
     } else {
-        const int n = win_count(d, 0), df = wf < n ? wf : wf - n;   // record wf >= n: the dual match
-        f = d.st->lo + df;
+        const int n = P.n, df = wf < n ? wf : wf - n;   // record wf >= n: the dual match
+        f = P.lo + df;
         cur = f % VO_RING;
-        prev = df == 0 || wf >= n ? d.st->prev_slot : (f - 1) % VO_RING;
+        prev = df == 0 || wf >= n ? P.prev0 : (f - 1) % VO_RING;
         const int es = d.ext_st[cur];
         const int base = seq_base(d, f);
         fl = f - base;
@@ -1695,9 +1726,10 @@ __device__ __forceinline__ void top2_merge(uint32_t& m1, uint32_t& m2, uint32_t 
 __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
 {
     const int wf = blockIdx.y;
-    if (wf >= vwin_count(d, stage)) return;
+    const VoPlan P = match_window(d, stage);
+    if (wf >= vwin_records(P)) return;
     MatchFrame m;
-    if (!match_header(d, stage, wf, m)) return;
+    if (!match_header(d, stage, P, wf, m)) return;
     __shared__ unsigned s_last;
     __shared__ int s_wsum[32];
     __shared__ uint4 s_cand4[1024];                  // 4096 prefixes
@@ -1810,9 +1842,10 @@ __device__ __forceinline__ uint32_t dist512(const uint32_t (&qw)[16], const uint
 __global__ void __launch_bounds__(256) k_match512(VoDev d, int stage)
 {
     const int wf = blockIdx.y;
-    if (wf >= vwin_count(d, stage)) return;
+    const VoPlan P = match_window(d, stage);
+    if (wf >= vwin_records(P)) return;
     MatchFrame m;
-    if (!match_header(d, stage, wf, m)) return;
+    if (!match_header(d, stage, P, wf, m)) return;
     __shared__ unsigned s_last;
     __shared__ int s_wsum[32];                      // match_compact: 8 rounds x 4 waves
     extern __shared__ uint4 s_tile[];        // MT512_TILE x 64 B
@@ -3042,10 +3075,14 @@ __device__ void finalize_body(const VoDev& d, VoFrameOut* out, int out_base)
     const int tid = threadIdx.x;
     VO_STAMP(d, 1996, 7);
     VoState* st = d.st;
-    const bool dual = st->dual != 0;
+    const VoPlan P = pass_plan(d);
+    const bool dual = P.dual != 0;
     if (tid == 0) {
         const int lo = st->lo;
-        const int n = win_count(d, 0);
+        // a window chosen before the previous pass committed holds only if it starts where the
+        // trajectory stands and its first frame was matched against the current desc1
+        // (vo_internal.h VoPlan); otherwise the pass is discarded
+        const int n = (P.lo == lo && P.prev0 == st->prev_slot) ? P.n : 0;
         s_lo = lo;
         s_n = n;
         s_copy = -1;
@@ -3079,7 +3116,10 @@ __device__ void finalize_body(const VoDev& d, VoFrameOut* out, int out_base)
     VO_STAMP(d, 1996, 0);
     const int n = s_n, lo = s_lo;
     if (n <= 0) {
-        if (tid == 0) d.plog[d.pass % VO_PLOG] = make_int2(lo, 0);   // k_traj: nothing committed
+        if (tid == 0) {
+            d.plog[d.pass % VO_PLOG] = make_int2(lo, 0);   // k_traj: nothing committed
+            d.snap[d.pass & (VO_PASS_RING - 1)] = VoSnap{st->lo, st->prev_slot, st->win, st->dual};
+        }
         return;
     }
     // 0
@@ -3197,6 +3237,7 @@ __device__ void finalize_body(const VoDev& d, VoFrameOut* out, int out_base)
         st->dual = nc < n && 2 * d.repair_win <= d.WB;
         st->last_valid = s_newlv;
         st->prev_slot = s_newprev;
+        d.snap[d.pass & (VO_PASS_RING - 1)] = VoSnap{st->lo, st->prev_slot, st->win, st->dual};
         const int m = s_model_wf;
         if (m >= 0) {
             const VoWork* w = d.work + (dual ? s_rec[m] : m);
@@ -3363,10 +3404,18 @@ __global__ void __launch_bounds__(256) k_reset(VoDev d)
         for (int i = 0; i < 16; ++i) st->Tcurr[i] = (i % 5 == 0) ? 1.0 : 0.0;
         st->scale_override = __longlong_as_double(0x7FF8000000000000ll);
     }
+    if (tid == 1) {
+        // the pass rings as if passes d.pass - 2 and d.pass - 1 had finalized the reset state and
+        // pass d.pass - 1 had an empty window: the next pass starts from the state
+        const VoSnap s0{0, 0, d.WB, 0};
+        d.snap[(d.pass + VO_PASS_RING - 2) & (VO_PASS_RING - 1)] = s0;
+        d.snap[(d.pass + VO_PASS_RING - 1) & (VO_PASS_RING - 1)] = s0;
+        d.plan[(d.pass + VO_PASS_RING - 1) & (VO_PASS_RING - 1)] = VoPlan{-1, 0, 0, -1};
+    }
     for (int i = tid; i < VO_SLOTS; i += nth) { d.ext_n[i] = 0; d.ext_st[i] = VO_STATUS_OK; }
     for (int i = tid; i < VO_HIST_BINS * d.B * VO_EXT_QUEUES; i += nth) d.hist[i] = 0u;
     uint32_t* w = reinterpret_cast<uint32_t*>(d.work);
-    for (int i = tid; i < (int)(sizeof(VoWork) / 4) * d.WB; i += nth) w[i] = 0u;
+    for (int i = tid; i < (int)(sizeof(VoWork) / 4) * 2 * d.WB; i += nth) w[i] = 0u;   // both window sets
     for (int i = tid; i < VO_CTR_WORDS; i += nth) d.ctr[i] = 0u;
 }
 
