@@ -283,6 +283,7 @@ int enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, 
     d.tilerows += (size_t)d.ntiles * 16 * B * eq;
     d.ckeys += (size_t)d.cand_cap * B * eq;
     d.selbits += ((size_t)d.cand_cap / 64 + 1) * B * eq;
+    d.selctl += B * eq;
     d.hist += (size_t)VO_HIST_BINS * B * eq;
     timed(c, ev, 0, q, [&] { vo::launch_stencil(d, img0, frame_bytes, nb, 0, q); });
     if (ev_stencil) HIPCHK(hipEventRecord(ev_stencil, q));
@@ -717,6 +718,13 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     if (hip_ok(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming)) != VO_OK) return bail(VO_ERR_HIP);
     d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
     if (d.sel_lds < 0) return bail(VO_ERR_HIP);
+    // select: banded (VO_SEL_BANDS workgroups per frame) from VO_SEL_BANDED_TILES stencil tiles up
+    // (1920x1080: select 3.45 -> 1.93 us/frame, 70k -> 78k frames/s), one 1024-thread workgroup per
+    // frame below (KITTI's 552 tiles: 0.45 vs 0.48 us/frame, 281-285k vs 276-277k frames/s);
+    // VO_SEL1=1 / 0 forces the single-workgroup / banded form.  A band too large for LDS: single.
+    d.sel_emit_lds = vo::select_emit_lds_bytes(W, H);
+    d.sel1 = getenv("VO_SEL1") ? atoi(getenv("VO_SEL1")) != 0 : ntiles < VO_SEL_BANDED_TILES;
+    if (d.sel_emit_lds < 0) d.sel1 = 1;
     const size_t np = (size_t)W * H;
     rc |= dalloc(&d.frame_in, np);
     d.bstride = vo_blur_stride(W);
@@ -728,6 +736,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc(&d.ckeys, (size_t)d.cand_cap * B * VO_EXT_QUEUES);
     rc |= dalloc(&d.selbits, ((size_t)d.cand_cap / 64 + 1) * B * VO_EXT_QUEUES);
     rc |= dalloc(&d.hist, (size_t)VO_HIST_BINS * B * VO_EXT_QUEUES);
+    rc |= dalloc(&d.selctl, (size_t)B * VO_EXT_QUEUES);
     rc |= dalloc(&d.kps, (size_t)N * VO_SLOTS);
     rc |= dalloc(&d.desc, (size_t)N * 8 * VO_SLOTS);
     rc |= dalloc(&d.pre, (size_t)N * VO_SLOTS);
@@ -771,6 +780,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     (void)hipMemset(d.kps, 0, sizeof(int2) * N * VO_SLOTS);
     (void)hipMemset(d.desc, 0, sizeof(uint64_t) * 8 * N * VO_SLOTS);
     (void)hipMemset(d.pre, 0, sizeof(uint32_t) * N * VO_SLOTS);
+    (void)hipMemset(d.selctl, 0, sizeof(VoSelCtl) * B * VO_EXT_QUEUES);   // arrival / boundary counters
     d.n_seq_starts = 0;
     d.origin = 0;
     if (ensure_out(c, 16) != VO_OK) return bail(VO_ERR_HIP);
@@ -791,7 +801,7 @@ void vo_destroy(vo_ctx* c)
     if (c->sf) (void)hipStreamSynchronize(c->sf);
     if (c->st) (void)hipStreamSynchronize(c->st);
     VoDev& d = c->d;
-    void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.tilerows, d.ckeys, d.selbits, d.hist, d.ext_n, d.ext_st, (void*)d.seq_starts,
+    void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.tilerows, d.ckeys, d.selbits, d.hist, d.selctl, d.ext_n, d.ext_st, (void*)d.seq_starts,
                     d.kps, d.desc, d.pre, d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.inlmask,
                     d.model_p, d.work, d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr, d.trec, d.plog, d.dbg,
                     d.plan, d.snap};

@@ -19,7 +19,8 @@
 //   response    f32 W*H            optional dense R map (debug / parity only)
 //   cand        u64 224/tile x B   NMS survivors per 56x16 tile, key = Rbits<<32 | row<<16 | col
 //   tilerows    u8  16/tile  x B   survivors per tile row (select emits raster order from them)
-//   ckeys       u64 224/tile x B   compact survivors (only when they overflow select's LDS)
+//   ckeys       u64 224/tile x B   boundary-bin keys of the banded select (single-workgroup
+//                                  select: compact survivors when they overflow its LDS)
 //   selbits     u64 4/tile   x B   selected-survivor bitmap (only when it overflows LDS)
 //   hist        u32 4096     x B   coarse histogram of candidate R (top-N boundary)
 //   kps         int2 N  x SLOTS    raster-ordered keypoints: ring slot f % VO_RING, carry, stage
@@ -41,6 +42,12 @@
 #include <stdint.h>
 
 #define VO_HIST_BINS 4096
+#ifndef VO_SEL_BANDS
+#define VO_SEL_BANDS 8     // select workgroups per frame: bands of tile rows (k_select_count / k_select_emit)
+#endif
+#ifndef VO_SEL_BANDED_TILES
+#define VO_SEL_BANDED_TILES 1024   // banded select for frames of at least this many stencil tiles
+#endif
 #ifndef VO_TILE_W
 #define VO_TILE_W 56       // stencil tile = half a wave's strip x 16 rows (k_stencil ST_TW, ST_TH)
 #endif
@@ -182,6 +189,20 @@ struct VoState {
     double scale_override;           // stage vo_pose scale
 };
 
+// Banded select's per-frame hand-off (x B x VO_EXT_QUEUES): k_select_count's workgroups publish
+// their band's count above the boundary bin and append the boundary bin's keys; the last one to
+// arrive ranks the boundary keys and writes the threshold and each band's first output position
+// for k_select_emit (the kernel boundary orders them).
+struct VoSelCtl {
+    uint32_t arrive;                 // workgroups of the frame arrived (reset by the last)
+    uint32_t nbnd;                   // boundary-bin keys appended (reset by the last)
+    int32_t dcount[VO_SEL_BANDS];    // per band: keys above the boundary bin
+    int32_t b;                       // boundary bin, -1: every key is selected
+    int32_t pad;
+    uint64_t Tb;                     // smallest selected key of the boundary bin
+    int32_t base[VO_SEL_BANDS];      // per band: its first keypoint position in raster order
+};
+
 // Everything a kernel needs, passed by value.
 struct VoDev {
     int W, H, N;
@@ -214,7 +235,10 @@ struct VoDev {
     uint8_t* tilerows;    // x B: per stencil tile the candidate count of each of its 16 rows
     uint64_t* ckeys;      // x B: select's compact keys when they exceed the LDS capacity
     uint64_t* selbits;    // x B: select's selected-key bitmap when it exceeds the LDS capacity
-    int sel_lds;          // select: dynamic LDS bytes
+    int sel_lds;          // select (single-workgroup form, VO_SEL1=1): dynamic LDS bytes
+    int sel_emit_lds;     // banded select: k_select_emit's dynamic LDS bytes (a band's segment counts)
+    int sel1;             // VO_SEL1=1: the single-workgroup select (one 1024-thread workgroup per frame)
+    VoSelCtl* selctl;     // x B x VO_EXT_QUEUES
     uint32_t* hist;       // x B (scratch of extract queue eq; x VO_EXT_QUEUES allocated)
     int2* kps;            // x SLOTS (N each)
     uint64_t* desc;       // x SLOTS (8N each)
@@ -257,6 +281,7 @@ namespace vo {
 void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int nb, int write_response, hipStream_t s);
 void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s);
 int select_lds_bytes(int W, int H, int* key_cap);     // sets the kernel attribute; <0 on failure
+int select_emit_lds_bytes(int W, int H);              // banded select: sets the attribute; <0 if the band does not fit
 void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned publish, hipStream_t s);
 void launch_ext_missing(const VoDev& d, int slot, hipStream_t s);   // extract side of a missing image
 // pose pass over the window (stage = 0) or over work[0] prepared by a stage API (stage = 1)

@@ -1253,6 +1253,421 @@ __device__ __forceinline__ void publish_seq(unsigned* flag, unsigned v)
     if (threadIdx.x == 0) __hip_atomic_store((gu32*)flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// ---------------------------------------------------------------------------
+// Banded select: the exact top-N of a frame's NMS survivors by (R, row, col) descending, emitted in
+// raster order (corner_detection_parallel_GPU.cpp:146-188, feature_extraction_parallel_GPU.cpp:
+// 235-265), on VO_SEL_BANDS workgroups per frame instead of one.  Workgroup w owns band w: a
+// contiguous run of tile rows, so the band's keys precede band w + 1's in raster order.
+//   k_select_count  every workgroup finds the boundary bin b of the stencil's histogram (the bin
+//                   where the count from the top reaches N), counts its band's keys above b and
+//                   appends the band's keys of bin b to the frame's boundary list; the last to
+//                   arrive ranks the boundary list (the (N - above)-th largest key is the
+//                   threshold Tb; keys carry row and col, so they are unique), and turns the band
+//                   counts into each band's first output position.
+//   k_select_emit   each band counts its selected keys per (row, tile) segment, scans the
+//                   segments in raster order and writes every selected key at its position.
+// A tile's keys are read by one wave, lane = key (tile-local raster order: ascending row, then
+// column), so a segment's keys are contiguous lanes and a key's rank inside its segment is a
+// popcount of the wave's selection ballot.
+// ---------------------------------------------------------------------------
+#define SL_T 256
+#define SL_RANK_MAX 256        // boundary lists up to this size are ranked pairwise in LDS; longer
+                               // ones by a radix select (8 bits a pass, from the top)
+#define SL_TOF_CAP 8192        // band keys up to this many: a key's tile from an LDS table (else a binary search)
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+__device__ __forceinline__ void st_sc1_u64(uint64_t* p, uint64_t v)
+{
+    __hip_atomic_store((gu64*)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1_u64(const uint64_t* p)
+{
+    return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// band w of the frame: tile rows [ty0, ty1)
+__host__ __device__ inline void sel_band(int nty, int w, int& ty0, int& ty1)
+{
+    const int nbr = (nty + VO_SEL_BANDS - 1) / VO_SEL_BANDS;
+    ty0 = w * nbr < nty ? w * nbr : nty;
+    ty1 = ty0 + nbr < nty ? ty0 + nbr : nty;
+}
+// dynamic LDS of the banded select kernels (bytes), for bands of at most ntm tiles (nbr tile rows)
+struct SelBandLayout {
+    int rows, pre, tof, bits, seg, total;
+};
+__host__ __device__ inline SelBandLayout sel_band_layout(int ntx, int nty)
+{
+    auto al = [](int v) { return (v + 15) & ~15; };
+    const int nbr = (nty + VO_SEL_BANDS - 1) / VO_SEL_BANDS, ntm = nbr * ntx;
+    SelBandLayout L;
+    L.rows = 0;                                              // uint4 row counts per band tile
+    L.pre = al(16 * ntm);                                    // int: first compact key index per tile (+ total)
+    L.tof = L.pre + al(4 * (ntm + 1));                       // u16: tile of each compact key
+    L.bits = L.tof + al(2 * SL_TOF_CAP);                     // u64: selected-key bitmap
+    L.seg = L.bits + al(8 * (ntm * ST_TCAP / 64 + 2));       // u16: per (row, tile) segment, pairs per word
+    L.total = L.seg + al(2 * (nbr * ST_TH * ntx + 1));
+    return L;
+}
+__device__ __forceinline__ int row_bytes(uint4 rc)
+{
+    uint32_t s = 0u;
+    s = __builtin_amdgcn_udot4(rc.x, 0x01010101u, s, false);
+    s = __builtin_amdgcn_udot4(rc.y, 0x01010101u, s, false);
+    s = __builtin_amdgcn_udot4(rc.z, 0x01010101u, s, false);
+    s = __builtin_amdgcn_udot4(rc.w, 0x01010101u, s, false);
+    return (int)s;
+}
+// block-wide inclusive suffix sum over SL_T threads (s_w: 4 words)
+__device__ __forceinline__ uint32_t sel_suffix(uint32_t v, uint32_t* s_w)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t suf = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t u = __shfl_down(suf, off);
+        if (lane + off < 64) suf += u;
+    }
+    if (lane == 0) s_w[wave] = suf;
+    __syncthreads();
+    for (int w = wave + 1; w < SL_T / 64; ++w) suf += s_w[w];
+    __syncthreads();
+    return suf;
+}
+// the band's tile table: row counts, each tile's first compact key index (keys numbered in tile
+// order), and each key's tile when the band holds at most SL_TOF_CAP keys.  Thread tid owns band
+// tiles [tid tpt, tid tpt + tpt).  Returns the band's key count.
+__device__ int sel_band_table(const uint8_t* tilerows, int t0, int nt, uint4* s_rows, int* s_pre, uint16_t* s_tof,
+                              uint32_t* s_w)
+{
+    const int tid = threadIdx.x, tpt = (nt + SL_T - 1) / SL_T;
+    const int k0 = min(tid * tpt, nt), k1 = min(k0 + tpt, nt);
+    int mine = 0;
+    for (int k = k0; k < k1; ++k) {
+        const uint4 rc = *reinterpret_cast<const uint4*>(tilerows + (size_t)(t0 + k) * ST_TH);
+        s_rows[k] = rc;
+        const int c = row_bytes(rc);
+        s_pre[k] = c;
+        mine += c;
+    }
+    const uint32_t after = sel_suffix((uint32_t)mine, s_w);
+    __shared__ int s_total;
+    if (tid == 0) s_total = (int)after;
+    __syncthreads();
+    const int total = s_total;
+    int base = total - (int)after;
+    for (int k = k0; k < k1; ++k) {
+        const int c = s_pre[k];
+        s_pre[k] = base;
+        if (total <= SL_TOF_CAP)
+            for (int i = 0; i < c; ++i) s_tof[base + i] = (uint16_t)k;
+        base += c;
+    }
+    if (tid == 0) s_pre[nt] = total;
+    __syncthreads();
+    return total;
+}
+// band tile of compact key g
+__device__ __forceinline__ int sel_tile_of(int g, int total, int nt, const int* s_pre, const uint16_t* s_tof)
+{
+    if (total <= SL_TOF_CAP) return s_tof[g];
+    int lo = 0, hi = nt - 1;                         // the last tile whose first key is <= g
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_pre[mid] <= g) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(SL_T) k_select_count(VoDev d, int f0, int slot_override, int nb)
+{
+    int z, w;
+    if (!xcd_frame(d, VO_SEL_BANDS, nb, z, w)) return;
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int N = d.N;
+    const int ntx = (d.W + ST_TW - 1) / ST_TW, nty = (d.H + ST_TH - 1) / ST_TH;
+    const SelBandLayout L = sel_band_layout(ntx, nty);
+    uint4* s_rows = reinterpret_cast<uint4*>(smem + L.rows);
+    int* s_pre = reinterpret_cast<int*>(smem + L.pre);
+    uint16_t* s_tof = reinterpret_cast<uint16_t*>(smem + L.tof);
+    const uint8_t* tilerows = d.tilerows + (size_t)z * d.ntiles * ST_TH;
+    const uint64_t* cand = d.cand + (size_t)z * d.cand_cap;
+    uint32_t* hist = d.hist + (size_t)z * VO_HIST_BINS;
+    VoSelCtl* ctl = d.selctl + z;
+    uint64_t* bnd = d.ckeys + (size_t)z * d.cand_cap;            // the frame's boundary-bin keys
+    __shared__ uint32_t s_w[4];
+    __shared__ int s_b, s_above, s_C, s_rem, s_dsel;
+    __shared__ uint32_t s_last;
+    __shared__ uint64_t s_tb;
+    __shared__ uint64_t s_key[SL_RANK_MAX];
+    __shared__ uint32_t s_dh[256];
+    __shared__ int s_cnt[VO_SEL_BANDS];
+    int ty0, ty1;
+    sel_band(nty, w, ty0, ty1);
+    const int t0 = ty0 * ntx, nt = (ty1 - ty0) * ntx;
+    // 1. boundary bin: thread tid holds bins 16 tid .. 16 tid + 15 (loads issued with the band table's)
+    uint32_t h[16], hs = 0u;
+    {
+        const uint4* hp = reinterpret_cast<const uint4*>(hist) + 4 * tid;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 v = hp[q];
+            h[4 * q] = v.x; h[4 * q + 1] = v.y; h[4 * q + 2] = v.z; h[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) hs += h[q];
+    }
+    const int total = sel_band_table(tilerows, t0, nt, s_rows, s_pre, s_tof, s_w);
+    if (tid == 0) { s_b = -1; s_above = 0; }
+    const uint32_t suf = sel_suffix(hs, s_w);            // keys in bins >= 16 tid
+    if (tid == 0) s_C = (int)suf;
+    __syncthreads();
+    const int C = s_C;
+    if (C > N) {
+        uint32_t run = suf - hs;                         // keys in bins above this thread's
+#pragma unroll
+        for (int q = 15; q >= 0; --q) {
+            if (run < (uint32_t)N && run + h[q] >= (uint32_t)N) { s_b = 16 * tid + q; s_above = (int)run; }
+            run += h[q];
+        }
+    }
+    __syncthreads();
+    const int b = s_b;
+    // 2. the band's keys above bin b, and its keys of bin b appended to the frame's boundary list
+    int D = 0;
+    if (b < 0) {
+        D = tid == 0 ? total : 0;
+    } else {
+        for (int g0 = 0; g0 < total; g0 += 4 * SL_T) {
+            uint64_t key[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int g = g0 + u * SL_T + tid;
+                key[u] = 0ull;
+                if (g < total) {
+                    const int k = sel_tile_of(g, total, nt, s_pre, s_tof);
+                    key[u] = cand[(size_t)(t0 + k) * ST_TCAP + (g - s_pre[k])];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int g = g0 + u * SL_T + tid;
+                const int bin = g < total ? (int)sel_bin(key[u], d.thr_bits) : -1;
+                D += bin > b ? 1 : 0;
+                const unsigned long long m = ballot64(bin == b);
+                if (m) {
+                    uint32_t p0 = 0u;
+                    if (lane == 0) p0 = atomicAdd(&ctl->nbnd, (unsigned)__popcll(m));
+                    p0 = __shfl(p0, 0);
+                    if (bin == b)
+                        st_sc1_u64(bnd + p0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)), key[u]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) D += __shfl_xor(D, off);
+    if (lane == 0) s_w[wave] = (uint32_t)D;
+    __syncthreads();
+    if (tid == 0) st_sc1(&ctl->dcount[w], (int)(s_w[0] + s_w[1] + s_w[2] + s_w[3]));
+    if (!arrive_last(&ctl->arrive, VO_SEL_BANDS, &s_last)) return;
+    // 3. last workgroup of the frame: the threshold key, each band's first position
+    const int nbk = (int)__hip_atomic_load((gu32*)&ctl->nbnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int need = N - s_above;                        // boundary keys to select (b >= 0)
+    uint64_t Tb = 0ull;
+    const bool in_lds = nbk <= SL_RANK_MAX;
+    if (b >= 0) {
+        if (in_lds) {
+            for (int e = tid; e < nbk; e += SL_T) s_key[e] = ld_sc1_u64(bnd + e);
+            __syncthreads();
+            for (int e = tid; e < nbk; e += SL_T) {
+                const uint64_t ke = s_key[e];
+                int rank = 0;
+                for (int f = 0; f < nbk; ++f) rank += s_key[f] > ke ? 1 : 0;
+                if (rank == need - 1) s_tb = ke;
+            }
+            __syncthreads();
+            Tb = s_tb;
+        } else {
+            uint64_t prefix = 0ull, pmask = 0ull;
+            int rem = need;
+            for (int shift = 56; shift >= 0; shift -= 8) {
+                s_dh[tid] = 0u;
+                __syncthreads();
+                for (int e = tid; e < nbk; e += SL_T) {
+                    const uint64_t v = ld_sc1_u64(bnd + e);
+                    if ((v & pmask) == prefix) atomicAdd(&s_dh[(v >> shift) & 0xFF], 1u);
+                }
+                __syncthreads();
+                // digit tid: keys of the prefix with digit >= tid; the selected digit is the one where
+                // that count first reaches rem
+                const uint32_t c = s_dh[tid];
+                const uint32_t ge = sel_suffix(c, s_w);
+                if (ge >= (uint32_t)rem && ge - c < (uint32_t)rem) { s_dsel = tid; s_rem = rem - (int)(ge - c); }
+                __syncthreads();
+                prefix |= (uint64_t)s_dsel << shift;
+                pmask |= 0xFFull << shift;
+                rem = s_rem;
+                __syncthreads();
+            }
+            Tb = prefix;                                 // one key matches all 64 bits
+        }
+    }
+    if (tid < VO_SEL_BANDS) s_cnt[tid] = ld_sc1(&ctl->dcount[tid]);
+    __syncthreads();
+    if (b >= 0) {
+        const int nbr = (nty + VO_SEL_BANDS - 1) / VO_SEL_BANDS;
+        for (int e = tid; e < nbk; e += SL_T) {
+            const uint64_t v = in_lds ? s_key[e] : ld_sc1_u64(bnd + e);
+            if (v >= Tb) atomicAdd(&s_cnt[(int)((v >> 16) & 0xFFFF) / ST_TH / nbr], 1);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int pre = 0;
+        for (int k = 0; k < VO_SEL_BANDS; ++k) { ctl->base[k] = pre; pre += s_cnt[k]; }
+        ctl->b = b;
+        ctl->Tb = Tb;
+        ctl->arrive = 0u;                                // for the next launch (the kernel boundary orders it)
+        ctl->nbnd = 0u;
+        const int slot = ext_slot(d, f0, z, slot_override);
+        d.ext_n[slot] = C < N ? C : N;
+        d.ext_st[slot] = VO_STATUS_OK;
+    }
+    // every band has read the histogram: leave it zeroed for the next frame's stencil
+    uint4* hp = reinterpret_cast<uint4*>(hist) + 4 * tid;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) hp[q] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+__global__ void __launch_bounds__(SL_T) k_select_emit(VoDev d, int f0, int slot_override, int nb)
+{
+    int z, w;
+    if (!xcd_frame(d, VO_SEL_BANDS, nb, z, w)) return;
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ uint32_t s_w[4];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int N = d.N;
+    const int ntx = (d.W + ST_TW - 1) / ST_TW, nty = (d.H + ST_TH - 1) / ST_TH;
+    const SelBandLayout L = sel_band_layout(ntx, nty);
+    uint4* s_rows = reinterpret_cast<uint4*>(smem + L.rows);
+    int* s_pre = reinterpret_cast<int*>(smem + L.pre);
+    uint16_t* s_tof = reinterpret_cast<uint16_t*>(smem + L.tof);
+    uint64_t* s_bits = reinterpret_cast<uint64_t*>(smem + L.bits);
+    uint16_t* s_seg = reinterpret_cast<uint16_t*>(smem + L.seg);  // per (row - r0) * ntx + tile column
+    uint32_t* s_seg32 = reinterpret_cast<uint32_t*>(smem + L.seg);
+    const uint8_t* tilerows = d.tilerows + (size_t)z * d.ntiles * ST_TH;
+    const uint64_t* cand = d.cand + (size_t)z * d.cand_cap;
+    const VoSelCtl* ctl = d.selctl + z;
+    const int b = ctl->b, base = ctl->base[w];
+    const uint64_t Tb = ctl->Tb;
+    int ty0, ty1;
+    sel_band(nty, w, ty0, ty1);
+    const int t0 = ty0 * ntx, nt = (ty1 - ty0) * ntx, r0 = ty0 * ST_TH, nseg = (ty1 - ty0) * ST_TH * ntx;
+    if (nt <= 0) return;
+    for (int s = tid; s < (nseg + 1) / 2; s += SL_T) s_seg32[s] = 0u;
+    const int total = sel_band_table(tilerows, t0, nt, s_rows, s_pre, s_tof, s_w);
+    auto selected = [&](uint64_t key) -> bool {
+        if (b < 0) return true;
+        const int bin = (int)sel_bin(key, d.thr_bits);
+        return bin > b || (bin == b && key >= Tb);
+    };
+    auto seg_of = [&](uint64_t key, int k) { return ((int)((key >> 16) & 0xFFFF) - r0) * ntx + (t0 + k) % ntx; };
+    // 1. selection bitmap (a wave's 64 keys are one word) and selected keys per segment (u16 pairs)
+    for (int g0 = 0; g0 < total; g0 += 4 * SL_T) {
+        uint64_t key[4];
+        int kk[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int g = g0 + u * SL_T + tid;
+            key[u] = 0ull;
+            kk[u] = 0;
+            if (g < total) {
+                kk[u] = sel_tile_of(g, total, nt, s_pre, s_tof);
+                key[u] = cand[(size_t)(t0 + kk[u]) * ST_TCAP + (g - s_pre[kk[u]])];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int g = g0 + u * SL_T + tid;
+            if (g0 + u * SL_T >= total) break;
+            const bool sel = g < total && selected(key[u]);
+            const unsigned long long m = ballot64(sel);
+            if (lane == 0 && g < total) s_bits[g >> 6] = m;
+            if (sel) {
+                const int sg = seg_of(key[u], kk[u]);
+                atomicAdd(&s_seg32[sg >> 1], 1u << (16 * (sg & 1)));
+            }
+        }
+    }
+    __syncthreads();
+    // 2. exclusive scan of the segments in raster order: thread tid owns [tid cw, tid cw + cw)
+    {
+        const int cw = (nseg + SL_T - 1) / SL_T;
+        const int s0 = min(tid * cw, nseg), s1 = min(s0 + cw, nseg);
+        uint32_t mine = 0u;
+        for (int s = s0; s < s1; ++s) mine += s_seg[s];
+        const uint32_t after = sel_suffix(mine, s_w);    // this thread's and every later thread's
+        __shared__ uint32_t s_sum;
+        if (tid == 0) s_sum = after;
+        __syncthreads();
+        uint32_t pre = s_sum - after;
+        for (int s = s0; s < s1; ++s) {
+            const uint32_t v = s_seg[s];
+            s_seg[s] = (uint16_t)pre;                    // <= N <= 4096
+            pre += v;
+        }
+    }
+    __syncthreads();
+    // 3. each selected key at base + its segment's start + the selected keys before it in the
+    //    segment (contiguous compact indices: a segment is one row of one tile)
+    const int slot = ext_slot(d, f0, z, slot_override);
+    int2* out = d.kps + (size_t)slot * N;
+    for (int g0 = 0; g0 < total; g0 += 4 * SL_T) {
+        uint64_t key[4];
+        int kk[4];
+        bool sel[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int g = g0 + u * SL_T + tid;
+            sel[u] = g < total && ((s_bits[g >> 6] >> (g & 63)) & 1ull);
+            key[u] = 0ull;
+            kk[u] = 0;
+            if (sel[u]) {
+                kk[u] = sel_tile_of(g, total, nt, s_pre, s_tof);
+                key[u] = cand[(size_t)(t0 + kk[u]) * ST_TCAP + (g - s_pre[kk[u]])];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (!sel[u]) continue;
+            const int g = g0 + u * SL_T + tid;
+            const int row = (int)((key[u] >> 16) & 0xFFFF), col = (int)(key[u] & 0xFFFF);
+            const int r = row & (ST_TH - 1);
+            // the segment's first compact index: the tile's first plus its row counts below r
+            const uint4 rc = s_rows[kk[u]];
+            const uint32_t w4[4] = {rc.x, rc.y, rc.z, rc.w};
+            int start = s_pre[kk[u]];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int sh = 8 * min(max(r - 4 * q, 0), 4);
+                const uint32_t msk = (uint32_t)(0xFFFFFFFFull >> (32 - sh));
+                start = (int)__builtin_amdgcn_udot4(w4[q] & msk, 0x01010101u, (uint32_t)start, false);
+            }
+            // selected keys in [start, g): at most two bitmap words (a segment holds <= 28 keys)
+            int within = 0;
+            for (int wi = start >> 6; wi <= (g >> 6); ++wi) {
+                uint64_t m = s_bits[wi];
+                if (wi == (start >> 6)) m &= ~0ull << (start & 63);
+                if (wi == (g >> 6)) m &= (g & 63) ? (~0ull >> (64 - (g & 63))) : 0ull;
+                within += __popcll(m);
+            }
+            const int pos = base + (int)s_seg[seg_of(key[u], kk[u])] + within;
+            if (pos < N) out[pos] = make_int2(col, row);  // < N by construction
+        }
+    }
+}
+
 // extract side of a missing image (VisualOdometry.cpp:77-82): the slot holds no keypoints
 __global__ void k_ext_missing(VoDev d, int slot)
 {
@@ -3507,7 +3922,27 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
 }
 void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_select, dim3(nb), dim3(1024), (size_t)d.sel_lds, s, d, f0, slot_override);
+    if (d.sel1) {
+        hipLaunchKernelGGL(k_select, dim3(nb), dim3(1024), (size_t)d.sel_lds, s, d, f0, slot_override);
+        return;
+    }
+    const dim3 g(xcd_grid(VO_SEL_BANDS, nb));
+    // the count kernel uses the layout's tile table only (rows, pre, tof)
+    const int cnt_lds = sel_band_layout((d.W + ST_TW - 1) / ST_TW, (d.H + ST_TH - 1) / ST_TH).bits;
+    hipLaunchKernelGGL(k_select_count, g, dim3(SL_T), (size_t)cnt_lds, s, d, f0, slot_override, nb);
+    hipLaunchKernelGGL(k_select_emit, g, dim3(SL_T), (size_t)d.sel_emit_lds, s, d, f0, slot_override, nb);
+}
+int select_emit_lds_bytes(int W, int H)
+{
+    const int ntx = (W + ST_TW - 1) / ST_TW, nty = (H + ST_TH - 1) / ST_TH;
+    const int bytes = sel_band_layout(ntx, nty).total;
+    if (bytes > 150 * 1024) return -1;
+    if (bytes > 64 * 1024) {
+        if (hipFuncSetAttribute((const void*)k_select_emit, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess ||
+            hipFuncSetAttribute((const void*)k_select_count, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
+            return -1;
+    }
+    return bytes;
 }
 void launch_ext_missing(const VoDev& d, int slot, hipStream_t s)
 {

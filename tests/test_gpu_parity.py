@@ -150,12 +150,24 @@ def test_extract_bit_exact(which, ctx_kitti, scene, factory):
     (1000, 300, 2000, "noise"),     # ragged: W, H not multiples of the 64x16 stencil tile
     (752, 480, 2000, "sparse"),     # fewer survivors than N: no top-N threshold
     (640, 480, 64, "scene"),        # tiny N: the boundary bin holds most of the ranking
+    (1280, 720, 500, "periodic"),   # identical blobs: thousands of equal responses in the boundary bin
+    (1280, 720, 1500, "periodic"),  #   (ranked by the radix select over the boundary list)
 ])
-def test_extract_sizes_bit_exact(W, H, N, kind):
+@pytest.mark.parametrize("sel1", ["", "0", "1"])
+def test_extract_sizes_bit_exact(W, H, N, kind, sel1, monkeypatch):
+    """Top-N select at every size, by the default form for the frame size ("": banded from 1024
+    stencil tiles up, one workgroup per frame below) and forced banded ("0") / single ("1")."""
+    if sel1:
+        monkeypatch.setenv("VO_SEL1", sel1)
     if kind == "scene":
         img = SceneSequence(W, H, nframes=2, step=0.05).frames()[1]
     elif kind == "noise":
         img = noise_frames(W, H, 1)[0]
+    elif kind == "periodic":
+        img = np.full((H, W), 60, np.uint8)
+        for y in range(40, H - 48, 12):
+            for x in range(40, W - 48, 12):
+                img[y:y + 5, x:x + 5] = 200
     else:
         img = np.full((H, W), 100, np.uint8)
         rng = np.random.default_rng(5)
