@@ -198,16 +198,21 @@ int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride, hipStream_t st)
     } else {
         for (int y = 0; y < H; ++y) std::memcpy(c->stage_host + (size_t)y * W, gray + (size_t)y * stride, W);
     }
-    HIPCHK(hipMemcpyAsync(c->d.frame_in, c->stage_host, (size_t)W * H, hipMemcpyHostToDevice, st));
+    // a copy kernel on the frame's own queue reads the pinned staging buffer (a copy-engine transfer
+    // measured 15 us plus a ~14 us engine -> compute-queue hand-off before the next kernel)
+    vo::launch_h2d(c->d.frame_in, c->stage_host, (size_t)W * H, st);
+    HIPCHK(hipGetLastError());
     return VO_OK;
 }
 
 // stage extract (vo_extract / vo_response): frame_in -> slot VO_STAGE_SLOT, scratch 0
 void enqueue_stage_extract(vo_ctx* c)
 {
-    vo::launch_stencil(c->d, c->d.frame_in, 0, 1, 0, c->s);
-    vo::launch_select(c->d, 0, 1, c->d.ring + 1, c->s);
-    vo::launch_describe(c->d, 0, 1, c->d.ring + 1, 0u, c->s);
+    VoDev d = c->d;
+    d.single = 1;                       // one frame: latency-shaped launches
+    vo::launch_stencil(d, d.frame_in, 0, 1, 0, c->s);
+    vo::launch_select(d, 0, 1, d.ring + 1, c->s);
+    vo::launch_describe(d, 0, 1, d.ring + 1, 0u, c->s);
 }
 
 // Timing: every timed launch is bracketed by two events on the stream it runs on (all
@@ -273,9 +278,10 @@ void timed(vo_ctx* c, EvRec* ev, int k, hipStream_t st, F&& launch)
 // q2 (optional): select and describe on a second queue after the stencil (event e_s)
 int enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, int nb, bool publish,
                     hipStream_t q, EvRec* ev, int eq, hipEvent_t ev_stencil = nullptr, hipStream_t q2 = nullptr,
-                    hipEvent_t e_s = nullptr)
+                    hipEvent_t e_s = nullptr, bool single = false)
 {
     VoDev d = c->d;
+    d.single = single ? 1 : 0;          // the single-frame call: latency-shaped extract launches
     const size_t B = (size_t)c->B;
     d.eq = eq;
     d.blurred += d.bplane * B * eq;
@@ -362,12 +368,17 @@ VoDev pass_dev(const vo_ctx* c, int p)
 // triangulation and finalize on the fit queue, so the next pass's match overlaps them; the pass
 // first waits for pass p - 2's finalize (its buffer set and its state snapshot).  Otherwise every
 // kernel on the pose queue and the window comes from the state (every earlier pass finalized).
-void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax, bool pipelined)
+void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax, bool pipelined, bool single = false)
 {
     hipStream_t s = c->s;
     const int p = c->npass++;
     VoDev d = pass_dev(c, p);
     d.gmax = gmax;
+    if (single) {
+        // one frame per call: its window holds at most two records (a repair window's dual ones)
+        d.single = 1;
+        d.gridw = std::min(2, d.WB);
+    }
     d.pass = p;
     d.nospec = pipelined ? 0 : 1;
     hipStream_t sf = pipelined ? c->sf : s;
@@ -385,8 +396,9 @@ void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax,
         timed(c, ev, 6, sf, [&] { vo::launch_triangulate(d, 0, sf); });
         timed(c, ev, 7, sf, [&] { vo::launch_finalize(d, out, out_base, sf); });
     }
-    // the T_curr chain and the pose rows on the trajectory queue (serial mode: the pose queue)
-    hipStream_t q = c->serial ? s : c->st;
+    // the T_curr chain and the pose rows on the trajectory queue (serial mode and the single-frame
+    // call: the pose queue, no cross-queue event)
+    hipStream_t q = c->serial || single ? s : c->st;
     hipEvent_t ef = pipelined ? c->ev_fn[p % vo_ctx::kPassEv] : c->ev_fin;
     if (q != sf || pipelined) {
         (void)hipEventRecord(ef, sf);
@@ -431,7 +443,6 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         for (hipStream_t q : c->se) HIPCHK(hipStreamWaitEvent(q, c->ev_reset, 0));
         c->reset_pending = false;
     }
-    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&c->d.st->end, end, 1, s));
     const std::vector<int> sched = batch_schedule(nf, B, hs ? VO_HOST_FIRST_BATCH : 0);
     // extract batch j on its queue (+ its event in event-wait mode)
     std::vector<int> f0s(sched.size() + 1, 0);
@@ -468,7 +479,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
             if (rc) return rc;
         } else {
             int rc = enqueue_extract(c, img0 + (size_t)f0 * frame_bytes, frame_bytes, base + f0, cnt, publish, q, ev,
-                                     eq, nullptr, q2, e_s);
+                                     eq, nullptr, q2, e_s, host_frame);
             if (rc) return rc;
         }
         hipStream_t qd = q2 ? q2 : q;
@@ -513,7 +524,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         }
         // the chunk's first pass sees every earlier pass finalized (the last call synchronised):
         // its window comes from the state; later passes are pipelined
-        enqueue_pass(c, out, out_base, ev, base + f0s[k + 1], multi && c->pipeline && k > 0);
+        enqueue_pass(c, out, out_base, ev, base + f0s[k + 1], multi && c->pipeline && k > 0, host_frame);
         return VO_OK;
     };
     if (!img0 && !hs) {
@@ -542,15 +553,22 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         HIPCHK(hipGetLastError());
         // the chunk's output rows (complete once the trajectory queue's last k_traj ran, which
         // waited for the last k_finalize) and the commit point
-        hipStream_t tq = c->serial ? s : c->st;
+        hipStream_t tq = c->serial || host_frame ? s : c->st;
         HIPCHK(hipMemcpyAsync(c->out_host + (base - out_base), out + (base - out_base), sizeof(VoFrameOut) * nf,
                               hipMemcpyDeviceToHost, tq));
-        // the commit point after the last finalize (the fit queue's, which the trajectory queue waited for)
-        HIPCHK(hipMemcpyAsync(c->lo_host, &c->d.st->lo, sizeof(int32_t), hipMemcpyDeviceToHost, tq));
+        // the commit point after the last finalize (the fit queue's, which the trajectory queue waited
+        // for).  A single frame's pass (window of one, no speculation) commits it: its row is read
+        // alone and checked to be that frame's
+        if (!host_frame)
+            HIPCHK(hipMemcpyAsync(c->lo_host, &c->d.st->lo, sizeof(int32_t), hipMemcpyDeviceToHost, tq));
         HIPCHK(hipStreamSynchronize(s));
-        if (c->sf) HIPCHK(hipStreamSynchronize(c->sf));
-        HIPCHK(hipStreamSynchronize(tq));
-        const int lo = *c->lo_host;
+        if (c->sf && !host_frame) HIPCHK(hipStreamSynchronize(c->sf));
+        if (tq != s) HIPCHK(hipStreamSynchronize(tq));
+        if (host_frame && nf == 1 && c->out_host[base - out_base].frame != base) {
+            fprintf(stderr, "[vo_mi355x] single-frame pass did not commit frame %d\n", base);
+            return VO_ERR_STATE;
+        }
+        const int lo = host_frame && nf == 1 ? end : *c->lo_host;
         if (lo >= end) break;
         if (lo < base || lo > end || round > nf || (round > 0 && lo <= prev_lo)) {
             fprintf(stderr, "[vo_mi355x] pose passes made no progress (committed %d of [%d, %d), round %d)\n", lo,
@@ -560,7 +578,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         prev_lo = lo;
         // frames after skipped ones: their windows restart at lo (extracts are complete)
         // (the host synchronised: every pass is finalized, so these run from the state, in order)
-        for (int k = 0; k < (end - lo + B - 1) / B; ++k) enqueue_pass(c, out, out_base, ev, end, false);
+        for (int k = 0; k < (end - lo + B - 1) / B; ++k) enqueue_pass(c, out, out_base, ev, end, false, host_frame);
     }
     return ev && ev->err ? ev->err : VO_OK;
 }
@@ -662,6 +680,8 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     d.B = B;
     d.WB = std::min(VO_MAX_WIN, 2 * B);
     if (getenv("VO_WIN")) d.WB = std::max(1, std::min(VO_MAX_WIN, atoi(getenv("VO_WIN"))));
+    d.gridw = d.WB;
+    d.single = 0;
     d.gmax = INT_MAX;
     d.W = W; d.H = H; d.N = N;
     d.ring = VO_RING_DEFAULT;
@@ -1413,6 +1433,24 @@ int vo_selftest_nullvec9(const double* S, const double* x0, double* f, int32_t* 
     HIPCHK(hipMemcpy(f, df, sizeof(double) * 9 * n, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(status, dst, sizeof(int) * n, hipMemcpyDeviceToHost));
     (void)hipFree(dS); (void)hipFree(dx); (void)hipFree(df); (void)hipFree(dst);
+    return VO_OK;
+}
+
+// test hook: one i8 16x16x64 MFMA on per-lane fragments (a, b: 64 x 16 bytes; c, d: 64 x 4 i32)
+int vo_selftest_mfma_i8(const int8_t* a, const int8_t* b, const int32_t* c, int32_t* d, int device)
+{
+    if (!a || !b || !c || !d) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(device));
+    void *da, *db, *dc, *dd;
+    HIPCHK(hipMalloc(&da, 1024)); HIPCHK(hipMalloc(&db, 1024)); HIPCHK(hipMalloc(&dc, 1024)); HIPCHK(hipMalloc(&dd, 1024));
+    HIPCHK(hipMemcpy(da, a, 1024, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(db, b, 1024, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dc, c, 1024, hipMemcpyHostToDevice));
+    vo::launch_selftest_mfma_i8(da, db, dc, dd, nullptr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(d, dd, 1024, hipMemcpyDeviceToHost));
+    (void)hipFree(da); (void)hipFree(db); (void)hipFree(dc); (void)hipFree(dd);
     return VO_OK;
 }
 

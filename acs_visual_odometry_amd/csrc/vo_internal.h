@@ -173,7 +173,7 @@ struct VoSnap {           // the trajectory state after pass p's k_finalize
 // (T_curr: by k_traj only).
 struct VoState {
     int32_t lo;           // frames committed since vo_reset (the next pass starts here)
-    int32_t end;          // end of the frames enqueued so far
+    int32_t end;          // unused (a pass's window is bounded by d.gmax, <= the frames enqueued)
     int32_t prev_slot;    // slot of the last valid frame's keypoints / descriptors (desc1)
     int32_t last_valid;   // VisualOdometry.cpp:62,164
     int32_t model_n;      // FundamentalMatrix model (VisualOdometry.cpp:49): inliers of the last fit
@@ -217,6 +217,8 @@ struct VoDev {
     int max_hyp;
     int B;                // extract batch capacity (frames)
     int WB;               // pose window capacity (frames): min(2 B, VO_MAX_WIN), VO_WIN overrides
+    int gridw;            // window records a pose-pass launch covers (blockIdx.y): WB; 2 for the single-frame call
+    int single;           // the single-frame call (vo_process_frame): latency-shaped launches
     int gmax;             // pose pass: frames < gmax are extracted (the pass's wait covers them)
     int eq;               // extract queue of this launch (its scratch copy and counters)
     int xcd_map;          // extract kernels place a frame's workgroups on one XCD (VO_XCD=0: off)
@@ -295,6 +297,10 @@ void launch_traj(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s); 
 void launch_traj_range(const VoDev& d, VoFrameOut* out, int out_base, int lo, int nc, hipStream_t s);   // vo_rechain
 void launch_pose_stage(const VoDev& d, int phase, hipStream_t s);   // vo_pose: 0 prepare, 1 choose
 void launch_reset(const VoDev& d, hipStream_t s);                   // vo_reset's device state
+// n bytes from pinned host memory to the device by a copy kernel on s (a single frame's upload:
+// no copy-engine -> compute-queue hand-off in front of the stencil)
+void launch_h2d(uint8_t* dst, const uint8_t* src_pinned, size_t n, hipStream_t s);
+void launch_selftest_mfma_i8(const void* a, const void* b, const void* c, void* d, hipStream_t s);
 void launch_selftest_nullvec9(const double* S, const double* x0, double* f, int* status, int n, hipStream_t s);
 void launch_selftest_arith(const float* fa, const float* fb, float* fo, const double* da,
                            const double* db, double* dout, int n, hipStream_t s);

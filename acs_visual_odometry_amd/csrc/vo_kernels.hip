@@ -559,7 +559,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
     const int c0 = xs - 8 + 2 * lane;                          // this lane's columns: c0, c0 + 1
     const int xl0 = refl101(c0, W), xl1 = refl101(c0 + 1, W);  // BORDER_REFLECT_101
     const bool out_lane = lane >= 4 && lane < 4 + ST_SW / 2;  // columns xs .. xs + ST_SW - 1
-    const int boff = out_lane ? c0 : 0x40000000;               // blurred store: out of range off the strip
+    // blurred store: out of range off the strip and past the image's last column pair (the plane's
+    // padding columns are never read)
+    const int boff = out_lane && c0 < W ? c0 : 0x40000000;
     const bool isB = lane >= 4 + ST_TW / 2;                   // the strip's second tile
     const bool hasB = 2 * sxi + 1 < ntx;
     // the wave's columns reach the image's outer two columns, where gradients (kernel .c:59-76)
@@ -629,10 +631,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             BE = st_f2{(float)((ha >> 16) & 255u), (float)((hb >> 16) & 255u)};
             if constexpr (P >= 3) {
                 // blurred row ys - 10 + k: the plane is padded to whole strips and 4 rows past the
-                // last tile, so every output lane stores (rows past the segment are the next
-                // segment's, the same values)
+                // last tile, so every output lane stores; rows past the segment are the next
+                // segment's (the same values, stored by its wave): their row offset is put out of
+                // range, so the store is dropped without a branch
+                const int brow = k < SEG + 10 ? (ys - 10 + k) * Wb : 0x40000000;
                 __builtin_amdgcn_raw_buffer_store_b16((unsigned short)__builtin_amdgcn_perm(hb, ha, 0x0c0c0602u), rblur, boff,
-                                                      (ys - 10 + k) * Wb, 0);
+                                                      brow, 0);
             }
         }
         if constexpr (P >= 2) {
@@ -1936,7 +1940,7 @@ __host__ __device__ inline int match_blocks(int N, int match_bits)
     return match_bits == 32 ? (N + MT_QPB - 1) / MT_QPB : (N + MT512_QPB - 1) / MT512_QPB;
 }
 
-// Window of a pose pass: frames [lo, lo + n), n = min(win, st->end - lo, d.gmax - lo) with
+// Window of a pose pass: frames [lo, lo + n), n = min(win, d.gmax - lo) (gmax <= the frames enqueued) with
 // win <= d.WB: up to WB frames (2 extract batches), but only frames the pass's extract wait
 // covers (d.gmax), so the window grows when the pose queue lags behind the extract queue and each
 // pass's fixed latency is spread over more frames.  win is WB, or d.repair_win after a pass whose
@@ -1965,7 +1969,7 @@ __device__ __forceinline__ VoPlan pass_window(const VoDev& d)
             P.lo = s.lo; P.dual = s.dual; P.prev0 = s.prev_slot; win = s.win;
         }
     }
-    P.n = max(0, min(min(st->end, d.gmax) - P.lo, win > 0 && win < d.WB ? win : d.WB));
+    P.n = max(0, min(d.gmax - P.lo, win > 0 && win < d.WB ? win : d.WB));
     return P;
 }
 __device__ __forceinline__ VoPlan pass_plan(const VoDev& d) { return d.plan[d.pass & (VO_PASS_RING - 1)]; }
@@ -2138,6 +2142,7 @@ __device__ __forceinline__ void top2_merge(uint32_t& m1, uint32_t& m2, uint32_t 
     m1 = n1v;
 }
 
+template <int QPL>
 __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
 {
     const int wf = blockIdx.y;
@@ -2148,12 +2153,12 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
     __shared__ unsigned s_last;
     __shared__ int s_wsum[32];
     __shared__ uint4 s_cand4[1024];                  // 4096 prefixes
-    __shared__ uint2 s_top[3][MT_QPL][64];
+    __shared__ uint2 s_top[3][QPL][64];
     uint32_t* s_cand = reinterpret_cast<uint32_t*>(s_cand4);
     const int N = d.N, n1 = m.n1, n2 = m.n2;
     // wave-uniform candidate range: scalar loop counter, key index an SGPR operand
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (blockIdx.x * MT_QPB < n1) {
+    if (blockIdx.x * (64 * QPL) < n1) {
         const uint32_t* cand = d.pre + (size_t)m.cur * N;
         for (int j0 = threadIdx.x; j0 < n2; j0 += 4 * 256) {
             uint32_t v[4];
@@ -2163,25 +2168,25 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
             for (int u = 0; u < 4; ++u)
                 if (j0 + u * 256 < n2) s_cand[j0 + u * 256] = v[u];
         }
-        // lane's queries: blockIdx.x * MT_QPB + 64 u + lane
-        uint32_t qv[MT_QPL];
+        // lane's queries: blockIdx.x * (64 * QPL) + 64 u + lane
+        uint32_t qv[QPL];
 #pragma unroll
-        for (int u = 0; u < MT_QPL; ++u) {
-            const int q = blockIdx.x * MT_QPB + 64 * u + lane;
+        for (int u = 0; u < QPL; ++u) {
+            const int q = blockIdx.x * (64 * QPL) + 64 * u + lane;
             qv[u] = q < n1 ? d.pre[(size_t)m.prev * N + q] : 0u;
         }
         // quarter of the candidates: [j0, j1), j0 a multiple of 4
         const int qs = ((n2 + 15) >> 4) << 2;
         const int j0 = min(wave * qs, n2), j1 = min(j0 + qs, n2);
-        uint32_t a1[MT_QPL], a2[MT_QPL], b1[MT_QPL], b2[MT_QPL];
+        uint32_t a1[QPL], a2[QPL], b1[QPL], b2[QPL];
 #pragma unroll
-        for (int u = 0; u < MT_QPL; ++u) a1[u] = a2[u] = b1[u] = b2[u] = 0xFFFFFFFFu;
+        for (int u = 0; u < QPL; ++u) a1[u] = a2[u] = b1[u] = b2[u] = 0xFFFFFFFFu;
         __syncthreads();
         int j = j0;
         for (; j + 4 <= j1; j += 4) {
             const uint4 c = s_cand4[j >> 2];
 #pragma unroll
-            for (int u = 0; u < MT_QPL; ++u) {
+            for (int u = 0; u < QPL; ++u) {
                 top2_insert2(((uint32_t)__popc(qv[u] ^ c.x) << 16) | (uint32_t)j,
                              ((uint32_t)__popc(qv[u] ^ c.y) << 16) | (uint32_t)(j + 1), a1[u], a2[u]);
                 top2_insert2(((uint32_t)__popc(qv[u] ^ c.z) << 16) | (uint32_t)(j + 2),
@@ -2191,28 +2196,152 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
         for (; j < j1; ++j) {
             const uint32_t cj = s_cand[j];
 #pragma unroll
-            for (int u = 0; u < MT_QPL; ++u) top2_insert(((uint32_t)__popc(qv[u] ^ cj) << 16) | (uint32_t)j, a1[u], a2[u]);
+            for (int u = 0; u < QPL; ++u) top2_insert(((uint32_t)__popc(qv[u] ^ cj) << 16) | (uint32_t)j, a1[u], a2[u]);
         }
 #pragma unroll
-        for (int u = 0; u < MT_QPL; ++u) {
+        for (int u = 0; u < QPL; ++u) {
             top2_merge(a1[u], a2[u], b1[u], b2[u]);
             if (wave > 0) s_top[wave - 1][u][lane] = make_uint2(a1[u], a2[u]);
         }
         __syncthreads();
         if (wave == 0) {
 #pragma unroll
-            for (int u = 0; u < MT_QPL; ++u) {
+            for (int u = 0; u < QPL; ++u) {
 #pragma unroll
                 for (int w = 0; w < 3; ++w) {
                     const uint2 o = s_top[w][u][lane];
                     top2_merge(a1[u], a2[u], o.x, o.y);
                 }
-                const int q = blockIdx.x * MT_QPB + 64 * u + lane;
+                const int q = blockIdx.x * (64 * QPL) + 64 * u + lane;
                 if (q < n1) st_sc1(m.match_j + q, ratio_accept(a1[u], a2[u], d.ratio));
             }
         }
     }
     if (blockIdx.x == 0) VO_STAMP(d, 1993, 1);
+    if (!arrive_last(&m.w->ctr[0], gridDim.x, &s_last)) return;
+    match_compact(d, wf, m, s_wsum);
+}
+
+// MFMA form of the 32-test matcher (k_match_mfma): the all-pairs Hamming distances of a frame
+// pair are an integer matrix product.  With a = +-1 per bit of a candidate's 32-bit prefix and
+// b = +-1 per bit of a query's, dot(a, b) = 32 - 2 dist, so one v_mfma_i32_16x16x64_i8 over
+// A' = -64 a (candidates: rows) and B' = 64 b (queries: columns) gives -4096 dot for 16 x 16 pairs.
+// The rest of K and the C input turn the product straight into the sort key the top-2 keeps:
+//   k = 32, 33   A = (t & 127, 64 (t >> 7)) of candidate tile t, B = (16, 32): + 16 t
+//   C            131072 + the candidate's row in the tile
+// so D = 4096 (32 - dot) + 16 t + row = 8192 dist + j: the (dist, first index) order of the
+// sequential loop (feature_matching_parallel.cpp:72-99), with no VALU per pair but the top-2
+// update.  Lane l holds A[l & 15][16 (l >> 4) + i] / B[16 (l >> 4) + i][l & 15] in byte i of its
+// fragments and D[4 (l >> 4) + r][l & 15] in register r (tests/test_gpu_parity.py
+// test_mfma_i8_operand_maps).  The cur frame's candidates are expanded once per workgroup into an
+// LDS table (32 B each); a wave owns MM_G groups of 16 queries and walks every candidate tile,
+// one ds_read_b128 and MM_G MFMAs per tile; the four lane groups of a query (rows 4h .. 4h + 3)
+// merge by shuffles at the end.  Results equal k_match's bit for bit.
+#define MM_G 4                        // query groups of 16 per wave: 64 queries per wave, 256 per workgroup
+typedef int mm_v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t mm_spread4(uint32_t n) { return (n * 0x00204081u) & 0x01010101u; }   // n < 16
+__host__ __device__ inline int mm_lds_bytes(int N)
+{
+    const int nt = (N + 15) / 16;
+    return nt * 16 * 32 + nt * 16 + 16;
+}
+__device__ __forceinline__ int ratio_accept13(uint32_t m1, uint32_t m2, float ratio)
+{
+    if (m1 == 0xFFFFFFFFu || m2 == 0xFFFFFFFFu) return -1;
+    const int d1 = (int)(m1 >> 13), d2 = (int)(m2 >> 13);
+    return ((float)d1 < ratio * (float)d2) ? (int)(m1 & 8191u) : -1;
+}
+
+__global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
+{
+    const int wf = blockIdx.y;
+    const VoPlan P = match_window(d, stage);
+    if (wf >= vwin_records(P)) return;
+    MatchFrame m;
+    if (!match_header(d, stage, P, wf, m)) return;
+    __shared__ unsigned s_last;
+    __shared__ int s_wsum[32];
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int N = d.N, n1 = m.n1, n2 = m.n2;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int q0 = blockIdx.x * 256;
+    if (q0 < n1) {
+        const int ntile = (n2 + 15) >> 4;                          // 0 tiles: every query rejected
+        uint4* s_tab = reinterpret_cast<uint4*>(smem);             // candidate j: s_tab[2 j] bits 0..15, [2 j + 1] 16..31
+        uint4* s_tt = s_tab + 2 * 16 * ntile;                      // tile t: its index bytes (k = 32, 33)
+        uint4* s_zero = s_tt + ntile;                              // k = 48 .. 63
+        const uint32_t* cpre = d.pre + (size_t)m.cur * N;
+        for (int j = tid; j < 16 * ntile; j += 256) {
+            const uint32_t p = j < n2 ? cpre[j] : 0u;
+            uint32_t w[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) w[q] = (mm_spread4((p >> (4 * q)) & 15u) << 7) | 0x40404040u;   // bit -> 0xC0 (-64)
+            s_tab[2 * j] = make_uint4(w[0], w[1], w[2], w[3]);
+            s_tab[2 * j + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+        }
+        for (int t = tid; t < ntile; t += 256)
+            s_tt[t] = make_uint4((uint32_t)(t & 127) | ((uint32_t)(64 * (t >> 7)) << 8), 0u, 0u, 0u);
+        if (tid == 0) *s_zero = make_uint4(0u, 0u, 0u, 0u);
+        // query fragments: B' = 64 b (bit -> 0x40, clear -> 0xC0); k = 32, 33 -> 16, 32
+        const int h = lane >> 4, col = lane & 15;
+        const uint32_t* qpre = d.pre + (size_t)m.prev * N;
+        mm_v4i b[MM_G];
+#pragma unroll
+        for (int g = 0; g < MM_G; ++g) {
+            const int q = q0 + wave * 64 + g * 16 + col;
+            const uint32_t p = q < n1 ? qpre[q] : 0u;
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            if (h < 2) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    w[i] = ((mm_spread4((p >> (16 * h + 4 * i)) & 15u) ^ 0x01010101u) << 7) | 0x40404040u;
+            } else if (h == 2) {
+                w[0] = 16u | (32u << 8);
+            }
+            b[g] = mm_v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+        }
+        const mm_v4i cc = {131072 + 4 * h, 131072 + 4 * h + 1, 131072 + 4 * h + 2, 131072 + 4 * h + 3};
+        __syncthreads();
+        const uint4* abase = h < 2 ? s_tab + 2 * col + h : (h == 2 ? s_tt : s_zero);
+        const int astep = h < 2 ? 32 : (h == 2 ? 1 : 0);          // uint4 per tile
+        uint32_t a1[MM_G], a2[MM_G], c1[MM_G], c2[MM_G];
+#pragma unroll
+        for (int g = 0; g < MM_G; ++g) a1[g] = a2[g] = c1[g] = c2[g] = 0xFFFFFFFFu;
+        const int full = n2 >> 4;                                  // tiles without padding rows
+        auto tile = [&](int t, bool pad) {
+            const uint4 av = abase[t * astep];
+            const mm_v4i a = {(int)av.x, (int)av.y, (int)av.z, (int)av.w};
+#pragma unroll
+            for (int g = 0; g < MM_G; ++g) {
+                mm_v4i dk = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b[g], cc, 0, 0, 0);
+                uint32_t k0 = (uint32_t)dk.x, k1 = (uint32_t)dk.y, k2 = (uint32_t)dk.z, k3 = (uint32_t)dk.w;
+                if (pad) {
+                    const int r0 = 16 * t + 4 * h;
+                    if (r0 >= n2) k0 = 0xFFFFFFFFu;
+                    if (r0 + 1 >= n2) k1 = 0xFFFFFFFFu;
+                    if (r0 + 2 >= n2) k2 = 0xFFFFFFFFu;
+                    if (r0 + 3 >= n2) k3 = 0xFFFFFFFFu;
+                }
+                top2_insert2(k0, k1, a1[g], a2[g]);
+                top2_insert2(k2, k3, c1[g], c2[g]);
+            }
+        };
+        int t = 0;
+        for (; t + 2 <= full; t += 2) { tile(t, false); tile(t + 1, false); }
+        for (; t < ntile; ++t) tile(t, t >= full);
+#pragma unroll
+        for (int g = 0; g < MM_G; ++g) {
+            top2_merge(a1[g], a2[g], c1[g], c2[g]);
+            // the query's four lane groups (rows 4h .. 4h + 3 of every tile)
+#pragma unroll
+            for (int off = 16; off <= 32; off <<= 1) {
+                const uint32_t o1 = __shfl_xor(a1[g], off), o2 = __shfl_xor(a2[g], off);
+                top2_merge(a1[g], a2[g], o1, o2);
+            }
+            const int q = q0 + wave * 64 + g * 16 + col;
+            if (h == 0 && q < n1) st_sc1(m.match_j + q, ratio_accept13(a1[g], a2[g], d.ratio));
+        }
+    }
     if (!arrive_last(&m.w->ctr[0], gridDim.x, &s_last)) return;
     match_compact(d, wf, m, s_wsum);
 }
@@ -3807,6 +3936,33 @@ __global__ void __launch_bounds__(256) k_traj_range(VoDev d, VoFrameOut* out, in
 
 // vo_reset on the device (VisualOdometry.cpp:50-62 initial state): trajectory state, slot
 // statuses, histograms, window records and cross-queue counters; no host round trip
+// a frame from pinned host memory (read over PCIe by the kernel) into device memory: four
+// 16-byte loads in flight per thread, the tail bytes by the first thread
+__global__ void __launch_bounds__(256) k_h2d(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, size_t n)
+{
+    const size_t n16 = n / 16, i0 = (size_t)blockIdx.x * 1024 + threadIdx.x;
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (i0 + 256 * u < n16) v[u] = s4[i0 + 256 * u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (i0 + 256 * u < n16) d4[i0 + 256 * u] = v[u];
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (size_t i = n16 * 16; i < n; ++i) dst[i] = src[i];
+}
+
+// test hook: one v_mfma_i32_16x16x64_i8 on per-lane fragments (16 bytes of A, 16 of B, 4 i32 of C
+// per lane) -- the operand lane maps the MFMA matcher relies on are pinned by tests/test_gpu_parity.py
+typedef int mf_v4i __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(64) k_selftest_mfma_i8(const mf_v4i* a, const mf_v4i* b, const mf_v4i* c, mf_v4i* d)
+{
+    const int l = threadIdx.x;
+    d[l] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[l], b[l], c[l], 0, 0, 0);
+}
+
 __global__ void __launch_bounds__(256) k_reset(VoDev d)
 {
     const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
@@ -3904,7 +4060,10 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
     ensure_tables();
     const int ntx = (d.W + ST_TW - 1) / ST_TW, nsx = (ntx + 1) / 2, nty = (d.H + ST_TH - 1) / ST_TH;
     static const int segt = getenv("VO_STSEG") ? atoi(getenv("VO_STSEG")) : ST_SEGT_DEFAULT;
-    const int st = write_response ? 4 : segt == 2 || segt == 6 || segt == 8 || segt == 12 ? segt : ST_SEGT_DEFAULT;
+    // one frame (the per-frame call): segments of one tile row, so the frame's waves (4x 8-tile
+    // segments' count) each walk 30 source rows instead of 142 -- the latency of the launch
+    const int st = write_response ? 4 : nb == 1 && d.single ? 1
+                 : segt == 2 || segt == 6 || segt == 8 || segt == 12 ? segt : ST_SEGT_DEFAULT;
     const int waves = nsx * ((nty + st - 1) / st);                 // one (strip, segment) per wave
     dim3 g(xcd_grid((waves + 3) / 4, nb));
     if (write_response)
@@ -3917,12 +4076,14 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
         hipLaunchKernelGGL((k_stencil<6, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
     else if (st == 2)
         hipLaunchKernelGGL((k_stencil<2, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
+    else if (st == 1)
+        hipLaunchKernelGGL((k_stencil<1, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
     else
         hipLaunchKernelGGL((k_stencil<4, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
 }
 void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s)
 {
-    if (d.sel1) {
+    if (d.sel1 && !(d.single && d.sel_emit_lds >= 0)) {   // single frames: always banded (8 workgroups, not 1)
         hipLaunchKernelGGL(k_select, dim3(nb), dim3(1024), (size_t)d.sel_lds, s, d, f0, slot_override);
         return;
     }
@@ -3970,14 +4131,31 @@ void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned
 void launch_match(const VoDev& d, int stage, hipStream_t s)
 {
     if (d.match_bits == 32)
-        hipLaunchKernelGGL(k_match, dim3(match_blocks(d.N, 32), stage ? 1 : d.WB), dim3(256), 0, s, d, stage);
+    {
+        static const int mm_env = getenv("VO_MATCH_MFMA") ? atoi(getenv("VO_MATCH_MFMA")) : 1;
+        static const bool mm_ok = [] {
+            return hipFuncSetAttribute((const void*)k_match_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       mm_lds_bytes(4096)) == hipSuccess;
+        }();
+        if (mm_env && mm_ok) {
+            // all-pairs distances on the matrix cores (k_match_mfma)
+            hipLaunchKernelGGL(k_match_mfma, dim3((d.N + 255) / 256, stage ? 1 : d.gridw), dim3(256),
+                               (size_t)mm_lds_bytes(d.N), s, d, stage);
+            return;
+        }
+        // single-frame calls: one query per lane (4x the workgroups, a quarter of the walk each)
+        if (d.single)
+            hipLaunchKernelGGL(k_match<1>, dim3((d.N + 63) / 64, stage ? 1 : d.gridw), dim3(256), 0, s, d, stage);
+        else
+            hipLaunchKernelGGL(k_match<MT_QPL>, dim3(match_blocks(d.N, 32), stage ? 1 : d.gridw), dim3(256), 0, s, d, stage);
+    }
     else {
         // 64 KB of dynamic LDS plus the static hand-off words: above the default 64 KB cap
         static const bool lds_ok = hipFuncSetAttribute((const void*)k_match512,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        MT512_TILE * 64) == hipSuccess;
         (void)lds_ok;
-        hipLaunchKernelGGL(k_match512, dim3(match_blocks(d.N, 512), stage ? 1 : d.WB), dim3(256),
+        hipLaunchKernelGGL(k_match512, dim3(match_blocks(d.N, 512), stage ? 1 : d.gridw), dim3(256),
                            (size_t)MT512_TILE * 64, s, d, stage);
     }
 }
@@ -3987,7 +4165,7 @@ void launch_match(const VoDev& d, int stage, hipStream_t s)
 // are enough hypotheses to fill the chip, so no wave repeats another's 8-point fit.
 void launch_ransac(const VoDev& d, int stage, hipStream_t s)
 {
-    const int nhyp = d.max_hyp, nb = stage ? 1 : d.WB;
+    const int nhyp = d.max_hyp, nb = stage ? 1 : d.gridw;
     // VO_HYP_CUT1: the second cut (VO_HYP_CHUNK1; >= max_hyp merges the last two chunks)
     static const int cut1 = getenv("VO_HYP_CUT1") ? std::max(VO_HYP_CHUNK0, atoi(getenv("VO_HYP_CUT1"))) : VO_HYP_CHUNK1;
     const int cut[3] = {std::min(nhyp, VO_HYP_CHUNK0), std::min(nhyp, cut1), nhyp};
@@ -4004,7 +4182,7 @@ void launch_ransac(const VoDev& d, int stage, hipStream_t s)
 }
 void launch_refit(const VoDev& d, int with_pose, int stage, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_refit, dim3(stage ? 1 : d.WB), dim3(RF_T), 0, s, d, with_pose, stage);
+    hipLaunchKernelGGL(k_refit, dim3(stage ? 1 : d.gridw), dim3(RF_T), 0, s, d, with_pose, stage);
 }
 void launch_triangulate(const VoDev& d, int stage, hipStream_t s, VoFrameOut* out, int out_base, int fin)
 {
@@ -4012,7 +4190,7 @@ void launch_triangulate(const VoDev& d, int stage, hipStream_t s, VoFrameOut* ou
     static const int bpf_env = getenv("VO_TRI_BPF") ? atoi(getenv("VO_TRI_BPF")) : TRI_BPF_DEFAULT;
     const int full = (4 * d.N + TRI_BLOCK - 1) / TRI_BLOCK;
     const int bpf = bpf_env > 0 ? std::min(bpf_env, full) : full;
-    hipLaunchKernelGGL(k_triangulate, dim3(bpf, stage ? 1 : d.WB), dim3(TRI_BLOCK), 0, s, d, stage, out, out_base, fin);
+    hipLaunchKernelGGL(k_triangulate, dim3(bpf, stage ? 1 : d.gridw), dim3(TRI_BLOCK), 0, s, d, stage, out, out_base, fin);
 }
 void launch_finalize(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s)
 {
@@ -4026,6 +4204,17 @@ void launch_traj(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s)
 void launch_traj_range(const VoDev& d, VoFrameOut* out, int out_base, int lo, int nc, hipStream_t s)
 {
     hipLaunchKernelGGL(k_traj_range, dim3(1), dim3(256), 0, s, d, out, out_base, lo, nc);
+}
+void launch_selftest_mfma_i8(const void* a, const void* b, const void* c, void* d, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_selftest_mfma_i8, dim3(1), dim3(64), 0, s, (const mf_v4i*)a, (const mf_v4i*)b,
+                       (const mf_v4i*)c, (mf_v4i*)d);
+}
+void launch_h2d(uint8_t* dst, const uint8_t* src, size_t n, hipStream_t s)
+{
+    const size_t n16 = n / 16;
+    const int blocks = (int)std::max<size_t>(1, (n16 + 4 * 256 - 1) / (4 * 256));
+    hipLaunchKernelGGL(k_h2d, dim3(blocks), dim3(256), 0, s, dst, src, n);
 }
 void launch_reset(const VoDev& d, hipStream_t s)
 {

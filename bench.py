@@ -95,11 +95,13 @@ def profile_row(prof, kernel: str):
     normalised by the passes (k_match calls) and the extract kernels by the batches (k_stencil)."""
     if not prof:
         return None
-    names = {ROCPROF_NAME[kernel]} | ({"k_match512"} if kernel == "match" else set())   # 512-test mode
+    # the forms a stage can take: the 512-test and MFMA matchers, the banded select's two kernels
+    names = {ROCPROF_NAME[kernel]} | {"match": {"k_match512", "k_match_mfma"},
+                                      "select": {"k_select_count", "k_select_emit"}}.get(kernel, set())
     rows = [r for k, r in prof.items() if k.split("<")[0] in names]
     if not rows:
         return None
-    ref = {"k_match", "k_match512"} if kernel in POSE_QUEUE or kernel == "trajectory" else {"k_stencil"}
+    ref = {"k_match", "k_match512", "k_match_mfma"} if kernel in POSE_QUEUE or kernel == "trajectory" else {"k_stencil"}
     ref_calls = [r["calls"] for k, r in prof.items() if k.split("<")[0] in ref]
     launches = max(ref_calls) if ref_calls else max(r["calls"] for r in rows)
 

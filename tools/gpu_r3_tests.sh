@@ -1,0 +1,10 @@
+# full -m gpu suite + smoke, then the per-frame call trace (tools/gpu_pf.sh)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r3tests}; mkdir -p $O
+timeout -k 10 840 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { echo PYTEST_FAIL; grep -E "FAILED|ERROR" $O/pytest.log | tail -5; tail -60 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo SMOKE_FAIL; tail -20 $O/smoke.log; exit 1; }
+cat $O/smoke.log
+bash tools/gpu_pf.sh ${1:-r3tests}/pf
