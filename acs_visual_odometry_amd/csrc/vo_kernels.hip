@@ -1911,6 +1911,14 @@ __device__ __forceinline__ void top2_insert2(uint32_t k1, uint32_t k2, uint32_t&
     asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(m1), "v"(k1), "v"(k2));   // left alone, LLVM emits two v_min_u32
     m1 = r;
 }
+// the same without inline asm: for keys straight out of an MFMA.  The compiler's hazard recognizer
+// does not see through inline asm, so an asm v_min3_u32 on MFMA results was scheduled right after the
+// MFMA that writes them, without the wait states (stale reads: rows differed from run to run)
+__device__ __forceinline__ void top2_insert2_c(uint32_t k1, uint32_t k2, uint32_t& m1, uint32_t& m2)
+{
+    m2 = min(med3_u32(m1, k1, k2), m2);
+    m1 = min(min(m1, k1), k2);
+}
 __device__ __forceinline__ void top2_wave(uint32_t& m1, uint32_t& m2)
 {
 #pragma unroll
@@ -2233,17 +2241,18 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
 // sequential loop (feature_matching_parallel.cpp:72-99), with no VALU per pair but the top-2
 // update.  Lane l holds A[l & 15][16 (l >> 4) + i] / B[16 (l >> 4) + i][l & 15] in byte i of its
 // fragments and D[4 (l >> 4) + r][l & 15] in register r (tests/test_gpu_parity.py
-// test_mfma_i8_operand_maps).  The cur frame's candidates are expanded once per workgroup into an
-// LDS table (32 B each); a wave owns MM_G groups of 16 queries and walks every candidate tile,
+// test_mfma_i8_operand_maps).  The cur frame's candidates are expanded per workgroup into an LDS
+// table (32 B each, MM_CH at a time); a wave owns MM_G groups of 16 queries and walks every candidate tile,
 // one ds_read_b128 and MM_G MFMAs per tile; the four lane groups of a query (rows 4h .. 4h + 3)
 // merge by shuffles at the end.  Results equal k_match's bit for bit.
 #define MM_G 4                        // query groups of 16 per wave: 64 queries per wave, 256 per workgroup
+#define MM_CH 512                     // candidates per LDS chunk (16 KB table: LDS stays free for the
+                                      // extract kernels co-running on the CU)
 typedef int mm_v4i __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t mm_spread4(uint32_t n) { return (n * 0x00204081u) & 0x01010101u; }   // n < 16
-__host__ __device__ inline int mm_lds_bytes(int N)
+__host__ __device__ inline int mm_lds_bytes(int)
 {
-    const int nt = (N + 15) / 16;
-    return nt * 16 * 32 + nt * 16 + 16;
+    return MM_CH * 32 + (MM_CH / 16) * 16 + 16;
 }
 __device__ __forceinline__ int ratio_accept13(uint32_t m1, uint32_t m2, float ratio)
 {
@@ -2266,21 +2275,10 @@ __global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int q0 = blockIdx.x * 256;
     if (q0 < n1) {
-        const int ntile = (n2 + 15) >> 4;                          // 0 tiles: every query rejected
-        uint4* s_tab = reinterpret_cast<uint4*>(smem);             // candidate j: s_tab[2 j] bits 0..15, [2 j + 1] 16..31
-        uint4* s_tt = s_tab + 2 * 16 * ntile;                      // tile t: its index bytes (k = 32, 33)
-        uint4* s_zero = s_tt + ntile;                              // k = 48 .. 63
+        uint4* s_tab = reinterpret_cast<uint4*>(smem);             // chunk candidate c: s_tab[2 c] bits 0..15, [2 c + 1] 16..31
+        uint4* s_tt = s_tab + 2 * MM_CH;                           // chunk tile u: its index bytes (k = 32, 33)
+        uint4* s_zero = s_tt + MM_CH / 16;                         // k = 48 .. 63
         const uint32_t* cpre = d.pre + (size_t)m.cur * N;
-        for (int j = tid; j < 16 * ntile; j += 256) {
-            const uint32_t p = j < n2 ? cpre[j] : 0u;
-            uint32_t w[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) w[q] = (mm_spread4((p >> (4 * q)) & 15u) << 7) | 0x40404040u;   // bit -> 0xC0 (-64)
-            s_tab[2 * j] = make_uint4(w[0], w[1], w[2], w[3]);
-            s_tab[2 * j + 1] = make_uint4(w[4], w[5], w[6], w[7]);
-        }
-        for (int t = tid; t < ntile; t += 256)
-            s_tt[t] = make_uint4((uint32_t)(t & 127) | ((uint32_t)(64 * (t >> 7)) << 8), 0u, 0u, 0u);
         if (tid == 0) *s_zero = make_uint4(0u, 0u, 0u, 0u);
         // query fragments: B' = 64 b (bit -> 0x40, clear -> 0xC0); k = 32, 33 -> 16, 32
         const int h = lane >> 4, col = lane & 15;
@@ -2301,20 +2299,21 @@ __global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
             b[g] = mm_v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
         }
         const mm_v4i cc = {131072 + 4 * h, 131072 + 4 * h + 1, 131072 + 4 * h + 2, 131072 + 4 * h + 3};
-        __syncthreads();
         const uint4* abase = h < 2 ? s_tab + 2 * col + h : (h == 2 ? s_tt : s_zero);
         const int astep = h < 2 ? 32 : (h == 2 ? 1 : 0);          // uint4 per tile
         uint32_t a1[MM_G], a2[MM_G], c1[MM_G], c2[MM_G];
 #pragma unroll
         for (int g = 0; g < MM_G; ++g) a1[g] = a2[g] = c1[g] = c2[g] = 0xFFFFFFFFu;
-        const int full = n2 >> 4;                                  // tiles without padding rows
-        auto tile = [&](int t, bool pad) {
-            const uint4 av = abase[t * astep];
-            const mm_v4i a = {(int)av.x, (int)av.y, (int)av.z, (int)av.w};
+        // software-pipelined by hand: a tile's MFMAs are issued, then the PREVIOUS tile's keys are
+        // consumed, with scheduling barriers between, so at least MM_G MFMAs (64+ cycles) separate an
+        // MFMA from the first VALU read of its result -- well past the MFMA -> VALU read wait states
+        // (the compiler's count for this VGPR-destination form read stale keys in one build)
+        const int ntile = (n2 + 15) >> 4;
+        // keys of candidate tile t into the top-2 chains; rows past n2 (the last tile only) excluded
+        auto consume = [&](const mm_v4i (&dk)[MM_G], bool pad, int t) {
 #pragma unroll
             for (int g = 0; g < MM_G; ++g) {
-                mm_v4i dk = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b[g], cc, 0, 0, 0);
-                uint32_t k0 = (uint32_t)dk.x, k1 = (uint32_t)dk.y, k2 = (uint32_t)dk.z, k3 = (uint32_t)dk.w;
+                uint32_t k0 = (uint32_t)dk[g].x, k1 = (uint32_t)dk[g].y, k2 = (uint32_t)dk[g].z, k3 = (uint32_t)dk[g].w;
                 if (pad) {
                     const int r0 = 16 * t + 4 * h;
                     if (r0 >= n2) k0 = 0xFFFFFFFFu;
@@ -2322,13 +2321,69 @@ __global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
                     if (r0 + 2 >= n2) k2 = 0xFFFFFFFFu;
                     if (r0 + 3 >= n2) k3 = 0xFFFFFFFFu;
                 }
-                top2_insert2(k0, k1, a1[g], a2[g]);
-                top2_insert2(k2, k3, c1[g], c2[g]);
+                top2_insert2_c(k0, k1, a1[g], a2[g]);
+                top2_insert2_c(k2, k3, c1[g], c2[g]);
             }
         };
-        int t = 0;
-        for (; t + 2 <= full; t += 2) { tile(t, false); tile(t + 1, false); }
-        for (; t < ntile; ++t) tile(t, t >= full);
+        auto issue = [&](mm_v4i (&dk)[MM_G], int u) {
+            const uint4 av = abase[u * astep];
+            const mm_v4i a = {(int)av.x, (int)av.y, (int)av.z, (int)av.w};
+#pragma unroll
+            for (int g = 0; g < MM_G; ++g) dk[g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b[g], cc, 0, 0, 0);
+        };
+        // ping-pong over two key sets: tile u's MFMAs are issued before tile u - 1's keys are read, with
+        // scheduling barriers between, so MM_G MFMAs (64+ cycles) separate an MFMA from the first VALU
+        // read of its result -- past the MFMA -> VALU wait states by construction (the compiler's count
+        // for this VGPR-destination form read stale keys in one build)
+        mm_v4i dA[MM_G], dB[MM_G];
+        bool pend = false;                                         // dB holds a tile not yet consumed
+        for (int t0 = 0; t0 < ntile; t0 += MM_CH / 16) {
+            const int nt = min(MM_CH / 16, ntile - t0);
+            if (t0 > 0) __syncthreads();                           // the previous chunk's table is read
+            // the chunk's candidates: A' = -64 a (bit set -> 0xC0, clear -> 0x40); index bytes per tile
+            for (int c = tid; c < 16 * nt; c += 256) {
+                const int j = 16 * t0 + c;
+                const uint32_t p = j < n2 ? cpre[j] : 0u;
+                uint32_t w[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) w[q] = (mm_spread4((p >> (4 * q)) & 15u) << 7) | 0x40404040u;
+                s_tab[2 * c] = make_uint4(w[0], w[1], w[2], w[3]);
+                s_tab[2 * c + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+            }
+            if (tid < nt) {
+                const int t = t0 + tid;
+                s_tt[tid] = make_uint4((uint32_t)(t & 127) | ((uint32_t)(64 * (t >> 7)) << 8), 0u, 0u, 0u);
+            }
+            __syncthreads();
+            int u = 0;
+            for (; u + 1 < nt; u += 2) {
+                issue(dA, u);
+                __builtin_amdgcn_sched_barrier(0);
+                if (pend) consume(dB, false, 0);                   // never the padded last tile
+                __builtin_amdgcn_sched_barrier(0);
+                issue(dB, u + 1);
+                __builtin_amdgcn_sched_barrier(0);
+                consume(dA, false, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                pend = true;
+            }
+            if (u < nt) {                                          // odd tile count: the chunk's last tile
+                issue(dA, u);
+                __builtin_amdgcn_sched_barrier(0);
+                if (pend) consume(dB, false, 0);
+                asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int g = 0; g < MM_G; ++g) dB[g] = dA[g];
+                __builtin_amdgcn_sched_barrier(0);
+                pend = true;
+            }
+        }
+        if (pend) {
+            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // the last tile's MFMAs have landed
+            __builtin_amdgcn_sched_barrier(0);
+            consume(dB, (n2 & 15) != 0, ntile - 1);
+        }
 #pragma unroll
         for (int g = 0; g < MM_G; ++g) {
             top2_merge(a1[g], a2[g], c1[g], c2[g]);

@@ -100,3 +100,27 @@ def test_config5_stream_of_8_sequences():
         sl = slice(s * F, (s + 1) * F)
         assert st[s * F] == 1
         _check(refs[s], poses[sl], st[sl], info[sl])
+
+
+def test_stream_repeats_bit_identical_under_timing_modes():
+    """The bench's stream (8 sequences at +1.0 m/frame, here 80 frames each) run five times from
+    vo_reset with every kernel-timing mode the bench uses (off, all launches bracketed by events,
+    every 4th launch of one kernel): the rows are identical every time.  Timing events move kernels
+    relative to each other, so a missing wait state or a cross-queue race shows up here as rows that
+    differ from run to run (an inline-asm read of MFMA results without its wait states did)."""
+    F, S = 80, 8
+    seqs = [SceneSequence(nframes=F, step=1.0, seq=s) for s in range(S)]
+    frames = render_sequences([(q.W, q.H, F, q.seq, 1.0) for q in seqs], 8)
+    ctx = Context(seqs[0].W, seqs[0].H, K=seqs[0].K)
+    df = ctx.device_frames(np.concatenate(frames))
+    gt = np.concatenate([q.gt() for q in seqs])
+    runs = []
+    for timing in (0, 1, 103, 0, 104):
+        ctx.reset()
+        ctx.set_ground_truth(gt)
+        ctx.set_sequence_starts([F * i for i in range(1, S)])
+        runs.append(ctx.process_frames_device(df, timing=timing))
+    df.free()
+    ctx.close()
+    for r in runs[1:]:
+        assert all(np.array_equal(a, b) for a, b in zip(runs[0], r))
