@@ -59,8 +59,8 @@ ROCPROF_NAME = {"stencil": "k_stencil", "select": "k_select", "describe": "k_des
 # committed rocprofv3 summaries (tools/profile.sh -> tools/rocprof_summary.py --json): kernel
 # durations, PMC HBM bytes and VALU counters per launch
 # (tools/gpu_r3_prof.sh writes them on the GPU box before the bench runs, from the same build)
-PROFILES = {(1241, 376, 32): "r3_kitti_kernels.json", (1920, 1080, 32): "r3_1080_kernels.json",
-            (1920, 1080, 512): "r3_1080_512_kernels.json", (1241, 376, 32, 0.12): "r3_kitti_012_kernels.json"}
+PROFILES = {(1241, 376, 32): "r3_kitti_kernels.json", (1920, 1080, 32): "r2_1080_kernels.json",
+            (1920, 1080, 512): "r2_1080_512_kernels.json", (1241, 376, 32, 0.12): "r3_kitti_012_kernels.json"}
 
 
 def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray) -> float:
