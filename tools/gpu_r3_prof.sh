@@ -6,7 +6,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r3prof}; shift; mkdir -p $O
-BUILD=$(cat BUILD_ID 2>/dev/null || echo unknown)
+BUILD=$(tr "\n" " " < BUILD_ID 2>/dev/null || echo unknown)
 for w in "$@"; do
   case $w in
     kitti) A="" ; T="kitti: bench.py --no-variants --no-check (8 sequences at 1.0 m/frame, the headline workload)";;
