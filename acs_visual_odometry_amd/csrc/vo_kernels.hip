@@ -2245,7 +2245,8 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
 // table (32 B each, MM_CH at a time); a wave owns MM_G groups of 16 queries and walks every candidate tile,
 // one ds_read_b128 and MM_G MFMAs per tile; the four lane groups of a query (rows 4h .. 4h + 3)
 // merge by shuffles at the end.  Results equal k_match's bit for bit.
-#define MM_G 4                        // query groups of 16 per wave: 64 queries per wave, 256 per workgroup
+#define MM_GROUPS 4                   // query groups of 16 per wave: 64 queries per wave, 256 per workgroup
+                                      // (the single-frame call: 1, 64 per workgroup, 4x the workgroups)
 #define MM_CH 512                     // candidates per LDS chunk (16 KB table: LDS stays free for the
                                       // extract kernels co-running on the CU)
 typedef int mm_v4i __attribute__((ext_vector_type(4)));
@@ -2261,6 +2262,7 @@ __device__ __forceinline__ int ratio_accept13(uint32_t m1, uint32_t m2, float ra
     return ((float)d1 < ratio * (float)d2) ? (int)(m1 & 8191u) : -1;
 }
 
+template <int MM_G>
 __global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
 {
     const int wf = blockIdx.y;
@@ -2273,7 +2275,7 @@ __global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
     extern __shared__ __align__(16) unsigned char smem[];
     const int N = d.N, n1 = m.n1, n2 = m.n2;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int q0 = blockIdx.x * 256;
+    const int q0 = blockIdx.x * 64 * MM_G;
     if (q0 < n1) {
         uint4* s_tab = reinterpret_cast<uint4*>(smem);             // chunk candidate c: s_tab[2 c] bits 0..15, [2 c + 1] 16..31
         uint4* s_tt = s_tab + 2 * MM_CH;                           // chunk tile u: its index bytes (k = 32, 33)
@@ -2286,7 +2288,7 @@ __global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
         mm_v4i b[MM_G];
 #pragma unroll
         for (int g = 0; g < MM_G; ++g) {
-            const int q = q0 + wave * 64 + g * 16 + col;
+            const int q = q0 + wave * 16 * MM_G + g * 16 + col;
             const uint32_t p = q < n1 ? qpre[q] : 0u;
             uint32_t w[4] = {0u, 0u, 0u, 0u};
             if (h < 2) {
@@ -2393,7 +2395,7 @@ __global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
                 const uint32_t o1 = __shfl_xor(a1[g], off), o2 = __shfl_xor(a2[g], off);
                 top2_merge(a1[g], a2[g], o1, o2);
             }
-            const int q = q0 + wave * 64 + g * 16 + col;
+            const int q = q0 + wave * 16 * MM_G + g * 16 + col;
             if (h == 0 && q < n1) st_sc1(m.match_j + q, ratio_accept13(a1[g], a2[g], d.ratio));
         }
     }
@@ -2480,6 +2482,144 @@ __global__ void __launch_bounds__(256) k_match512(VoDev d, int stage)
             }
         }
         if (q < n1) st_sc1(m.match_j + q, ratio_accept(m1, m2, d.ratio));
+    }
+    if (!arrive_last(&m.w->ctr[0], gridDim.x, &s_last)) return;
+    match_compact(d, wf, m, s_wsum);
+}
+
+// MFMA form of the 512-test matcher (k_match512_mfma): the same +-1 products as k_match_mfma over
+// all 512 tests, eight chained v_mfma_i32_16x16x64_i8 per (candidate tile, query group), so
+// D = 4096 (512 - dot) + C = 8192 dist + j with the index in C (C = 2^21 + 16 t + row: K is taken
+// by the tests).  Candidates are expanded MM5_CH at a time into an LDS table (512 B each: step s,
+// lane half h at bytes 64 s + 16 h); a wave owns MM5_G groups of 16 queries.  Keys are read with the
+// next tile's MFMAs in between (ping-pong, as k_match_mfma).  Results equal k_match512's.
+#define MM5_G 4                       // query groups of 16 per wave: 64 queries per wave, 256 per workgroup
+#define MM5_CH 64                     // candidates per LDS chunk (32 KB)
+__global__ void __launch_bounds__(256) k_match512_mfma(VoDev d, int stage)
+{
+    const int wf = blockIdx.y;
+    const VoPlan P = match_window(d, stage);
+    if (wf >= vwin_records(P)) return;
+    MatchFrame m;
+    if (!match_header(d, stage, P, wf, m)) return;
+    __shared__ unsigned s_last;
+    __shared__ int s_wsum[32];
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int N = d.N, n1 = m.n1, n2 = m.n2;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int q0 = blockIdx.x * 256;
+    if (q0 < n1) {
+        uint4* s_tab = reinterpret_cast<uint4*>(smem);             // candidate c, step s, half h: s_tab[32 c + 4 s + h]
+        const uint32_t* cdesc = reinterpret_cast<const uint32_t*>(d.desc + (size_t)m.cur * N * 8);
+        const uint32_t* qdesc = reinterpret_cast<const uint32_t*>(d.desc + (size_t)m.prev * N * 8);
+        const int h = lane >> 4, col = lane & 15;
+        // query fragments: step s, half h = tests 64 s + 16 h .. + 15 (B' = 64 b: bit -> 0x40, clear -> 0xC0)
+        mm_v4i b[MM5_G][8];
+#pragma unroll
+        for (int g = 0; g < MM5_G; ++g) {
+            const int q = q0 + wave * 64 + g * 16 + col;
+#pragma unroll
+            for (int st = 0; st < 8; ++st) {
+                const uint32_t wd = q < n1 ? qdesc[(size_t)q * 16 + 2 * st + (h >> 1)] : 0u;
+                const uint32_t p = (wd >> (16 * (h & 1))) & 0xFFFFu;
+                uint32_t w[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[i] = ((mm_spread4((p >> (4 * i)) & 15u) ^ 0x01010101u) << 7) | 0x40404040u;
+                b[g][st] = mm_v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+            }
+        }
+        const mm_v4i cc0 = {2097152 + 4 * h, 2097152 + 4 * h + 1, 2097152 + 4 * h + 2, 2097152 + 4 * h + 3};
+        uint32_t a1[MM5_G], a2[MM5_G], c1[MM5_G], c2[MM5_G];
+#pragma unroll
+        for (int g = 0; g < MM5_G; ++g) a1[g] = a2[g] = c1[g] = c2[g] = 0xFFFFFFFFu;
+        const int ntile = (n2 + 15) >> 4;
+        auto consume = [&](const mm_v4i (&dk)[MM5_G], bool pad, int t) {
+#pragma unroll
+            for (int g = 0; g < MM5_G; ++g) {
+                uint32_t k0 = (uint32_t)dk[g].x, k1 = (uint32_t)dk[g].y, k2 = (uint32_t)dk[g].z, k3 = (uint32_t)dk[g].w;
+                if (pad) {
+                    const int r0 = 16 * t + 4 * h;
+                    if (r0 >= n2) k0 = 0xFFFFFFFFu;
+                    if (r0 + 1 >= n2) k1 = 0xFFFFFFFFu;
+                    if (r0 + 2 >= n2) k2 = 0xFFFFFFFFu;
+                    if (r0 + 3 >= n2) k3 = 0xFFFFFFFFu;
+                }
+                top2_insert2_c(k0, k1, a1[g], a2[g]);
+                top2_insert2_c(k2, k3, c1[g], c2[g]);
+            }
+        };
+        // tile u of the chunk = candidate tile t: eight chained MFMAs per query group
+        auto issue = [&](mm_v4i (&dk)[MM5_G], int u, int t) {
+            const uint4* ab = s_tab + 32 * (16 * u + col) + h;
+            const mm_v4i ct = cc0 + 16 * t;
+#pragma unroll
+            for (int g = 0; g < MM5_G; ++g) dk[g] = ct;
+#pragma unroll
+            for (int st = 0; st < 8; ++st) {
+                const uint4 av = ab[4 * st];
+                const mm_v4i a = {(int)av.x, (int)av.y, (int)av.z, (int)av.w};
+#pragma unroll
+                for (int g = 0; g < MM5_G; ++g) dk[g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b[g][st], dk[g], 0, 0, 0);
+            }
+        };
+        mm_v4i dA[MM5_G], dB[MM5_G];
+        bool pend = false;                                         // dB holds a tile not yet consumed
+        for (int t0 = 0; t0 < ntile; t0 += MM5_CH / 16) {
+            const int nt = min(MM5_CH / 16, ntile - t0);
+            if (t0 > 0) __syncthreads();                           // the previous chunk's table is read
+            // the chunk's candidates: A' = -64 a (bit set -> 0xC0, clear -> 0x40); word e of candidate c
+            // (tests 32 e .. 32 e + 31) -> bytes 128 e (d (e / 2) ...) at step e / 2, halves 2 (e & 1), + 1
+            for (int x = tid; x < 16 * nt * 16; x += 256) {
+                const int c = x >> 4, e = x & 15, j = 16 * t0 + c;
+                const uint32_t p = j < n2 ? cdesc[(size_t)j * 16 + e] : 0u;
+                uint32_t w[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) w[q] = (mm_spread4((p >> (4 * q)) & 15u) << 7) | 0x40404040u;
+                uint4* dst = s_tab + 32 * c + 4 * (e >> 1) + 2 * (e & 1);
+                dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+                dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+            }
+            __syncthreads();
+            int u = 0;
+            for (; u + 1 < nt; u += 2) {
+                issue(dA, u, t0 + u);
+                __builtin_amdgcn_sched_barrier(0);
+                if (pend) consume(dB, false, 0);                   // never the padded last tile
+                __builtin_amdgcn_sched_barrier(0);
+                issue(dB, u + 1, t0 + u + 1);
+                __builtin_amdgcn_sched_barrier(0);
+                consume(dA, false, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                pend = true;
+            }
+            if (u < nt) {
+                issue(dA, u, t0 + u);
+                __builtin_amdgcn_sched_barrier(0);
+                if (pend) consume(dB, false, 0);
+                asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int g = 0; g < MM5_G; ++g) dB[g] = dA[g];
+                __builtin_amdgcn_sched_barrier(0);
+                pend = true;
+            }
+        }
+        if (pend) {
+            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            consume(dB, (n2 & 15) != 0, ntile - 1);
+        }
+#pragma unroll
+        for (int g = 0; g < MM5_G; ++g) {
+            top2_merge(a1[g], a2[g], c1[g], c2[g]);
+#pragma unroll
+            for (int off = 16; off <= 32; off <<= 1) {
+                const uint32_t o1 = __shfl_xor(a1[g], off), o2 = __shfl_xor(a2[g], off);
+                top2_merge(a1[g], a2[g], o1, o2);
+            }
+            const int q = q0 + wave * 64 + g * 16 + col;
+            if (h == 0 && q < n1) st_sc1(m.match_j + q, ratio_accept13(a1[g], a2[g], d.ratio));
+        }
     }
     if (!arrive_last(&m.w->ctr[0], gridDim.x, &s_last)) return;
     match_compact(d, wf, m, s_wsum);
@@ -4188,14 +4328,15 @@ void launch_match(const VoDev& d, int stage, hipStream_t s)
     if (d.match_bits == 32)
     {
         static const int mm_env = getenv("VO_MATCH_MFMA") ? atoi(getenv("VO_MATCH_MFMA")) : 1;
-        static const bool mm_ok = [] {
-            return hipFuncSetAttribute((const void*)k_match_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       mm_lds_bytes(4096)) == hipSuccess;
-        }();
+        static const bool mm_ok = mm_lds_bytes(4096) <= 64 * 1024;   // the default dynamic LDS cap
         if (mm_env && mm_ok) {
             // all-pairs distances on the matrix cores (k_match_mfma)
-            hipLaunchKernelGGL(k_match_mfma, dim3((d.N + 255) / 256, stage ? 1 : d.gridw), dim3(256),
-                               (size_t)mm_lds_bytes(d.N), s, d, stage);
+            if (d.single)
+                hipLaunchKernelGGL(k_match_mfma<1>, dim3((d.N + 63) / 64, stage ? 1 : d.gridw), dim3(256),
+                                   (size_t)mm_lds_bytes(d.N), s, d, stage);
+            else
+                hipLaunchKernelGGL(k_match_mfma<MM_GROUPS>, dim3((d.N + 64 * MM_GROUPS - 1) / (64 * MM_GROUPS), stage ? 1 : d.gridw),
+                                   dim3(256), (size_t)mm_lds_bytes(d.N), s, d, stage);
             return;
         }
         // single-frame calls: one query per lane (4x the workgroups, a quarter of the walk each)
@@ -4210,8 +4351,16 @@ void launch_match(const VoDev& d, int stage, hipStream_t s)
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        MT512_TILE * 64) == hipSuccess;
         (void)lds_ok;
-        hipLaunchKernelGGL(k_match512, dim3(match_blocks(d.N, 512), stage ? 1 : d.gridw), dim3(256),
-                           (size_t)MT512_TILE * 64, s, d, stage);
+        static const int mm_env = getenv("VO_MATCH_MFMA") ? atoi(getenv("VO_MATCH_MFMA")) : 1;
+        static const bool mm5_ok = hipFuncSetAttribute((const void*)k_match512_mfma,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       MM5_CH * 512) == hipSuccess;
+        if (mm_env && mm5_ok)
+            hipLaunchKernelGGL(k_match512_mfma, dim3((d.N + 255) / 256, stage ? 1 : d.gridw), dim3(256),
+                               (size_t)MM5_CH * 512, s, d, stage);
+        else
+            hipLaunchKernelGGL(k_match512, dim3(match_blocks(d.N, 512), stage ? 1 : d.gridw), dim3(256),
+                               (size_t)MT512_TILE * 64, s, d, stage);
     }
 }
 // hypotheses in three chunks, [0, C0), [C0, C1), [C1, max_hyp): a frame's later chunks exit at
