@@ -2065,7 +2065,7 @@ __device__ __forceinline__ bool match_header(const VoDev& d, int stage, const Vo
     return status == VO_STATUS_OK;
 }
 
-// The frame's last workgroup (256 threads): ordered compaction of the accepted queries into
+// The frame's last workgroup (its first 256 threads): ordered compaction of the accepted queries into
 // (prev, cur) pairs and f64 points, thread t owning queries [t*per, (t+1)*per); M, scored and
 // the < 8 matches status (VisualOdometry.cpp:108-123).
 __device__ void match_compact(const VoDev& d, int wf, const MatchFrame& m, int* s_wsum)
@@ -2076,6 +2076,7 @@ __device__ void match_compact(const VoDev& d, int wf, const MatchFrame& m, int* 
     constexpr int RC = 8;                         // rounds per pass (s_wsum holds RC x 4 counts)
     const int N = d.N, n1 = m.n1, lane = threadIdx.x & 63;
     const int tid = threadIdx.x, wave = tid >> 6;
+    const bool act = tid < 256;                   // wider workgroups: the extra waves only meet the barriers
     const int2* kp1 = d.kps + (size_t)m.prev * N;
     const int2* kp2 = d.kps + (size_t)m.cur * N;
     int2* match_pairs = d.match_pairs + (size_t)wf * N;
@@ -2087,7 +2088,7 @@ __device__ void match_compact(const VoDev& d, int wf, const MatchFrame& m, int* 
 #pragma unroll
         for (int u = 0; u < RC; ++u) {
             const int i = (r0 + u) * 256 + tid;
-            js[u] = i < n1 ? ld_sc1(m.match_j + i) : -1;
+            js[u] = act && i < n1 ? ld_sc1(m.match_j + i) : -1;
         }
         int2 ka[RC], kb[RC];
 #pragma unroll
@@ -2099,7 +2100,7 @@ __device__ void match_compact(const VoDev& d, int wf, const MatchFrame& m, int* 
 #pragma unroll
         for (int u = 0; u < RC; ++u) {
             bal[u] = ballot64(js[u] >= 0);
-            if (lane == 0) s_wsum[u * 4 + wave] = __popcll(bal[u]);
+            if (lane == 0 && act) s_wsum[u * 4 + wave] = __popcll(bal[u]);
         }
         __syncthreads();
         int pos = pos0;
@@ -2495,7 +2496,8 @@ __global__ void __launch_bounds__(256) k_match512(VoDev d, int stage)
 // next tile's MFMAs in between (ping-pong, as k_match_mfma).  Results equal k_match512's.
 #define MM5_G 4                       // query groups of 16 per wave: 64 queries per wave, 256 per workgroup
 #define MM5_CH 64                     // candidates per LDS chunk (32 KB)
-__global__ void __launch_bounds__(256) k_match512_mfma(VoDev d, int stage)
+#define MM5_W 8                       // waves per workgroup: 512 queries share one expansion of the candidates
+__global__ void __launch_bounds__(64 * MM5_W) k_match512_mfma(VoDev d, int stage)
 {
     const int wf = blockIdx.y;
     const VoPlan P = match_window(d, stage);
@@ -2507,7 +2509,7 @@ __global__ void __launch_bounds__(256) k_match512_mfma(VoDev d, int stage)
     extern __shared__ __align__(16) unsigned char smem[];
     const int N = d.N, n1 = m.n1, n2 = m.n2;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int q0 = blockIdx.x * 256;
+    const int q0 = blockIdx.x * 64 * MM5_W;
     if (q0 < n1) {
         uint4* s_tab = reinterpret_cast<uint4*>(smem);             // candidate c, step s, half h: s_tab[32 c + 4 s + h]
         const uint32_t* cdesc = reinterpret_cast<const uint32_t*>(d.desc + (size_t)m.cur * N * 8);
@@ -2569,7 +2571,7 @@ __global__ void __launch_bounds__(256) k_match512_mfma(VoDev d, int stage)
             if (t0 > 0) __syncthreads();                           // the previous chunk's table is read
             // the chunk's candidates: A' = -64 a (bit set -> 0xC0, clear -> 0x40); word e of candidate c
             // (tests 32 e .. 32 e + 31) -> bytes 128 e (d (e / 2) ...) at step e / 2, halves 2 (e & 1), + 1
-            for (int x = tid; x < 16 * nt * 16; x += 256) {
+            for (int x = tid; x < 16 * nt * 16; x += 64 * MM5_W) {
                 const int c = x >> 4, e = x & 15, j = 16 * t0 + c;
                 const uint32_t p = j < n2 ? cdesc[(size_t)j * 16 + e] : 0u;
                 uint32_t w[8];
@@ -4356,8 +4358,8 @@ void launch_match(const VoDev& d, int stage, hipStream_t s)
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        MM5_CH * 512) == hipSuccess;
         if (mm_env && mm5_ok)
-            hipLaunchKernelGGL(k_match512_mfma, dim3((d.N + 255) / 256, stage ? 1 : d.gridw), dim3(256),
-                               (size_t)MM5_CH * 512, s, d, stage);
+            hipLaunchKernelGGL(k_match512_mfma, dim3((d.N + 64 * MM5_W - 1) / (64 * MM5_W), stage ? 1 : d.gridw),
+                               dim3(64 * MM5_W), (size_t)MM5_CH * 512, s, d, stage);
         else
             hipLaunchKernelGGL(k_match512, dim3(match_blocks(d.N, 512), stage ? 1 : d.gridw), dim3(256),
                                (size_t)MT512_TILE * 64, s, d, stage);

@@ -59,8 +59,8 @@ ROCPROF_NAME = {"stencil": "k_stencil", "select": "k_select", "describe": "k_des
 # committed rocprofv3 summaries (tools/profile.sh -> tools/rocprof_summary.py --json): kernel
 # durations, PMC HBM bytes and VALU counters per launch
 # (tools/gpu_r3_prof.sh writes them on the GPU box before the bench runs, from the same build)
-PROFILES = {(1241, 376, 32): "r3_kitti_kernels.json", (1920, 1080, 32): "r2_1080_kernels.json",
-            (1920, 1080, 512): "r2_1080_512_kernels.json", (1241, 376, 32, 0.12): "r3_kitti_012_kernels.json"}
+PROFILES = {(1241, 376, 32): "r3_kitti_kernels.json", (1920, 1080, 32): "r3_1080_kernels.json",
+            (1920, 1080, 512): "r3_1080_512_kernels.json", (1241, 376, 32, 0.12): "r3_kitti_012_kernels.json"}
 
 
 def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray) -> float:
@@ -96,12 +96,13 @@ def profile_row(prof, kernel: str):
     if not prof:
         return None
     # the forms a stage can take: the 512-test and MFMA matchers, the banded select's two kernels
-    names = {ROCPROF_NAME[kernel]} | {"match": {"k_match512", "k_match_mfma"},
+    names = {ROCPROF_NAME[kernel]} | {"match": {"k_match512", "k_match_mfma", "k_match512_mfma"},
                                       "select": {"k_select_count", "k_select_emit"}}.get(kernel, set())
     rows = [r for k, r in prof.items() if k.split("<")[0] in names]
     if not rows:
         return None
-    ref = {"k_match", "k_match512", "k_match_mfma"} if kernel in POSE_QUEUE or kernel == "trajectory" else {"k_stencil"}
+    ref = ({"k_match", "k_match512", "k_match_mfma", "k_match512_mfma"} if kernel in POSE_QUEUE or kernel == "trajectory"
+           else {"k_stencil"})
     ref_calls = [r["calls"] for k, r in prof.items() if k.split("<")[0] in ref]
     launches = max(ref_calls) if ref_calls else max(r["calls"] for r in rows)
 
