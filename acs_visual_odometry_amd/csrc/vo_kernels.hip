@@ -2340,13 +2340,26 @@ __global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
         // for this VGPR-destination form read stale keys in one build)
         mm_v4i dA[MM_G], dB[MM_G];
         bool pend = false;                                         // dB holds a tile not yet consumed
+        // a chunk's prefixes, thread tid: candidates tid + 256 k; the next chunk's are loaded while
+        // this one is computed
+        constexpr int KC = MM_CH / 256;
+        uint32_t pc[KC];
+        auto fetch = [&](int t0) {
+#pragma unroll
+            for (int k = 0; k < KC; ++k) {
+                const int j = 16 * t0 + tid + 256 * k;
+                pc[k] = j < n2 ? cpre[j] : 0u;
+            }
+        };
+        if (ntile > 0) fetch(0);
         for (int t0 = 0; t0 < ntile; t0 += MM_CH / 16) {
             const int nt = min(MM_CH / 16, ntile - t0);
             if (t0 > 0) __syncthreads();                           // the previous chunk's table is read
             // the chunk's candidates: A' = -64 a (bit set -> 0xC0, clear -> 0x40); index bytes per tile
-            for (int c = tid; c < 16 * nt; c += 256) {
-                const int j = 16 * t0 + c;
-                const uint32_t p = j < n2 ? cpre[j] : 0u;
+#pragma unroll
+            for (int k = 0; k < KC; ++k) {
+                const int c = tid + 256 * k;
+                const uint32_t p = pc[k];
                 uint32_t w[8];
 #pragma unroll
                 for (int q = 0; q < 8; ++q) w[q] = (mm_spread4((p >> (4 * q)) & 15u) << 7) | 0x40404040u;
@@ -2358,6 +2371,7 @@ __global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
                 s_tt[tid] = make_uint4((uint32_t)(t & 127) | ((uint32_t)(64 * (t >> 7)) << 8), 0u, 0u, 0u);
             }
             __syncthreads();
+            if (t0 + MM_CH / 16 < ntile) fetch(t0 + MM_CH / 16);
             int u = 0;
             for (; u + 1 < nt; u += 2) {
                 issue(dA, u);
@@ -2495,7 +2509,7 @@ __global__ void __launch_bounds__(256) k_match512(VoDev d, int stage)
 // lane half h at bytes 64 s + 16 h); a wave owns MM5_G groups of 16 queries.  Keys are read with the
 // next tile's MFMAs in between (ping-pong, as k_match_mfma).  Results equal k_match512's.
 #define MM5_G 4                       // query groups of 16 per wave: 64 queries per wave, 256 per workgroup
-#define MM5_CH 64                     // candidates per LDS chunk (32 KB)
+#define MM5_CH 128                    // candidates per LDS chunk (64 KB; the next chunk's words are loaded during this one)
 #define MM5_W 8                       // waves per workgroup: 512 queries share one expansion of the candidates
 __global__ void __launch_bounds__(64 * MM5_W) k_match512_mfma(VoDev d, int stage)
 {
@@ -2566,22 +2580,38 @@ __global__ void __launch_bounds__(64 * MM5_W) k_match512_mfma(VoDev d, int stage
         };
         mm_v4i dA[MM5_G], dB[MM5_G];
         bool pend = false;                                         // dB holds a tile not yet consumed
+        // a chunk's descriptor words, thread tid: words tid + 64 MM5_W k of the chunk (candidate x / 16,
+        // word x % 16); the next chunk's are loaded while this one is computed
+        constexpr int KW = (MM5_CH * 16 + 64 * MM5_W - 1) / (64 * MM5_W);
+        uint32_t pw[KW];
+        auto fetch = [&](int t0) {
+#pragma unroll
+            for (int k = 0; k < KW; ++k) {
+                const int x = tid + 64 * MM5_W * k, j = 16 * t0 + (x >> 4);
+                pw[k] = x < MM5_CH * 16 && j < n2 ? cdesc[(size_t)j * 16 + (x & 15)] : 0u;
+            }
+        };
+        if (ntile > 0) fetch(0);
         for (int t0 = 0; t0 < ntile; t0 += MM5_CH / 16) {
             const int nt = min(MM5_CH / 16, ntile - t0);
             if (t0 > 0) __syncthreads();                           // the previous chunk's table is read
             // the chunk's candidates: A' = -64 a (bit set -> 0xC0, clear -> 0x40); word e of candidate c
             // (tests 32 e .. 32 e + 31) -> bytes 128 e (d (e / 2) ...) at step e / 2, halves 2 (e & 1), + 1
-            for (int x = tid; x < 16 * nt * 16; x += 64 * MM5_W) {
-                const int c = x >> 4, e = x & 15, j = 16 * t0 + c;
-                const uint32_t p = j < n2 ? cdesc[(size_t)j * 16 + e] : 0u;
-                uint32_t w[8];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) w[q] = (mm_spread4((p >> (4 * q)) & 15u) << 7) | 0x40404040u;
-                uint4* dst = s_tab + 32 * c + 4 * (e >> 1) + 2 * (e & 1);
-                dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
-                dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+            for (int k = 0; k < KW; ++k) {
+                const int x = tid + 64 * MM5_W * k, c = x >> 4, e = x & 15;
+                if (x < MM5_CH * 16) {
+                    const uint32_t p = pw[k];
+                    uint32_t w[8];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) w[q] = (mm_spread4((p >> (4 * q)) & 15u) << 7) | 0x40404040u;
+                    uint4* dst = s_tab + 32 * c + 4 * (e >> 1) + 2 * (e & 1);
+                    dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+                    dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+                }
             }
             __syncthreads();
+            if (t0 + MM5_CH / 16 < ntile) fetch(t0 + MM5_CH / 16);
             int u = 0;
             for (; u + 1 < nt; u += 2) {
                 issue(dA, u, t0 + u);
