@@ -20,9 +20,11 @@ namespace vo {
 // ---------------------------------------------------------------------------
 // constant tables
 // ---------------------------------------------------------------------------
-// per pair t: dx, dy (f32) and 1/|d| split into rh = f32(1/|d|), rl = f32(1/|d| - rh).
-// (ic*d)/|d| in f32 == fmaf(ic*d, rh, (ic*d) * rl) for every ic in [-255,255], every pair and
-// both components (tests/test_describe_division.py, exhaustive; up to the sign of a zero term)
+// per pair t and component c = x, y: the unit direction d_c/|d| split into A_c = f32(d_c/|d|) and
+// B_c = f32(d_c/|d| - A_c) (|d| the reference's f32 norm, the quotient in f64).
+// (ic*d_c)/|d| in f32 == fmaf(ic, A_c, ic * B_c) for every ic in [-255,255], every pair and both
+// components (tests/test_describe_division.py, exhaustive; up to the sign of a zero term): one
+// product and one fma per term and component instead of two products and an fma
 // Rows p of the pair order padded to whole groups of DS_OG terms with zero terms (dx = dy = 0:
 // the term is a zero, which leaves a sum that is never -0 unchanged), so the describe loop has
 // no remainder iterations.
@@ -54,9 +56,9 @@ static void ensure_tables()
     for (int t = 0; t < VO_FREAK_NPAIRS; ++t) {
         const float dx = (float)(px[pp[t]] - px[pq[t]]), dy = (float)(py[pp[t]] - py[pq[t]]);
         const float nrm = sqrtf(dx * dx + dy * dy);    // host sqrtf: correctly rounded
-        const double rn = 1.0 / (double)nrm;
-        const float rh = (float)rn, rl = (float)(rn - (double)rh);
-        orient[o++] = make_float4(dx, dy, rh, rl);
+        const double ux = (double)dx / (double)nrm, uy = (double)dy / (double)nrm;
+        const float ax = (float)ux, ay = (float)uy;
+        orient[o++] = make_float4(ax, ay, (float)(ux - (double)ax), (float)(uy - (double)ay));
         if (pq[t] == VO_FREAK_NPOINTS - 1)             // end of row p: pad to a whole group
             while (o % DS_OG) orient[o++] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
@@ -1689,7 +1691,7 @@ __global__ void k_ext_missing(VoDev d, int slot)
 // keypoint itself, in order (one sample difference serves both components), reading its
 // samples from its own LDS column; pair p's sample stays in a register over the pairs (p, q),
 // the pair table arrives by scalar loads (the pair index is wave-uniform).  The term
-// (ic*d)/|d| is fmaf(x, rh, x * rl) with the reciprocal split into two f32 (equal to the f32
+// (ic*d)/|d| is fmaf(ic, A, ic * B) with the unit direction split into two f32 (equal to the f32
 // division for every reachable ic and pair, tests/test_describe_division.py), so the sums use
 // no f64.  The rotated samples stay in registers and the 512 tests, unrolled with the pattern's
 // pair indices as compile-time constants, are register compares shifted into 32-bit words.
@@ -1725,15 +1727,14 @@ constexpr DsTables ds_make_tables()
 }
 constexpr DsTables kDs = ds_make_tables();
 
-// one orientation term of both components: (ic*dx)/|d|, (ic*dy)/|d| (c = dx, dy, rh, rl), the
+// one orientation term of both components: (ic*dx)/|d|, (ic*dy)/|d| (c = Ax, Ay, Bx, By), the
 // two components as one packed-FP32 pair (v_pk_mul/fma/add_f32: two lanes' worth per
 // instruction, tools/valu_rate.hip; IEEE per element, so the sums are those of the scalar form)
 typedef float ds_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void orient_term(float ic, const float4& c, ds_f2& o)
 {
-    const ds_f2 d = {c.x, c.y};
-    const ds_f2 x = ic * d;                                          // exact: |ic*d| < 2^15
-    o = o + __builtin_elementwise_fma(x, ds_f2{c.z, c.z}, x * ds_f2{c.w, c.w});
+    const ds_f2 i2 = {ic, ic};
+    o = o + __builtin_elementwise_fma(i2, ds_f2{c.x, c.y}, i2 * ds_f2{c.z, c.w});   // fmaf(ic, A, ic * B)
 }
 
 // the 32 tests 32 W .. 32 W + 31 of a keypoint's rotated samples r: bit i = test 32 W + i

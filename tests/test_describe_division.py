@@ -1,8 +1,9 @@
 """The orientation term (ic*d)/|d| (kernels/feature_extraction_kernel_functions.c:159-160, f32
 with a correctly rounded division).  The oracle evaluates it as (float)((double)(ic*d) * (1/|d|));
-the describe kernel as fmaf(x, rh, x * rl) with x = ic*d and rh + rl the reciprocal 1/|d| split
-into two f32 (rh = f32(1/|d|), rl = f32(1/|d| - rh)).  This checks, for every pair of the FREAK
-pattern, both components and every intensity difference ic in [-255, 255], that all three give
+the describe kernel as fmaf(ic, A, ic * B) with the unit direction d/|d| split into two f32
+(A = f32(d/|d|), B = f32(d/|d| - A), the quotient in f64; round 2's kernel used fmaf(x, rh, x * rl)
+with x = ic*d and the reciprocal 1/|d| split the same way).  This checks, for every pair of the FREAK
+pattern, both components and every intensity difference ic in [-255, 255], that all four give
 the same f32 value (the hi/lo form may return +0 where the division returns -0; the orientation
 sums start at +0 and an f32 sum is -0 only if both addends are, so the sums are identical)."""
 import os
@@ -67,5 +68,12 @@ def test_orientation_term_forms_agree_exhaustively():
                 hl = fma32(num, np.full_like(num, rh), num * rl)
                 assert np.array_equal(hl, ref)                  # value equality: +0 == -0
                 assert np.array_equal(hl.view(np.uint32) & 0x7FFFFFFF, ref.view(np.uint32) & 0x7FFFFFFF)
+                # the kernel's form (vo_kernels.hip ensure_tables / orient_term)
+                u = np.float64(dd) / np.float64(nrm)
+                A = np.float32(u)
+                B = np.float32(u - np.float64(A))
+                ab = fma32(ic, np.full_like(ic, A), ic * B)
+                assert np.array_equal(ab, ref)
+                assert np.array_equal(ab.view(np.uint32) & 0x7FFFFFFF, ref.view(np.uint32) & 0x7FFFFFFF)
                 checked += num.size
     assert checked == 903 * 2 * 511
