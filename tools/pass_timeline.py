@@ -45,7 +45,7 @@ def main():
             print(f"   {name:28s} n {len(v):4d}  sum {sum(v):8.1f}  mean {np.mean(v):7.1f}  gap-before mean "
                   f"{np.mean(g):6.1f}")
     # one pose pass in the middle of the selection
-    m = [i for i, k in enumerate(sel) if k["name"] == "k_match"]
+    m = [i for i, k in enumerate(sel) if k["name"].startswith("k_match")]
     if len(m) >= 3:
         i0 = m[len(m) // 2]
         q = sel[i0]["q"]

@@ -34,13 +34,13 @@ def main():
     a, b = spans[idx]
     seg = ks[a:b]
     t0 = seg[0]["s"]
-    pq = Counter(k["q"] for k in seg if k["n"] == "k_match").most_common(1)[0][0]
+    pq = Counter(k["q"] for k in seg if k["n"].startswith("k_match")).most_common(1)[0][0]
     print("interval", idx, "stencil starts (us):", [round((k["s"] - t0) / 1e3) for k in seg if k["n"] == "k_stencil"])
     passes, cur = [], None
     for k in seg:
         if k["q"] != pq or not k["n"].startswith("k_"):
             continue
-        if k["n"] == "k_match":
+        if k["n"].startswith("k_match"):
             cur = [k]
             passes.append(cur)
         elif cur is not None:
