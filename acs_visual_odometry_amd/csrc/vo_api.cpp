@@ -698,11 +698,11 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
         d.maxit_initial = to_int_x86(std::log(1.0 - k.ransac_p) / std::log(1.0 - std::pow(1.0 - outlierRatio, 8.0)));
     }
     d.max_hyp = std::max(VO_MAX_HYP, std::min(d.maxit_initial, 1 << 20));
-    // stencil tiles of VO_TILE_W x VO_TILE_H, at most 1/4 of a tile's pixels are strict maxima
+    // stencil tiles of VO_TILE_W x VO_TILE_H, at most VO_TILE_CAP strict maxima each
     const int ntiles = ((W + VO_TILE_W - 1) / VO_TILE_W) * ((H + VO_TILE_H - 1) / VO_TILE_H);
     if (ntiles > 3072) { delete c; return VO_ERR_ARG; }      // SEL_MAX_TILES (select kernel LDS)
     d.ntiles = ntiles;
-    d.cand_cap = (uint32_t)ntiles * (VO_TILE_W * VO_TILE_H / 4);
+    d.cand_cap = (uint32_t)ntiles * VO_TILE_CAP;
     int rc = VO_OK;
     auto bail = [&](int r) { vo_destroy(c); return r; };
     c->serial = getenv("VO_SERIAL") && atoi(getenv("VO_SERIAL")) != 0;
@@ -960,7 +960,7 @@ int vo_extract(vo_ctx* c, const uint8_t* gray, size_t stride, vo_kp* kps, uint64
     if (desc && nk)
         HIPCHK(hipMemcpy(desc, c->d.desc + stg * N * 8, sizeof(uint64_t) * 8 * nk, hipMemcpyDeviceToHost));
     if (blurred)
-        HIPCHK(hipMemcpy2D(blurred, (size_t)c->cfg.width, c->d.blurred, (size_t)c->d.bstride, (size_t)c->cfg.width,
+        HIPCHK(hipMemcpy2D(blurred, (size_t)c->cfg.width, c->d.blurred + VO_BLUR_X0, (size_t)c->d.bstride, (size_t)c->cfg.width,
                            (size_t)c->cfg.height, hipMemcpyDeviceToHost));
     return VO_OK;
 }

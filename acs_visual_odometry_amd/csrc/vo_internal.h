@@ -15,11 +15,11 @@
 // FREAK_feature_descriptor_parallel_GPU.cpp:53-78).  x B = one copy per frame of a batch.
 //   frame_in    u8  W*H            staging for host-supplied frames
 //   blurred     u8  Wb*Hb    x B   7x7 Gaussian output (read back by describe); rows of
-//                                  Wb = whole stencil strips, Hb = whole tiles + 4 rows
+//                                  Wb >= whole stencil strips + 2, Hb = whole tiles + 4 rows
 //   response    f32 W*H            optional dense R map (debug / parity only)
-//   cand        u64 224/tile x B   NMS survivors per 56x16 tile, key = Rbits<<32 | row<<16 | col
+//   cand        u64 232/tile x B   NMS survivors per 57x16 tile, key = Rbits<<32 | row<<16 | col
 //   tilerows    u8  16/tile  x B   survivors per tile row (select emits raster order from them)
-//   ckeys       u64 224/tile x B   boundary-bin keys of the banded select (single-workgroup
+//   ckeys       u64 232/tile x B   boundary-bin keys of the banded select (single-workgroup
 //                                  select: compact survivors when they overflow its LDS)
 //   selbits     u64 4/tile   x B   selected-survivor bitmap (only when it overflows LDS)
 //   hist        u32 4096     x B   coarse histogram of candidate R (top-N boundary)
@@ -49,14 +49,24 @@
 #define VO_SEL_BANDED_TILES 1024   // banded select for frames of at least this many stencil tiles
 #endif
 #ifndef VO_TILE_W
-#define VO_TILE_W 56       // stencil tile = half a wave's strip x 16 rows (k_stencil ST_TW, ST_TH)
+#define VO_TILE_W 57       // stencil tile = half a wave's strip x 16 rows (k_stencil ST_TW, ST_TH)
 #endif
 #define VO_TILE_H 16
-#define VO_STRIP_W (2 * VO_TILE_W)   // stencil strip = one wave: two tiles side by side (<= 112: 64 lanes
+#define VO_STRIP_W (2 * VO_TILE_W)   // stencil strip = one wave: two tiles side by side (<= 114: 64 lanes
                                      // of column pairs hold the strip and 7 halo columns each side)
+// survivors per tile: strict 3x3 maxima are at most one per 2x2 cell
+#define VO_TILE_CAP (((VO_TILE_W + 1) / 2) * ((VO_TILE_H + 1) / 2))
+// a stencil lane's first column is xs - VO_STRIP_XL + 2 lane (xs: the strip's first output column)
+#define VO_STRIP_XL (128 - VO_STRIP_W - 7 - (128 - VO_STRIP_W - 14) / 2)
+// blurred plane column x is stored at byte x + VO_BLUR_X0 of its row, so that the stencil's
+// column pairs (even VO_STRIP_XL: even first columns) are 2-byte aligned
+#define VO_BLUR_X0 (VO_STRIP_XL & 1)
 // blurred plane of a W x H frame: row stride and rows (every stencil wave stores whole rows of
-// its strip, up to 4 rows past its segment)
-inline int vo_blur_stride(int W) { return ((W + 2 * VO_TILE_W - 1) / (2 * VO_TILE_W)) * VO_STRIP_W; }
+// its strip, up to 4 rows past its segment; a column pair may reach one column past the strips)
+inline int vo_blur_stride(int W)
+{
+    return (((W + VO_STRIP_W - 1) / VO_STRIP_W) * VO_STRIP_W + VO_BLUR_X0 + 1 + 3) & ~3;
+}
 inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_TILE_H + 4; }
 // keypoint/descriptor slots: frame f (since vo_reset) is extracted into ring slot
 // f % VO_RING; the last valid frame's copy lives in the carry slot during a skip run; the

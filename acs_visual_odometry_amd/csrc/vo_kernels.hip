@@ -40,6 +40,12 @@ constexpr int ds_onpad()                            // sum over p of ceil((42 - 
 }
 #define DS_ONPAD (ds_onpad())
 __constant__ float4 c_orient[DS_ONPAD];
+// the same entries unpadded, in pair order (the fully unrolled describe, DS_UNROLL), plus one
+// block of zeros read by the last block's prefetch
+#ifndef DS_UB
+#define DS_UB 8                // terms per block of the unrolled sum (one table request per block)
+#endif
+__constant__ float4 c_orient_u[VO_FREAK_NPAIRS + DS_UB];
 
 static bool g_tables_ready = false;
 static void ensure_tables()
@@ -52,18 +58,21 @@ static void ensure_tables()
     for (int p = 0; p < VO_FREAK_NPOINTS; ++p)
         for (int q = p + 1; q < VO_FREAK_NPOINTS; ++q) { pp[e] = (uint8_t)p; pq[e] = (uint8_t)q; ++e; }
     static float4 orient[DS_ONPAD];
+    static float4 orient_u[VO_FREAK_NPAIRS + DS_UB];
     int o = 0;
     for (int t = 0; t < VO_FREAK_NPAIRS; ++t) {
         const float dx = (float)(px[pp[t]] - px[pq[t]]), dy = (float)(py[pp[t]] - py[pq[t]]);
         const float nrm = sqrtf(dx * dx + dy * dy);    // host sqrtf: correctly rounded
         const double ux = (double)dx / (double)nrm, uy = (double)dy / (double)nrm;
         const float ax = (float)ux, ay = (float)uy;
-        orient[o++] = make_float4(ax, ay, (float)(ux - (double)ax), (float)(uy - (double)ay));
+        orient_u[t] = make_float4(ax, ay, (float)(ux - (double)ax), (float)(uy - (double)ay));
+        orient[o++] = orient_u[t];
         if (pq[t] == VO_FREAK_NPOINTS - 1)             // end of row p: pad to a whole group
             while (o % DS_OG) orient[o++] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     if (o != DS_ONPAD) fprintf(stderr, "[vo_mi355x] orientation table size %d != %d\n", o, DS_ONPAD);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_orient), orient, sizeof(orient));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_orient_u), orient_u, sizeof(orient_u));
     g_tables_ready = true;
 }
 
@@ -357,10 +366,10 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // stencil: blur7x7 -> gradients -> 5x5 response -> strict 3x3 NMS candidates
 // kernels/feature_extraction_kernel_functions.c:43-120, corner_detection_parallel_GPU.cpp:146-180
 //
-// Column-streaming form: one wave owns a strip of ST_SW = 112 output columns (two 56-column
+// Column-streaming form: one wave owns a strip of ST_SW = 114 output columns (two 57-column
 // tiles) and walks down a segment of 16 SEGT output rows.  Lane L holds the column PAIR
-// c0 = xs - 8 + 2L, c0 + 1 in every stage (128 columns: the strip, 7 halo columns on each
-// side, 2 spare).  Vertical neighbours are register histories (one new source row per step);
+// c0 = xs - 7 + 2L, c0 + 1 in every stage (128 columns: the strip and 7 halo columns on each
+// side; lanes 0..31 hold tile A's columns, lanes 32..63 tile B's).  Vertical neighbours are register histories (one new source row per step);
 // horizontal neighbours are the lane's other column or a DPP wave shift (v_mov_b32_dpp
 // wave_shr:1 / wave_shl:1), so a shift serves two columns.  No LDS, no barrier.
 // Source row k of the segment (y = ys - 7 + k) completes blurred row ys - 10 + k, gradient
@@ -370,9 +379,9 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // The wave's row and column conditions are uniform branches or lane masks, so the scalar
 // unit (one per CU, shared by its four SIMDs) stays well below the VALU's issue rate.
 // ---------------------------------------------------------------------------
-#define ST_TW VO_TILE_W                // tile width: 56 (48 measured: KITTI within noise, 1080p -3 %)
+#define ST_TW VO_TILE_W                // tile width: 57 (56: 12 strips per KITTI row instead of 11; 48: 1080p -3 %)
 #define ST_TH VO_TILE_H                // tile height (select reads 16 row counts per tile)
-#define ST_SW VO_STRIP_W               // strip width = two tiles: 112 output columns per wave
+#define ST_SW VO_STRIP_W               // strip width = two tiles: 114 output columns per wave
 #ifndef ST_RSEL_ASM
 #define ST_RSEL_ASM 1                  // the response's rounding selects ordered by hand (no s_nop)
 #endif
@@ -383,12 +392,13 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #define ST_DPP_ADD 1                   // box sums with v_add_f32_dpp (0: v_mov_b32_dpp + packed adds)
 #endif
 #define ST_HALO 7                      // blur 3 + gradient 1 + window 2 + nms 1
-#define ST_TCAP (ST_TW * ST_TH / 4)    // candidates per tile (strict maxima: at most 1 in 4)
+#define ST_TCAP VO_TILE_CAP            // candidates per tile (strict maxima: at most one per 2x2 cell)
 #ifndef ST_SEGT_DEFAULT
 #define ST_SEGT_DEFAULT 8              // tiles per wave segment (VO_STSEG picks 2 / 4 / 6 / 8 / 12; KITTI: 8 measured
                                        // 260k vs 246k frames/s for 4 -- 14 halo rows per 128 instead of per 64 --, 12 257k, 24 231k)
 #endif
-static_assert(ST_SW + 2 * ST_HALO + 1 <= 128, "strip + halo within one wave of column pairs");
+static_assert(ST_SW + 2 * ST_HALO <= 128, "strip + halo within one wave of column pairs");
+static_assert(VO_STRIP_XL + ST_TW - 1 == 63, "tile A in lanes 0..31, tile B in lanes 32..63");
 
 __device__ __forceinline__ int refl101(int i, int n)
 {
@@ -558,17 +568,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
     const int Wb = d.bstride;
 
     const int xs = sxi * ST_SW, ys = seg * SEG;
-    const int c0 = xs - 8 + 2 * lane;                          // this lane's columns: c0, c0 + 1
+    const int c0 = xs - VO_STRIP_XL + 2 * lane;                // this lane's columns: c0, c0 + 1
     const int xl0 = refl101(c0, W), xl1 = refl101(c0 + 1, W);  // BORDER_REFLECT_101
-    const bool out_lane = lane >= 4 && lane < 4 + ST_SW / 2;  // columns xs .. xs + ST_SW - 1
-    // blurred store: out of range off the strip and past the image's last column pair (the plane's
-    // padding columns are never read)
-    const int boff = out_lane && c0 < W ? c0 : 0x40000000;
-    const bool isB = lane >= 4 + ST_TW / 2;                   // the strip's second tile
+    auto outc = [&](int x) { return x >= xs && x < xs + ST_SW; };   // the strip's output columns
+    // blurred store (bytes c0, c0 + 1 at plane offset c0 + VO_BLUR_X0: 2-byte aligned): out of
+    // range for pairs off the strip and past the image's last column.  A pair half off the strip
+    // stores its neighbour strip's column too -- the same value that strip's wave stores.
+    const int boff = (outc(c0) || outc(c0 + 1)) && c0 < W ? c0 + VO_BLUR_X0 : 0x40000000;
+    const bool isB = lane >= 32;                              // the strip's second tile
     const bool hasB = 2 * sxi + 1 < ntx;
     // the wave's columns reach the image's outer two columns, where gradients (kernel .c:59-76)
     // are 0: the lane masks apply only then
-    const bool colfix = xs - 8 < 2 || xs + 120 > W - 2;
+    const bool colfix = xs - VO_STRIP_XL < 2 || xs - VO_STRIP_XL + 128 > W - 2;
     const bool g0 = c0 >= 1 && c0 <= W - 2, g1 = c0 + 1 >= 1 && c0 + 1 <= W - 2;
     // lane masks folded into lane constants, so a row's tests are one compare each: responses
     // outside 2 <= j <= W-3 are 0 (kernel .c:97-114): their threshold is +inf; an NMS centre
@@ -577,13 +588,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
     const float thr0 = c0 >= 2 && c0 <= W - 3 ? thr : __builtin_inff();
     const float thr1 = c0 + 1 >= 2 && c0 + 1 <= W - 3 ? thr : __builtin_inff();
     const int hk = d.nms_k / 2;
-    auto ncol = [&](int x) { return out_lane && x >= hk && x < W - hk && x >= d.bcol && x <= W - d.bcol; };
+    auto ncol = [&](int x) { return outc(x) && x >= hk && x < W - hk && x >= d.bcol && x <= W - d.bcol; };
     const int nmsk0 = ncol(c0) ? 0 : 0x7FFFFFFF, nmsk1 = ncol(c0 + 1) ? 0 : 0x7FFFFFFF;
     const int nlo = max(hk, d.brow), nhi = max(nlo, min(H - hk, H - d.brow + 1));   // NMS rows [nlo, nhi)
     const uint32_t thr_bits = d.thr_bits;
-    constexpr unsigned long long mT = (1ull << (ST_TW / 2)) - 1ull;
-    constexpr unsigned long long mA = mT << 4;                 // lanes 4 .. 3 + TW/2: tile 2 sxi
-    constexpr unsigned long long mB = mT << (4 + ST_TW / 2);   // the next TW/2 lanes: tile 2 sxi + 1
+    // (halo columns are never maxima: their NMS masks, so a tile's lane masks are halves of the wave)
+    constexpr unsigned long long mA = 0xFFFFFFFFull;          // lanes 0 .. 31: tile 2 sxi
+    constexpr unsigned long long mB = mA << 32;               // lanes 32 .. 63: tile 2 sxi + 1
 
     // register histories (index 0 oldest); source rows packed: column c0 low half, c0 + 1 high
     uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0;
@@ -719,14 +730,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             const int o0 = ((rv.x > thr0) & rrow) ? __float_as_int(rv.x) : 0;
             const int o1 = ((rv.y > thr1) & rrow) ? __float_as_int(rv.y) : 0;
             if constexpr (DBG) {
-                if (write_response && yr >= ys && yr < min(ys + SEG, H) && out_lane) {
+                if (write_response && yr >= ys && yr < min(ys + SEG, H)) {
                     float* R = d.response + (size_t)yr * W;
                     const float w0 = write_response == 2 ? SX.x : write_response == 3 ? SY.x
                                    : write_response == 4 ? SS.x : __int_as_float(o0);
                     const float w1 = write_response == 2 ? SX.y : write_response == 3 ? SY.y
                                    : write_response == 4 ? SS.y : __int_as_float(o1);
-                    if (c0 < W) R[c0] = w0;
-                    if (c0 + 1 < W) R[c0 + 1] = w1;
+                    if (outc(c0) && c0 >= 0 && c0 < W) R[c0] = w0;
+                    if (outc(c0 + 1) && c0 + 1 < W) R[c0 + 1] = w1;
                 }
             }
             ru0 = rm0; rm0 = rd0; rd0 = o0;
@@ -942,7 +953,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     uint64_t* s_bitsl = reinterpret_cast<uint64_t*>(smem + L.bits);
     uint16_t* s_wpre = reinterpret_cast<uint16_t*>(smem + L.chunk);   // selected keys before 4-segment word w
     uint64_t* s_keys = reinterpret_cast<uint64_t*>(smem + L.keys);
-    const size_t TCAP = ST_TW * ST_TH / 4;
+    const size_t TCAP = ST_TCAP;
     if (tid == 0) {
         s_nbnd = 0; s_b = -1; s_above = 0;
         s_slot = ext_slot(d, f0, z, slot_override);
@@ -1705,6 +1716,10 @@ __global__ void k_ext_missing(VoDev d, int slot)
 #define DS_WAVES 4
 #endif
 #define DS_KPB (DS_KPW * DS_WAVES)
+#ifndef DS_UNROLL
+#define DS_UNROLL 0            // 1: the orientation sums fully unrolled from sample registers (describe
+                               // 0.92 -> 0.85 us/frame but KITTI 278-285k vs 283-289k: 110 VGPRs, 30 KB code)
+#endif
 
 // the FREAK lists of include/vo_freak_tables.h as compile-time tables; pair e is the e-th
 // (p, q), p < q, row-major (ensure_tables enumerates the same order)
@@ -1768,6 +1783,51 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
     // lanes past n sample around a keypoint inside the margin: every address stays in bounds
     // and the gathers need no branches (their values are never used)
     const int2 kp = valid ? d.kps[(size_t)cur * d.N + base + lane] : make_int2(d.bcol, d.brow);
+    ds_f2 oxy = {0.0f, 0.0f};
+#if DS_UNROLL
+    // 1. the 43 pattern samples, in registers
+    float smp[NP];
+    {
+        uint32_t v[NP];
+        st_for([&](auto U) {
+            constexpr int u = decltype(U)::value;
+            v[u] = img[(size_t)(kp.y + kDs.py[u]) * Wb + (kp.x + kDs.px[u])];
+        }, std::make_integer_sequence<int, NP>{});
+        st_for([&](auto U) { smp[U] = (float)v[U]; }, std::make_integer_sequence<int, NP>{});
+    }
+    (void)s_I0;
+    VO_STAMP(d, stamp_slot, 1);
+    // 2. O = sum over pairs t = 0..902 of (ic * d) / |d|, each component in order in f32, fully
+    //    unrolled: the pair (p, q) of term t is a compile-time constant, so ic = I(p) - I(q) reads
+    //    two sample registers and the sums need no LDS, no padding terms and no loop control.  The
+    //    table arrives by scalar loads, one block of DS_UB entries ahead of the block being summed.
+    {
+        constexpr int NB = (VO_FREAK_NPAIRS + DS_UB - 1) / DS_UB;
+        float4 tb[DS_UB], tbn[DS_UB];
+#pragma unroll
+        for (int u = 0; u < DS_UB; ++u) tb[u] = c_orient_u[u];
+        st_for([&](auto Bk) {
+            constexpr int b = decltype(Bk)::value;
+            // block b's entries (requested during block b - 1) have arrived; request block b + 1
+            __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0)
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (b + 1 < NB) {
+#pragma unroll
+                for (int u = 0; u < DS_UB; ++u) tbn[u] = c_orient_u[(b + 1) * DS_UB + u];
+            }
+            __builtin_amdgcn_sched_barrier(0);          // the requests stay ahead of the sums
+            st_for([&](auto U) {
+                constexpr int t = b * DS_UB + decltype(U)::value;
+                if constexpr (t < VO_FREAK_NPAIRS) orient_term(smp[kDs.pp[t]] - smp[kDs.pq[t]], tb[U], oxy);
+            }, std::make_integer_sequence<int, DS_UB>{});
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (b + 1 < NB) {
+#pragma unroll
+                for (int u = 0; u < DS_UB; ++u) tb[u] = tbn[u];
+            }
+        }, std::make_integer_sequence<int, NB>{});
+    }
+#else
     // 1. the 43 pattern samples -> this lane's LDS column (all loads in flight first)
     {
         uint32_t v[NP];
@@ -1784,7 +1844,6 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
     //    (pairs (p, q), q > p) in groups of DS_OG, the last one padded with zero terms that read
     //    the zero rows past the samples.  Software-pipelined: the samples and table entries of
     //    group g + 1 are requested before group g is summed.
-    ds_f2 oxy = {0.0f, 0.0f};
     {
         constexpr int NG = DS_ONPAD / DS_OG;
         const float* col = &s_I0[0][lane];
@@ -1822,6 +1881,7 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
             for (int u = 0; u < DS_OG; ++u) { iq[u] = iqn[u]; tb[u] = tbn[u]; }
         }
     }
+#endif
     VO_STAMP(d, stamp_slot, 2);
     const float ox = oxy.x, oy = oxy.y;
     // 3. angle and rotation
@@ -1865,7 +1925,7 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
 __global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int slot_override, unsigned publish,
                                                             int nb)
 {
-    __shared__ float s_I0[DS_WAVES][DS_OROWS][DS_KPW];
+    __shared__ float s_I0[DS_WAVES][DS_UNROLL ? 1 : DS_OROWS][DS_KPW];   // sample columns (the looped sums)
     int z, bx;
     if (xcd_frame(d, (d.N + DS_KPB - 1) / DS_KPB, nb, z, bx)) {
         const int cur = ext_slot(d, f0, z, slot_override);
@@ -1873,7 +1933,7 @@ __global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const int base = bx * DS_KPB + wave * DS_KPW;
         if (base < n)                    // wave-uniform; no barrier inside
-            describe_wave(d, d.blurred + (size_t)z * d.bplane, cur, n, base, s_I0[wave]);
+            describe_wave(d, d.blurred + (size_t)z * d.bplane + VO_BLUR_X0, cur, n, base, s_I0[wave]);
     }
     if (!publish) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -192,7 +192,9 @@ def test_extract_bit_exact(which, ctx_kitti, scene, factory):
 @pytest.mark.parametrize("W,H,N,kind", [
     (1920, 1080, 4096, "scene"),    # ~37k survivors: select stages keys in global scratch
     (1920, 1080, 4096, "noise"),    # ~53k survivors
-    (1000, 300, 2000, "noise"),     # ragged: W, H not multiples of the 64x16 stencil tile
+    (1000, 300, 2000, "noise"),     # ragged: W, H not multiples of the 57x16 stencil tile
+    (913, 250, 2000, "noise"),      # one column past whole 114-column strips
+    (1025, 150, 1000, "scene"),     # one column short of whole strips
     (752, 480, 2000, "sparse"),     # fewer survivors than N: no top-N threshold
     (640, 480, 64, "scene"),        # tiny N: the boundary bin holds most of the ranking
     (1280, 720, 500, "periodic"),   # identical blobs: thousands of equal responses in the boundary bin

@@ -1,0 +1,80 @@
+"""Repeat the bench's headline stream (8 x 200 KITTI frames, 1.0 m/frame) under changing timing
+modes and report where a repeat first differs from the first run: per sequence the first frame
+whose status / info / pose differs, with both rows, so the stage that diverged can be read off
+(keypoint count: extract; matches: match; inliers: RANSAC; pose only: refit / pose).  Then the
+batched extract alone, repeated, keypoints and descriptors compared frame by frame.
+
+  python tools/det_stress.py [repeats] [extract_repeats]
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from acs_visual_odometry_amd import Context  # noqa: E402
+from acs_visual_odometry_amd.synth import SceneSequence, render_sequences  # noqa: E402
+
+W, H, F, S = 1241, 376, 200, 8
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 12
+xreps = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+rendered = render_sequences([(W, H, F, s, 1.0) for s in range(S)], 16)
+seqs = [SceneSequence(W, H, nframes=F, seq=s, step=1.0) for s in range(S)]
+ctx = Context(W, H, K=seqs[0].K, max_kpts=2000)
+dall = ctx.device_frames(np.concatenate(rendered))
+gt_all = np.concatenate([s.gt() for s in seqs])
+starts = [F * i for i in range(1, S)]
+
+
+def step(timing):
+    ctx.reset()
+    ctx.set_ground_truth(gt_all)
+    ctx.set_sequence_starts(starts)
+    return ctx.process_frames_device(dall, timing=timing)
+
+
+modes = [0, 100, 1, 0, 104, 103, 0, 1, 105, 0, 100, 1]
+if os.environ.get("DET_MODES"):
+    modes = [int(m) for m in os.environ["DET_MODES"].split(",")]
+ref = step(0)
+bad = 0
+t0 = time.time()
+for r in range(reps):
+    m = modes[r % len(modes)]
+    p, st, info = step(m)
+    same = np.array_equal(p, ref[0]) and np.array_equal(st, ref[1]) and np.array_equal(info, ref[2])
+    print(f"rep {r} timing {m}: {'same' if same else 'DIFFERS'} ({time.time() - t0:.1f} s)", flush=True)
+    if same:
+        continue
+    bad += 1
+    for s in range(S):
+        sl = slice(s * F, (s + 1) * F)
+        d = np.nonzero((st[sl] != ref[1][sl]) | (info[sl] != ref[2][sl]).any(1) |
+                       (p[sl] != ref[0][sl]).reshape(F, -1).any(1))[0]
+        if d.size == 0:
+            continue
+        f = int(d[0])
+        print(f"  seq {s}: {d.size} frames differ, first {f}")
+        for g in range(max(0, f - 1), min(F, f + 2)):
+            print(f"    frame {g}: ref st {ref[1][s * F + g]} info {ref[2][s * F + g].tolist()}"
+                  f" | now st {st[s * F + g]} info {info[s * F + g].tolist()}"
+                  f" | pose diff {np.abs(p[s * F + g] - ref[0][s * F + g]).max():.3g}")
+print(f"full path: {bad} of {reps} repeats differ", flush=True)
+
+nk0, k0, d0 = ctx.extract_frames_device(dall, outputs=True)
+xbad = 0
+for r in range(xreps):
+    nk, k, d = ctx.extract_frames_device(dall, timing=(0, 1, 100)[r % 3], outputs=True)
+    diff = [f for f in range(len(nk)) if nk[f] != nk0[f] or not np.array_equal(k[f], k0[f])
+            or not np.array_equal(d[f], d0[f])]
+    print(f"extract rep {r}: {len(diff)} frames differ" + (f", first {diff[:5]}" if diff else ""), flush=True)
+    for f in diff[:2]:
+        kd = np.nonzero((k[f] != k0[f]).any(1))[0] if nk[f] == nk0[f] else None
+        dd = np.nonzero((d[f] != d0[f]).any(1))[0] if nk[f] == nk0[f] else None
+        print(f"    frame {f}: n {nk0[f]} -> {nk[f]}; kps differ at {None if kd is None else kd[:8].tolist()}"
+              f"; desc differ at {None if dd is None else dd[:8].tolist()}")
+    xbad += bool(diff)
+print(f"extract: {xbad} of {xreps} repeats differ")
+dall.free()
+ctx.close()
