@@ -784,8 +784,8 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc(&d.ctr, VO_CTR_WORDS);
     rc |= dalloc(&d.trec, VO_SLOTS);
     rc |= dalloc(&d.plog, VO_PLOG);
-#ifdef VO_STAMPS
-    rc |= dalloc(&d.dbg, (size_t)d.max_hyp * 16);
+#if defined(VO_STAMPS) || (defined(MM_VERIFY) && MM_VERIFY)
+    rc |= dalloc(&d.dbg, (size_t)d.max_hyp * 16);   // stamps / diagnostic counters (words 6000..6003)
 #endif
     if (rc != VO_OK) return bail(VO_ERR_HIP);
     const std::vector<uint16_t>& tab = maxit_table(N, k.ransac_p);
@@ -1387,6 +1387,23 @@ int vo_debug_stamps(vo_ctx* c, unsigned long long* out, int n)
     HIPCHK(hipStreamSynchronize(c->s));
     HIPCHK(hipMemcpy(out, c->d.dbg, sizeof(unsigned long long) * m, hipMemcpyDeviceToHost));
     return m;
+}
+
+// diagnostics (tools/det_stress.py): the ring slots of frames [f0, f0 + n) as the last call left
+// them -- keypoint counts, keypoints (n x N int2) and 32-test prefixes (n x N u32)
+extern "C" int vo_debug_ring(vo_ctx* c, int f0, int n, int32_t* nk, int32_t* kps, uint32_t* pre)
+{
+    if (!c || f0 < 0 || n <= 0 || n > c->d.ring || !nk || !kps || !pre) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipDeviceSynchronize());
+    const size_t N = (size_t)c->cfg.max_kpts;
+    for (int i = 0; i < n; ++i) {
+        const int slot = (f0 + i) % c->d.ring;
+        HIPCHK(hipMemcpy(nk + i, c->d.ext_n + slot, sizeof(int32_t), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(kps + (size_t)i * N * 2, c->d.kps + (size_t)slot * N, sizeof(int32_t) * 2 * N, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(pre + (size_t)i * N, c->d.pre + (size_t)slot * N, sizeof(uint32_t) * N, hipMemcpyDeviceToHost));
+    }
+    return VO_OK;
 }
 
 int vo_device_alloc(vo_ctx* c, size_t bytes, void** dptr)

@@ -2151,6 +2151,17 @@ __device__ void match_compact(const VoDev& d, int wf, const MatchFrame& m, int* 
             const int i = (r0 + u) * 256 + tid;
             js[u] = act && i < n1 ? ld_sc1(m.match_j + i) : -1;
         }
+#if MM_VERIFY
+#pragma unroll
+        for (int u = 0; u < RC; ++u) {
+            const int i = (r0 + u) * 256 + tid;
+            if (act && i < n1 && d.dbg) {
+                const int fresh = __hip_atomic_fetch_add((gi32*)(m.match_j + i), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (fresh != js[u]) atomicAdd(&d.dbg[6002], 1ull);
+                atomicAdd(&d.dbg[6003], 1ull);
+            }
+        }
+#endif
         int2 ka[RC], kb[RC];
 #pragma unroll
         for (int u = 0; u < RC; ++u) {
@@ -2317,6 +2328,9 @@ __host__ __device__ inline int mm_lds_bytes(int)
 {
     return MM_CH * 32 + (MM_CH / 16) * 16 + 16;
 }
+#ifndef MM_VERIFY
+#define MM_VERIFY 0                   // diagnostic build: every MFMA key re-derived with popc (d.dbg counters)
+#endif
 __device__ __forceinline__ int ratio_accept13(uint32_t m1, uint32_t m2, float ratio)
 {
     if (m1 == 0xFFFFFFFFu || m2 == 0xFFFFFFFFu) return -1;
@@ -2374,10 +2388,26 @@ __global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
         // (the compiler's count for this VGPR-destination form read stale keys in one build)
         const int ntile = (n2 + 15) >> 4;
         // keys of candidate tile t into the top-2 chains; rows past n2 (the last tile only) excluded
+        [[maybe_unused]] unsigned long long vbad = 0, vchk = 0;
         auto consume = [&](const mm_v4i (&dk)[MM_G], bool pad, int t) {
 #pragma unroll
             for (int g = 0; g < MM_G; ++g) {
                 uint32_t k0 = (uint32_t)dk[g].x, k1 = (uint32_t)dk[g].y, k2 = (uint32_t)dk[g].z, k3 = (uint32_t)dk[g].w;
+#if MM_VERIFY
+                {
+                    const int q = q0 + wave * 16 * MM_G + g * 16 + col;
+                    const uint32_t qp = q < n1 ? qpre[q] : 0u;
+                    const uint32_t kk[4] = {k0, k1, k2, k3};
+                    for (int r = 0; r < 4; ++r) {
+                        const int j = 16 * t + 4 * h + r;
+                        if (j < n2 && q < n1) {
+                            const uint32_t e = 8192u * (uint32_t)__popc(qp ^ cpre[j]) + (uint32_t)j;
+                            vchk += 1;
+                            vbad += e != kk[r];
+                        }
+                    }
+                }
+#endif
                 if (pad) {
                     const int r0 = 16 * t + 4 * h;
                     if (r0 >= n2) k0 = 0xFFFFFFFFu;
@@ -2401,6 +2431,7 @@ __global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
         // for this VGPR-destination form read stale keys in one build)
         mm_v4i dA[MM_G], dB[MM_G];
         bool pend = false;                                         // dB holds a tile not yet consumed
+        int tB = 0;                                                // dB's tile
         // a chunk's prefixes, thread tid: candidates tid + 256 k; the next chunk's are loaded while
         // this one is computed
         constexpr int KC = MM_CH / 256;
@@ -2437,18 +2468,20 @@ __global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
             for (; u + 1 < nt; u += 2) {
                 issue(dA, u);
                 __builtin_amdgcn_sched_barrier(0);
-                if (pend) consume(dB, false, 0);                   // never the padded last tile
+                if (pend) consume(dB, false, tB);                  // never the padded last tile
                 __builtin_amdgcn_sched_barrier(0);
                 issue(dB, u + 1);
                 __builtin_amdgcn_sched_barrier(0);
-                consume(dA, false, 0);
+                consume(dA, false, t0 + u);
                 __builtin_amdgcn_sched_barrier(0);
                 pend = true;
+                tB = t0 + u + 1;
             }
             if (u < nt) {                                          // odd tile count: the chunk's last tile
                 issue(dA, u);
                 __builtin_amdgcn_sched_barrier(0);
-                if (pend) consume(dB, false, 0);
+                if (pend) consume(dB, false, tB);
+                tB = t0 + u;
                 asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -2474,6 +2507,12 @@ __global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
             const int q = q0 + wave * 16 * MM_G + g * 16 + col;
             if (h == 0 && q < n1) st_sc1(m.match_j + q, ratio_accept13(a1[g], a2[g], d.ratio));
         }
+#if MM_VERIFY
+        if (vchk && d.dbg) {
+            atomicAdd(&d.dbg[6000], vbad);
+            atomicAdd(&d.dbg[6001], vchk);
+        }
+#endif
     }
     if (!arrive_last(&m.w->ctr[0], gridDim.x, &s_last)) return;
     match_compact(d, wf, m, s_wsum);

@@ -37,14 +37,51 @@ def step(timing):
 modes = [0, 100, 1, 0, 104, 103, 0, 1, 105, 0, 100, 1]
 if os.environ.get("DET_MODES"):
     modes = [int(m) for m in os.environ["DET_MODES"].split(",")]
+dbg = os.environ.get("DET_DBG") == "1"       # MM_VERIFY builds: MFMA key / hand-off counters in d.dbg
+if dbg:
+    import ctypes as C
+    L = ctx.lib
+    L.vo_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    dbuf = np.zeros(6004, np.uint64)
+
+    def counters():
+        L.vo_debug_stamps(ctx.h, dbuf.ctypes.data_as(C.c_void_p), dbuf.size)
+        return dbuf[6000:6004].astype(np.int64).copy()
+    c_prev = counters()
+ring = os.environ.get("DET_RING") == "1"     # compare the extracted ring slots too (vo_debug_ring)
+if ring:
+    import ctypes as C
+    ctx.lib.vo_debug_ring.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+    NF = S * F
+
+    def ring_read():
+        nk = np.zeros(NF, np.int32)
+        kp = np.zeros((NF, 2000, 2), np.int32)
+        pr = np.zeros((NF, 2000), np.uint32)
+        rc = ctx.lib.vo_debug_ring(ctx.h, 0, NF, nk.ctypes.data_as(C.c_void_p), kp.ctypes.data_as(C.c_void_p),
+                                   pr.ctypes.data_as(C.c_void_p))
+        assert rc == 0, rc
+        return nk, kp, pr
 ref = step(0)
+ring_ref = ring_read() if ring else None
 bad = 0
 t0 = time.time()
 for r in range(reps):
     m = modes[r % len(modes)]
     p, st, info = step(m)
     same = np.array_equal(p, ref[0]) and np.array_equal(st, ref[1]) and np.array_equal(info, ref[2])
-    print(f"rep {r} timing {m}: {'same' if same else 'DIFFERS'} ({time.time() - t0:.1f} s)", flush=True)
+    msg = ""
+    if dbg:
+        c_now = counters()
+        dc = c_now - c_prev
+        c_prev = c_now
+        msg = f" mfma keys wrong {dc[0]} of {dc[1]}, stale match_j {dc[2]} of {dc[3]}"
+    if ring:
+        nk, kp, pr = ring_read()
+        fd = [f for f in range(NF) if nk[f] != ring_ref[0][f] or not np.array_equal(kp[f, :nk[f]], ring_ref[1][f, :nk[f]])
+              or not np.array_equal(pr[f, :nk[f]], ring_ref[2][f, :nk[f]])]
+        msg += f" ring frames differing: {len(fd)}" + (f" {fd[:6]}" if fd else "")
+    print(f"rep {r} timing {m}: {'same' if same else 'DIFFERS'} ({time.time() - t0:.1f} s){msg}", flush=True)
     if same:
         continue
     bad += 1
