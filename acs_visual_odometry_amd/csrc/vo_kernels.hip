@@ -28,6 +28,9 @@ namespace vo {
 // Rows p of the pair order padded to whole groups of DS_OG terms with zero terms (dx = dy = 0:
 // the term is a zero, which leaves a sum that is never -0 unchanged), so the describe loop has
 // no remainder iterations.
+#ifndef MM_VERIFY
+#define MM_VERIFY 0     // diagnostic build: MFMA keys re-derived with popc, hand-off and histogram checks (d.dbg counters)
+#endif
 #ifndef DS_OG
 #define DS_OG 8
 #endif
@@ -388,6 +391,12 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #ifndef ST_SOFF_HOIST
 #define ST_SOFF_HOIST 1                // a row group's source-row offsets read into SGPRs before its rows
 #endif
+#ifndef ST_NODOT
+#define ST_NODOT 0                     // diagnostic: the horizontal blur without v_dot2_u32_u16
+#endif
+#ifndef ST_LTMASK_ASM
+#define ST_LTMASK_ASM 1                // the NMS maxima's lane masks straight from an asm v_cmp
+#endif
 #ifndef ST_DPP_ADD
 #define ST_DPP_ADD 1                   // box sums with v_add_f32_dpp (0: v_mov_b32_dpp + packed adds)
 #endif
@@ -413,8 +422,14 @@ __device__ __forceinline__ int refl101(int i, int n)
 #ifndef VO_DPP_PIN
 #define VO_DPP_PIN 1
 #endif
+#ifndef ST_DPP_NOP
+#define ST_DPP_NOP 0                   // diagnostic: wait states before every wave shift
+#endif
 __device__ __forceinline__ int from_left(int v)
 {
+#if ST_DPP_NOP
+    asm volatile("s_nop %c1" : "+v"(v) : "i"(ST_DPP_NOP - 1));
+#endif
     int r = __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true);   // bound_ctrl: edge lanes read 0, no old operand
 #if VO_DPP_PIN
     asm volatile("" : "+v"(r));
@@ -423,6 +438,9 @@ __device__ __forceinline__ int from_left(int v)
 }
 __device__ __forceinline__ int from_right(int v)
 {
+#if ST_DPP_NOP
+    asm volatile("s_nop %c1" : "+v"(v) : "i"(ST_DPP_NOP - 1));
+#endif
     int r = __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true);   // bound_ctrl: edge lanes read 0, no old operand
 #if VO_DPP_PIN
     asm volatile("" : "+v"(r));
@@ -636,7 +654,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             const uint32_t V = as_u32(v);
             const uint32_t VL = (uint32_t)from_left((int)V), VR = (uint32_t)from_right((int)V);
             const uint32_t VL2 = (uint32_t)from_left((int)VL), VR2 = (uint32_t)from_right((int)VR);
+#if ST_NODOT
+            auto dot = [](uint32_t a, st_w2 w, uint32_t c) { return (a & 0xFFFFu) * (uint32_t)w.x + (a >> 16) * (uint32_t)w.y + c; };
+#else
             auto dot = [](uint32_t a, st_w2 w, uint32_t c) { return __builtin_amdgcn_udot2(as_u16x2(a), w, c, false); };
+#endif
             // column c0: 72 I(c0) + 56 (I(c0-1) + I(c0+1)) + 28 (I(c0-2) + I(c0+2)) + 8 (I(c0-3) + I(c0+3))
             const uint32_t ha = dot(VR, st_w2{28, 8}, dot(VL2, st_w2{0, 8}, dot(VL, st_w2{28, 56}, dot(V, st_w2{72, 56}, 32768u))));
             const uint32_t hb = dot(VR2, st_w2{8, 0}, dot(VR, st_w2{56, 28}, dot(VL, st_w2{8, 28}, dot(V, st_w2{56, 72}, 32768u))));
@@ -692,6 +714,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             {
                 float pX, pY, pS, xX, yX, xY, yY, xS, yS;
                 asm volatile(
+#if ST_DPP_NOP
+                    "s_nop 7\n\t"
+#endif
                     "v_add_f32 %[pX], %[ax], %[ay]\n\t"
                     "v_add_f32 %[pY], %[bx], %[by]\n\t"
                     "v_add_f32 %[pS], %[cx], %[cy]\n\t"
@@ -758,9 +783,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             // rok materialised the lane bools and compared them again, 4 VALU a row); rok is
             // wave-uniform and masks them as scalars, and inside the branch it holds
             auto lt_mask = [](int a, int b) {
+#if ST_LTMASK_ASM
                 unsigned long long m;
                 asm("v_cmp_lt_i32_e64 %0, %1, %2" : "=s"(m) : "v"(a), "v"(b));
                 return m;
+#else
+                return (unsigned long long)__builtin_amdgcn_ballot_w64(a < b);
+#endif
             };
             const unsigned long long b0 = rok ? lt_mask(nb0, rm0) : 0ull, b1 = rok ? lt_mask(nb1, rm1) : 0ull;
             const bool mx0 = nb0 < rm0, mx1 = nb1 < rm1;
@@ -954,9 +983,15 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     uint16_t* s_wpre = reinterpret_cast<uint16_t*>(smem + L.chunk);   // selected keys before 4-segment word w
     uint64_t* s_keys = reinterpret_cast<uint64_t*>(smem + L.keys);
     const size_t TCAP = ST_TCAP;
+#if MM_VERIFY
+    __shared__ unsigned long long s_ck;                 // diagnostic: checksum of the frame's key list
+#endif
     if (tid == 0) {
         s_nbnd = 0; s_b = -1; s_above = 0;
         s_slot = ext_slot(d, f0, z, slot_override);
+#if MM_VERIFY
+        s_ck = 0ull;
+#endif
     }
     VO_STAMP(d, 1990, 0);
     // A
@@ -1017,6 +1052,13 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
         }
     }
     __syncthreads();
+#if MM_VERIFY
+    {
+        unsigned long long ck = 0ull;
+        for (int g = tid; g < C; g += 1024) ck += mix64(keys[g] + (unsigned long long)g);
+        atomicAdd(&s_ck, ck);
+    }
+#endif
     VO_STAMP(d, 1990, 1);
     // C
     int b = -1;
@@ -1104,6 +1146,16 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
             Tb = s_tb;
         }
         if (tid == 0 && d.dbg) d.dbg[1990 * 16 + 10] = (unsigned long long)nb;
+#if MM_VERIFY
+        if (tid == 0 && d.dbg) {
+            // the stencil's histogram against the frame's key list (diagnostic builds)
+            uint32_t total = 0;
+            for (int w = 0; w < 16; ++w) total += s_hs[w];
+            if (total != (uint32_t)C) atomicAdd(&d.dbg[6004], 1ull);
+            if (need > nb) atomicAdd(&d.dbg[6005], 1ull);
+            atomicAdd(&d.dbg[6006], 1ull);
+        }
+#endif
     }
     __syncthreads();                                    // s_bnd aliases the segment counts
     for (int w = tid; w < (nseg + 3) / 4; w += 1024) s_segw[w] = 0u;
@@ -1220,6 +1272,15 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     VO_STAMP(d, 1990, 6);
     // select is the histogram's only reader: leave it zeroed for the next frame's stencil
     for (int i = tid; i < VO_HIST_BINS; i += 1024) hist[i] = 0u;
+#if MM_VERIFY
+    __syncthreads();
+    if (tid == 0 && d.dbg && slot < 4000) {
+        d.dbg[8000 + slot] = s_ck;
+        d.dbg[12000 + slot] = (unsigned long long)C;
+        d.dbg[16000 + slot] = Tb;
+        d.dbg[20000 + slot] = (unsigned long long)(uint32_t)b;
+    }
+#endif
     if (tid == 0) {
         d.ext_n[slot] = ovf ? 0 : (C < N ? C : N);
         d.ext_st[slot] = ovf ? VO_STATUS_OVERFLOW : VO_STATUS_OK;
@@ -2328,9 +2389,6 @@ __host__ __device__ inline int mm_lds_bytes(int)
 {
     return MM_CH * 32 + (MM_CH / 16) * 16 + 16;
 }
-#ifndef MM_VERIFY
-#define MM_VERIFY 0                   // diagnostic build: every MFMA key re-derived with popc (d.dbg counters)
-#endif
 __device__ __forceinline__ int ratio_accept13(uint32_t m1, uint32_t m2, float ratio)
 {
     if (m1 == 0xFFFFFFFFu || m2 == 0xFFFFFFFFu) return -1;
@@ -4459,7 +4517,7 @@ void launch_match(const VoDev& d, int stage, hipStream_t s)
 {
     if (d.match_bits == 32)
     {
-        static const int mm_env = getenv("VO_MATCH_MFMA") ? atoi(getenv("VO_MATCH_MFMA")) : 1;
+        static const int mm_env = getenv("VO_MATCH_MFMA") ? atoi(getenv("VO_MATCH_MFMA")) : 0;
         static const bool mm_ok = mm_lds_bytes(4096) <= 64 * 1024;   // the default dynamic LDS cap
         if (mm_env && mm_ok) {
             // all-pairs distances on the matrix cores (k_match_mfma)
@@ -4483,7 +4541,7 @@ void launch_match(const VoDev& d, int stage, hipStream_t s)
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        MT512_TILE * 64) == hipSuccess;
         (void)lds_ok;
-        static const int mm_env = getenv("VO_MATCH_MFMA") ? atoi(getenv("VO_MATCH_MFMA")) : 1;
+        static const int mm_env = getenv("VO_MATCH_MFMA") ? atoi(getenv("VO_MATCH_MFMA")) : 0;
         static const bool mm5_ok = hipFuncSetAttribute((const void*)k_match512_mfma,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        MM5_CH * 512) == hipSuccess;

@@ -42,11 +42,11 @@ if dbg:
     import ctypes as C
     L = ctx.lib
     L.vo_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
-    dbuf = np.zeros(6004, np.uint64)
+    dbuf = np.zeros(22000, np.uint64)
 
     def counters():
         L.vo_debug_stamps(ctx.h, dbuf.ctypes.data_as(C.c_void_p), dbuf.size)
-        return dbuf[6000:6004].astype(np.int64).copy()
+        return dbuf[6000:6008].astype(np.int64).copy()
     c_prev = counters()
 ring = os.environ.get("DET_RING") == "1"     # compare the extracted ring slots too (vo_debug_ring)
 if ring:
@@ -64,6 +64,9 @@ if ring:
         return nk, kp, pr
 ref = step(0)
 ring_ref = ring_read() if ring else None
+if dbg:
+    counters()
+    sel_ref = dbuf[8000:21600].copy()
 bad = 0
 t0 = time.time()
 for r in range(reps):
@@ -75,12 +78,26 @@ for r in range(reps):
         c_now = counters()
         dc = c_now - c_prev
         c_prev = c_now
-        msg = f" mfma keys wrong {dc[0]} of {dc[1]}, stale match_j {dc[2]} of {dc[3]}"
+        msg = (f" mfma keys wrong {dc[0]} of {dc[1]}, stale match_j {dc[2]} of {dc[3]},"
+               f" select: hist total != keys {dc[4]}, need > boundary keys {dc[5]} of {dc[6]} frames")
     if ring:
         nk, kp, pr = ring_read()
         fd = [f for f in range(NF) if nk[f] != ring_ref[0][f] or not np.array_equal(kp[f, :nk[f]], ring_ref[1][f, :nk[f]])
               or not np.array_equal(pr[f, :nk[f]], ring_ref[2][f, :nk[f]])]
         msg += f" ring frames differing: {len(fd)}" + (f" {fd[:6]}" if fd else "")
+        for f in fd[:2]:
+            if dbg:
+                sel = dbuf[8000:21600]
+                msg += (f"\n    select frame {f}: key-list checksum {'same' if sel[f] == sel_ref[f] else 'DIFFERS'},"
+                        f" C {sel_ref[4000 + f]} -> {sel[4000 + f]}, Tb {hex(int(sel_ref[8000 + f]))} -> {hex(int(sel[8000 + f]))},"
+                        f" b {sel_ref[12000 + f]} -> {sel[12000 + f]}")
+            n0 = ring_ref[0][f]
+            kd = np.nonzero((kp[f, :n0] != ring_ref[1][f, :n0]).any(1))[0]
+            pd = np.nonzero(pr[f, :n0] != ring_ref[2][f, :n0])[0]
+            msg += (f"\n    ring frame {f}: n {n0} -> {nk[f]}; {kd.size} keypoints differ {kd[:6].tolist()}"
+                    f" (ref {ring_ref[1][f, kd[:3]].tolist()} now {kp[f, kd[:3]].tolist()});"
+                    f" {pd.size} prefixes differ {pd[:6].tolist()}"
+                    f" (ref {[hex(v) for v in ring_ref[2][f, pd[:3]]]} now {[hex(v) for v in pr[f, pd[:3]]]})")
     print(f"rep {r} timing {m}: {'same' if same else 'DIFFERS'} ({time.time() - t0:.1f} s){msg}", flush=True)
     if same:
         continue
