@@ -22,7 +22,8 @@ EXPORTS = [
     "vo_response", "vo_match", "vo_ransac_F", "vo_ransac_run", "vo_fit_F", "vo_pose", "vo_set_ground_truth", "vo_set_sequence_starts", "vo_set_frame_origin",
     "vo_trajectory_state", "vo_ring_slots", "vo_rechain", "vo_process_frame",
     "vo_process_frames_device", "vo_process_frames_host", "vo_extract_frames_device", "vo_host_alloc", "vo_host_free", "vo_imread_gray", "vo_device_alloc", "vo_device_free", "vo_device_upload", "vo_reset",
-    "vo_last_kernel_times", "vo_last_kernel_stats", "vo_enable_kernel_timing", "vo_unpack_descriptor",
+    "vo_last_kernel_times", "vo_last_kernel_stats", "vo_enable_kernel_timing", "vo_kernel_form",
+    "vo_unpack_descriptor",
 ]
 
 
@@ -85,6 +86,8 @@ def load():
     L.vo_last_kernel_times.argtypes = [P, C.POINTER(C.c_char_p), C.POINTER(C.c_float), I]
     L.vo_last_kernel_stats.argtypes = [P, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.POINTER(C.c_float), I]
     L.vo_enable_kernel_timing.argtypes = [P, I]
+    L.vo_kernel_form.argtypes = [P, I]
+    L.vo_kernel_form.restype = C.c_char_p
     L.vo_unpack_descriptor.argtypes = [P, P]
     L.vo_unpack_descriptor.restype = None
     L.vo_selftest_arith.argtypes = [P, P, P, P, P, P, I, I]

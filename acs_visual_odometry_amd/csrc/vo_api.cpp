@@ -81,6 +81,8 @@ struct vo_ctx {
     std::vector<int> kcount;          // timed launches per kernel
     std::vector<int> klaunch;         // launches per kernel in the last call
     int last_frames = 0;
+    struct Buf { const char* name; uint64_t ptr, bytes; };
+    std::vector<Buf> layout;          // device buffers allocated by vo_create (vo_debug_layout)
 };
 
 namespace {
@@ -138,6 +140,14 @@ template <typename T>
 int dalloc(T** p, size_t n)
 {
     return hip_ok(hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T)));
+}
+// dalloc of a context buffer, recorded for vo_debug_layout (which buffer an address falls in)
+template <typename T>
+int dalloc_rec(vo_ctx* c, const char* name, T** p, size_t n)
+{
+    const int rc = dalloc(p, n);
+    if (rc == VO_OK) c->layout.push_back({name, (uint64_t)(uintptr_t)*p, (uint64_t)(std::max<size_t>(n, 1) * sizeof(T))});
+    return rc;
 }
 
 int sync_all(vo_ctx* c)
@@ -284,6 +294,7 @@ int enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, 
     d.single = single ? 1 : 0;          // the single-frame call: latency-shaped extract launches
     const size_t B = (size_t)c->B;
     d.eq = eq;
+    d.diag_f0 = f0;
     d.blurred += d.bplane * B * eq;
     d.cand += (size_t)d.cand_cap * B * eq;
     d.tilerows += (size_t)d.ntiles * 16 * B * eq;
@@ -291,6 +302,7 @@ int enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, 
     d.selbits += ((size_t)d.cand_cap / 64 + 1) * B * eq;
     d.selctl += B * eq;
     d.hist += (size_t)VO_HIST_BINS * B * eq;
+    if (d.tile_ck) d.tile_ck += (size_t)d.ntiles * B * eq;
     timed(c, ev, 0, q, [&] { vo::launch_stencil(d, img0, frame_bytes, nb, 0, q); });
     if (ev_stencil) HIPCHK(hipEventRecord(ev_stencil, q));
     if (q2) {
@@ -746,46 +758,53 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     d.sel1 = getenv("VO_SEL1") ? atoi(getenv("VO_SEL1")) != 0 : ntiles < VO_SEL_BANDED_TILES;
     if (d.sel_emit_lds < 0) d.sel1 = 1;
     const size_t np = (size_t)W * H;
-    rc |= dalloc(&d.frame_in, np);
+    rc |= dalloc_rec(c, "frame_in", &d.frame_in, np);
     d.bstride = vo_blur_stride(W);
     d.bplane = (size_t)d.bstride * vo_blur_rows(H);
-    rc |= dalloc(&d.blurred, d.bplane * B * VO_EXT_QUEUES);
-    rc |= dalloc(&d.response, np);
-    rc |= dalloc(&d.cand, (size_t)d.cand_cap * B * VO_EXT_QUEUES);
-    rc |= dalloc(&d.tilerows, (size_t)ntiles * 16 * B * VO_EXT_QUEUES);
-    rc |= dalloc(&d.ckeys, (size_t)d.cand_cap * B * VO_EXT_QUEUES);
-    rc |= dalloc(&d.selbits, ((size_t)d.cand_cap / 64 + 1) * B * VO_EXT_QUEUES);
-    rc |= dalloc(&d.hist, (size_t)VO_HIST_BINS * B * VO_EXT_QUEUES);
-    rc |= dalloc(&d.selctl, (size_t)B * VO_EXT_QUEUES);
-    rc |= dalloc(&d.kps, (size_t)N * VO_SLOTS);
-    rc |= dalloc(&d.desc, (size_t)N * 8 * VO_SLOTS);
-    rc |= dalloc(&d.pre, (size_t)N * VO_SLOTS);
+    rc |= dalloc_rec(c, "blurred", &d.blurred, d.bplane * B * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "response", &d.response, np);
+    rc |= dalloc_rec(c, "cand", &d.cand, (size_t)d.cand_cap * B * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "tilerows", &d.tilerows, (size_t)ntiles * 16 * B * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "ckeys", &d.ckeys, (size_t)d.cand_cap * B * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "selbits", &d.selbits, ((size_t)d.cand_cap / 64 + 1) * B * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "hist", &d.hist, (size_t)VO_HIST_BINS * B * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "selctl", &d.selctl, (size_t)B * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "kps", &d.kps, (size_t)N * VO_SLOTS);
+    rc |= dalloc_rec(c, "desc", &d.desc, (size_t)N * 8 * VO_SLOTS);
+    rc |= dalloc_rec(c, "pre", &d.pre, (size_t)N * VO_SLOTS);
     const int WB = d.WB;                                       // pose window buffers: two sets (pass p uses set p & 1)
     d.mask_words = (N + 63) / 64;
     const size_t per[9] = {(size_t)N * WB, (size_t)N * WB, (size_t)N * 4 * WB, (size_t)d.max_hyp * 9 * WB,
                            (size_t)d.max_hyp * WB, (size_t)N * WB, (size_t)d.max_hyp * d.mask_words * WB,
                            (size_t)N * 4 * WB, (size_t)WB};
     std::memcpy(c->set_off, per, sizeof(per));
-    rc |= dalloc(&d.match_j, 2 * per[0]);
-    rc |= dalloc(&d.match_pairs, 2 * per[1]);
-    rc |= dalloc(&d.pts, 2 * per[2]);
-    rc |= dalloc(&d.hypF, 2 * per[3]);
-    rc |= dalloc(&d.counts, 2 * per[4]);
-    rc |= dalloc(&d.inl, 2 * per[5]);
-    rc |= dalloc(&d.inlmask, 2 * per[6]);
-    rc |= dalloc(&d.model_p, 2 * per[7]);
-    rc |= dalloc(&d.work, 2 * per[8]);
-    rc |= dalloc(&d.plan, VO_PASS_RING);
-    rc |= dalloc(&d.snap, VO_PASS_RING);
-    rc |= dalloc(&d.st, 1);
-    rc |= dalloc(&d.ext_n, VO_SLOTS);
-    rc |= dalloc(&d.ext_st, VO_SLOTS);
-    rc |= dalloc(&d.seq_starts, VO_MAX_SEQ_STARTS);
-    rc |= dalloc(&d.ctr, VO_CTR_WORDS);
-    rc |= dalloc(&d.trec, VO_SLOTS);
-    rc |= dalloc(&d.plog, VO_PLOG);
-#if defined(VO_STAMPS) || (defined(MM_VERIFY) && MM_VERIFY)
-    rc |= dalloc(&d.dbg, (size_t)d.max_hyp * 16);   // stamps / diagnostic counters (words 6000..6003)
+    rc |= dalloc_rec(c, "match_j", &d.match_j, 2 * per[0]);
+    rc |= dalloc_rec(c, "match_pairs", &d.match_pairs, 2 * per[1]);
+    rc |= dalloc_rec(c, "pts", &d.pts, 2 * per[2]);
+    rc |= dalloc_rec(c, "hypF", &d.hypF, 2 * per[3]);
+    rc |= dalloc_rec(c, "counts", &d.counts, 2 * per[4]);
+    rc |= dalloc_rec(c, "inl", &d.inl, 2 * per[5]);
+    rc |= dalloc_rec(c, "inlmask", &d.inlmask, 2 * per[6]);
+    rc |= dalloc_rec(c, "model_p", &d.model_p, 2 * per[7]);
+    rc |= dalloc_rec(c, "work", &d.work, 2 * per[8]);
+    rc |= dalloc_rec(c, "plan", &d.plan, VO_PASS_RING);
+    rc |= dalloc_rec(c, "snap", &d.snap, VO_PASS_RING);
+    rc |= dalloc_rec(c, "st", &d.st, 1);
+    rc |= dalloc_rec(c, "ext_n", &d.ext_n, VO_SLOTS);
+    rc |= dalloc_rec(c, "ext_st", &d.ext_st, VO_SLOTS);
+    rc |= dalloc_rec(c, "seq_starts", &d.seq_starts, VO_MAX_SEQ_STARTS);
+    rc |= dalloc_rec(c, "ctr", &d.ctr, VO_CTR_WORDS);
+    rc |= dalloc_rec(c, "trec", &d.trec, VO_SLOTS);
+    rc |= dalloc_rec(c, "plog", &d.plog, VO_PLOG);
+#if defined(VO_STAMPS) || (defined(MM_VERIFY) && MM_VERIFY) || ST_DIAG
+    rc |= dalloc_rec(c, "dbg", &d.dbg, (size_t)d.max_hyp * 16);   // stamps / diagnostic counters (words 6000..6003)
+#endif
+#if ST_DIAG
+    rc |= dalloc_rec(c, "tile_ck", &d.tile_ck, (size_t)ntiles * B * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "diag_tile", &d.diag_tile, (size_t)ntiles * VO_DIAG_FRAMES);
+    rc |= dalloc_rec(c, "diag_src", &d.diag_src, (size_t)ntiles * VO_DIAG_FRAMES);
+    rc |= dalloc_rec(c, "diag_resp", &d.diag_resp, (size_t)ntiles * VO_DIAG_FRAMES);
+    rc |= dalloc_rec(c, "diag_keys", &d.diag_keys, (size_t)VO_DIAG_KEYS * VO_DIAG_FRAMES);
 #endif
     if (rc != VO_OK) return bail(VO_ERR_HIP);
     const std::vector<uint16_t>& tab = maxit_table(N, k.ransac_p);
@@ -801,6 +820,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     (void)hipMemset(d.desc, 0, sizeof(uint64_t) * 8 * N * VO_SLOTS);
     (void)hipMemset(d.pre, 0, sizeof(uint32_t) * N * VO_SLOTS);
     (void)hipMemset(d.selctl, 0, sizeof(VoSelCtl) * B * VO_EXT_QUEUES);   // arrival / boundary counters
+    if (d.dbg) (void)hipMemset(d.dbg, 0, sizeof(unsigned long long) * (size_t)d.max_hyp * 16);
     d.n_seq_starts = 0;
     d.origin = 0;
     if (ensure_out(c, 16) != VO_OK) return bail(VO_ERR_HIP);
@@ -824,7 +844,7 @@ void vo_destroy(vo_ctx* c)
     void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.tilerows, d.ckeys, d.selbits, d.hist, d.selctl, d.ext_n, d.ext_st, (void*)d.seq_starts,
                     d.kps, d.desc, d.pre, d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.inlmask,
                     d.model_p, d.work, d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr, d.trec, d.plog, d.dbg,
-                    d.plan, d.snap};
+                    d.plan, d.snap, d.tile_ck, d.diag_tile, d.diag_src, d.diag_resp, d.diag_keys};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->out_host) (void)hipHostFree(c->out_host);
@@ -1379,6 +1399,15 @@ int vo_last_kernel_stats(vo_ctx* c, const char** names, float* ms_per_launch, fl
     return nk;
 }
 
+// the kernel symbol(s) (base names, comma-separated) that stage k of the batched path launches in
+// this context, k as vo_last_kernel_stats numbers the stages: which rows of a rocprofv3 summary of
+// the same run belong to the stage (the matcher has four forms, the select two)
+const char* vo_kernel_form(vo_ctx* c, int k)
+{
+    if (!c || k < 0 || k >= vo::kernel_count()) return nullptr;
+    return vo::kernel_form(c->d, k);
+}
+
 // diagnostics: copy the stamp buffer (VO_STAMPS builds; returns 0 entries otherwise)
 int vo_debug_stamps(vo_ctx* c, unsigned long long* out, int n)
 {
@@ -1391,6 +1420,35 @@ int vo_debug_stamps(vo_ctx* c, unsigned long long* out, int n)
 
 // diagnostics (tools/det_stress.py): the ring slots of frames [f0, f0 + n) as the last call left
 // them -- keypoint counts, keypoints (n x N int2) and 32-test prefixes (n x N u32)
+// device buffer i of the context (name, address, bytes), i = 0 .. count - 1; returns the count
+// (i out of range: only the count).  Diagnostics: which buffer a device address falls in.
+extern "C" int vo_debug_layout(vo_ctx* c, int i, const char** name, uint64_t* ptr, uint64_t* bytes)
+{
+    if (!c) return VO_ERR_ARG;
+    const int n = (int)c->layout.size();
+    if (i >= 0 && i < n) {
+        if (name) *name = c->layout[i].name;
+        if (ptr) *ptr = c->layout[i].ptr;
+        if (bytes) *bytes = c->layout[i].bytes;
+    }
+    return n;
+}
+
+// ST_DIAG builds: rows [f0, f0 + n) of diagnostic array `what` (0 diag_tile, 1 diag_src, 2 diag_resp:
+// ntiles words per frame; 3 diag_keys: VO_DIAG_KEYS words per frame).  Returns the words per frame.
+extern "C" int vo_debug_diag(vo_ctx* c, int what, int f0, int n, unsigned long long* out)
+{
+    if (!c) return VO_ERR_ARG;
+    const VoDev& d = c->d;
+    unsigned long long* src[4] = {d.diag_tile, d.diag_src, d.diag_resp, d.diag_keys};
+    if (what < 0 || what > 3 || !src[what]) return 0;
+    const size_t per = what == 3 ? (size_t)VO_DIAG_KEYS : (size_t)d.ntiles;
+    if (f0 < 0 || n < 0 || f0 + n > VO_DIAG_FRAMES) return VO_ERR_ARG;
+    SYNC_ALL(c);
+    if (out && n) HIPCHK(hipMemcpy(out, src[what] + (size_t)f0 * per, per * n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return (int)per;
+}
+
 extern "C" int vo_debug_ring(vo_ctx* c, int f0, int n, int32_t* nk, int32_t* kps, uint32_t* pre)
 {
     if (!c || f0 < 0 || n <= 0 || n > c->d.ring || !nk || !kps || !pre) return VO_ERR_ARG;

@@ -42,6 +42,11 @@
 #include <stdint.h>
 
 #define VO_HIST_BINS 4096
+#ifndef ST_DIAG
+#define ST_DIAG 0          // diagnostic build: per-tile key checksums stencil -> select (d.tile_ck, d.dbg 24000..)
+#endif
+#define VO_DIAG_FRAMES 4096
+#define VO_DIAG_KEYS 8192
 #ifndef VO_SEL_BANDS
 #define VO_SEL_BANDS 8     // select workgroups per frame: bands of tile rows (k_select_count / k_select_emit)
 #endif
@@ -282,6 +287,13 @@ struct VoDev {
     VoPlan* plan;         // x VO_PASS_RING
     VoSnap* snap;         // x VO_PASS_RING
     unsigned long long* dbg;   // diagnostic s_memtime stamps (VO_STAMPS builds only)
+    unsigned long long* tile_ck;   // ST_DIAG builds: x B x VO_EXT_QUEUES, per tile the stencil's key checksum
+    // ST_DIAG builds, per frame f < VO_DIAG_FRAMES of the call (frame index since vo_reset):
+    unsigned long long* diag_tile;   // [f][tile]  select: checksum of the tile's keys as read
+    unsigned long long* diag_src;    // [f][tile]  stencil: checksum of the source rows a wave consumed (even tiles)
+    unsigned long long* diag_resp;   // [f][tile]  stencil: checksum of the responses a wave computed (even tiles)
+    unsigned long long* diag_keys;   // [f][VO_DIAG_KEYS] select: the frame's compact key list (first VO_DIAG_KEYS)
+    int diag_f0;                     // frame index of batch frame 0 (enqueue_extract)
 };
 
 // launch wrappers (vo_kernels.hip)
@@ -315,5 +327,6 @@ void launch_selftest_nullvec9(const double* S, const double* x0, double* f, int*
 void launch_selftest_arith(const float* fa, const float* fb, float* fo, const double* da,
                            const double* db, double* dout, int n, hipStream_t s);
 int kernel_count();
+const char* kernel_form(const VoDev& d, int k);   // the kernel symbol(s) stage k launches (profiles)
 const char* kernel_name(int i);
 }  // namespace vo

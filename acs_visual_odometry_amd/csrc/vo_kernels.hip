@@ -552,7 +552,13 @@ __device__ __forceinline__ void st_for(F&& f, std::integer_sequence<int, I...>)
 {
     (f(std::integral_constant<int, I>{}), ...);
 }
-#define ST_BUF_DW3 0x00020000      // gfx9 buffer descriptor word 3 (raw bytes, no format)
+#define ST_BUF_DW3 0x00020000
+#ifndef LDS_POISON
+#define LDS_POISON 0      // diagnostic build: k_select / k_describe poison their LDS first
+#endif
+#ifndef ST_DROP_SOFFSET
+#define ST_DROP_SOFFSET 0
+#endif      // gfx9 buffer descriptor word 3 (raw bytes, no format)
 
 // grid xcd_grid(ceil(waves / 4), nb): 4 waves per workgroup, one (strip, segment) per wave
 #ifndef ST_WAVES_PER_EU
@@ -593,6 +599,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
     // range for pairs off the strip and past the image's last column.  A pair half off the strip
     // stores its neighbour strip's column too -- the same value that strip's wave stores.
     const int boff = (outc(c0) || outc(c0 + 1)) && c0 < W ? c0 + VO_BLUR_X0 : 0x40000000;
+    int boffq = boff;                  // the voffset of a group's last 4 rows (set per group below)
     const bool isB = lane >= 32;                              // the strip's second tile
     const bool hasB = 2 * sxi + 1 < ntx;
     // the wave's columns reach the image's outer two columns, where gradients (kernel .c:59-76)
@@ -624,6 +631,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
     int ru0 = 0, rm0 = 0, rd0 = 0, ru1 = 0, rm1 = 0, rd1 = 0;               // response rows (f32 bits)
     int toffA = 0, toffB = 0;                                                // candidates so far per tile
     int trows = 0;                                                           // lane r (16 + r): tile A (B) row r count
+#if ST_DIAG
+    unsigned long long dck = 0ull;                                           // checksum of the keys this lane stored
+    unsigned long long sck = 0ull, rck = 0ull;                               // source rows consumed, responses computed
+    const int dfr = d.diag_f0 + z;                                           // frame index (diagnostic arrays)
+#endif
 
     // lane u of the result: byte offset of source row ys - 7 + k0 + u (u < 16)
     auto row_offsets = [&](int k0) {
@@ -642,6 +654,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         constexpr int P = decltype(PH)::value;
         constexpr int r = decltype(R)::value;
         s0 = s1; s1 = s2; s2 = s3; s3 = s4; s4 = s5; s5 = s6; s6 = src;
+#if ST_DIAG
+        sck += mix64((uint64_t)src ^ ((uint64_t)(uint32_t)k << 32));
+#endif
         if constexpr (P >= 1) {
             // 1. 7x7 blur (cv::GaussianBlur 8U fixed point, A.1): vertical taps on both columns
             //    in 16-bit halves (<= 65280); the horizontal taps as dot products of 16-bit pairs
@@ -666,12 +681,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             BE = st_f2{(float)((ha >> 16) & 255u), (float)((hb >> 16) & 255u)};
             if constexpr (P >= 3) {
                 // blurred row ys - 10 + k: the plane is padded to whole strips and 4 rows past the
-                // last tile, so every output lane stores; rows past the segment are the next
-                // segment's (the same values, stored by its wave): their row offset is put out of
-                // range, so the store is dropped without a branch
+                // last tile, so every output lane stores; rows past the segment (k >= SEG + 10:
+                // the last 4 rows of the segment's last tile row group) are the next segment's
+                // (the same values, stored by its wave), so their store is dropped by an
+                // out-of-range *voffset* (boffq).  The row offset rides in soffset, which gfx950's
+                // range check does not include (tests/hip/buffer_range_probe.hip): round 3 put
+                // the drop there and those stores landed 1 GiB past the plane.
+#if ST_DROP_SOFFSET
+                // round 3's form, kept for the A/B evidence run only (tools/gpu_det.sh): the drop in soffset
                 const int brow = k < SEG + 10 ? (ys - 10 + k) * Wb : 0x40000000;
                 __builtin_amdgcn_raw_buffer_store_b16((unsigned short)__builtin_amdgcn_perm(hb, ha, 0x0c0c0602u), rblur, boff,
                                                       brow, 0);
+                (void)boffq;
+#else
+                if constexpr (P == 5 && r >= ST_TH - 4) {
+                    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)__builtin_amdgcn_perm(hb, ha, 0x0c0c0602u), rblur,
+                                                          boffq, (ys - 10 + k) * Wb, 0);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)__builtin_amdgcn_perm(hb, ha, 0x0c0c0602u), rblur,
+                                                          boff, (ys - 10 + k) * Wb, 0);
+                }
+#endif
             }
         }
         if constexpr (P >= 2) {
@@ -767,6 +797,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             }
             ru0 = rm0; rm0 = rd0; rd0 = o0;
             ru1 = rm1; rm1 = rd1; rd1 = o1;
+#if ST_DIAG
+            rck += mix64((((uint64_t)(uint32_t)o0 << 32) | (uint32_t)o1) ^ ((uint64_t)(uint32_t)k << 48));
+#endif
         }
         if constexpr (P >= 5) {
             // 5. strict 3x3 NMS of row yn = tile row r inside the retinal margin
@@ -812,11 +845,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                     *(uint64_t*)(tc + base * 8u) = ((uint64_t)(uint32_t)rm0 << 32) | key_lo;
                     const uint32_t bin = min(((uint32_t)rm0 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1));
                     atomicAdd(&hist[bin], 1u);
+#if ST_DIAG
+                    dck += mix64((((uint64_t)(uint32_t)rm0 << 32) | key_lo) ^ ((uint64_t)base << 48));
+#endif
                 }
                 if (mx1) {
                     *(uint64_t*)(tc + (base + (mx0 ? 1u : 0u)) * 8u) = ((uint64_t)(uint32_t)rm1 << 32) | (key_lo + 1u);
                     const uint32_t bin = min(((uint32_t)rm1 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1));
                     atomicAdd(&hist[bin], 1u);
+#if ST_DIAG
+                    dck += mix64((((uint64_t)(uint32_t)rm1 << 32) | (key_lo + 1u)) ^ ((uint64_t)(base + (mx0 ? 1u : 0u)) << 48));
+#endif
                 }
             }
             toffA += cA; toffB += cB;
@@ -859,6 +898,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         const int k0 = 14 + ST_TH * i;
         const int rows = row_offsets(k0 + LA);
         toffA = 0; toffB = 0;
+        // rows k0 + 12 .. k0 + 15 reach past the segment (k >= SEG + 10) only in its last group
+        static_assert(14 + ST_TH * (SEGT - 1) + (ST_TH - 4) == SEG + 10, "segment tail rows");
+        boffq = i == SEGT - 1 ? 0x40000000 : boff;
         // the group's 16 row offsets to SGPRs up front: a v_readlane right before the buffer load
         // whose offset it feeds costs the wave five wait states (s_nop 4) per row
         int soff[ST_TH];
@@ -878,6 +920,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         // the 16 row counts of tile A (lanes 0..15) and B (16..31) are contiguous
         const int tileA = (ys / ST_TH + i) * ntx + 2 * sxi;
         if (lane < (hasB ? 2 * ST_TH : ST_TH)) tilerows[tileA * ST_TH + lane] = (uint8_t)trows;
+#if ST_DIAG
+        // per tile: the sum over its keys of mix64(key ^ slot << 48), lanes 0..31 tile A, 32..63 tile B
+#pragma unroll
+        for (int off = 1; off < 32; off <<= 1) dck += __shfl_xor(dck, off);
+        if (d.tile_ck && (lane == 0 || (lane == 32 && hasB)))
+            d.tile_ck[(size_t)z * d.ntiles + tileA + (lane >> 5)] = dck;
+        dck = 0ull;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            sck += __shfl_xor(sck, off);
+            rck += __shfl_xor(rck, off);
+        }
+        if (d.diag_src && lane == 0 && dfr < VO_DIAG_FRAMES) {
+            d.diag_src[(size_t)dfr * d.ntiles + tileA] = sck;
+            d.diag_resp[(size_t)dfr * d.ntiles + tileA] = rck;
+        }
+        sck = 0ull; rck = 0ull;
+#endif
     }
 }
 
@@ -986,6 +1046,19 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
 #if MM_VERIFY
     __shared__ unsigned long long s_ck;                 // diagnostic: checksum of the frame's key list
 #endif
+#if LDS_POISON
+    // diagnostic build: the whole dynamic LDS and the static words filled with a launch-varying
+    // pattern first, so a read of LDS this workgroup did not write shows up as a result change
+    {
+        const uint32_t pz = (uint32_t)wall_clock64() * 0x9E3779B9u ^ (uint32_t)blockIdx.x;
+        uint32_t* w = reinterpret_cast<uint32_t*>(smem);
+        for (int i = threadIdx.x; i < d.sel_lds / 4; i += 1024) w[i] = pz + (uint32_t)i * 0x85EBCA6Bu;
+        if (threadIdx.x < 16) { s_hs[threadIdx.x] = pz; s_wsum[threadIdx.x] = (int)pz; }
+        if (threadIdx.x < 256) s_dh[threadIdx.x] = pz;
+        if (threadIdx.x == 0) { s_tb = ((uint64_t)pz << 32) | pz; s_dsel = (int)pz; s_rem = (int)pz; }
+        __syncthreads();
+    }
+#endif
     if (tid == 0) {
         s_nbnd = 0; s_b = -1; s_above = 0;
         s_slot = ext_slot(d, f0, z, slot_override);
@@ -1042,6 +1115,12 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     for (int t = tid; t < ntiles; t += 1024) {
         const int b = s_tpre[t], n = s_tpre[t + 1] - b;
         const uint64_t* src = cand + (size_t)t * TCAP;
+#if ST_DIAG
+        unsigned long long ck = 0ull;
+        uint32_t prev_lo = 0u;
+        int bad = -1;
+        const int tr = t / ntx, tx = t % ntx;
+#endif
         for (int i = 0; i < n; i += 4) {
             uint64_t v[4];
 #pragma unroll
@@ -1049,9 +1128,46 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 if (i + u < n) keys[b + i + u] = v[u];
+#if ST_DIAG
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + u < n) {
+                    // the slot index: tile A's keys from 0, tile B's from ST_TCAP (k_stencil base)
+                    const uint64_t slot = (uint64_t)(i + u) + ((tx & 1) ? ST_TCAP : 0);
+                    ck += mix64(v[u] ^ (slot << 48));
+                    const uint32_t lo = (uint32_t)v[u], row = lo >> 16, col = lo & 0xFFFF;
+                    const bool ok = (int)row / ST_TH == tr && (int)col / ST_TW == tx && (uint32_t)(v[u] >> 32) > d.thr_bits &&
+                                    (i + u == 0 || lo > prev_lo);
+                    if (!ok && bad < 0) bad = i + u;
+                    prev_lo = lo;
+                }
+#endif
         }
+#if ST_DIAG
+        if (d.diag_tile && f0 + z < VO_DIAG_FRAMES) d.diag_tile[(size_t)(f0 + z) * ntiles + t] = ck;
+        if (d.dbg && d.tile_ck) {
+            const unsigned long long want = d.tile_ck[(size_t)z * ntiles + t];
+            atomicAdd(&d.dbg[24000], 1ull);
+            if (want != ck || bad >= 0) {
+                atomicAdd(&d.dbg[want != ck ? 24001 : 24002], 1ull);
+                if (atomicCAS(&d.dbg[24003], 0ull, (unsigned long long)(f0 + z + 1)) == 0ull) {
+                    d.dbg[24004] = (unsigned long long)t;
+                    d.dbg[24005] = want;
+                    d.dbg[24006] = ck;
+                    d.dbg[24007] = (unsigned long long)n;
+                    d.dbg[24008] = (unsigned long long)(bad + 1);
+                    for (int i = 0; i < n && i < 24; ++i) d.dbg[24010 + i] = src[i];
+                }
+            }
+        }
+#endif
     }
     __syncthreads();
+#if ST_DIAG
+    if (d.diag_keys && f0 + z < VO_DIAG_FRAMES)
+        for (int g = tid; g < VO_DIAG_KEYS; g += 1024)
+            d.diag_keys[(size_t)(f0 + z) * VO_DIAG_KEYS + g] = g < C ? keys[g] : 0ull;
+#endif
 #if MM_VERIFY
     {
         unsigned long long ck = 0ull;
@@ -1987,6 +2103,14 @@ __global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int
                                                             int nb)
 {
     __shared__ float s_I0[DS_WAVES][DS_UNROLL ? 1 : DS_OROWS][DS_KPW];   // sample columns (the looped sums)
+#if LDS_POISON
+    {
+        const uint32_t pz = (uint32_t)wall_clock64() * 0x9E3779B9u ^ (uint32_t)blockIdx.x;
+        float* w = &s_I0[0][0][0];
+        for (int i = threadIdx.x; i < (int)(sizeof(s_I0) / 4); i += 64 * DS_WAVES) w[i] = __uint_as_float(pz + (uint32_t)i);
+        __syncthreads();
+    }
+#endif
     int z, bx;
     if (xcd_frame(d, (d.N + DS_KPB - 1) / DS_KPB, nb, z, bx)) {
         const int cur = ext_slot(d, f0, z, slot_override);
@@ -2379,6 +2503,9 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
 // table (32 B each, MM_CH at a time); a wave owns MM_G groups of 16 queries and walks every candidate tile,
 // one ds_read_b128 and MM_G MFMAs per tile; the four lane groups of a query (rows 4h .. 4h + 3)
 // merge by shuffles at the end.  Results equal k_match's bit for bit.
+#ifndef VO_MATCH_MFMA_DEFAULT
+#define VO_MATCH_MFMA_DEFAULT 0       // VO_MATCH_MFMA unset: the VALU matchers
+#endif
 #define MM_GROUPS 4                   // query groups of 16 per wave: 64 queries per wave, 256 per workgroup
                                       // (the single-frame call: 1, 64 per workgroup, 4x the workgroups)
 #define MM_CH 512                     // candidates per LDS chunk (16 KB table: LDS stays free for the
@@ -4513,13 +4640,37 @@ void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned
     hipLaunchKernelGGL(k_describe, dim3(xcd_grid((d.N + DS_KPB - 1) / DS_KPB, nb)), dim3(64 * DS_WAVES), 0, s, d, f0,
                        slot_override, publish, nb);
 }
+// the matcher form launch_match runs: the MFMA forms unless VO_MATCH_MFMA=0
+static bool match_uses_mfma()
+{
+    static const int mm_env = getenv("VO_MATCH_MFMA") ? atoi(getenv("VO_MATCH_MFMA")) : VO_MATCH_MFMA_DEFAULT;
+    return mm_env != 0;
+}
+// the kernel symbol(s) (base names, comma-separated) stage k of the batched path launches for
+// this context -- what a rocprofv3 summary of the same run lists (bench.py profile_row)
+const char* kernel_form(const VoDev& d, int k)
+{
+    switch (k) {
+    case 0: return "k_stencil";
+    case 1: return d.sel1 ? "k_select" : "k_select_count,k_select_emit";
+    case 2: return "k_describe";
+    case 3:
+        if (d.match_bits == 32) return match_uses_mfma() ? "k_match_mfma" : "k_match";
+        return match_uses_mfma() ? "k_match512_mfma" : "k_match512";
+    case 4: return "k_ransac_hyp";
+    case 5: return "k_refit";
+    case 6: return "k_triangulate";
+    case 7: return "k_finalize";
+    case 8: return "k_traj";
+    }
+    return "";
+}
 void launch_match(const VoDev& d, int stage, hipStream_t s)
 {
     if (d.match_bits == 32)
     {
-        static const int mm_env = getenv("VO_MATCH_MFMA") ? atoi(getenv("VO_MATCH_MFMA")) : 0;
         static const bool mm_ok = mm_lds_bytes(4096) <= 64 * 1024;   // the default dynamic LDS cap
-        if (mm_env && mm_ok) {
+        if (match_uses_mfma() && mm_ok) {
             // all-pairs distances on the matrix cores (k_match_mfma)
             if (d.single)
                 hipLaunchKernelGGL(k_match_mfma<1>, dim3((d.N + 63) / 64, stage ? 1 : d.gridw), dim3(256),
@@ -4541,11 +4692,10 @@ void launch_match(const VoDev& d, int stage, hipStream_t s)
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        MT512_TILE * 64) == hipSuccess;
         (void)lds_ok;
-        static const int mm_env = getenv("VO_MATCH_MFMA") ? atoi(getenv("VO_MATCH_MFMA")) : 0;
         static const bool mm5_ok = hipFuncSetAttribute((const void*)k_match512_mfma,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        MM5_CH * 512) == hipSuccess;
-        if (mm_env && mm5_ok)
+        if (match_uses_mfma() && mm5_ok)
             hipLaunchKernelGGL(k_match512_mfma, dim3((d.N + 64 * MM5_W - 1) / (64 * MM5_W), stage ? 1 : d.gridw),
                                dim3(64 * MM5_W), (size_t)MM5_CH * 512, s, d, stage);
         else

@@ -229,6 +229,12 @@ class Context:
         k = self.lib.vo_last_kernel_stats(self.h, names, ms, fpl, 32)
         return {names[i].decode(): (ms[i], fpl[i]) for i in range(k) if ms[i] >= 0}
 
+    def kernel_forms(self):
+        """{stage: [kernel symbols]} the batched path of this context launches (vo_kernel_form):
+        which rows of a rocprofv3 summary belong to each stage."""
+        stages = ["stencil", "select", "describe", "match", "ransac", "refit", "triangulate", "finalize", "trajectory"]
+        return {k: self.lib.vo_kernel_form(self.h, i).decode().split(",") for i, k in enumerate(stages)}
+
 
 class DeviceFrames:
     """A batch of frames resident in HBM (uploaded once)."""

@@ -89,20 +89,19 @@ def load_profile(W: int, H: int, bits: int, motion: float = 1.0):
         return None, None
 
 
-def profile_row(prof, kernel: str):
+def profile_row(prof, kernel: str, forms: dict):
     """The profile's per-launch figures of `kernel`, a launch as the live timing counts it: one
-    pose pass launches k_ransac_hyp three times (hypothesis chunks), so the pose-queue kernels are
-    normalised by the passes (k_match calls) and the extract kernels by the batches (k_stencil)."""
+    pose pass launches k_ransac_hyp twice (hypothesis chunks), so the pose-queue kernels are
+    normalised by the passes (matcher calls) and the extract kernels by the batches (k_stencil).
+    forms = Context.kernel_forms(): the exact kernel symbols each stage launched in this run, so a
+    profile of another matcher or select form is never read as this one's (None then)."""
     if not prof:
         return None
-    # the forms a stage can take: the 512-test and MFMA matchers, the banded select's two kernels
-    names = {ROCPROF_NAME[kernel]} | {"match": {"k_match512", "k_match_mfma", "k_match512_mfma"},
-                                      "select": {"k_select_count", "k_select_emit"}}.get(kernel, set())
+    names = set(forms[kernel])
     rows = [r for k, r in prof.items() if k.split("<")[0] in names]
-    if not rows:
-        return None
-    ref = ({"k_match", "k_match512", "k_match_mfma", "k_match512_mfma"} if kernel in POSE_QUEUE or kernel == "trajectory"
-           else {"k_stencil"})
+    if len({k.split("<")[0] for k in prof if k.split("<")[0] in names}) != len(names):
+        return None                                  # the profile ran another form of this stage
+    ref = set(forms["match"]) if kernel in POSE_QUEUE or kernel == "trajectory" else {"k_stencil"}
     ref_calls = [r["calls"] for k, r in prof.items() if k.split("<")[0] in ref]
     launches = max(ref_calls) if ref_calls else max(r["calls"] for r in rows)
 
@@ -112,10 +111,11 @@ def profile_row(prof, kernel: str):
         return sum(r[key] * r["calls"] for r in rows) / launches
     vi, gc = per("valu_insts"), per("grbm_cycles")
     return {"avg_us": per("avg_us"), "hbm_bytes": per("hbm_bytes_per_launch"), "valu_insts": vi,
-            "valu_issue_frac": vi * VALU_CYCLES / (VALU_SIMDS * gc / 8) if vi is not None and gc else None}
+            "valu_issue_frac": vi * VALU_CYCLES / (VALU_SIMDS * gc / 8) if vi is not None and gc else None,
+            "symbols": sorted({k for k in prof if k.split("<")[0] in names})}
 
 
-def roofline_entry(kernel: str, live: list, info: np.ndarray, W: int, H: int, prof, psrc) -> dict:
+def roofline_entry(kernel: str, live: list, info: np.ndarray, W: int, H: int, prof, psrc, forms: dict) -> dict:
     """roofline object of `kernel`: SURVEY 8(d)'s algorithmic bytes per launch over its average
     launch time, the launches timed live with HIP events on its own stream (`live`: kernel_stats()
     of the timed calls); traffic and VALU issue from the committed PMC profile."""
@@ -125,8 +125,8 @@ def roofline_entry(kernel: str, live: list, info: np.ndarray, W: int, H: int, pr
     dom_fpl = float(np.mean(fpl)) if fpl else float("nan")
     abytes = algorithmic_bytes(kernel, W, H, info) * dom_fpl
     achieved = abytes / (dom_ms * 1e-3) / 1e9
-    prow = profile_row(prof, kernel)
-    return {"bound": "hbm", "kernel": kernel, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    prow = profile_row(prof, kernel, forms)
+    return {"bound": "hbm", "kernel": kernel, "symbols": forms[kernel], "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": prow["hbm_bytes"] if prow else None, "traffic_source": psrc,
             "avg_launch_ms": dom_ms, "frames_per_launch": dom_fpl, "algorithmic_bytes_per_launch": abytes,
@@ -139,8 +139,12 @@ def roofline_entry(kernel: str, live: list, info: np.ndarray, W: int, H: int, pr
 
 
 # -- multi-GPU harness (config 5) --------------------------------------------------------
-def rank_sequences(n_seq: int, rank: int, world: int):
-    """Sequence s runs on rank s mod G."""
+def rank_sequences(n_seq: int, rank: int, world: int, scaling: str = "strong"):
+    """The sequences rank `rank` runs.  strong (config 5): n_seq sequences in all, sequence s on
+    rank s mod G; weak: n_seq sequences per rank, rank r owning r*n_seq .. r*n_seq+n_seq-1
+    (every rank runs the N = 1 workload on sequences of its own seeds)."""
+    if scaling == "weak":
+        return [rank * n_seq + i for i in range(n_seq)]
     return [s for s in range(n_seq) if s % world == rank]
 
 
@@ -173,20 +177,32 @@ def aggregate(dist, dt: float, frames_per_rank: int, world: int, backend: str = 
     return dt, frames_per_rank * world / dt
 
 
-def gather_poses(dist, local_rows: dict, n_seq: int, nframes: int, backend: str = "nccl", local: int = 0):
-    """Every sequence's (nframes, 13) rows -- 12 pose values and the status -- on every rank:
-    each rank fills its own sequences into a zero (n_seq, nframes, 13) f64 tensor and one SUM
-    all-reduce assembles them (each sequence is owned by exactly one rank)."""
+def gather_poses(dist, local_rows: dict, owners: list, nframes: int, backend: str = "nccl", local: int = 0):
+    """Every sequence's (nframes, 13) rows -- 12 pose values and the status -- on every rank, by
+    sequence id: owners[r] lists rank r's sequences.  Each rank packs its rows into a (k, nframes,
+    13) block, viewed as int64 so the collective moves raw bits (a SUM all-reduce turned -0.0 into
+    +0.0), and one all_gather assembles the blocks."""
+    n_seq = 1 + max(s for o in owners for s in o)
     out = np.zeros((n_seq, nframes, 13))
-    for s, rows in local_rows.items():
-        out[s] = rows
+    rank = dist.get_rank() if dist is not None else 0
+    kmax = max(len(o) for o in owners)
+    buf = np.zeros((kmax, nframes, 13))
+    for i, s in enumerate(owners[rank]):
+        buf[i] = local_rows[s]
     if dist is None:
+        for i, s in enumerate(owners[0]):
+            out[s] = buf[i]
         return out
     import torch
     dev = f"cuda:{local}" if backend == "nccl" else "cpu"
-    t = torch.from_numpy(out).to(dev)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return t.cpu().numpy()
+    t = torch.from_numpy(buf.view(np.int64).copy()).to(dev)
+    parts = [torch.empty_like(t) for _ in owners]
+    dist.all_gather(parts, t)
+    for r, o in enumerate(owners):
+        blk = parts[r].cpu().numpy().view(np.float64)
+        for i, s in enumerate(o):
+            out[s] = blk[i]
+    return out
 
 
 # -- CPU baseline ------------------------------------------------------------------------
@@ -305,7 +321,7 @@ def run_variants(args, ctx, W, H, frames0, gt0, extra, Context) -> dict:
                 go(timing=100 + KERNELS.index(dom))
                 live.append(ctx.kernel_stats())
             prof, psrc = load_profile(W, H, 32, motion=seq.step)
-            out[tag]["roofline"] = roofline_entry(dom, live, info, W, H, prof, psrc)
+            out[tag]["roofline"] = roofline_entry(dom, live, info, W, H, prof, psrc, ctx.kernel_forms())
         df.free()
     # extract only (config 2), device-resident frames of sequence 0
     df = ctx.device_frames(frames0)
@@ -371,12 +387,13 @@ def run_variants(args, ctx, W, H, frames0, gt0, extra, Context) -> dict:
             _, st, info = g()
             ks = breakdown(cx, g)
             prof, src = load_profile(seq.W, seq.H, bits)
-            prow = profile_row(prof, "match")
+            prow = profile_row(prof, "match", cx.kernel_forms())
             out[f"x1080_{bits}bit"] = {
                 "fps": rate, "frames": fr.shape[0], "match_bits": bits, "motion_m_per_frame": seq.step,
                 "frames_ok": int((st == 0).sum()), "mean_matches": float(info[1:, 1].mean()),
                 "match_us_per_launch": ks.get("match", (float("nan"), 0))[0] * 1e3,
                 "match_frames_per_launch": ks.get("match", (0, 0))[1],
+                "match_kernel": cx.kernel_forms()["match"],
                 "match_rocprof_avg_us": prow["avg_us"] if prow else None,
                 "match_valu_issue_frac": prow["valu_issue_frac"] if prow else None, "profile": src,
                 "kernels_us_per_frame": {k: round(v[0] / v[1] * 1e3, 3) for k, v in ks.items() if v[1] > 0}}
@@ -472,7 +489,11 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=200, help="frames per sequence")
-    ap.add_argument("--sequences", type=int, default=8, help="sequences of the job (config 5: 8)")
+    ap.add_argument("--sequences", type=int, default=8,
+                    help="sequences per rank (--scaling weak) or of the whole job (strong; config 5: 8)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: every rank runs --sequences sequences of its own (the N = 1 workload per GPU); "
+                         "strong: --sequences sequences in all, sequence s on rank s mod G (config 5)")
     ap.add_argument("--width", type=int, default=1241)
     ap.add_argument("--height", type=int, default=376)
     ap.add_argument("--max-kpts", type=int, default=2000)
@@ -499,8 +520,10 @@ def main():
     if args.shard_sequence:
         return shard_main(args, world, rank, local)
     W, H, F = args.width, args.height, args.frames
-    S = max(args.sequences, world)          # every rank gets at least one sequence
-    my_seqs = rank_sequences(S, rank, world)
+    S = args.sequences if args.scaling == "weak" else max(args.sequences, world)   # strong: >= 1 per rank
+    my_seqs = rank_sequences(S, rank, world, args.scaling)
+    owners = [rank_sequences(S, r, world, args.scaling) for r in range(world)]
+    n_total = sum(len(o) for o in owners)
     lead = rank == 0 and world == 1
 
     # -- host-side preparation, before anything touches the GPU (forked workers) --
@@ -511,8 +534,6 @@ def main():
     if lead and not args.no_variants:
         extra_specs = {"motion_0.05": (W, H, F, 0, 0.05), "low_inlier_0.12": (W, H, F, 0, 0.12),
                        "x1080": (1920, 1080, 64, 0, args.motion), "stream": (W, H, 1000, 0, args.motion)}
-    if rank == 0 and world > 1:        # rank 0 runs every sequence alone to check the gather
-        specs += [(W, H, F, s, args.motion) for s in range(S) if s not in my_seqs]
     rendered = render_sequences(specs + list(extra_specs.values()), workers)
     seqs = {sp[3]: (SceneSequence(W, H, nframes=F, seq=sp[3], step=args.motion), rendered[i])
             for i, sp in enumerate(specs)}
@@ -591,12 +612,13 @@ def main():
                        for s in my_seqs)
     rows = {s: np.concatenate([last[s][0].reshape(F, 12), last[s][1].reshape(F, 1).astype(np.float64)], axis=1)
             for s in my_seqs}
-    gathered = gather_poses(dist, rows, S, F, local=local)
-    # rank 0 runs every sequence of the job alone, as the reference would (one run() each), and
-    # checks the gathered rows of the stream(s) against them bit for bit
+    gathered = gather_poses(dist, rows, owners, F, local=local)
+    # every rank runs each of its sequences alone, as the reference would (one run() each); those
+    # rows are gathered too and rank 0 checks every sequence's stream rows against them bit for bit
     gather_ok = None
-    if rank == 0 and not args.no_check:
-        gather_ok = all(bool(np.array_equal(separate(s, seqs[s][1]), gathered[s])) for s in range(S))
+    if not args.no_check:
+        sep = gather_poses(dist, {s: separate(s, seqs[s][1]) for s in my_seqs}, owners, F, local=local)
+        gather_ok = bool(np.array_equal(sep.view(np.int64), gathered.view(np.int64)))
     # the CPU oracle's rows of the first sequence (the cpu_baseline leg's first complete pass)
     # against the GPU's rows of that sequence in the timed stream, bit for bit
     oracle_ok = None
@@ -614,14 +636,15 @@ def main():
 
     if rank == 0:
         prof, psrc = load_profile(W, H, args.match_bits)
-        roof = roofline_entry(dominant, live, info_all, W, H, prof, psrc)
+        forms = ctx.kernel_forms()
+        roof = roofline_entry(dominant, live, info_all, W, H, prof, psrc, forms)
         path_bytes = algorithmic_bytes("path", W, H, info_all)
         kern = {}
         for k in KERNELS:
             if k not in ks:
                 continue
-            r = profile_row(prof, k)
-            kern[k] = {"us_per_frame": round(per_frame[k] * 1e3, 4), "us_per_launch": round(ks[k][0] * 1e3, 2),
+            r = profile_row(prof, k, forms)
+            kern[k] = {"symbols": forms[k],"us_per_frame": round(per_frame[k] * 1e3, 4), "us_per_launch": round(ks[k][0] * 1e3, 2),
                        "frames_per_launch": round(ks[k][1], 2),
                        "algorithmic_bytes_per_frame": round(algorithmic_bytes(k, W, H, info_all), 1),
                        "queue": "pose" if k in POSE_QUEUE else ("trajectory" if k == "trajectory" else "extract"),
@@ -631,13 +654,15 @@ def main():
         line = {
             "metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "u8/f32/u32/f64", "data": "synthetic",
+            "scaling": args.scaling, "vs_baseline": None, "dtype": "u8/f32/u32/f64", "data": "synthetic",
             "config": {"workload": ("kitti_1241x376_2000kpts_full_path" if (W, H) == (1241, 376)
                                     else f"{W}x{H}_{args.max_kpts}kpts_full_path"),
-                       "sequences": S, "frames_per_sequence": F, "sequences_per_gpu": len(my_seqs),
+                       "sequences": n_total, "frames_per_sequence": F, "sequences_per_gpu": len(my_seqs),
                        "width": W, "height": H, "max_kpts": args.max_kpts, "match_bits": args.match_bits,
                        "motion": f"+{args.motion} m/frame along z, 0.1 deg/frame yaw (SURVEY 8(d) scene generator)",
-                       "parallelism": f"config 5: sequence s on GPU s mod {world}, no data-path collective",
+                       "parallelism": (f"{world} GPU(s) x {S} sequences each (weak scaling: sequences r*{S} .. "
+                                       f"r*{S}+{S - 1} on GPU r), no data-path collective" if args.scaling == "weak"
+                                       else f"config 5: sequence s on GPU s mod {world}, no data-path collective"),
                        "frame_batch": ctx.cfg.frame_batch or 64, "inputs": "device-resident (HBM) before timing",
                        "mean_kpts": float(info_all[:, 0].mean()), "mean_matches": float(info_all[:, 1].mean()),
                        "mean_inliers": float(info_all[:, 2].mean()),
@@ -656,6 +681,8 @@ def main():
             "kernels": kern,
             "determinism": {"timed_rows_equal_warmup_rows": bool(repeat_equal),
                             "gathered_rows_equal_separate_runs": gather_ok,
+                            "gather": "all_gather of raw int64 bits (stream rows and separate-run rows of every "
+                                      "sequence)",
                             "oracle_rows_equal": oracle_ok,
                             "oracle_rows_checked": f"sequence {my_seqs[0]}: {F} frames (pose rows + statuses) against "
                                                    f"the CPU oracle's run in the cpu_baseline leg" if oracle_ok is not None

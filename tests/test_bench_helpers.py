@@ -12,16 +12,40 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
+def forms_of(prof, bits):
+    """The stage -> kernel symbols map of the run a profile was taken from (its kernel list)."""
+    base = {k.split("<")[0] for k in prof}
+    match = [m for m in (["k_match_mfma", "k_match"] if bits == 32 else ["k_match512_mfma", "k_match512"])
+             if m in base][:1]
+    sel = ["k_select"] if "k_select" in base else ["k_select_count", "k_select_emit"]
+    return {"stencil": ["k_stencil"], "select": sel, "describe": ["k_describe"], "match": match,
+            "ransac": ["k_ransac_hyp"], "refit": ["k_refit"], "triangulate": ["k_triangulate"],
+            "finalize": ["k_finalize"], "trajectory": ["k_traj"]}
+
+
 @pytest.mark.parametrize("W,H,bits", [(1241, 376, 32), (1920, 1080, 32), (1920, 1080, 512)])
 def test_committed_profiles_have_every_kernel(W, H, bits):
     prof, src = bench.load_profile(W, H, bits)
     assert prof is not None and os.path.exists(os.path.join(ROOT, src))
+    forms = forms_of(prof, bits)
     for k in ["stencil", "select", "describe", "match", "ransac", "refit", "triangulate", "finalize"]:
-        row = bench.profile_row(prof, k)
+        row = bench.profile_row(prof, k, forms)
         assert row is not None, k
         assert row["avg_us"] > 0 and row["hbm_bytes"] > 0, k
+        assert {s.split("<")[0] for s in row["symbols"]} == set(forms[k]), (k, row["symbols"])
         if k in ("stencil", "describe", "match"):
             assert 0.0 < row["valu_issue_frac"] <= 1.0, (k, row)
+
+
+def test_profile_row_refuses_another_form():
+    """A profile of the MFMA matcher is not read as the VALU matcher's (round 3 unioned them)."""
+    prof = {"k_stencil<8,false>": {"calls": 10, "avg_us": 100.0, "hbm_bytes_per_launch": 1.0},
+            "k_match_mfma": {"calls": 12, "avg_us": 80.0, "hbm_bytes_per_launch": 2.0}}
+    forms = {"match": ["k_match"], "stencil": ["k_stencil"]}
+    assert bench.profile_row(prof, "match", forms) is None
+    forms["match"] = ["k_match_mfma"]
+    row = bench.profile_row(prof, "match", forms)
+    assert row["avg_us"] == 80.0 and row["symbols"] == ["k_match_mfma"]
 
 
 def test_algorithmic_bytes_follow_the_survey():

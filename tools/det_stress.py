@@ -21,13 +21,59 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 12
 xreps = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 rendered = render_sequences([(W, H, F, s, 1.0) for s in range(S)], 16)
 seqs = [SceneSequence(W, H, nframes=F, seq=s, step=1.0) for s in range(S)]
+# (after the forked renderers; torch initialises the GPU before the library does)
+# DET_LOAD=gemm[:n]: n bf16 8192^3 GEMMs (torch / hipBLASLt, matrix cores) queued on a torch stream of
+# their own before every step, so unrelated MFMA work co-runs with the path (whatever matcher runs)
+load = os.environ.get("DET_LOAD", "")
+if load.startswith("gemm"):
+    import torch
+    n_gemm = int(load.split(":")[1]) if ":" in load else 16
+    ga = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+    gb = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+    gc = torch.empty(8192, 8192, device="cuda", dtype=torch.bfloat16)
+    gstream = torch.cuda.Stream()
+
+
 ctx = Context(W, H, K=seqs[0].K, max_kpts=2000)
 dall = ctx.device_frames(np.concatenate(rendered))
 gt_all = np.concatenate([s.gt() for s in seqs])
 starts = [F * i for i in range(1, S)]
 
 
+def layout():
+    """The context's device buffers and the frames, and which of them the range
+    [blurred + 1 GiB, + blurred bytes) overlaps: where round 3's soffset-dropped blurred-row
+    stores land if the range check ignores soffset (tests/hip/buffer_range_probe.hip)."""
+    import ctypes as C
+    L = ctx.lib
+    L.vo_debug_layout.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_uint64),
+                                  C.POINTER(C.c_uint64)]
+    bufs = []
+    for i in range(L.vo_debug_layout(ctx.h, -1, None, None, None)):
+        nm, pt, nb = C.c_char_p(), C.c_uint64(), C.c_uint64()
+        L.vo_debug_layout(ctx.h, i, C.byref(nm), C.byref(pt), C.byref(nb))
+        bufs.append((nm.value.decode(), pt.value, nb.value))
+    bufs.append(("frames", int(dall.ptr.value), int(dall.frame_bytes) * int(dall.n)))
+    bl = [b for b in bufs if b[0] == "blurred"][0]
+    lo, hi = bl[1] + (1 << 30), bl[1] + (1 << 30) + bl[2]
+    for nm, pt, nb in sorted(bufs, key=lambda b: b[1]):
+        hit = " <-- blurred + 1 GiB overlaps" if pt < hi and pt + nb > lo else ""
+        print(f"  {nm:12s} {pt:#014x} {nb:12d}{hit}")
+    print(f"  blurred + 1 GiB = [{lo:#014x}, {hi:#014x})", flush=True)
+
+
+layout()
+
+
+def background():
+    if load.startswith("gemm"):
+        with torch.cuda.stream(gstream):
+            for _ in range(n_gemm):
+                torch.matmul(ga, gb, out=gc)
+
+
 def step(timing):
+    background()
     ctx.reset()
     ctx.set_ground_truth(gt_all)
     ctx.set_sequence_starts(starts)
@@ -48,6 +94,30 @@ if dbg:
         L.vo_debug_stamps(ctx.h, dbuf.ctypes.data_as(C.c_void_p), dbuf.size)
         return dbuf[6000:6008].astype(np.int64).copy()
     c_prev = counters()
+diag = os.environ.get("DET_DIAG") == "1"     # ST_DIAG builds: stencil -> select per-tile key checksums
+if diag:
+    import ctypes as C
+    ctx.lib.vo_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    dgbuf = np.zeros(24040, np.uint64)
+
+    def diag_read():
+        ctx.lib.vo_debug_stamps(ctx.h, dgbuf.ctypes.data_as(C.c_void_p), dgbuf.size)
+        return dgbuf[24000:24040].copy()
+    dg_prev = None
+    ctx.lib.vo_debug_diag.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    NFd = S * F
+
+    def diag_arr(what, f0=0, n=NFd):
+        per = ctx.lib.vo_debug_diag(ctx.h, what, 0, 0, None)
+        out = np.zeros((n, per), np.uint64)
+        assert ctx.lib.vo_debug_diag(ctx.h, what, f0, n, out.ctypes.data_as(C.c_void_p)) == per
+        return out
+    NTX = (W + 56) // 57
+
+    def key_str(k):
+        k = int(k)
+        r = np.array([k >> 32], np.uint32).view(np.float32)[0]
+        return f"(x {k & 0xFFFF}, y {(k >> 16) & 0xFFFF}, R {r:.7g})"
 ring = os.environ.get("DET_RING") == "1"     # compare the extracted ring slots too (vo_debug_ring)
 if ring:
     import ctypes as C
@@ -63,6 +133,9 @@ if ring:
         assert rc == 0, rc
         return nk, kp, pr
 ref = step(0)
+if diag:
+    dref = [diag_arr(w) for w in (0, 1, 2)]
+    kref = diag_arr(3)
 ring_ref = ring_read() if ring else None
 if dbg:
     counters()
@@ -80,6 +153,26 @@ for r in range(reps):
         c_prev = c_now
         msg = (f" mfma keys wrong {dc[0]} of {dc[1]}, stale match_j {dc[2]} of {dc[3]},"
                f" select: hist total != keys {dc[4]}, need > boundary keys {dc[5]} of {dc[6]} frames")
+    if diag:
+        dg = diag_read()
+        if dg_prev is None or not np.array_equal(dg[1:], dg_prev[1:]):
+            msg += (f" diag: tiles {int(dg[0])} checksum mismatches {int(dg[1])} invalid keys {int(dg[2])}"
+                    + (f"; first: frame {int(dg[3]) - 1} tile {int(dg[4])} stencil ck {int(dg[5]):#x} select ck"
+                       f" {int(dg[6]):#x} n {int(dg[7])} bad index {int(dg[8]) - 1} keys"
+                       f" {[hex(int(k)) for k in dg[10:10 + min(int(dg[7]), 24)]]}" if dg[3] else ""))
+        dg_prev = dg
+        dnow = [diag_arr(w) for w in (0, 1, 2)]
+        names = ("select key ck", "stencil source ck", "stencil response ck")
+        fr_d = sorted(set(int(f) for w in range(3) for f in np.nonzero((dnow[w] != dref[w]).any(1))[0]))
+        for f in fr_d[:3]:
+            msg += f"\n    diag frame {f}:"
+            for w in range(3):
+                t = np.nonzero(dnow[w][f] != dref[w][f])[0]
+                msg += f" {names[w]} tiles {[(int(x), divmod(int(x), NTX)) for x in t[:4]]}"
+            kn = diag_arr(3, f, 1)[0]
+            a, b = set(kref[f][kref[f] != 0].tolist()), set(kn[kn != 0].tolist())
+            msg += (f"\n      keys only in ref: {[key_str(k) for k in sorted(a - b)[:6]]}"
+                    f"\n      keys only now:   {[key_str(k) for k in sorted(b - a)[:6]]}")
     if ring:
         nk, kp, pr = ring_read()
         fd = [f for f in range(NF) if nk[f] != ring_ref[0][f] or not np.array_equal(kp[f, :nk[f]], ring_ref[1][f, :nk[f]])
@@ -119,6 +212,7 @@ print(f"full path: {bad} of {reps} repeats differ", flush=True)
 nk0, k0, d0 = ctx.extract_frames_device(dall, outputs=True)
 xbad = 0
 for r in range(xreps):
+    background()
     nk, k, d = ctx.extract_frames_device(dall, timing=(0, 1, 100)[r % 3], outputs=True)
     diff = [f for f in range(len(nk)) if nk[f] != nk0[f] or not np.array_equal(k[f], k0[f])
             or not np.array_equal(d[f], d0[f])]

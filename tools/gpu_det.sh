@@ -1,11 +1,23 @@
-# determinism probe: the bench's row checks under execution knobs
+# Determinism evidence on the GPU box (replaces round 3's one-off gpu_det*/gpu_m*/gpu_trace* scripts).
+#   tools/gpu_det.sh <tag> <repeats> "<lib>[:ENV=V,...] ..."
+# For each library (acs_visual_odometry_amd/<lib>) and environment: tools/det_stress.py <repeats>
+# (the bench's 8 x 200-frame stream repeated under changing kernel-timing modes, ring slots
+# compared), with the device buffer layout printed first.  Logs: gpurun_out/<tag>/det_<n>.txt
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/${1:-det}; mkdir -p $O
-shift
-for e in "$@"; do
-  env $e timeout -k 10 200 python -u bench.py --no-cpu --no-variants --steps 10 > $O/b.json 2> $O/b.err || { echo FAIL "$e"; tail -5 $O/b.err; exit 1; }
-  python3 -c "import json;d=json.load(open('$O/b.json'));print('$e', round(d['value']), d['determinism']['timed_rows_equal_warmup_rows'], d['determinism']['gathered_rows_equal_separate_runs'], d['config']['fitted_fraction'])"
+TAG=${1:-det}; REPS=${2:-100}; RUNS=${3:-"libvo_mi355x.so:VO_MATCH_MFMA=1"}; XREPS=${4:-0}
+O=gpurun_out/$TAG; mkdir -p $O
+if [ -x acs_visual_odometry_amd/bin/buffer_range_probe ]; then
+  timeout -k 10 60 acs_visual_odometry_amd/bin/buffer_range_probe > $O/buffer_range_probe.txt || { echo PROBE_FAIL; exit 1; }
+  cat $O/buffer_range_probe.txt
+fi
+n=0
+for run in $RUNS; do
+  lib=${run%%:*}; envs=""; [ "$run" != "$lib" ] && envs=$(echo ${run#*:} | tr ',' ' ')
+  n=$((n + 1))
+  echo "== $lib $envs ($REPS repeats)"
+  env $envs VO_LIB_PATH=$PWD/acs_visual_odometry_amd/$lib DET_RING=1 timeout -k 10 600 python -u tools/det_stress.py $REPS $XREPS > $O/det_$n.txt 2>&1 || { echo DET_FAIL; tail -20 $O/det_$n.txt; exit 1; }
+  grep -E "full path|extract:" $O/det_$n.txt
 done
 echo DONE
