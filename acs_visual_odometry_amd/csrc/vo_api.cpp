@@ -16,12 +16,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
 #include <climits>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <utility>
@@ -74,13 +76,18 @@ struct vo_ctx {
     uint8_t* stage_host = nullptr;    // pinned frame staging
     uint16_t* tab_dev = nullptr;
     double stage_F[9] = {0};          // vo_ransac_F's FundamentalMatrix (persists across calls)
-    std::map<double, uint16_t*> tab_by_p;   // vo_ransac_run: maxIterations tables of other probabilities
+    std::map<double, uint16_t*> tab_by_p;   // vo_ransac_run: the maxIterations table of the last other probability
     int timing = 0;                   // 0 off, 1 all kernels, 100+k only kernel k
     std::vector<hipEvent_t> ev_pool;
     std::vector<float> ktime_ms;
     std::vector<int> kcount;          // timed launches per kernel
     std::vector<int> klaunch;         // launches per kernel in the last call
     int last_frames = 0;
+    // VO_PF_PROFILE=1: host-side phases of vo_process_frame (us, summed; printed by vo_destroy)
+    bool pf_profile = false;
+    double pf_t[5] = {0, 0, 0, 0, 0};     // sync, copy, enqueue, wait, total
+    long pf_n = 0;
+    double pf_enq_end = 0, pf_wait_end = 0;
     struct Buf { const char* name; uint64_t ptr, bytes; };
     std::vector<Buf> layout;          // device buffers allocated by vo_create (vo_debug_layout)
 };
@@ -111,19 +118,24 @@ int to_int_x86(double q)
 // maxIterations after a strictly better count (ransac.cpp:179-190), evaluated with the
 // host libm exactly as the reference evaluates it; 0xFFFF = "denom == 0: no update".
 // Table row M holds entries best = 0..M at offset M(M+1)/2.
+// Bounded: at most VO_TAB_CACHE tables (a caller cycling through probabilities would otherwise grow
+// host memory without bound, ~17 MB per table at N = 4096); callers hold a shared_ptr while they use one.
+#define VO_TAB_CACHE 4
 std::mutex g_tab_mu;
-std::map<std::pair<int, double>, std::vector<uint16_t>> g_tab_cache;
+std::vector<std::pair<std::pair<int, double>, std::shared_ptr<const std::vector<uint16_t>>>> g_tab_cache;
 
-const std::vector<uint16_t>& maxit_table(int N, double prob)
+std::shared_ptr<const std::vector<uint16_t>> maxit_table(int N, double prob)
 {
-    std::lock_guard<std::mutex> lk(g_tab_mu);
-    auto key = std::make_pair(N, prob);
-    auto it = g_tab_cache.find(key);
-    if (it != g_tab_cache.end()) return it->second;
-    std::vector<uint16_t> tab((size_t)(N + 1) * (N + 2) / 2, 0xFFFFu);
+    const auto key = std::make_pair(N, prob);
+    {
+        std::lock_guard<std::mutex> lk(g_tab_mu);
+        for (const auto& e : g_tab_cache)
+            if (e.first == key) return e.second;
+    }
+    auto tab = std::make_shared<std::vector<uint16_t>>((size_t)(N + 1) * (N + 2) / 2, 0xFFFFu);
     const double lp = std::log(1.0 - prob);
     for (int M = 8; M <= N; ++M) {
-        uint16_t* row = tab.data() + (size_t)M * (M + 1) / 2;
+        uint16_t* row = tab->data() + (size_t)M * (M + 1) / 2;
         for (int best = 1; best <= M; ++best) {
             double outlierRatio = 1.0 - (double)best / (double)M;
             double denom = std::log(1.0 - std::pow(1.0 - outlierRatio, 8.0));
@@ -133,7 +145,10 @@ const std::vector<uint16_t>& maxit_table(int N, double prob)
             row[best] = (uint16_t)v;
         }
     }
-    return g_tab_cache.emplace(key, std::move(tab)).first->second;
+    std::lock_guard<std::mutex> lk(g_tab_mu);
+    if (g_tab_cache.size() >= VO_TAB_CACHE) g_tab_cache.erase(g_tab_cache.begin());   // the oldest
+    g_tab_cache.emplace_back(key, tab);
+    return tab;
 }
 
 template <typename T>
@@ -198,11 +213,18 @@ void stage_work(VoWork* w, int ring)
 }
 
 // host frame (any stride) -> frame_in on stream `st`, via the pinned staging buffer
+double now_us()
+{
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride, hipStream_t st)
 {
     const int W = c->cfg.width, H = c->cfg.height;
     if (stride == 0) stride = (size_t)W;
+    const double t0 = c->pf_profile ? now_us() : 0.0;
     SYNC_ALL(c);                          // staging buffer / frame_in may still be in use
+    const double t1 = c->pf_profile ? now_us() : 0.0;
     if (stride == (size_t)W) {
         std::memcpy(c->stage_host, gray, (size_t)W * H);
     } else {
@@ -210,6 +232,11 @@ int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride, hipStream_t st)
     }
     // a copy kernel on the frame's own queue reads the pinned staging buffer (a copy-engine transfer
     // measured 15 us plus a ~14 us engine -> compute-queue hand-off before the next kernel)
+    if (c->pf_profile) {
+        const double t2 = now_us();
+        c->pf_t[0] += t1 - t0;
+        c->pf_t[1] += t2 - t1;
+    }
     vo::launch_h2d(c->d.frame_in, c->stage_host, (size_t)W * H, st);
     HIPCHK(hipGetLastError());
     return VO_OK;
@@ -573,7 +600,9 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         // alone and checked to be that frame's
         if (!host_frame)
             HIPCHK(hipMemcpyAsync(c->lo_host, &c->d.st->lo, sizeof(int32_t), hipMemcpyDeviceToHost, tq));
+        if (c->pf_profile && host_frame) c->pf_enq_end = now_us();
         HIPCHK(hipStreamSynchronize(s));
+        if (c->pf_profile && host_frame) c->pf_wait_end = now_us();
         if (c->sf && !host_frame) HIPCHK(hipStreamSynchronize(c->sf));
         if (tq != s) HIPCHK(hipStreamSynchronize(tq));
         if (host_frame && nf == 1 && c->out_host[base - out_base].frame != base) {
@@ -724,6 +753,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     c->event_wait = !(getenv("VO_EVENT_WAIT") && atoi(getenv("VO_EVENT_WAIT")) == 0);
     d.xcd_map = getenv("VO_XCD") ? atoi(getenv("VO_XCD")) : 1;
     c->fuse_fin = getenv("VO_FUSE_FIN") && atoi(getenv("VO_FUSE_FIN")) != 0;
+    c->pf_profile = getenv("VO_PF_PROFILE") && atoi(getenv("VO_PF_PROFILE")) != 0;
     c->pipeline = !c->serial && !(getenv("VO_PIPELINE") && atoi(getenv("VO_PIPELINE")) == 0);
     c->force_wait_refusal = getenv("VO_FORCE_WAIT_REFUSAL") && atoi(getenv("VO_FORCE_WAIT_REFUSAL")) != 0;
     c->split = VO_EXT_QUEUES >= 2 && (getenv("VO_SPLIT") ? atoi(getenv("VO_SPLIT")) != 0 : VO_SPLIT_DEFAULT != 0);
@@ -736,17 +766,30 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     int p_lo = 0, p_hi = 0;
     if (prio) (void)hipDeviceGetStreamPriorityRange(&p_lo, &p_hi);
     const int p_pose = prio > 0 ? p_hi : p_lo, p_ext = prio < 0 ? p_hi : p_lo;
-    if (hip_ok(hipStreamCreateWithPriority(&c->s, hipStreamNonBlocking, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
-    if (hip_ok(hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
+    // VO_CU_SPLIT=q (1..3, experiment): the extract queues on CUs i with i % 4 < q, the pose, fit and
+    // trajectory queues on the others (hipExtStreamCreateWithCUMask), so no extract kernel shares a
+    // CU with a pose-pass kernel
+    const int cu_split = getenv("VO_CU_SPLIT") ? std::max(0, std::min(3, atoi(getenv("VO_CU_SPLIT")))) : 0;
+    int ncu = 0;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->cfg.device);
+    auto make_stream = [&](hipStream_t* q, bool ext, int prio_) -> hipError_t {
+        if (!cu_split || ncu <= 0) return hipStreamCreateWithPriority(q, hipStreamNonBlocking, prio_);
+        std::vector<uint32_t> m((size_t)(ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; ++i)
+            if (((i % 4) < cu_split) == ext) m[(size_t)i / 32] |= 1u << (i % 32);
+        return hipExtStreamCreateWithCUMask(q, (uint32_t)m.size(), m.data());
+    };
+    if (hip_ok(make_stream(&c->s, false, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(make_stream(&c->st, false, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK)
         return bail(VO_ERR_HIP);
-    if (hip_ok(hipStreamCreateWithPriority(&c->sf, hipStreamNonBlocking, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(make_stream(&c->sf, false, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
     for (int i = 0; i < vo_ctx::kPassEv; ++i)
         if (hip_ok(hipEventCreateWithFlags(&c->ev_rs[i], hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK ||
             hip_ok(hipEventCreateWithFlags(&c->ev_fn[i], hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK)
             return bail(VO_ERR_HIP);
     for (hipStream_t& q : c->se)
-        if (hip_ok(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, p_ext)) != VO_OK) return bail(VO_ERR_HIP);
+        if (hip_ok(make_stream(&q, true, p_ext)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming)) != VO_OK) return bail(VO_ERR_HIP);
     d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
     if (d.sel_lds < 0) return bail(VO_ERR_HIP);
@@ -807,7 +850,8 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc_rec(c, "diag_keys", &d.diag_keys, (size_t)VO_DIAG_KEYS * VO_DIAG_FRAMES);
 #endif
     if (rc != VO_OK) return bail(VO_ERR_HIP);
-    const std::vector<uint16_t>& tab = maxit_table(N, k.ransac_p);
+    const auto tabp = maxit_table(N, k.ransac_p);
+    const std::vector<uint16_t>& tab = *tabp;
     if (dalloc(&c->tab_dev, tab.size()) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipMemcpy(c->tab_dev, tab.data(), tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice)) != VO_OK)
         return bail(VO_ERR_HIP);
@@ -833,6 +877,10 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
 
 void vo_destroy(vo_ctx* c)
 {
+    if (c && c->pf_profile && c->pf_n)
+        fprintf(stderr, "[vo_mi355x] vo_process_frame host phases over %ld calls (us/call): sync %.1f copy %.1f "
+                        "enqueue %.1f wait %.1f total %.1f\n", c->pf_n, c->pf_t[0] / c->pf_n, c->pf_t[1] / c->pf_n,
+                c->pf_t[2] / c->pf_n, c->pf_t[3] / c->pf_n, c->pf_t[4] / c->pf_n);
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
     for (hipStream_t q : c->se)
@@ -1078,18 +1126,21 @@ int vo_ransac_run(vo_ctx* c, const double* pts, int m, double probability, doubl
     if (d.maxit_initial > d.max_hyp) return VO_ERR_CAPACITY;
     d.sampson_thr = sampson_thr;
     d.T = num_threads;
+    SYNC_ALL(c);
     if (probability != c->cfg.ransac_p) {
+        // one device table besides cfg.ransac_p's: the last other probability's (the device is idle here)
         auto it = c->tab_by_p.find(probability);
         if (it == c->tab_by_p.end()) {
-            const std::vector<uint16_t>& tab = maxit_table(c->cfg.max_kpts, probability);
+            for (auto& kv : c->tab_by_p) (void)hipFree(kv.second);
+            c->tab_by_p.clear();
+            const auto tab = maxit_table(c->cfg.max_kpts, probability);
             uint16_t* t = nullptr;
-            HIPCHK(hipMalloc((void**)&t, tab.size() * sizeof(uint16_t)));
-            HIPCHK(hipMemcpy(t, tab.data(), tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+            HIPCHK(hipMalloc((void**)&t, tab->size() * sizeof(uint16_t)));
+            HIPCHK(hipMemcpy(t, tab->data(), tab->size() * sizeof(uint16_t), hipMemcpyHostToDevice));
             it = c->tab_by_p.emplace(probability, t).first;
         }
         d.maxit_tab = it->second;
     }
-    SYNC_ALL(c);
     HIPCHK(hipMemcpy(d.pts, pts, sizeof(double) * 4 * (size_t)m, hipMemcpyHostToDevice));
     VoWork w;
     stage_work(&w, d.ring);
@@ -1182,15 +1233,23 @@ int vo_pose(vo_ctx* c, const double F[9], const float* p1, const float* p2, int 
 int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_out[12], int* status, int32_t* info)
 {
     if (!c) return VO_ERR_ARG;
+    const double t0 = c->pf_profile ? now_us() : 0.0;
     HIPCHK(hipSetDevice(c->cfg.device));
     if (gray) {
         int rc = upload_frame(c, gray, stride, c->s);
         if (rc) return rc;
     }
+    const double t1 = c->pf_profile ? now_us() : 0.0;
     const int f = c->fidx;
     // one frame: extract on the pose queue, a window of one (no speculation)
     int rc = run_chunk(c, gray ? c->d.frame_in : nullptr, 0, 1, c->out_dev, f, nullptr, true);
     if (rc) return rc;
+    if (c->pf_profile) {
+        c->pf_t[2] += c->pf_enq_end - t1;
+        c->pf_t[3] += c->pf_wait_end - c->pf_enq_end;
+        c->pf_t[4] += now_us() - t0;
+        c->pf_n += 1;
+    }
     const VoFrameOut& o = c->out_host[0];
     if (pose_out) std::memcpy(pose_out, o.pose, sizeof(o.pose));
     if (status) *status = o.status;

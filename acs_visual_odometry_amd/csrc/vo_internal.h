@@ -43,7 +43,8 @@
 
 #define VO_HIST_BINS 4096
 #ifndef ST_DIAG
-#define ST_DIAG 0          // diagnostic build: per-tile key checksums stencil -> select (d.tile_ck, d.dbg 24000..)
+#define ST_DIAG 0          // diagnostic build: 1 select archives each frame's key list and per-tile checksums;
+                           // 2 + the stencil's own per-tile key / source / response checksums (d.tile_ck, d.dbg 24000..)
 #endif
 #define VO_DIAG_FRAMES 4096
 #define VO_DIAG_KEYS 8192

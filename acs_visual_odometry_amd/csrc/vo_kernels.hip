@@ -425,8 +425,20 @@ __device__ __forceinline__ int refl101(int i, int n)
 #ifndef ST_DPP_NOP
 #define ST_DPP_NOP 0                   // diagnostic: wait states before every wave shift
 #endif
+#ifndef ST_SHIFT_BPERM
+#define ST_SHIFT_BPERM 0               // diagnostic: wave shifts through ds_bpermute instead of DPP
+#endif
+__device__ __forceinline__ int shift_bperm(int v, int d)
+{
+    const int l = (int)(threadIdx.x & 63), src = l + d;
+    const int r = __builtin_amdgcn_ds_bpermute(src << 2, v);
+    return (src < 0 || src > 63) ? 0 : r;
+}
 __device__ __forceinline__ int from_left(int v)
 {
+#if ST_SHIFT_BPERM
+    return shift_bperm(v, -1);
+#endif
 #if ST_DPP_NOP
     asm volatile("s_nop %c1" : "+v"(v) : "i"(ST_DPP_NOP - 1));
 #endif
@@ -438,6 +450,9 @@ __device__ __forceinline__ int from_left(int v)
 }
 __device__ __forceinline__ int from_right(int v)
 {
+#if ST_SHIFT_BPERM
+    return shift_bperm(v, 1);
+#endif
 #if ST_DPP_NOP
     asm volatile("s_nop %c1" : "+v"(v) : "i"(ST_DPP_NOP - 1));
 #endif
@@ -495,11 +510,18 @@ typedef unsigned short st_w2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float from_leftf(float v) { return __int_as_float(from_left(__float_as_int(v))); }
 __device__ __forceinline__ float from_rightf(float v) { return __int_as_float(from_right(__float_as_int(v))); }
 // (a.x - b.y, b.x - a.y) in one v_pk_add_f32: cross halves through op_sel, signs through neg
+#ifndef ST_XSUB_ASM
+#define ST_XSUB_ASM 1
+#endif
 __device__ __forceinline__ st_f2 st_xsub(st_f2 a, st_f2 b)
 {
+#if ST_XSUB_ASM
     st_f2 r;
     asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
     return r;
+#else
+    return st_f2{a.x - b.y, b.x - a.y};
+#endif
 }
 __device__ __forceinline__ st_f2 st_fma(st_f2 a, st_f2 b, st_f2 c) { return __builtin_elementwise_fma(a, b, c); }
 // the pair's response, kernel .c:108-114 (f32, in the reference's order): det = (jx2 jy2) -
@@ -526,7 +548,7 @@ __device__ __forceinline__ st_f2 st_response2(st_f2 jx2, st_f2 jy2, st_f2 sxy)
     {
         unsigned long long ma, mb, mc, md;
         float tx, ty;
-        asm volatile(
+        asm(
             "v_cmp_ge_f32_e64 %[mc], 0, %[rmx]\n\t"
             "v_cmp_ge_f32_e64 %[md], 0, %[rmy]\n\t"
             "v_cmp_lt_f32_e64 %[ma], 0, %[rpx]\n\t"
@@ -553,6 +575,9 @@ __device__ __forceinline__ void st_for(F&& f, std::integer_sequence<int, I...>)
     (f(std::integral_constant<int, I>{}), ...);
 }
 #define ST_BUF_DW3 0x00020000
+#ifndef ST_FLAT_DEFAULT
+#define ST_FLAT_DEFAULT 1     // launch_stencil: the branch-free FLAT form where the margins allow it
+#endif
 #ifndef LDS_POISON
 #define LDS_POISON 0      // diagnostic build: k_select / k_describe poison their LDS first
 #endif
@@ -564,7 +589,14 @@ __device__ __forceinline__ void st_for(F&& f, std::integer_sequence<int, I...>)
 #ifndef ST_WAVES_PER_EU
 #define ST_WAVES_PER_EU 4
 #endif
-template <int SEGT, bool DBG>
+// FLAT (launch_stencil: NMS margins of 5+ rows and columns, no response map): the image's border
+// rows and columns cannot reach a maximum inside the margins (a response at row y needs gradient
+// rows y - 2 .. y + 2, an NMS centre at row >= 5 has neighbours at rows >= 4: gradient rows >= 2,
+// and likewise at the bottom and the sides), so their gradient masks are dropped; the candidate
+// keys and histogram counts are stored through buffer descriptors whose out-of-range offset drops
+// the lanes that hold no maximum (tests/test_buffer_range.py).  A 16-row group is then one basic
+// block with no branch, and the scheduler overlaps consecutive rows' dependency chains.
+template <int SEGT, bool DBG, bool FLAT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAVES_PER_EU))) k_stencil(VoDev d, const uint8_t* __restrict__ img0, size_t frame_bytes,
                                                   int write_response, int nb)
 {
@@ -589,7 +621,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
     uint64_t* __restrict__ cand = d.cand + (size_t)z * d.cand_cap;
     uint8_t* __restrict__ tilerows = d.tilerows + (size_t)z * d.ntiles * ST_TH;
     uint32_t* __restrict__ hist = d.hist + (size_t)z * VO_HIST_BINS;
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t rcand =
+        __builtin_amdgcn_make_buffer_rsrc((void*)cand, 0, (int)(d.cand_cap * 8u), ST_BUF_DW3);
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t rhist =
+        __builtin_amdgcn_make_buffer_rsrc((void*)hist, 0, VO_HIST_BINS * 4, ST_BUF_DW3);
     const int Wb = d.bstride;
+    // wave shifts: pinned against sinking into a masked arm, except in the FLAT form (no masked arm)
+    auto shl = [](int v) { if constexpr (FLAT && !ST_SHIFT_BPERM) return __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true); else return from_right(v); };
+    auto shr = [](int v) { if constexpr (FLAT && !ST_SHIFT_BPERM) return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true); else return from_left(v); };
+    auto shrf = [&](float v) { return __int_as_float(shr(__float_as_int(v))); };
+    auto shlf = [&](float v) { return __int_as_float(shl(__float_as_int(v))); };
 
     const int xs = sxi * ST_SW, ys = seg * SEG;
     const int c0 = xs - VO_STRIP_XL + 2 * lane;                // this lane's columns: c0, c0 + 1
@@ -631,10 +672,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
     int ru0 = 0, rm0 = 0, rd0 = 0, ru1 = 0, rm1 = 0, rd1 = 0;               // response rows (f32 bits)
     int toffA = 0, toffB = 0;                                                // candidates so far per tile
     int trows = 0;                                                           // lane r (16 + r): tile A (B) row r count
-#if ST_DIAG
+#if ST_DIAG & 2
     unsigned long long dck = 0ull;                                           // checksum of the keys this lane stored
     unsigned long long sck = 0ull, rck = 0ull;                               // source rows consumed, responses computed
     const int dfr = d.diag_f0 + z;                                           // frame index (diagnostic arrays)
+#elif ST_DIAG & 4
+    uint32_t lsck = 0u;                                                      // light: source rows consumed (one mad a row)
+    const int dfr = d.diag_f0 + z;
 #endif
 
     // lane u of the result: byte offset of source row ys - 7 + k0 + u (u < 16)
@@ -654,8 +698,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         constexpr int P = decltype(PH)::value;
         constexpr int r = decltype(R)::value;
         s0 = s1; s1 = s2; s2 = s3; s3 = s4; s4 = s5; s5 = s6; s6 = src;
-#if ST_DIAG
+#if ST_DIAG & 2
         sck += mix64((uint64_t)src ^ ((uint64_t)(uint32_t)k << 32));
+#elif ST_DIAG & 4
+        lsck = lsck * 0x01000193u + src;
 #endif
         if constexpr (P >= 1) {
             // 1. 7x7 blur (cv::GaussianBlur 8U fixed point, A.1): vertical taps on both columns
@@ -667,8 +713,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                                (as_u16x2(s1) + as_u16x2(s5)) * (unsigned short)28 +
                                (as_u16x2(s2) + as_u16x2(s4)) * (unsigned short)56 + as_u16x2(s3) * (unsigned short)72;
             const uint32_t V = as_u32(v);
-            const uint32_t VL = (uint32_t)from_left((int)V), VR = (uint32_t)from_right((int)V);
-            const uint32_t VL2 = (uint32_t)from_left((int)VL), VR2 = (uint32_t)from_right((int)VR);
+            const uint32_t VL = (uint32_t)shr((int)V), VR = (uint32_t)shl((int)V);
+            const uint32_t VL2 = (uint32_t)shr((int)VL), VR2 = (uint32_t)shl((int)VR);
 #if ST_NODOT
             auto dot = [](uint32_t a, st_w2 w, uint32_t c) { return (a & 0xFFFFu) * (uint32_t)w.x + (a >> 16) * (uint32_t)w.y + c; };
 #else
@@ -709,21 +755,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             //    the reference's f32 values are these integers (all below 2^11)
             const int yg = ys - 11 + k;
             const st_f2 DV = BA - BE, SV = st_fma(BM, st_f2{2.0f, 2.0f}, BA + BE);
-            const st_f2 Y = {from_leftf(DV.y), from_rightf(DV.x)};   // dv of columns c0 - 1, c0 + 2
-            const st_f2 Z = {from_leftf(SV.y), from_rightf(SV.x)};
+            const st_f2 Y = {shrf(DV.y), shlf(DV.x)};                 // dv of columns c0 - 1, c0 + 2
+            const st_f2 Z = {shrf(SV.y), shlf(SV.x)};
             st_f2 JX = st_fma(DV, st_f2{2.0f, 2.0f}, Y + DV.yx);      // (dL + 2 dv0 + dv1, dv0 + 2 dv1 + dR)
             st_f2 JY = st_xsub(Z, SV);                                // (sL - sv1, sv0 - sR)
             st_f2 JXY = st_xsub(Y, DV);                               // (dL - dv1, dv0 - dR)
             // both conditions are wave-uniform and rare (the image's outer columns and rows): the
             // empty volatile asm keeps them branches (if-converted, they cost 12 selects a row)
-            if (colfix) {
-                asm volatile("");
-                if (!g0) JX.x = JY.x = JXY.x = 0.0f;
-                if (!g1) JX.y = JY.y = JXY.y = 0.0f;
-            }
-            if ((unsigned)(yg - 1) > (unsigned)(H - 3)) {
-                asm volatile("");
-                JX = JY = JXY = z2;
+            if constexpr (!FLAT) {
+                if (colfix) {
+                    asm volatile("");
+                    if (!g0) JX.x = JY.x = JXY.x = 0.0f;
+                    if (!g1) JX.y = JY.y = JXY.y = 0.0f;
+                }
+                if ((unsigned)(yg - 1) > (unsigned)(H - 3)) {
+                    asm volatile("");
+                    JX = JY = JXY = z2;
+                }
             }
             // 3. 5x5 window sums (kernel .c:97-107): vertical running sums, then horizontal
             const st_f2 X2 = JX * JX, Y2 = JY * JY;
@@ -743,7 +791,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             float sx0, sx1, sy0, sy1, ss0, ss1;
             {
                 float pX, pY, pS, xX, yX, xY, yY, xS, yS;
-                asm volatile(
+                asm(
 #if ST_DPP_NOP
                     "s_nop 7\n\t"
 #endif
@@ -797,7 +845,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             }
             ru0 = rm0; rm0 = rd0; rd0 = o0;
             ru1 = rm1; rm1 = rd1; rd1 = o1;
-#if ST_DIAG
+#if ST_DIAG & 2
             rck += mix64((((uint64_t)(uint32_t)o0 << 32) | (uint32_t)o1) ^ ((uint64_t)(uint32_t)k << 48));
 #endif
         }
@@ -808,7 +856,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             //    order as the values do and the window maximum is an integer max3
             const int yn = ys - 14 + k;
             const int cm0 = max(max(ru0, rm0), rd0), cm1 = max(max(ru1, rm1), rd1);
-            const int cL = from_left(cm1), cR = from_right(cm0);
+            const int cL = shr(cm1), cR = shl(cm0);
             const int nb0 = max(max(cL, cm1), max(max(ru0, rd0), nmsk0));
             const int nb1 = max(max(cm0, cR), max(max(ru1, rd1), nmsk1));
             const bool rok = (unsigned)(yn - nlo) < (unsigned)(nhi - nlo);
@@ -824,13 +872,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                 return (unsigned long long)__builtin_amdgcn_ballot_w64(a < b);
 #endif
             };
-            const unsigned long long b0 = rok ? lt_mask(nb0, rm0) : 0ull, b1 = rok ? lt_mask(nb1, rm1) : 0ull;
-            const bool mx0 = nb0 < rm0, mx1 = nb1 < rm1;
+            const unsigned long long rokm = rok ? ~0ull : 0ull;      // (a select, not a branch around the compare)
+            const unsigned long long b0 = lt_mask(nb0, rm0) & rokm, b1 = lt_mask(nb1, rm1) & rokm;
+            // (rok: the NMS rows; the general form reaches the stores only through b0 | b1, which rok masks)
+            const bool mx0 = rok && nb0 < rm0, mx1 = rok && nb1 < rm1;
             const int cA = __popcll(b0 & mA) + __popcll(b1 & mA);
             const int cB = __popcll(b0 & mB) + __popcll(b1 & mB);
             asm("v_writelane_b32 %0, %1, %2" : "+v"(trows) : "s"(cA), "n"(r));
             asm("v_writelane_b32 %0, %1, %2" : "+v"(trows) : "s"(cB), "n"(16 + r));
-            if (b0 | b1) {
+            if constexpr (FLAT) {
+                // every lane stores; a lane without a maximum gets an out-of-range offset (dropped)
+                const uint32_t pos0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32),
+                                      __builtin_amdgcn_mbcnt_lo((uint32_t)b1,
+                                      __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32),
+                                      __builtin_amdgcn_mbcnt_lo((uint32_t)b0, 0u))));
+                const uint32_t base = (uint32_t)(isB ? ST_TCAP + toffB - cA : toffA) + pos0;
+                const uint32_t slot0 = (uint32_t)((yn / ST_TH) * ntx + 2 * sxi) * ST_TCAP + base;
+                const uint32_t key_lo = ((uint32_t)yn << 16) | (uint32_t)c0;
+                const int o0 = mx0 ? (int)(slot0 * 8u) : 0x7FFFFFF0;
+                const int o1 = mx1 ? (int)((slot0 + (mx0 ? 1u : 0u)) * 8u) : 0x7FFFFFF0;
+                typedef unsigned int st_u2 __attribute__((ext_vector_type(2)));
+                __builtin_amdgcn_raw_buffer_store_b64(st_u2{key_lo, (uint32_t)rm0}, rcand, o0, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(st_u2{key_lo + 1u, (uint32_t)rm1}, rcand, o1, 0, 0);
+                const int h0 = mx0 ? (int)(min(((uint32_t)rm0 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1)) * 4u) : 0x7FFFFFF0;
+                const int h1 = mx1 ? (int)(min(((uint32_t)rm1 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1)) * 4u) : 0x7FFFFFF0;
+                (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rhist, h0, 0, 0);
+                (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rhist, h1, 0, 0);
+            } else if (b0 | b1) {
                 // tile-local raster order: rows before this one, then columns before: the lower
                 // lanes' pairs, and c0 before c0 + 1
                 const uint32_t pos0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32),
@@ -845,7 +913,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                     *(uint64_t*)(tc + base * 8u) = ((uint64_t)(uint32_t)rm0 << 32) | key_lo;
                     const uint32_t bin = min(((uint32_t)rm0 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1));
                     atomicAdd(&hist[bin], 1u);
-#if ST_DIAG
+#if ST_DIAG & 2
                     dck += mix64((((uint64_t)(uint32_t)rm0 << 32) | key_lo) ^ ((uint64_t)base << 48));
 #endif
                 }
@@ -853,7 +921,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                     *(uint64_t*)(tc + (base + (mx0 ? 1u : 0u)) * 8u) = ((uint64_t)(uint32_t)rm1 << 32) | (key_lo + 1u);
                     const uint32_t bin = min(((uint32_t)rm1 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1));
                     atomicAdd(&hist[bin], 1u);
-#if ST_DIAG
+#if ST_DIAG & 2
                     dck += mix64((((uint64_t)(uint32_t)rm1 << 32) | (key_lo + 1u)) ^ ((uint64_t)(base + (mx0 ? 1u : 0u)) << 48));
 #endif
                 }
@@ -920,7 +988,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         // the 16 row counts of tile A (lanes 0..15) and B (16..31) are contiguous
         const int tileA = (ys / ST_TH + i) * ntx + 2 * sxi;
         if (lane < (hasB ? 2 * ST_TH : ST_TH)) tilerows[tileA * ST_TH + lane] = (uint8_t)trows;
-#if ST_DIAG
+#if ST_DIAG & 2
         // per tile: the sum over its keys of mix64(key ^ slot << 48), lanes 0..31 tile A, 32..63 tile B
 #pragma unroll
         for (int off = 1; off < 32; off <<= 1) dck += __shfl_xor(dck, off);
@@ -937,6 +1005,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             d.diag_resp[(size_t)dfr * d.ntiles + tileA] = rck;
         }
         sck = 0ull; rck = 0ull;
+#elif ST_DIAG & 4
+        // per lane group of 16 (lanes 0-15, 16-31: tile A's columns; 32-47, 48-63: tile B's) a word
+        // of the (f, tileA) entry: the checksums of the four quarter-waves
+        {
+            uint32_t q = lsck;
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) q = q * 0x9E3779B1u + (uint32_t)__shfl_xor((int)q, off);
+            const uint32_t q0 = __shfl(q, 0), q1 = __shfl(q, 16), q2 = __shfl(q, 32), q3 = __shfl(q, 48);
+            if (d.diag_src && lane == 0 && dfr < VO_DIAG_FRAMES) {
+                d.diag_src[(size_t)dfr * d.ntiles + tileA] = ((unsigned long long)q1 << 32) | q0;
+                if (hasB) d.diag_src[(size_t)dfr * d.ntiles + tileA + 1] = ((unsigned long long)q3 << 32) | q2;
+            }
+        }
+        lsck = 0u;
 #endif
     }
 }
@@ -1145,7 +1227,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
         }
 #if ST_DIAG
         if (d.diag_tile && f0 + z < VO_DIAG_FRAMES) d.diag_tile[(size_t)(f0 + z) * ntiles + t] = ck;
-        if (d.dbg && d.tile_ck) {
+        if ((ST_DIAG & 2) && d.dbg && d.tile_ck) {
             const unsigned long long want = d.tile_ck[(size_t)z * ntiles + t];
             atomicAdd(&d.dbg[24000], 1ull);
             if (want != ck || bad >= 0) {
@@ -1398,8 +1480,13 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     }
 #endif
     if (tid == 0) {
-        d.ext_n[slot] = ovf ? 0 : (C < N ? C : N);
-        d.ext_st[slot] = ovf ? VO_STATUS_OVERFLOW : VO_STATUS_OK;
+        // the keypoints emitted: min(C, N) by construction; a frame whose count disagrees (inconsistent
+        // stencil output) is marked OVERFLOW, so no later kernel reads a slot entry nobody wrote
+        int sel = 0;
+        for (int w = 0; w < 16; ++w) sel += s_wsum[w];
+        const bool bad = !ovf && sel != (C < N ? C : N);
+        d.ext_n[slot] = ovf || bad ? 0 : (C < N ? C : N);
+        d.ext_st[slot] = ovf || bad ? VO_STATUS_OVERFLOW : VO_STATUS_OK;
     }
 }
 
@@ -1725,8 +1812,11 @@ __global__ void __launch_bounds__(SL_T) k_select_count(VoDev d, int f0, int slot
         ctl->arrive = 0u;                                // for the next launch (the kernel boundary orders it)
         ctl->nbnd = 0u;
         const int slot = ext_slot(d, f0, z, slot_override);
-        d.ext_n[slot] = C < N ? C : N;
-        d.ext_st[slot] = VO_STATUS_OK;
+        // the keypoints the bands will emit (pre) is min(C, N) by construction; an inconsistent
+        // stencil output marks the frame OVERFLOW, so nothing reads a slot entry nobody wrote
+        const bool bad = pre != (C < N ? C : N);
+        d.ext_n[slot] = bad ? 0 : (C < N ? C : N);
+        d.ext_st[slot] = bad ? VO_STATUS_OVERFLOW : VO_STATUS_OK;
     }
     // every band has read the histogram: leave it zeroed for the next frame's stencil
     uint4* hp = reinterpret_cast<uint4*>(hist) + 4 * tid;
@@ -4576,22 +4666,30 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
     // segments' count) each walk 30 source rows instead of 142 -- the latency of the launch
     const int st = write_response ? 4 : nb == 1 && d.single ? 1
                  : segt == 2 || segt == 6 || segt == 8 || segt == 12 ? segt : ST_SEGT_DEFAULT;
-    const int waves = nsx * ((nty + st - 1) / st);                 // one (strip, segment) per wave
+    // the FLAT form for NMS margins of 5+ (the reference's 35 / 37; VO_ST_FLAT=0 turns it off); the
+    // general form keeps the border masks (small margins, the response map)
+    static const int flat_env = getenv("VO_ST_FLAT") ? atoi(getenv("VO_ST_FLAT")) : ST_FLAT_DEFAULT;
+    const bool flat = flat_env && !write_response && d.brow >= 5 && d.bcol >= 5;
+    const int stv = flat ? st : (st == 1 ? 1 : 8);                 // the general form: 8-tile or 1-tile segments
+    const int waves = nsx * ((nty + (write_response ? 4 : stv) - 1) / (write_response ? 4 : stv));   // one (strip, segment) per wave
     dim3 g(xcd_grid((waves + 3) / 4, nb));
     if (write_response)
-        hipLaunchKernelGGL((k_stencil<4, true>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response, nb);
-    else if (st == 12)
-        hipLaunchKernelGGL((k_stencil<12, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
+        hipLaunchKernelGGL((k_stencil<4, true, false>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response, nb);
+    else if (!flat) {
+        if (stv == 1) hipLaunchKernelGGL((k_stencil<1, false, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
+        else hipLaunchKernelGGL((k_stencil<8, false, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
+    } else if (st == 12)
+        hipLaunchKernelGGL((k_stencil<12, false, true>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
     else if (st == 8)
-        hipLaunchKernelGGL((k_stencil<8, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
+        hipLaunchKernelGGL((k_stencil<8, false, true>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
     else if (st == 6)
-        hipLaunchKernelGGL((k_stencil<6, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
+        hipLaunchKernelGGL((k_stencil<6, false, true>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
     else if (st == 2)
-        hipLaunchKernelGGL((k_stencil<2, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
+        hipLaunchKernelGGL((k_stencil<2, false, true>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
     else if (st == 1)
-        hipLaunchKernelGGL((k_stencil<1, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
+        hipLaunchKernelGGL((k_stencil<1, false, true>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
     else
-        hipLaunchKernelGGL((k_stencil<4, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
+        hipLaunchKernelGGL((k_stencil<4, false, true>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
 }
 void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s)
 {

@@ -6,7 +6,9 @@ cv::imread(..., IMREAD_GRAYSCALE) (VisualOdometry.cpp:76).
 from __future__ import annotations
 
 import os
+import math
 import re
+import sys
 from typing import Optional, Sequence
 
 import numpy as np
@@ -66,7 +68,13 @@ def read_gt_line(line: str) -> np.ndarray:
                 T[i] = 0.0
                 break
             end = e.end()
-        T[i] = float(line[pos:end])
+        v = float(line[pos:end])
+        if math.isinf(v):
+            # libstdc++ __convert_to_v (LWG 23): an out-of-range value stores +-DBL_MAX and fails the
+            # stream, so every later entry keeps its identity value
+            T[i] = math.copysign(sys.float_info.max, v)
+            break
+        T[i] = v
         pos = end
     return np.array(T, dtype=np.float64)
 

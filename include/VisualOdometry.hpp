@@ -160,7 +160,9 @@ public:
         std::vector<int32_t> inl(data.size());
         Matrix3d F;
         int fitted = 0, n_inl = 0, n_eval = 0;
-        check(vo_ransac_run(pool.handle(), p.data(), (int)data.size(), probability, sampsonThreshold, numThreads, seed,
+        // an unbound pool falls back to the default context, as FundamentalMatrix::fit and getPose do
+        vo_ctx* ctx = pool.handle() ? pool.handle() : detail::default_ctx();
+        check(vo_ransac_run(ctx, p.data(), (int)data.size(), probability, sampsonThreshold, numThreads, seed,
                             F.a, &fitted, inl.data(), &n_inl, &n_eval),
               "vo_ransac_run");
         last_iterations = n_eval;

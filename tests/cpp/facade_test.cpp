@@ -59,8 +59,21 @@ int main(int argc, char** argv)
                                    Point{(double)kpts2[i2].x, (double)kpts2[i2].y});
     FundamentalMatrix model;
     Ransac ransac;
-    const uint64_t seed = DevicePool::frame_seed(vo.pool().seed, vo.pool().calls);
+    const int64_t calls0 = vo.pool().calls;
+    const uint64_t seed = DevicePool::frame_seed(vo.pool().seed, calls0);
     ransac.run(model, matchedPoints, 0.99, 1.0, T, vo.pool());
+    {
+        // a pool never bound to a context (built the way the reference builds its thread_pool) runs
+        // on the default context: the same draw gives the same model
+        DevicePool unbound(nullptr, vo.pool().seed);
+        unbound.calls = calls0;
+        FundamentalMatrix m2;
+        Ransac r2;
+        r2.run(m2, matchedPoints, 0.99, 1.0, T, unbound);
+        const Matrix3d a = model.getMatrix(), b = m2.getMatrix();
+        std::fprintf(f, "unbound_pool_same %d\n",
+                     (int)(std::equal(a.a, a.a + 9, b.a) && m2.getInliers().size() == model.getInliers().size()));
+    }
     std::fprintf(f, "ransac_seed %llu iterations %d\n", (unsigned long long)seed, ransac.last_iterations);
     const Matrix3d F = model.getMatrix();
     const auto& inliers = model.getInliers();

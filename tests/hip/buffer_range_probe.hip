@@ -14,6 +14,8 @@
 //   case 2: store, voffset = 4000 + 2 lane,       soffset = 0      (straddles num_records)
 //   case 3: store, voffset = 2 lane,              soffset = 4000   (straddles with soffset)
 //   case 4: load,  voffset = 2 lane,              soffset = 0x40000000 (of a 0x5A5A pattern)
+//   case 5: atomic add of 1 (u32), voffset = 0x40000000 + 4 lane (out of range)
+//   case 6: atomic add of 1 (u32), voffset = 4 lane (in range)
 // Output: one JSON object per case on stdout.
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -35,6 +37,8 @@ __global__ void k_probe(uint8_t* base, int mode, uint16_t* loaded)
     case 2: __builtin_amdgcn_raw_buffer_store_b16(v, r, 4000 + 2 * lane, 0, 0); break;
     case 3: __builtin_amdgcn_raw_buffer_store_b16(v, r, 2 * lane, 4000, 0); break;
     case 4: loaded[lane] = __builtin_amdgcn_raw_buffer_load_b16(r, 2 * lane, 0x40000000, 0); break;
+    case 5: (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, r, 0x40000000 + 4 * lane, 0, 0); break;
+    case 6: (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, r, 4 * lane, 0, 0); break;
     }
 }
 
@@ -53,7 +57,7 @@ int main()
     uint16_t* dl = nullptr;
     if (check(hipMalloc(&d, TOTAL), "hipMalloc") || check(hipMalloc(&dl, 128), "hipMalloc")) return 1;
     std::vector<uint16_t> lo(2048), hi(64), ld(64);
-    for (int mode = 0; mode < 5; ++mode) {
+    for (int mode = 0; mode < 7; ++mode) {
         if (check(hipMemset(d, 0xAB, TOTAL), "memset")) return 1;
         if (mode == 4 && check(hipMemset(d + GIB, 0x5A, 128), "memset")) return 1;
         if (check(hipMemset(dl, 0, 128), "memset")) return 1;
@@ -78,9 +82,14 @@ int main()
             loaded_pattern += ld[i] == 0x5A5A;
             loaded_zero += mode == 4 && ld[i] == 0;
         }
-        printf("{\"case\": %d, \"stores_in_range\": %d, \"first_byte\": %d, \"last_byte\": %d, "
+        int atomics_in_range = 0;
+        if (mode >= 5) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(lo.data());
+            for (int i = 0; i < 64; ++i) atomics_in_range += w[i] == 0xABABABABu + 1u;
+        }
+        printf("{\"atomics_in_range\": %d, \"case\": %d, \"stores_in_range\": %d, \"first_byte\": %d, \"last_byte\": %d, "
                "\"stores_at_1gib\": %d, \"loads_of_1gib_pattern\": %d, \"loads_zero\": %d}\n",
-               mode, in_range, first_lo, last_lo, at_gib, loaded_pattern, loaded_zero);
+               atomics_in_range, mode, in_range, first_lo, last_lo, at_gib, loaded_pattern, loaded_zero);
     }
     (void)hipFree(d);
     (void)hipFree(dl);

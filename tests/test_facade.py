@@ -91,6 +91,8 @@ def test_facade_stage_calls_match_oracle(tmp_path, case, T):
     assert np.array_equal(pose[:9], R.reshape(9)) and np.array_equal(pose[9:], t)
     # a Ransac::run on 5 points: the model keeps F and its inliers
     assert got["leak"] == ["1", str(len(inl))]
+    # Ransac::run with a pool bound to no context: the default context, the same model
+    assert got["unbound_pool_same"] == ["1"]
 
 
 def _lines(path):

@@ -199,9 +199,10 @@ def test_gt_reader_and_csv_match_libstdcxx(tmp_path, gt_tool):
 
 def test_gt_token_edge_cases_match_libstdcxx(tmp_path, gt_tool):
     """Tokens libstdc++'s num_get accumulates past a valid prefix ("1e", "1e+", "2E-": 0 and the
-    stream fails), exponents, a lone '\r' inside a line (getline keeps it, >> skips it), CRLF."""
+    stream fails), exponents, overflow ("1e999": +-DBL_MAX and the stream fails, LWG 23) and
+    underflow, a lone '\r' inside a line (getline keeps it, >> skips it), CRLF."""
     lines = ["1e 5 6", "1e+ 7", "3 2E- 8 9", "4 1e5x 6", "5 1.5e3.25 7", "6\r7 8", "9 10\r", ". 1", "+ 2", "-.5e2 .e3",
-             "1E+2 1e-0 1e09 7 8 9 10 11 12 13 14 15"]
+             "1E+2 1e-0 1e09 7 8 9 10 11 12 13 14 15", "1 1e999 3 4", "2 -1e999 5", "1e-999 4 5"]
     gt = tmp_path / "gt.txt"
     gt.write_bytes(("\n".join(lines) + "\r\n" + "42\n").encode())
     rows = read_kitti_poses(str(gt))

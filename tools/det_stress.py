@@ -104,6 +104,7 @@ if diag:
         ctx.lib.vo_debug_stamps(ctx.h, dgbuf.ctypes.data_as(C.c_void_p), dgbuf.size)
         return dgbuf[24000:24040].copy()
     dg_prev = None
+    diag_frames, diag_tiles = 0, []
     ctx.lib.vo_debug_diag.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
     NFd = S * F
 
@@ -164,6 +165,8 @@ for r in range(reps):
         dnow = [diag_arr(w) for w in (0, 1, 2)]
         names = ("select key ck", "stencil source ck", "stencil response ck")
         fr_d = sorted(set(int(f) for w in range(3) for f in np.nonzero((dnow[w] != dref[w]).any(1))[0]))
+        diag_frames += len(fr_d)
+        diag_tiles.extend(int(t) for f in fr_d for t in np.nonzero(dnow[0][f] != dref[0][f])[0])
         for f in fr_d[:3]:
             msg += f"\n    diag frame {f}:"
             for w in range(3):
@@ -171,6 +174,9 @@ for r in range(reps):
                 msg += f" {names[w]} tiles {[(int(x), divmod(int(x), NTX)) for x in t[:4]]}"
             kn = diag_arr(3, f, 1)[0]
             a, b = set(kref[f][kref[f] != 0].tolist()), set(kn[kn != 0].tolist())
+            ts = np.nonzero(dnow[1][f] != dref[1][f])[0]
+            for t in ts[:4]:
+                msg += f"\n      source ck tile {int(t)}: ref {int(dref[1][f][t]):#018x} now {int(dnow[1][f][t]):#018x}"
             msg += (f"\n      keys only in ref: {[key_str(k) for k in sorted(a - b)[:6]]}"
                     f"\n      keys only now:   {[key_str(k) for k in sorted(b - a)[:6]]}")
     if ring:
@@ -208,6 +214,10 @@ for r in range(reps):
                   f" | now st {st[s * F + g]} info {info[s * F + g].tolist()}"
                   f" | pose diff {np.abs(p[s * F + g] - ref[0][s * F + g]).max():.3g}")
 print(f"full path: {bad} of {reps} repeats differ", flush=True)
+if diag:
+    odd = sum(1 for t in diag_tiles if (t % NTX) % 2 == 1)
+    print(f"diag: {diag_frames} frame computations differ over the repeats; tiles {len(diag_tiles)}, "
+          f"of them in odd tile columns (lanes 32-63) {odd}", flush=True)
 
 nk0, k0, d0 = ctx.extract_frames_device(dall, outputs=True)
 xbad = 0

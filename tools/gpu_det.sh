@@ -18,6 +18,6 @@ for run in $RUNS; do
   n=$((n + 1))
   echo "== $lib $envs ($REPS repeats)"
   env $envs VO_LIB_PATH=$PWD/acs_visual_odometry_amd/$lib DET_RING=1 timeout -k 10 600 python -u tools/det_stress.py $REPS $XREPS > $O/det_$n.txt 2>&1 || { echo DET_FAIL; tail -20 $O/det_$n.txt; exit 1; }
-  grep -E "full path|extract:" $O/det_$n.txt
+  grep -E "full path|extract:|^diag:" $O/det_$n.txt
 done
 echo DONE
