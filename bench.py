@@ -58,9 +58,12 @@ ROCPROF_NAME = {"stencil": "k_stencil", "select": "k_select", "describe": "k_des
                 "finalize": "k_finalize", "trajectory": "k_traj"}
 # committed rocprofv3 summaries (tools/profile.sh -> tools/rocprof_summary.py --json): kernel
 # durations, PMC HBM bytes and VALU counters per launch
-# (tools/gpu_r3_prof.sh writes them on the GPU box before the bench runs, from the same build)
-PROFILES = {(1241, 376, 32): "r3_kitti_kernels.json", (1920, 1080, 32): "r3_1080_kernels.json",
-            (1920, 1080, 512): "r3_1080_512_kernels.json", (1241, 376, 32, 0.12): "r3_kitti_012_kernels.json"}
+# (tools/gpu_evidence.sh writes them on the GPU box before the bench runs, from the same build;
+# PROFILE_ROUND names the round whose files are read)
+PROFILE_ROUND = os.environ.get("VO_PROFILE_ROUND", "r4")
+PROFILES = {(1241, 376, 32): f"{PROFILE_ROUND}_kitti_kernels.json", (1920, 1080, 32): f"{PROFILE_ROUND}_1080_kernels.json",
+            (1920, 1080, 512): f"{PROFILE_ROUND}_1080_512_kernels.json",
+            (1241, 376, 32, 0.12): f"{PROFILE_ROUND}_kitti_012_kernels.json"}
 
 
 def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray) -> float:
@@ -79,14 +82,20 @@ def algorithmic_bytes(kernel: str, W: int, H: int, info: np.ndarray) -> float:
 
 
 def load_profile(W: int, H: int, bits: int, motion: float = 1.0):
+    """The committed profile of this workload: PROFILE_ROUND's, else the newest earlier round's
+    (profile_row then refuses its rows if they are of another kernel form than this run's)."""
     name = PROFILES.get((W, H, bits)) if motion == 1.0 else PROFILES.get((W, H, bits, motion))
     if not name:
         return None, None
-    path = os.path.join(ROOT, "profiles", name)
-    try:
-        return json.load(open(path))["kernels"], os.path.relpath(path, ROOT)
-    except (OSError, KeyError, ValueError):
-        return None, None
+    rounds = sorted({f.split("_")[0] for f in os.listdir(os.path.join(ROOT, "profiles")) if f[:1] == "r"},
+                    key=lambda r: int(r[1:]) if r[1:].isdigit() else -1, reverse=True)
+    for r in [PROFILE_ROUND] + [r for r in rounds if r != PROFILE_ROUND]:
+        path = os.path.join(ROOT, "profiles", name.replace(PROFILE_ROUND + "_", r + "_", 1))
+        try:
+            return json.load(open(path))["kernels"], os.path.relpath(path, ROOT)
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
 
 def profile_row(prof, kernel: str, forms: dict):

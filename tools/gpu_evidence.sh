@@ -1,11 +1,12 @@
-# round-3 evidence, profile first and bench second from one build: rocprofv3 duration + PMC
-# passes of the given workloads (tools/profile.sh), summarised into profiles/r3_<tag>_kernels.{md,json}
-# on the box (bench.py reads them) and copied to gpurun_out; then the default bench line.
-# Usage: gpu_r3_prof.sh <out-tag> <workloads: kitti kitti_012 1080 1080_512 ...> [bench]
+# Round evidence, profiles first and the bench second from one build: rocprofv3 duration + PMC
+# passes of the given workloads (tools/profile.sh), summarised into profiles/<round>_<w>_kernels.{md,json}
+# on the box (bench.py reads them: PROFILES) and copied to gpurun_out; then the default bench line.
+# Usage: gpu_evidence.sh <round: r4> <out-tag> <workloads: kitti kitti_012 1080 1080_512 ...> [bench]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/${1:-r3prof}; shift; mkdir -p $O
+R=${1:-r4}; shift
+O=gpurun_out/${1:-${R}prof}; shift; mkdir -p $O
 BUILD=$(tr "\n" " " < BUILD_ID 2>/dev/null || echo unknown)
 for w in "$@"; do
   case $w in
@@ -17,10 +18,10 @@ for w in "$@"; do
     *) echo "unknown workload $w"; exit 1;;
   esac
   bash tools/profile.sh $O/prof_$w $A > $O/prof_$w.log 2>&1 || { echo PROF_FAIL $w; tail -20 $O/prof_$w.log; exit 1; }
-  python3 tools/rocprof_summary.py $O/prof_$w "r3 (build $BUILD) $T" --fetch-x2 --json profiles/r3_${w}_kernels.json > profiles/r3_${w}_kernels.md || { echo SUM_FAIL $w; exit 1; }
-  cp $O/prof_$w/stats_kernel_stats.csv profiles/r3_${w}_kernel_stats.csv
-  cp profiles/r3_${w}_kernels.* profiles/r3_${w}_kernel_stats.csv $O/
-  head -16 profiles/r3_${w}_kernels.md | tail -12
+  python3 tools/rocprof_summary.py $O/prof_$w "$R (build $BUILD) $T" --fetch-x2 --json profiles/${R}_${w}_kernels.json > profiles/${R}_${w}_kernels.md || { echo SUM_FAIL $w; exit 1; }
+  cp $O/prof_$w/stats_kernel_stats.csv profiles/${R}_${w}_kernel_stats.csv
+  cp profiles/${R}_${w}_kernels.* profiles/${R}_${w}_kernel_stats.csv $O/
+  head -16 profiles/${R}_${w}_kernels.md | tail -12
 done
 case " $* " in *" bench "*)
   timeout -k 10 600 python -u bench.py --breakdown > $O/bench.json 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
