@@ -92,7 +92,6 @@ def load():
     L.vo_unpack_descriptor.restype = None
     L.vo_selftest_arith.argtypes = [P, P, P, P, P, P, I, I]
     L.vo_selftest_nullvec9.argtypes = [P, P, P, P, I, I]
-    L.vo_selftest_mfma_i8.argtypes = [P, P, P, P, I]
     _lib = L
     return L
 

@@ -429,6 +429,12 @@ void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax,
         (void)hipStreamWaitEvent(sf, c->ev_rs[p % vo_ctx::kPassEv], 0);
     }
     timed(c, ev, 5, sf, [&] { vo::launch_refit(d, 1, 0, sf); });
+    if (single) {
+        // one frame: triangulation, finalize and the trajectory chain in one launch (its last
+        // workgroup), on the pose queue
+        timed(c, ev, 6, sf, [&] { vo::launch_triangulate(d, 0, sf, out, out_base, 2); });
+        return;
+    }
     if (c->fuse_fin) {
         timed(c, ev, 6, sf, [&] { vo::launch_triangulate(d, 0, sf, out, out_base, 1); });
     } else {
@@ -766,19 +772,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     int p_lo = 0, p_hi = 0;
     if (prio) (void)hipDeviceGetStreamPriorityRange(&p_lo, &p_hi);
     const int p_pose = prio > 0 ? p_hi : p_lo, p_ext = prio < 0 ? p_hi : p_lo;
-    // VO_CU_SPLIT=q (1..3, experiment): the extract queues on CUs i with i % 4 < q, the pose, fit and
-    // trajectory queues on the others (hipExtStreamCreateWithCUMask), so no extract kernel shares a
-    // CU with a pose-pass kernel
-    const int cu_split = getenv("VO_CU_SPLIT") ? std::max(0, std::min(3, atoi(getenv("VO_CU_SPLIT")))) : 0;
-    int ncu = 0;
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->cfg.device);
-    auto make_stream = [&](hipStream_t* q, bool ext, int prio_) -> hipError_t {
-        if (!cu_split || ncu <= 0) return hipStreamCreateWithPriority(q, hipStreamNonBlocking, prio_);
-        std::vector<uint32_t> m((size_t)(ncu + 31) / 32, 0u);
-        for (int i = 0; i < ncu; ++i)
-            if (((i % 4) < cu_split) == ext) m[(size_t)i / 32] |= 1u << (i % 32);
-        return hipExtStreamCreateWithCUMask(q, (uint32_t)m.size(), m.data());
-    };
+    auto make_stream = [&](hipStream_t* q, bool, int prio_) { return hipStreamCreateWithPriority(q, hipStreamNonBlocking, prio_); };
     if (hip_ok(make_stream(&c->s, false, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(make_stream(&c->st, false, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK)
@@ -1570,23 +1564,6 @@ int vo_selftest_nullvec9(const double* S, const double* x0, double* f, int32_t* 
     return VO_OK;
 }
 
-// test hook: one i8 16x16x64 MFMA on per-lane fragments (a, b: 64 x 16 bytes; c, d: 64 x 4 i32)
-int vo_selftest_mfma_i8(const int8_t* a, const int8_t* b, const int32_t* c, int32_t* d, int device)
-{
-    if (!a || !b || !c || !d) return VO_ERR_ARG;
-    HIPCHK(hipSetDevice(device));
-    void *da, *db, *dc, *dd;
-    HIPCHK(hipMalloc(&da, 1024)); HIPCHK(hipMalloc(&db, 1024)); HIPCHK(hipMalloc(&dc, 1024)); HIPCHK(hipMalloc(&dd, 1024));
-    HIPCHK(hipMemcpy(da, a, 1024, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(db, b, 1024, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(dc, c, 1024, hipMemcpyHostToDevice));
-    vo::launch_selftest_mfma_i8(da, db, dc, dd, nullptr);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpy(d, dd, 1024, hipMemcpyDeviceToHost));
-    (void)hipFree(da); (void)hipFree(db); (void)hipFree(dc); (void)hipFree(dd);
-    return VO_OK;
-}
 
 // test hook: device arithmetic self-test (sqrtf, f32 '/', f64 sqrt and '/', det-math)
 int vo_selftest_arith(const float* fa, const float* fb, float* fo, const double* da, const double* db, double* dout,

@@ -323,7 +323,6 @@ void launch_reset(const VoDev& d, hipStream_t s);                   // vo_reset'
 // n bytes from pinned host memory to the device by a copy kernel on s (a single frame's upload:
 // no copy-engine -> compute-queue hand-off in front of the stencil)
 void launch_h2d(uint8_t* dst, const uint8_t* src_pinned, size_t n, hipStream_t s);
-void launch_selftest_mfma_i8(const void* a, const void* b, const void* c, void* d, hipStream_t s);
 void launch_selftest_nullvec9(const double* S, const double* x0, double* f, int* status, int n, hipStream_t s);
 void launch_selftest_arith(const float* fa, const float* fb, float* fo, const double* da,
                            const double* db, double* dout, int n, hipStream_t s);

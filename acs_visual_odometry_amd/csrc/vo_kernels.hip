@@ -5,7 +5,9 @@
 // of oracle/vo_oracle.c (which cites the reference file:line it restates), so keypoints,
 // descriptor bits, matches, per-hypothesis inlier counts, F, R and t are bit-identical
 // to the CPU oracle on the same inputs.  No MFMA: the path is stencil / bit-count /
-// small-f64 bound.
+// small-f64 bound, and a matrix-core matcher co-running with k_stencil perturbed the stencil's
+// packed-FP32 results in lanes 32-63 ("Matrix cores and the stencil"), so
+// none ships (tests/test_no_mfma.py checks the code object).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
@@ -28,9 +30,6 @@ namespace vo {
 // Rows p of the pair order padded to whole groups of DS_OG terms with zero terms (dx = dy = 0:
 // the term is a zero, which leaves a sum that is never -0 unchanged), so the describe loop has
 // no remainder iterations.
-#ifndef MM_VERIFY
-#define MM_VERIFY 0     // diagnostic build: MFMA keys re-derived with popc, hand-off and histogram checks (d.dbg counters)
-#endif
 #ifndef DS_OG
 #define DS_OG 8
 #endif
@@ -576,7 +575,8 @@ __device__ __forceinline__ void st_for(F&& f, std::integer_sequence<int, I...>)
 }
 #define ST_BUF_DW3 0x00020000
 #ifndef ST_FLAT_DEFAULT
-#define ST_FLAT_DEFAULT 1     // launch_stencil: the branch-free FLAT form where the margins allow it
+#define ST_FLAT_DEFAULT 0     // VO_ST_FLAT=1: the branch-free FLAT form where the margins allow it (measured slower:
+                              // KITTI 264k vs 283k frames/s, stencil 2.01 vs 1.81 us/frame; parity-tested as a knob)
 #endif
 #ifndef LDS_POISON
 #define LDS_POISON 0      // diagnostic build: k_select / k_describe poison their LDS first
@@ -1125,9 +1125,6 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     uint16_t* s_wpre = reinterpret_cast<uint16_t*>(smem + L.chunk);   // selected keys before 4-segment word w
     uint64_t* s_keys = reinterpret_cast<uint64_t*>(smem + L.keys);
     const size_t TCAP = ST_TCAP;
-#if MM_VERIFY
-    __shared__ unsigned long long s_ck;                 // diagnostic: checksum of the frame's key list
-#endif
 #if LDS_POISON
     // diagnostic build: the whole dynamic LDS and the static words filled with a launch-varying
     // pattern first, so a read of LDS this workgroup did not write shows up as a result change
@@ -1144,9 +1141,6 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     if (tid == 0) {
         s_nbnd = 0; s_b = -1; s_above = 0;
         s_slot = ext_slot(d, f0, z, slot_override);
-#if MM_VERIFY
-        s_ck = 0ull;
-#endif
     }
     VO_STAMP(d, 1990, 0);
     // A
@@ -1250,13 +1244,6 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
         for (int g = tid; g < VO_DIAG_KEYS; g += 1024)
             d.diag_keys[(size_t)(f0 + z) * VO_DIAG_KEYS + g] = g < C ? keys[g] : 0ull;
 #endif
-#if MM_VERIFY
-    {
-        unsigned long long ck = 0ull;
-        for (int g = tid; g < C; g += 1024) ck += mix64(keys[g] + (unsigned long long)g);
-        atomicAdd(&s_ck, ck);
-    }
-#endif
     VO_STAMP(d, 1990, 1);
     // C
     int b = -1;
@@ -1344,16 +1331,6 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
             Tb = s_tb;
         }
         if (tid == 0 && d.dbg) d.dbg[1990 * 16 + 10] = (unsigned long long)nb;
-#if MM_VERIFY
-        if (tid == 0 && d.dbg) {
-            // the stencil's histogram against the frame's key list (diagnostic builds)
-            uint32_t total = 0;
-            for (int w = 0; w < 16; ++w) total += s_hs[w];
-            if (total != (uint32_t)C) atomicAdd(&d.dbg[6004], 1ull);
-            if (need > nb) atomicAdd(&d.dbg[6005], 1ull);
-            atomicAdd(&d.dbg[6006], 1ull);
-        }
-#endif
     }
     __syncthreads();                                    // s_bnd aliases the segment counts
     for (int w = tid; w < (nseg + 3) / 4; w += 1024) s_segw[w] = 0u;
@@ -1470,15 +1447,6 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     VO_STAMP(d, 1990, 6);
     // select is the histogram's only reader: leave it zeroed for the next frame's stencil
     for (int i = tid; i < VO_HIST_BINS; i += 1024) hist[i] = 0u;
-#if MM_VERIFY
-    __syncthreads();
-    if (tid == 0 && d.dbg && slot < 4000) {
-        d.dbg[8000 + slot] = s_ck;
-        d.dbg[12000 + slot] = (unsigned long long)C;
-        d.dbg[16000 + slot] = Tb;
-        d.dbg[20000 + slot] = (unsigned long long)(uint32_t)b;
-    }
-#endif
     if (tid == 0) {
         // the keypoints emitted: min(C, N) by construction; a frame whose count disagrees (inconsistent
         // stencil output) is marked OVERFLOW, so no later kernel reads a slot entry nobody wrote
@@ -2247,14 +2215,6 @@ __device__ __forceinline__ void top2_insert2(uint32_t k1, uint32_t k2, uint32_t&
     asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(m1), "v"(k1), "v"(k2));   // left alone, LLVM emits two v_min_u32
     m1 = r;
 }
-// the same without inline asm: for keys straight out of an MFMA.  The compiler's hazard recognizer
-// does not see through inline asm, so an asm v_min3_u32 on MFMA results was scheduled right after the
-// MFMA that writes them, without the wait states (stale reads: rows differed from run to run)
-__device__ __forceinline__ void top2_insert2_c(uint32_t k1, uint32_t k2, uint32_t& m1, uint32_t& m2)
-{
-    m2 = min(med3_u32(m1, k1, k2), m2);
-    m1 = min(min(m1, k1), k2);
-}
 __device__ __forceinline__ void top2_wave(uint32_t& m1, uint32_t& m2)
 {
 #pragma unroll
@@ -2426,17 +2386,6 @@ __device__ void match_compact(const VoDev& d, int wf, const MatchFrame& m, int* 
             const int i = (r0 + u) * 256 + tid;
             js[u] = act && i < n1 ? ld_sc1(m.match_j + i) : -1;
         }
-#if MM_VERIFY
-#pragma unroll
-        for (int u = 0; u < RC; ++u) {
-            const int i = (r0 + u) * 256 + tid;
-            if (act && i < n1 && d.dbg) {
-                const int fresh = __hip_atomic_fetch_add((gi32*)(m.match_j + i), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (fresh != js[u]) atomicAdd(&d.dbg[6002], 1ull);
-                atomicAdd(&d.dbg[6003], 1ull);
-            }
-        }
-#endif
         int2 ka[RC], kb[RC];
 #pragma unroll
         for (int u = 0; u < RC; ++u) {
@@ -2578,221 +2527,6 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
     match_compact(d, wf, m, s_wsum);
 }
 
-// MFMA form of the 32-test matcher (k_match_mfma): the all-pairs Hamming distances of a frame
-// pair are an integer matrix product.  With a = +-1 per bit of a candidate's 32-bit prefix and
-// b = +-1 per bit of a query's, dot(a, b) = 32 - 2 dist, so one v_mfma_i32_16x16x64_i8 over
-// A' = -64 a (candidates: rows) and B' = 64 b (queries: columns) gives -4096 dot for 16 x 16 pairs.
-// The rest of K and the C input turn the product straight into the sort key the top-2 keeps:
-//   k = 32, 33   A = (t & 127, 64 (t >> 7)) of candidate tile t, B = (16, 32): + 16 t
-//   C            131072 + the candidate's row in the tile
-// so D = 4096 (32 - dot) + 16 t + row = 8192 dist + j: the (dist, first index) order of the
-// sequential loop (feature_matching_parallel.cpp:72-99), with no VALU per pair but the top-2
-// update.  Lane l holds A[l & 15][16 (l >> 4) + i] / B[16 (l >> 4) + i][l & 15] in byte i of its
-// fragments and D[4 (l >> 4) + r][l & 15] in register r (tests/test_gpu_parity.py
-// test_mfma_i8_operand_maps).  The cur frame's candidates are expanded per workgroup into an LDS
-// table (32 B each, MM_CH at a time); a wave owns MM_G groups of 16 queries and walks every candidate tile,
-// one ds_read_b128 and MM_G MFMAs per tile; the four lane groups of a query (rows 4h .. 4h + 3)
-// merge by shuffles at the end.  Results equal k_match's bit for bit.
-#ifndef VO_MATCH_MFMA_DEFAULT
-#define VO_MATCH_MFMA_DEFAULT 0       // VO_MATCH_MFMA unset: the VALU matchers
-#endif
-#define MM_GROUPS 4                   // query groups of 16 per wave: 64 queries per wave, 256 per workgroup
-                                      // (the single-frame call: 1, 64 per workgroup, 4x the workgroups)
-#define MM_CH 512                     // candidates per LDS chunk (16 KB table: LDS stays free for the
-                                      // extract kernels co-running on the CU)
-typedef int mm_v4i __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint32_t mm_spread4(uint32_t n) { return (n * 0x00204081u) & 0x01010101u; }   // n < 16
-__host__ __device__ inline int mm_lds_bytes(int)
-{
-    return MM_CH * 32 + (MM_CH / 16) * 16 + 16;
-}
-__device__ __forceinline__ int ratio_accept13(uint32_t m1, uint32_t m2, float ratio)
-{
-    if (m1 == 0xFFFFFFFFu || m2 == 0xFFFFFFFFu) return -1;
-    const int d1 = (int)(m1 >> 13), d2 = (int)(m2 >> 13);
-    return ((float)d1 < ratio * (float)d2) ? (int)(m1 & 8191u) : -1;
-}
-
-template <int MM_G>
-__global__ void __launch_bounds__(256) k_match_mfma(VoDev d, int stage)
-{
-    const int wf = blockIdx.y;
-    const VoPlan P = match_window(d, stage);
-    if (wf >= vwin_records(P)) return;
-    MatchFrame m;
-    if (!match_header(d, stage, P, wf, m)) return;
-    __shared__ unsigned s_last;
-    __shared__ int s_wsum[32];
-    extern __shared__ __align__(16) unsigned char smem[];
-    const int N = d.N, n1 = m.n1, n2 = m.n2;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int q0 = blockIdx.x * 64 * MM_G;
-    if (q0 < n1) {
-        uint4* s_tab = reinterpret_cast<uint4*>(smem);             // chunk candidate c: s_tab[2 c] bits 0..15, [2 c + 1] 16..31
-        uint4* s_tt = s_tab + 2 * MM_CH;                           // chunk tile u: its index bytes (k = 32, 33)
-        uint4* s_zero = s_tt + MM_CH / 16;                         // k = 48 .. 63
-        const uint32_t* cpre = d.pre + (size_t)m.cur * N;
-        if (tid == 0) *s_zero = make_uint4(0u, 0u, 0u, 0u);
-        // query fragments: B' = 64 b (bit -> 0x40, clear -> 0xC0); k = 32, 33 -> 16, 32
-        const int h = lane >> 4, col = lane & 15;
-        const uint32_t* qpre = d.pre + (size_t)m.prev * N;
-        mm_v4i b[MM_G];
-#pragma unroll
-        for (int g = 0; g < MM_G; ++g) {
-            const int q = q0 + wave * 16 * MM_G + g * 16 + col;
-            const uint32_t p = q < n1 ? qpre[q] : 0u;
-            uint32_t w[4] = {0u, 0u, 0u, 0u};
-            if (h < 2) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    w[i] = ((mm_spread4((p >> (16 * h + 4 * i)) & 15u) ^ 0x01010101u) << 7) | 0x40404040u;
-            } else if (h == 2) {
-                w[0] = 16u | (32u << 8);
-            }
-            b[g] = mm_v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
-        }
-        const mm_v4i cc = {131072 + 4 * h, 131072 + 4 * h + 1, 131072 + 4 * h + 2, 131072 + 4 * h + 3};
-        const uint4* abase = h < 2 ? s_tab + 2 * col + h : (h == 2 ? s_tt : s_zero);
-        const int astep = h < 2 ? 32 : (h == 2 ? 1 : 0);          // uint4 per tile
-        uint32_t a1[MM_G], a2[MM_G], c1[MM_G], c2[MM_G];
-#pragma unroll
-        for (int g = 0; g < MM_G; ++g) a1[g] = a2[g] = c1[g] = c2[g] = 0xFFFFFFFFu;
-        // software-pipelined by hand: a tile's MFMAs are issued, then the PREVIOUS tile's keys are
-        // consumed, with scheduling barriers between, so at least MM_G MFMAs (64+ cycles) separate an
-        // MFMA from the first VALU read of its result -- well past the MFMA -> VALU read wait states
-        // (the compiler's count for this VGPR-destination form read stale keys in one build)
-        const int ntile = (n2 + 15) >> 4;
-        // keys of candidate tile t into the top-2 chains; rows past n2 (the last tile only) excluded
-        [[maybe_unused]] unsigned long long vbad = 0, vchk = 0;
-        auto consume = [&](const mm_v4i (&dk)[MM_G], bool pad, int t) {
-#pragma unroll
-            for (int g = 0; g < MM_G; ++g) {
-                uint32_t k0 = (uint32_t)dk[g].x, k1 = (uint32_t)dk[g].y, k2 = (uint32_t)dk[g].z, k3 = (uint32_t)dk[g].w;
-#if MM_VERIFY
-                {
-                    const int q = q0 + wave * 16 * MM_G + g * 16 + col;
-                    const uint32_t qp = q < n1 ? qpre[q] : 0u;
-                    const uint32_t kk[4] = {k0, k1, k2, k3};
-                    for (int r = 0; r < 4; ++r) {
-                        const int j = 16 * t + 4 * h + r;
-                        if (j < n2 && q < n1) {
-                            const uint32_t e = 8192u * (uint32_t)__popc(qp ^ cpre[j]) + (uint32_t)j;
-                            vchk += 1;
-                            vbad += e != kk[r];
-                        }
-                    }
-                }
-#endif
-                if (pad) {
-                    const int r0 = 16 * t + 4 * h;
-                    if (r0 >= n2) k0 = 0xFFFFFFFFu;
-                    if (r0 + 1 >= n2) k1 = 0xFFFFFFFFu;
-                    if (r0 + 2 >= n2) k2 = 0xFFFFFFFFu;
-                    if (r0 + 3 >= n2) k3 = 0xFFFFFFFFu;
-                }
-                top2_insert2_c(k0, k1, a1[g], a2[g]);
-                top2_insert2_c(k2, k3, c1[g], c2[g]);
-            }
-        };
-        auto issue = [&](mm_v4i (&dk)[MM_G], int u) {
-            const uint4 av = abase[u * astep];
-            const mm_v4i a = {(int)av.x, (int)av.y, (int)av.z, (int)av.w};
-#pragma unroll
-            for (int g = 0; g < MM_G; ++g) dk[g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b[g], cc, 0, 0, 0);
-        };
-        // ping-pong over two key sets: tile u's MFMAs are issued before tile u - 1's keys are read, with
-        // scheduling barriers between, so MM_G MFMAs (64+ cycles) separate an MFMA from the first VALU
-        // read of its result -- past the MFMA -> VALU wait states by construction (the compiler's count
-        // for this VGPR-destination form read stale keys in one build)
-        mm_v4i dA[MM_G], dB[MM_G];
-        bool pend = false;                                         // dB holds a tile not yet consumed
-        int tB = 0;                                                // dB's tile
-        // a chunk's prefixes, thread tid: candidates tid + 256 k; the next chunk's are loaded while
-        // this one is computed
-        constexpr int KC = MM_CH / 256;
-        uint32_t pc[KC];
-        auto fetch = [&](int t0) {
-#pragma unroll
-            for (int k = 0; k < KC; ++k) {
-                const int j = 16 * t0 + tid + 256 * k;
-                pc[k] = j < n2 ? cpre[j] : 0u;
-            }
-        };
-        if (ntile > 0) fetch(0);
-        for (int t0 = 0; t0 < ntile; t0 += MM_CH / 16) {
-            const int nt = min(MM_CH / 16, ntile - t0);
-            if (t0 > 0) __syncthreads();                           // the previous chunk's table is read
-            // the chunk's candidates: A' = -64 a (bit set -> 0xC0, clear -> 0x40); index bytes per tile
-#pragma unroll
-            for (int k = 0; k < KC; ++k) {
-                const int c = tid + 256 * k;
-                const uint32_t p = pc[k];
-                uint32_t w[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) w[q] = (mm_spread4((p >> (4 * q)) & 15u) << 7) | 0x40404040u;
-                s_tab[2 * c] = make_uint4(w[0], w[1], w[2], w[3]);
-                s_tab[2 * c + 1] = make_uint4(w[4], w[5], w[6], w[7]);
-            }
-            if (tid < nt) {
-                const int t = t0 + tid;
-                s_tt[tid] = make_uint4((uint32_t)(t & 127) | ((uint32_t)(64 * (t >> 7)) << 8), 0u, 0u, 0u);
-            }
-            __syncthreads();
-            if (t0 + MM_CH / 16 < ntile) fetch(t0 + MM_CH / 16);
-            int u = 0;
-            for (; u + 1 < nt; u += 2) {
-                issue(dA, u);
-                __builtin_amdgcn_sched_barrier(0);
-                if (pend) consume(dB, false, tB);                  // never the padded last tile
-                __builtin_amdgcn_sched_barrier(0);
-                issue(dB, u + 1);
-                __builtin_amdgcn_sched_barrier(0);
-                consume(dA, false, t0 + u);
-                __builtin_amdgcn_sched_barrier(0);
-                pend = true;
-                tB = t0 + u + 1;
-            }
-            if (u < nt) {                                          // odd tile count: the chunk's last tile
-                issue(dA, u);
-                __builtin_amdgcn_sched_barrier(0);
-                if (pend) consume(dB, false, tB);
-                tB = t0 + u;
-                asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int g = 0; g < MM_G; ++g) dB[g] = dA[g];
-                __builtin_amdgcn_sched_barrier(0);
-                pend = true;
-            }
-        }
-        if (pend) {
-            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // the last tile's MFMAs have landed
-            __builtin_amdgcn_sched_barrier(0);
-            consume(dB, (n2 & 15) != 0, ntile - 1);
-        }
-#pragma unroll
-        for (int g = 0; g < MM_G; ++g) {
-            top2_merge(a1[g], a2[g], c1[g], c2[g]);
-            // the query's four lane groups (rows 4h .. 4h + 3 of every tile)
-#pragma unroll
-            for (int off = 16; off <= 32; off <<= 1) {
-                const uint32_t o1 = __shfl_xor(a1[g], off), o2 = __shfl_xor(a2[g], off);
-                top2_merge(a1[g], a2[g], o1, o2);
-            }
-            const int q = q0 + wave * 16 * MM_G + g * 16 + col;
-            if (h == 0 && q < n1) st_sc1(m.match_j + q, ratio_accept13(a1[g], a2[g], d.ratio));
-        }
-#if MM_VERIFY
-        if (vchk && d.dbg) {
-            atomicAdd(&d.dbg[6000], vbad);
-            atomicAdd(&d.dbg[6001], vchk);
-        }
-#endif
-    }
-    if (!arrive_last(&m.w->ctr[0], gridDim.x, &s_last)) return;
-    match_compact(d, wf, m, s_wsum);
-}
-
 // Full-length 512-test matcher (matching_serial.cpp:24-40,58; config 4's LDS descriptor-tile
 // stress).  Lane = query: each thread holds its query's 512 bits in 16 VGPRs and keeps its own
 // top-2 keys, so no cross-lane merge is needed.  The cur frame's descriptors stream through an
@@ -2877,160 +2611,6 @@ __global__ void __launch_bounds__(256) k_match512(VoDev d, int stage)
     match_compact(d, wf, m, s_wsum);
 }
 
-// MFMA form of the 512-test matcher (k_match512_mfma): the same +-1 products as k_match_mfma over
-// all 512 tests, eight chained v_mfma_i32_16x16x64_i8 per (candidate tile, query group), so
-// D = 4096 (512 - dot) + C = 8192 dist + j with the index in C (C = 2^21 + 16 t + row: K is taken
-// by the tests).  Candidates are expanded MM5_CH at a time into an LDS table (512 B each: step s,
-// lane half h at bytes 64 s + 16 h); a wave owns MM5_G groups of 16 queries.  Keys are read with the
-// next tile's MFMAs in between (ping-pong, as k_match_mfma).  Results equal k_match512's.
-#define MM5_G 4                       // query groups of 16 per wave: 64 queries per wave, 256 per workgroup
-#define MM5_CH 128                    // candidates per LDS chunk (64 KB; the next chunk's words are loaded during this one)
-#define MM5_W 8                       // waves per workgroup: 512 queries share one expansion of the candidates
-__global__ void __launch_bounds__(64 * MM5_W) k_match512_mfma(VoDev d, int stage)
-{
-    const int wf = blockIdx.y;
-    const VoPlan P = match_window(d, stage);
-    if (wf >= vwin_records(P)) return;
-    MatchFrame m;
-    if (!match_header(d, stage, P, wf, m)) return;
-    __shared__ unsigned s_last;
-    __shared__ int s_wsum[32];
-    extern __shared__ __align__(16) unsigned char smem[];
-    const int N = d.N, n1 = m.n1, n2 = m.n2;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int q0 = blockIdx.x * 64 * MM5_W;
-    if (q0 < n1) {
-        uint4* s_tab = reinterpret_cast<uint4*>(smem);             // candidate c, step s, half h: s_tab[32 c + 4 s + h]
-        const uint32_t* cdesc = reinterpret_cast<const uint32_t*>(d.desc + (size_t)m.cur * N * 8);
-        const uint32_t* qdesc = reinterpret_cast<const uint32_t*>(d.desc + (size_t)m.prev * N * 8);
-        const int h = lane >> 4, col = lane & 15;
-        // query fragments: step s, half h = tests 64 s + 16 h .. + 15 (B' = 64 b: bit -> 0x40, clear -> 0xC0)
-        mm_v4i b[MM5_G][8];
-#pragma unroll
-        for (int g = 0; g < MM5_G; ++g) {
-            const int q = q0 + wave * 64 + g * 16 + col;
-#pragma unroll
-            for (int st = 0; st < 8; ++st) {
-                const uint32_t wd = q < n1 ? qdesc[(size_t)q * 16 + 2 * st + (h >> 1)] : 0u;
-                const uint32_t p = (wd >> (16 * (h & 1))) & 0xFFFFu;
-                uint32_t w[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) w[i] = ((mm_spread4((p >> (4 * i)) & 15u) ^ 0x01010101u) << 7) | 0x40404040u;
-                b[g][st] = mm_v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
-            }
-        }
-        const mm_v4i cc0 = {2097152 + 4 * h, 2097152 + 4 * h + 1, 2097152 + 4 * h + 2, 2097152 + 4 * h + 3};
-        uint32_t a1[MM5_G], a2[MM5_G], c1[MM5_G], c2[MM5_G];
-#pragma unroll
-        for (int g = 0; g < MM5_G; ++g) a1[g] = a2[g] = c1[g] = c2[g] = 0xFFFFFFFFu;
-        const int ntile = (n2 + 15) >> 4;
-        auto consume = [&](const mm_v4i (&dk)[MM5_G], bool pad, int t) {
-#pragma unroll
-            for (int g = 0; g < MM5_G; ++g) {
-                uint32_t k0 = (uint32_t)dk[g].x, k1 = (uint32_t)dk[g].y, k2 = (uint32_t)dk[g].z, k3 = (uint32_t)dk[g].w;
-                if (pad) {
-                    const int r0 = 16 * t + 4 * h;
-                    if (r0 >= n2) k0 = 0xFFFFFFFFu;
-                    if (r0 + 1 >= n2) k1 = 0xFFFFFFFFu;
-                    if (r0 + 2 >= n2) k2 = 0xFFFFFFFFu;
-                    if (r0 + 3 >= n2) k3 = 0xFFFFFFFFu;
-                }
-                top2_insert2_c(k0, k1, a1[g], a2[g]);
-                top2_insert2_c(k2, k3, c1[g], c2[g]);
-            }
-        };
-        // tile u of the chunk = candidate tile t: eight chained MFMAs per query group
-        auto issue = [&](mm_v4i (&dk)[MM5_G], int u, int t) {
-            const uint4* ab = s_tab + 32 * (16 * u + col) + h;
-            const mm_v4i ct = cc0 + 16 * t;
-#pragma unroll
-            for (int g = 0; g < MM5_G; ++g) dk[g] = ct;
-#pragma unroll
-            for (int st = 0; st < 8; ++st) {
-                const uint4 av = ab[4 * st];
-                const mm_v4i a = {(int)av.x, (int)av.y, (int)av.z, (int)av.w};
-#pragma unroll
-                for (int g = 0; g < MM5_G; ++g) dk[g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b[g][st], dk[g], 0, 0, 0);
-            }
-        };
-        mm_v4i dA[MM5_G], dB[MM5_G];
-        bool pend = false;                                         // dB holds a tile not yet consumed
-        // a chunk's descriptor words, thread tid: words tid + 64 MM5_W k of the chunk (candidate x / 16,
-        // word x % 16); the next chunk's are loaded while this one is computed
-        constexpr int KW = (MM5_CH * 16 + 64 * MM5_W - 1) / (64 * MM5_W);
-        uint32_t pw[KW];
-        auto fetch = [&](int t0) {
-#pragma unroll
-            for (int k = 0; k < KW; ++k) {
-                const int x = tid + 64 * MM5_W * k, j = 16 * t0 + (x >> 4);
-                pw[k] = x < MM5_CH * 16 && j < n2 ? cdesc[(size_t)j * 16 + (x & 15)] : 0u;
-            }
-        };
-        if (ntile > 0) fetch(0);
-        for (int t0 = 0; t0 < ntile; t0 += MM5_CH / 16) {
-            const int nt = min(MM5_CH / 16, ntile - t0);
-            if (t0 > 0) __syncthreads();                           // the previous chunk's table is read
-            // the chunk's candidates: A' = -64 a (bit set -> 0xC0, clear -> 0x40); word e of candidate c
-            // (tests 32 e .. 32 e + 31) -> bytes 128 e (d (e / 2) ...) at step e / 2, halves 2 (e & 1), + 1
-#pragma unroll
-            for (int k = 0; k < KW; ++k) {
-                const int x = tid + 64 * MM5_W * k, c = x >> 4, e = x & 15;
-                if (x < MM5_CH * 16) {
-                    const uint32_t p = pw[k];
-                    uint32_t w[8];
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) w[q] = (mm_spread4((p >> (4 * q)) & 15u) << 7) | 0x40404040u;
-                    uint4* dst = s_tab + 32 * c + 4 * (e >> 1) + 2 * (e & 1);
-                    dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
-                    dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
-                }
-            }
-            __syncthreads();
-            if (t0 + MM5_CH / 16 < ntile) fetch(t0 + MM5_CH / 16);
-            int u = 0;
-            for (; u + 1 < nt; u += 2) {
-                issue(dA, u, t0 + u);
-                __builtin_amdgcn_sched_barrier(0);
-                if (pend) consume(dB, false, 0);                   // never the padded last tile
-                __builtin_amdgcn_sched_barrier(0);
-                issue(dB, u + 1, t0 + u + 1);
-                __builtin_amdgcn_sched_barrier(0);
-                consume(dA, false, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                pend = true;
-            }
-            if (u < nt) {
-                issue(dA, u, t0 + u);
-                __builtin_amdgcn_sched_barrier(0);
-                if (pend) consume(dB, false, 0);
-                asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int g = 0; g < MM5_G; ++g) dB[g] = dA[g];
-                __builtin_amdgcn_sched_barrier(0);
-                pend = true;
-            }
-        }
-        if (pend) {
-            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-            consume(dB, (n2 & 15) != 0, ntile - 1);
-        }
-#pragma unroll
-        for (int g = 0; g < MM5_G; ++g) {
-            top2_merge(a1[g], a2[g], c1[g], c2[g]);
-#pragma unroll
-            for (int off = 16; off <= 32; off <<= 1) {
-                const uint32_t o1 = __shfl_xor(a1[g], off), o2 = __shfl_xor(a2[g], off);
-                top2_merge(a1[g], a2[g], o1, o2);
-            }
-            const int q = q0 + wave * 64 + g * 16 + col;
-            if (h == 0 && q < n1) st_sc1(m.match_j + q, ratio_accept13(a1[g], a2[g], d.ratio));
-        }
-    }
-    if (!arrive_last(&m.w->ctr[0], gridDim.x, &s_last)) return;
-    match_compact(d, wf, m, s_wsum);
-}
 
 // ---------------------------------------------------------------------------
 // RANSAC: every hypothesis k < max_hyp in one launch, one per wavefront (ransac.cpp:138-176);
@@ -4104,10 +3684,15 @@ __device__ __forceinline__ void nullvec4(const double* A, double* x)
                                // 128 (point, candidate) pairs; 0.05 m/frame within noise)
 #endif
 __device__ void finalize_body(const VoDev& d, VoFrameOut* out, int out_base);
+__device__ void traj_chain(const VoDev& d, VoFrameOut* out, int out_base, int lo, int nc);
 // fin: the pass's k_finalize runs in the workgroup that arrives last (every workgroup arrives,
 // with or without work; the cheirality counts are agent-scope atomics, read back with agent-scope
 // loads), saving the pass a launch and a queue gap
-__global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d, int stage, VoFrameOut* out, int out_base, int fin)
+// FIN: 0 triangulation only; 1 + the pass's finalize in the last workgroup to arrive (VO_FUSE_FIN);
+// 2 (the single-frame call, whose trajectory runs on the same queue) + finalize + the T_curr chain
+// and pose row (k_traj's work): two launches and their gaps less per vo_process_frame
+template <int FIN>
+__global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d, int stage, VoFrameOut* out, int out_base)
 {
     const int wf = blockIdx.y;
     VoWork* w = d.work + wf;
@@ -4169,10 +3754,17 @@ __global__ void __launch_bounds__(TRI_BLOCK) k_triangulate(VoDev d, int stage, V
         __hip_atomic_fetch_add((gi32*)&w->counts4[threadIdx.x], s_cnt[threadIdx.x], __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (!fin) return;
+    if constexpr (FIN == 0) return;
     if (!arrive_last(d.ctr + VO_CTR_FIN, gridDim.x * gridDim.y, &s_last)) return;
     if (threadIdx.x == 0) d.ctr[VO_CTR_FIN] = 0u;      // the next pass's launch (kernel boundary orders it)
     finalize_body(d, out, out_base);
+    if constexpr (FIN == 2) {
+        // k_traj: the pass log entry finalize_body wrote (this workgroup's own global stores)
+        __threadfence_block();
+        __syncthreads();
+        const int2 lg = d.plog[d.pass % VO_PLOG];
+        if (lg.y > 0) traj_chain(d, out, out_base, lg.x, lg.y);
+    }
 }
 
 // lane 4q + k of each quad -> every lane of the quad (DPP quad_perm [k, k, k, k])
@@ -4423,7 +4015,7 @@ __device__ void finalize_body(const VoDev& d, VoFrameOut* out, int out_base)
 //      the four products
 //   3  per committed frame: the pose row; thread 255: T_curr
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void traj_chain(const VoDev& d, VoFrameOut* out, int out_base, int lo, int nc)
+__device__ void traj_chain(const VoDev& d, VoFrameOut* out, int out_base, int lo, int nc)
 {
     constexpr int MW = VO_MAX_WIN;
     __shared__ double s_Trel[MW + 2][16];             // + 2: step 2 reads two frames ahead
@@ -4556,14 +4148,6 @@ __global__ void __launch_bounds__(256) k_h2d(uint8_t* __restrict__ dst, const ui
         for (size_t i = n16 * 16; i < n; ++i) dst[i] = src[i];
 }
 
-// test hook: one v_mfma_i32_16x16x64_i8 on per-lane fragments (16 bytes of A, 16 of B, 4 i32 of C
-// per lane) -- the operand lane maps the MFMA matcher relies on are pinned by tests/test_gpu_parity.py
-typedef int mf_v4i __attribute__((ext_vector_type(4)));
-__global__ void __launch_bounds__(64) k_selftest_mfma_i8(const mf_v4i* a, const mf_v4i* b, const mf_v4i* c, mf_v4i* d)
-{
-    const int l = threadIdx.x;
-    d[l] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[l], b[l], c[l], 0, 0, 0);
-}
 
 __global__ void __launch_bounds__(256) k_reset(VoDev d)
 {
@@ -4738,12 +4322,6 @@ void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned
     hipLaunchKernelGGL(k_describe, dim3(xcd_grid((d.N + DS_KPB - 1) / DS_KPB, nb)), dim3(64 * DS_WAVES), 0, s, d, f0,
                        slot_override, publish, nb);
 }
-// the matcher form launch_match runs: the MFMA forms unless VO_MATCH_MFMA=0
-static bool match_uses_mfma()
-{
-    static const int mm_env = getenv("VO_MATCH_MFMA") ? atoi(getenv("VO_MATCH_MFMA")) : VO_MATCH_MFMA_DEFAULT;
-    return mm_env != 0;
-}
 // the kernel symbol(s) (base names, comma-separated) stage k of the batched path launches for
 // this context -- what a rocprofv3 summary of the same run lists (bench.py profile_row)
 const char* kernel_form(const VoDev& d, int k)
@@ -4752,9 +4330,7 @@ const char* kernel_form(const VoDev& d, int k)
     case 0: return "k_stencil";
     case 1: return d.sel1 ? "k_select" : "k_select_count,k_select_emit";
     case 2: return "k_describe";
-    case 3:
-        if (d.match_bits == 32) return match_uses_mfma() ? "k_match_mfma" : "k_match";
-        return match_uses_mfma() ? "k_match512_mfma" : "k_match512";
+    case 3: return d.match_bits == 32 ? "k_match" : "k_match512";
     case 4: return "k_ransac_hyp";
     case 5: return "k_refit";
     case 6: return "k_triangulate";
@@ -4765,40 +4341,20 @@ const char* kernel_form(const VoDev& d, int k)
 }
 void launch_match(const VoDev& d, int stage, hipStream_t s)
 {
-    if (d.match_bits == 32)
-    {
-        static const bool mm_ok = mm_lds_bytes(4096) <= 64 * 1024;   // the default dynamic LDS cap
-        if (match_uses_mfma() && mm_ok) {
-            // all-pairs distances on the matrix cores (k_match_mfma)
-            if (d.single)
-                hipLaunchKernelGGL(k_match_mfma<1>, dim3((d.N + 63) / 64, stage ? 1 : d.gridw), dim3(256),
-                                   (size_t)mm_lds_bytes(d.N), s, d, stage);
-            else
-                hipLaunchKernelGGL(k_match_mfma<MM_GROUPS>, dim3((d.N + 64 * MM_GROUPS - 1) / (64 * MM_GROUPS), stage ? 1 : d.gridw),
-                                   dim3(256), (size_t)mm_lds_bytes(d.N), s, d, stage);
-            return;
-        }
+    if (d.match_bits == 32) {
         // single-frame calls: one query per lane (4x the workgroups, a quarter of the walk each)
         if (d.single)
             hipLaunchKernelGGL(k_match<1>, dim3((d.N + 63) / 64, stage ? 1 : d.gridw), dim3(256), 0, s, d, stage);
         else
             hipLaunchKernelGGL(k_match<MT_QPL>, dim3(match_blocks(d.N, 32), stage ? 1 : d.gridw), dim3(256), 0, s, d, stage);
-    }
-    else {
+    } else {
         // 64 KB of dynamic LDS plus the static hand-off words: above the default 64 KB cap
         static const bool lds_ok = hipFuncSetAttribute((const void*)k_match512,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        MT512_TILE * 64) == hipSuccess;
         (void)lds_ok;
-        static const bool mm5_ok = hipFuncSetAttribute((const void*)k_match512_mfma,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       MM5_CH * 512) == hipSuccess;
-        if (match_uses_mfma() && mm5_ok)
-            hipLaunchKernelGGL(k_match512_mfma, dim3((d.N + 64 * MM5_W - 1) / (64 * MM5_W), stage ? 1 : d.gridw),
-                               dim3(64 * MM5_W), (size_t)MM5_CH * 512, s, d, stage);
-        else
-            hipLaunchKernelGGL(k_match512, dim3(match_blocks(d.N, 512), stage ? 1 : d.gridw), dim3(256),
-                               (size_t)MT512_TILE * 64, s, d, stage);
+        hipLaunchKernelGGL(k_match512, dim3(match_blocks(d.N, 512), stage ? 1 : d.gridw), dim3(256),
+                           (size_t)MT512_TILE * 64, s, d, stage);
     }
 }
 // hypotheses in three chunks, [0, C0), [C0, C1), [C1, max_hyp): a frame's later chunks exit at
@@ -4832,7 +4388,10 @@ void launch_triangulate(const VoDev& d, int stage, hipStream_t s, VoFrameOut* ou
     static const int bpf_env = getenv("VO_TRI_BPF") ? atoi(getenv("VO_TRI_BPF")) : TRI_BPF_DEFAULT;
     const int full = (4 * d.N + TRI_BLOCK - 1) / TRI_BLOCK;
     const int bpf = bpf_env > 0 ? std::min(bpf_env, full) : full;
-    hipLaunchKernelGGL(k_triangulate, dim3(bpf, stage ? 1 : d.gridw), dim3(TRI_BLOCK), 0, s, d, stage, out, out_base, fin);
+    const dim3 g(bpf, stage ? 1 : d.gridw);
+    if (fin == 2) hipLaunchKernelGGL(k_triangulate<2>, g, dim3(TRI_BLOCK), 0, s, d, stage, out, out_base);
+    else if (fin) hipLaunchKernelGGL(k_triangulate<1>, g, dim3(TRI_BLOCK), 0, s, d, stage, out, out_base);
+    else hipLaunchKernelGGL(k_triangulate<0>, g, dim3(TRI_BLOCK), 0, s, d, stage, out, out_base);
 }
 void launch_finalize(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s)
 {
@@ -4846,11 +4405,6 @@ void launch_traj(const VoDev& d, VoFrameOut* out, int out_base, hipStream_t s)
 void launch_traj_range(const VoDev& d, VoFrameOut* out, int out_base, int lo, int nc, hipStream_t s)
 {
     hipLaunchKernelGGL(k_traj_range, dim3(1), dim3(256), 0, s, d, out, out_base, lo, nc);
-}
-void launch_selftest_mfma_i8(const void* a, const void* b, const void* c, void* d, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_selftest_mfma_i8, dim3(1), dim3(64), 0, s, (const mf_v4i*)a, (const mf_v4i*)b,
-                       (const mf_v4i*)c, (mf_v4i*)d);
 }
 void launch_h2d(uint8_t* dst, const uint8_t* src, size_t n, hipStream_t s)
 {

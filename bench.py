@@ -601,9 +601,8 @@ def main():
           for k in KERNELS if any(k in b for b in bd)}
     info_all = np.concatenate([last[s][2] for s in my_seqs])
     per_frame = {k: ks[k][0] / ks[k][1] if k in ks and ks[k][1] > 0 else 0.0 for k in KERNELS}
-    # the roofline kernel: the largest per-frame time of any kernel -- the stencil since the MFMA
-    # matcher shortened the pose queue (the extract queue it runs on is busy ~89 % of a step, the
-    # critical path; tools/step_timeline.py on a kernel trace)
+    # the roofline kernel: the largest per-frame time of any kernel (the stencil: the extract queue it
+    # runs on is the critical path of a step; tools/step_timeline.py on a kernel trace)
     dominant = max((k for k in KERNELS if k != "trajectory"), key=lambda k: per_frame[k])
     kidx = KERNELS.index(dominant)
 

@@ -222,7 +222,7 @@ int  vo_last_kernel_stats(vo_ctx* ctx, const char** names, float* ms_per_launch,
                           int cap);
 int  vo_enable_kernel_timing(vo_ctx* ctx, int on);
 /* The kernel symbol(s) stage k (numbered as vo_last_kernel_stats names them) launches on the
- * batched path of this context, as base names ("k_match_mfma"; the banded select:
+ * batched path of this context, as base names ("k_match"; the banded select:
  * "k_select_count,k_select_emit"): the rows of a rocprofv3 summary that belong to the stage. */
 const char* vo_kernel_form(vo_ctx* ctx, int k);
 

@@ -16,7 +16,7 @@ def forms_of(prof, bits):
     """The stage -> kernel symbols map of the run a profile was taken from (its kernel list)."""
     base = {k.split("<")[0] for k in prof}
     match = [m for m in (["k_match_mfma", "k_match"] if bits == 32 else ["k_match512_mfma", "k_match512"])
-             if m in base][:1]
+             if m in base][:1]          # (round-3 profiles may hold the matrix-core matchers)
     sel = ["k_select"] if "k_select" in base else ["k_select_count", "k_select_emit"]
     return {"stencil": ["k_stencil"], "select": sel, "describe": ["k_describe"], "match": match,
             "ransac": ["k_ransac_hyp"], "refit": ["k_refit"], "triangulate": ["k_triangulate"],

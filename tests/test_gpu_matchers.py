@@ -1,14 +1,13 @@
 """Every matcher form the library can run, against the oracle (feature_matching_parallel.cpp:39-113
-for the reference's 32-test matcher, matching_serial.cpp:24-40,58 for the full 512-test one).
-
-The form is chosen once per process (VO_MATCH_MFMA, read by launch_match), so each form runs in a
-child process: the VALU matchers (k_match, k_match512) and the matrix-core ones (k_match_mfma,
-k_match512_mfma), each through
+for the reference's 32-test matcher, matching_serial.cpp:24-40,58 for the full 512-test one):
+k_match<MT_QPL> (batched windows), k_match<1> (the single-frame call, one query per lane) and
+k_match512 (LDS candidate tiles), each through
   - the stage API (vo_match) at N = 2000 / 4096 with ragged sizes around the tile edges,
   - the batched path (vo_process_frames_device): the leak sequence (32 tests) and 1920x1080 /
     N = 4096 (512 tests),
-  - the single-frame call (vo_process_frame: the one-query-per-lane / k_match_mfma<1> launch).
-Matches, rows, statuses and counts must equal the oracle's bit for bit."""
+  - the single-frame call (vo_process_frame) over the leak sequence.
+Matches, rows, statuses and counts must equal the oracle's bit for bit.  (The matrix-core forms of
+round 3 are gone: DESIGN.md section 3, tests/test_no_mfma.py.)"""
 import os
 import subprocess
 import sys
@@ -60,7 +59,7 @@ for tag, ok in out:
 
 @pytest.fixture(scope="module")
 def cases(tmp_path_factory, leak_case):
-    """Inputs and the oracle's answers, computed once for both forms."""
+    """Inputs and the oracle's answers."""
     arrs = {}
     # stage matcher inputs: KITTI N = 2000 (32 tests), 1920x1080 N = 4096 (512 tests)
     for pre, (W, H, N, bits) in (("k", (1241, 376, 2000, 32)), ("x", (1920, 1080, 4096, 512))):
@@ -91,10 +90,8 @@ def cases(tmp_path_factory, leak_case):
     return path
 
 
-@pytest.mark.parametrize("mfma", ["0", "1"])
-def test_matcher_forms_match_oracle(cases, mfma):
-    r = subprocess.run([sys.executable, "-c", _CHILD, ROOT, str(cases)], capture_output=True, text=True, timeout=300,
-                       env={**os.environ, "VO_MATCH_MFMA": mfma})
+def test_matcher_forms_match_oracle(cases):
+    r = subprocess.run([sys.executable, "-c", _CHILD, ROOT, str(cases)], capture_output=True, text=True, timeout=300)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("MATCH_")]
     assert r.returncode == 0 and lines, (r.stdout[-2000:], r.stderr[-2000:])
     bad = [ln for ln in lines if ln.startswith("MATCH_DIFF")]

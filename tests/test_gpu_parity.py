@@ -72,51 +72,6 @@ def test_device_arithmetic_matches_host():
     assert np.array_equal(fo[:4096, 3], ref_s.astype(np.float32))
 
 
-def _mfma_i8_maps(kmap):
-    """(row or column, k) of byte i of lane l's 16-byte fragment, for a candidate K map."""
-    rc = np.zeros((64, 16), np.int64)
-    kk = np.zeros((64, 16), np.int64)
-    for l in range(64):
-        for i in range(16):
-            rc[l, i] = l & 15
-            kk[l, i] = kmap(l, i)
-    return rc, kk
-
-
-_MFMA_K_MAPS = {
-    "contiguous": lambda l, i: 16 * (l >> 4) + i,                                   # k = 16 (l / 16) + i
-    "halves": lambda l, i: 8 * (l >> 4) + i if i < 8 else 32 + 8 * (l >> 4) + i - 8,   # two K = 32 steps
-}
-
-
-def test_mfma_i8_operand_maps():
-    """v_mfma_i32_16x16x64_i8 operand maps the MFMA matcher is built on: lane l holds row / column
-    l & 15 of A / B (k = 16 (l >> 4) + i in byte i of its 16-byte fragments), and D[4 (l >> 4) + r]
-    [l & 15] in register r (exact integer data, asymmetric operands)."""
-    L = load()
-    rng = np.random.default_rng(11)
-    A = rng.integers(-128, 128, (16, 64)).astype(np.int64)
-    B = rng.integers(-128, 128, (64, 16)).astype(np.int64)
-    C = rng.integers(-1 << 20, 1 << 20, (16, 16)).astype(np.int64)
-    ref = A @ B + C
-    dmap = np.array([[(4 * (l >> 4) + r, l & 15) for r in range(4)] for l in range(64)])
-    c_frag = np.array([[C[dmap[l, r, 0], dmap[l, r, 1]] for r in range(4)] for l in range(64)], np.int32)
-    found = []
-    for name, km in _MFMA_K_MAPS.items():
-        rc, kk = _mfma_i8_maps(km)
-        a_frag = A[rc, kk].astype(np.int8)
-        b_frag = B[kk, rc].astype(np.int8)
-        d = np.zeros((64, 4), np.int32)
-        assert L.vo_selftest_mfma_i8(_p(a_frag), _p(b_frag), _p(c_frag), _p(d), 0) == 0
-        got = np.array([[ref[dmap[l, r, 0], dmap[l, r, 1]] for r in range(4)] for l in range(64)])
-        if np.array_equal(d, got):
-            found.append(name)
-    # the order of k inside a lane's fragment is invisible to the product when A and B follow the same
-    # map (both candidate maps pass): the matcher places each bit, and the index bytes, at the same
-    # (lane half, byte) in A and B, so only the row / column and D maps matter
-    assert "contiguous" in found, found
-
-
 def test_refit_nullvec_solver_bit_exact():
     """k_refit's null-vector solver (ls_nullvec9_par) against the oracle's on matrices reaching each
     of its exits -- converged, certified in the null space after the 32-step cap (the bench

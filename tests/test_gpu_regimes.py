@@ -107,7 +107,7 @@ def test_stream_repeats_bit_identical_under_timing_modes():
     vo_reset with every kernel-timing mode the bench uses (off, all launches bracketed by events,
     every 4th launch of one kernel): the rows are identical every time.  Timing events move kernels
     relative to each other, so a missing wait state or a cross-queue race shows up here as rows that
-    differ from run to run (an inline-asm read of MFMA results without its wait states did)."""
+    differ from run to run (round 3's inline-asm read of MFMA results without its wait states did)."""
     F, S = 80, 8
     seqs = [SceneSequence(nframes=F, step=1.0, seq=s) for s in range(S)]
     frames = render_sequences([(q.W, q.H, F, q.seq, 1.0) for q in seqs], 8)
