@@ -463,10 +463,14 @@ std::vector<int> batch_schedule(int nf, int B, int first_default = 0)
 {
     // experiment knob: VO_FIRST = size of the first batch (pipeline fill), default B
     static const int env_first = getenv("VO_FIRST") ? atoi(getenv("VO_FIRST")) : -1;
+    // experiment knob: VO_LAST = size of the batches the chunk's last B frames are split into (the
+    // drain: the last pass covers only the last small batch)
+    static const int env_last = getenv("VO_LAST") ? atoi(getenv("VO_LAST")) : 0;
     const int first = env_first >= 0 ? env_first : first_default;
     std::vector<int> v;
     for (int done = 0; done < nf;) {
-        const int want = (done == 0 && first > 0 && first < B) ? first : B;
+        int want = (done == 0 && first > 0 && first < B) ? first : B;
+        if (env_last > 0 && env_last < B && nf - done <= B) want = env_last;
         v.push_back(std::min(want, nf - done));
         done += v.back();
     }

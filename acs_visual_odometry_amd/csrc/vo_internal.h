@@ -87,7 +87,7 @@ inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_T
 // frames per host chunk: a chunk never extracts over a slot one of its passes still reads
 // (frame f's slot is rewritten by frame f + VO_RING; passes read frames >= lo - 1)
 #define VO_CHUNK (d.ring - 1)
-#define VO_MAX_BATCH 64
+#define VO_MAX_BATCH 128
 #ifndef VO_MAX_WIN
 #define VO_MAX_WIN 128       // pose window capacity (k_finalize / k_traj LDS; < 255: thread 255 keeps the loop state).
                              // Windows measured: 64 227k, 96 258k, 128 268k, 160 / 192 within noise of 128

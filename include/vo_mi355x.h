@@ -69,7 +69,7 @@ typedef struct {
     uint64_t seed;            /* RANSAC sampler seed (replaces std::random_device)     */
     double K[9];              /* PoseUpdate.hpp:36-39                                  */
     int device;               /* HIP device ordinal                                    */
-    int frame_batch;          /* frames per extract batch / pose-pass window (1..64);
+    int frame_batch;          /* frames per extract batch / pose-pass window (1..128);
                                  0 = default 64.  Results do not depend on it.         */
 } vo_config;
 

@@ -55,7 +55,7 @@ def _device_run(seq, frames, ref=None, host=None, **ctx_kw):
     return ref
 
 
-@pytest.mark.parametrize("batch", [8, 16, 64])
+@pytest.mark.parametrize("batch", [8, 16, 64, 112, 128])
 def test_finalize_leak_and_few_inliers_paths(leak_case, batch):
     """k_finalize's fallback model (fitted == 0, >= 8 matches): the leaked (R, t) comes from an
     earlier frame of the same window, from the previous pass (window start), or is absent
@@ -74,7 +74,7 @@ def test_cross_queue_wait_modes(leak_case, monkeypatch, mode):
     _device_run(seq, frames, ref=ref, frame_batch=16)
 
 
-@pytest.mark.parametrize("host,batch", [("pinned", 64), ("pinned", 8), ("pageable", 16), ("staged", 16)])
+@pytest.mark.parametrize("host,batch", [("pinned", 64), ("pinned", 128), ("pinned", 8), ("pageable", 16), ("staged", 16)])
 def test_host_streaming_matches_oracle(leak_case, host, batch, monkeypatch):
     """vo_process_frames_host: frames from host memory, H2D of batch k+1 on the copy queue
     while batch k is extracted (ring of 3 device batch slots).  pageable: registered for the
