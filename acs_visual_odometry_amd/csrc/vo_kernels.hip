@@ -402,8 +402,10 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #define ST_HALO 7                      // blur 3 + gradient 1 + window 2 + nms 1
 #define ST_TCAP VO_TILE_CAP            // candidates per tile (strict maxima: at most one per 2x2 cell)
 #ifndef ST_SEGT_DEFAULT
-#define ST_SEGT_DEFAULT 8              // tiles per wave segment (VO_STSEG picks 2 / 4 / 6 / 8 / 12; KITTI: 8 measured
-                                       // 260k vs 246k frames/s for 4 -- 14 halo rows per 128 instead of per 64 --, 12 257k, 24 231k)
+#define ST_SEGT_DEFAULT 6              // tiles per wave segment (VO_STSEG picks 4 / 5 / 6 / 8).  KITTI, alternating runs
+                                       // (round 4, gpurun_out r4o): 6 290k, 5 286k, 8 281k, 4 273k -- six-tile segments
+                                       // give 44 waves a frame (2.75 workgroups per CU at 64 frames, 8: 33 waves,
+                                       // 2.25) at 14 halo rows per 96
 #endif
 static_assert(ST_SW + 2 * ST_HALO <= 128, "strip + halo within one wave of column pairs");
 static_assert(VO_STRIP_XL + ST_TW - 1 == 63, "tile A in lanes 0..31, tile B in lanes 32..63");
@@ -585,6 +587,10 @@ __device__ __forceinline__ void st_for(F&& f, std::integer_sequence<int, I...>)
 #define ST_DROP_SOFFSET 0
 #endif      // gfx9 buffer descriptor word 3 (raw bytes, no format)
 
+#ifndef ST_KEYS_LDS
+#define ST_KEYS_LDS 1     // the general form stages a tile pair's keys in LDS and writes them once per
+                          // 16-row group, contiguously (0: a divergent 8-byte global store per maximum)
+#endif
 // grid xcd_grid(ceil(waves / 4), nb): 4 waves per workgroup, one (strip, segment) per wave
 #ifndef ST_WAVES_PER_EU
 #define ST_WAVES_PER_EU 4
@@ -611,6 +617,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
     if (g >= nsx * nseg) return;
     const int sxi = g % nsx, seg = g / nsx;
     const int lane = threadIdx.x & 63;
+#if ST_KEYS_LDS
+    __shared__ uint64_t s_keys[4][2 * ST_TCAP];                // this wave's tile pair's keys (general form)
+    uint64_t* __restrict__ wkeys = s_keys[threadIdx.x >> 6];
+#endif
     // image rows and blurred rows through buffer descriptors: the row offset is a scalar
     // operand of the access (no per-row address arithmetic), and a lane whose offset is past
     // the plane (the halo lanes' stores) is dropped by the range check
@@ -906,11 +916,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                                       __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32),
                                       __builtin_amdgcn_mbcnt_lo((uint32_t)b0, 0u))));
                 const uint32_t base = (uint32_t)(isB ? ST_TCAP + toffB - cA : toffA) + pos0;
-                const int tileA = (yn / ST_TH) * ntx + 2 * sxi;
-                char* __restrict__ tc = (char*)(cand + (size_t)tileA * ST_TCAP);
                 const uint32_t key_lo = ((uint32_t)yn << 16) | (uint32_t)c0;
+#if ST_KEYS_LDS
+                uint64_t* __restrict__ tk = wkeys;
+#else
+                const int tileA = (yn / ST_TH) * ntx + 2 * sxi;
+                uint64_t* __restrict__ tk = cand + (size_t)tileA * ST_TCAP;
+#endif
                 if (mx0) {
-                    *(uint64_t*)(tc + base * 8u) = ((uint64_t)(uint32_t)rm0 << 32) | key_lo;
+                    tk[base] = ((uint64_t)(uint32_t)rm0 << 32) | key_lo;
                     const uint32_t bin = min(((uint32_t)rm0 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1));
                     atomicAdd(&hist[bin], 1u);
 #if ST_DIAG & 2
@@ -918,7 +932,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
 #endif
                 }
                 if (mx1) {
-                    *(uint64_t*)(tc + (base + (mx0 ? 1u : 0u)) * 8u) = ((uint64_t)(uint32_t)rm1 << 32) | (key_lo + 1u);
+                    tk[base + (mx0 ? 1u : 0u)] = ((uint64_t)(uint32_t)rm1 << 32) | (key_lo + 1u);
                     const uint32_t bin = min(((uint32_t)rm1 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1));
                     atomicAdd(&hist[bin], 1u);
 #if ST_DIAG & 2
@@ -988,6 +1002,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         // the 16 row counts of tile A (lanes 0..15) and B (16..31) are contiguous
         const int tileA = (ys / ST_TH + i) * ntx + 2 * sxi;
         if (lane < (hasB ? 2 * ST_TH : ST_TH)) tilerows[tileA * ST_TH + lane] = (uint8_t)trows;
+#if ST_KEYS_LDS
+        if constexpr (!FLAT) {
+            // the group's keys: tile A's toffA from slot 0, tile B's toffB from ST_TCAP (tile A + 1's
+            // region of cand), copied out in order by consecutive lanes.  LDS operations of one wave
+            // complete in order, so the next group's writes cannot overtake these reads.
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            uint64_t* __restrict__ dst = cand + (size_t)tileA * ST_TCAP;
+            for (int j = lane; j < toffA; j += 64) dst[j] = wkeys[j];
+            for (int j = lane; j < toffB; j += 64) dst[ST_TCAP + j] = wkeys[ST_TCAP + j];
+        }
+#endif
 #if ST_DIAG & 2
         // per tile: the sum over its keys of mix64(key ^ slot << 48), lanes 0..31 tile A, 32..63 tile B
 #pragma unroll
@@ -4249,31 +4274,34 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
     // one frame (the per-frame call): segments of one tile row, so the frame's waves (4x 8-tile
     // segments' count) each walk 30 source rows instead of 142 -- the latency of the launch
     const int st = write_response ? 4 : nb == 1 && d.single ? 1
-                 : segt == 2 || segt == 6 || segt == 8 || segt == 12 ? segt : ST_SEGT_DEFAULT;
-    // the FLAT form for NMS margins of 5+ (the reference's 35 / 37; VO_ST_FLAT=0 turns it off); the
+                 : segt == 4 || segt == 5 || segt == 6 || segt == 8 ? segt : ST_SEGT_DEFAULT;
+    // the FLAT form for NMS margins of 5+ (the reference's 35 / 37; VO_ST_FLAT=1 turns it on); the
     // general form keeps the border masks (small margins, the response map)
     static const int flat_env = getenv("VO_ST_FLAT") ? atoi(getenv("VO_ST_FLAT")) : ST_FLAT_DEFAULT;
     const bool flat = flat_env && !write_response && d.brow >= 5 && d.bcol >= 5;
-    const int stv = flat ? st : (st == 1 ? 1 : 8);                 // the general form: 8-tile or 1-tile segments
-    const int waves = nsx * ((nty + (write_response ? 4 : stv) - 1) / (write_response ? 4 : stv));   // one (strip, segment) per wave
+    const int waves = nsx * ((nty + st - 1) / st);             // one (strip, segment) per wave
     dim3 g(xcd_grid((waves + 3) / 4, nb));
+#define ST_LAUNCH(S, F) hipLaunchKernelGGL((k_stencil<S, false, F>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb)
     if (write_response)
         hipLaunchKernelGGL((k_stencil<4, true, false>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response, nb);
     else if (!flat) {
-        if (stv == 1) hipLaunchKernelGGL((k_stencil<1, false, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
-        else hipLaunchKernelGGL((k_stencil<8, false, false>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
-    } else if (st == 12)
-        hipLaunchKernelGGL((k_stencil<12, false, true>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
-    else if (st == 8)
-        hipLaunchKernelGGL((k_stencil<8, false, true>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
-    else if (st == 6)
-        hipLaunchKernelGGL((k_stencil<6, false, true>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
-    else if (st == 2)
-        hipLaunchKernelGGL((k_stencil<2, false, true>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
-    else if (st == 1)
-        hipLaunchKernelGGL((k_stencil<1, false, true>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
-    else
-        hipLaunchKernelGGL((k_stencil<4, false, true>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb);
+        switch (st) {
+        case 1: ST_LAUNCH(1, false); break;
+        case 4: ST_LAUNCH(4, false); break;
+        case 5: ST_LAUNCH(5, false); break;
+        case 6: ST_LAUNCH(6, false); break;
+        default: ST_LAUNCH(8, false); break;
+        }
+    } else {
+        switch (st) {
+        case 1: ST_LAUNCH(1, true); break;
+        case 4: ST_LAUNCH(4, true); break;
+        case 5: ST_LAUNCH(5, true); break;
+        case 6: ST_LAUNCH(6, true); break;
+        default: ST_LAUNCH(8, true); break;
+        }
+    }
+#undef ST_LAUNCH
 }
 void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s)
 {
