@@ -1976,6 +1976,9 @@ __global__ void k_ext_missing(VoDev d, int slot)
 #define DS_WAVES 4
 #endif
 #define DS_KPB (DS_KPW * DS_WAVES)
+#ifndef DS_PKSUB
+#define DS_PKSUB 1             // the orientation sums' sample differences two per v_pk_add_f32
+#endif
 #ifndef DS_UNROLL
 #define DS_UNROLL 0            // 1: the orientation sums fully unrolled from sample registers (describe
                                // 0.92 -> 0.85 us/frame but KITTI 278-285k vs 283-289k: 110 VGPRs, 30 KB code)
@@ -2031,8 +2034,12 @@ __device__ __forceinline__ uint32_t ds_word(const uint32_t (&r)[VO_FREAK_NPOINTS
     return word;
 }
 
+// LT (diagnostic, VO_DS_LDS_TABLE=1 for the per-frame call): the orientation pair table read from an
+// LDS copy instead of through the scalar cache.  Measured slower for a single frame too (26 -> 30 us),
+// so the per-frame describe is not waiting on scalar-cache misses of the table.
+template <bool LT>
 __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __restrict__ img, int cur, int n,
-                                              int base, float (*s_I0)[DS_KPW])
+                                              int base, float (*s_I0)[DS_KPW], const float4* __restrict__ s_tab)
 {
     constexpr int NP = VO_FREAK_NPOINTS;
     const int lane = threadIdx.x & 63;
@@ -2111,7 +2118,7 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
         float ip = col[0], iq[DS_OG];
         float4 tb[DS_OG];
 #pragma unroll
-        for (int u = 0; u < DS_OG; ++u) { iq[u] = col[(qs + u) * DS_KPW]; tb[u] = c_orient[u]; }
+        for (int u = 0; u < DS_OG; ++u) { iq[u] = col[(qs + u) * DS_KPW]; tb[u] = LT ? s_tab[u] : c_orient[u]; }
 #ifndef DS_GUNROLL
 #define DS_GUNROLL 4          // orientation groups unrolled (2: 269k vs 277k frames/s in alternating A/B)
 #endif
@@ -2131,10 +2138,21 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
             float iqn[DS_OG];
             float4 tbn[DS_OG];
 #pragma unroll
-            for (int u = 0; u < DS_OG; ++u) { iqn[u] = col[(qn + u) * DS_KPW]; tbn[u] = c_orient[gn * DS_OG + u]; }
+            for (int u = 0; u < DS_OG; ++u) { iqn[u] = col[(qn + u) * DS_KPW]; tbn[u] = LT ? s_tab[gn * DS_OG + u] : c_orient[gn * DS_OG + u]; }
             __builtin_amdgcn_sched_barrier(0);          // the requests stay ahead of the sums
 #pragma unroll
+#if DS_PKSUB
+            // two sample differences per packed subtract (exact: integers), each broadcast into
+            // its term's packed product by op_sel
+            for (int u = 0; u < DS_OG; u += 2) {
+                static_assert(DS_OG % 2 == 0, "pairs of terms");
+                const ds_f2 dd = ds_f2{ip, ip} - ds_f2{iq[u], iq[u + 1]};
+                orient_term(dd.x, tb[u], oxy);
+                orient_term(dd.y, tb[u + 1], oxy);
+            }
+#else
             for (int u = 0; u < DS_OG; ++u) orient_term(ip - iq[u], tb[u], oxy);
+#endif
             __builtin_amdgcn_sched_barrier(0);
             p = pn; qs = qn; ip = ipn;
 #pragma unroll
@@ -2182,10 +2200,16 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
 // grid xcd_grid(N / DS_KPB, nb) (frame z of the batch, workgroup bx of the frame, xcd_frame).
 // publish > 0: the last workgroup of the launch tells the pose queue that frames < publish are
 // extracted (every workgroup of the grid arrives, padding included)
+template <bool LT>
 __global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int slot_override, unsigned publish,
                                                             int nb)
 {
     __shared__ float s_I0[DS_WAVES][DS_UNROLL ? 1 : DS_OROWS][DS_KPW];   // sample columns (the looped sums)
+    __shared__ float4 s_tab[LT ? DS_ONPAD : 1];                          // LT: the pair table
+    if constexpr (LT) {
+        for (int i = threadIdx.x; i < DS_ONPAD; i += 64 * DS_WAVES) s_tab[i] = c_orient[i];
+        __syncthreads();
+    }
 #if LDS_POISON
     {
         const uint32_t pz = (uint32_t)wall_clock64() * 0x9E3779B9u ^ (uint32_t)blockIdx.x;
@@ -2201,7 +2225,7 @@ __global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const int base = bx * DS_KPB + wave * DS_KPW;
         if (base < n)                    // wave-uniform; no barrier inside
-            describe_wave(d, d.blurred + (size_t)z * d.bplane + VO_BLUR_X0, cur, n, base, s_I0[wave]);
+            describe_wave<LT>(d, d.blurred + (size_t)z * d.bplane + VO_BLUR_X0, cur, n, base, s_I0[wave], s_tab);
     }
     if (!publish) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2263,6 +2287,9 @@ __device__ __forceinline__ int ratio_accept(uint32_t m1, uint32_t m2, float rati
 #define MT_QPL 4
 #endif
 #define MT_QPB (64 * MT_QPL)
+#ifndef MT_SINGLE_WAVES
+#define MT_SINGLE_WAVES 16            // single-frame calls: waves per 64 queries (each walks 1/16 of the candidates)
+#endif
 #define MT512_QPB 256                 // 512-test matcher: queries per workgroup (one per thread)
 __host__ __device__ inline int match_blocks(int N, int match_bits)
 {
@@ -2472,9 +2499,10 @@ __device__ __forceinline__ void top2_merge(uint32_t& m1, uint32_t& m2, uint32_t 
     m1 = n1v;
 }
 
-template <int QPL>
-__global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
+template <int QPL, int NW = 4>
+__global__ void __launch_bounds__(64 * NW) k_match(VoDev d, int stage)
 {
+    constexpr int NT = 64 * NW;                      // threads; NW waves split the candidates
     const int wf = blockIdx.y;
     const VoPlan P = match_window(d, stage);
     if (wf >= vwin_records(P)) return;
@@ -2483,20 +2511,20 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
     __shared__ unsigned s_last;
     __shared__ int s_wsum[32];
     __shared__ uint4 s_cand4[1024];                  // 4096 prefixes
-    __shared__ uint2 s_top[3][QPL][64];
+    __shared__ uint2 s_top[NW - 1][QPL][64];
     uint32_t* s_cand = reinterpret_cast<uint32_t*>(s_cand4);
     const int N = d.N, n1 = m.n1, n2 = m.n2;
     // wave-uniform candidate range: scalar loop counter, key index an SGPR operand
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (blockIdx.x * (64 * QPL) < n1) {
         const uint32_t* cand = d.pre + (size_t)m.cur * N;
-        for (int j0 = threadIdx.x; j0 < n2; j0 += 4 * 256) {
+        for (int j0 = threadIdx.x; j0 < n2; j0 += 4 * NT) {
             uint32_t v[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = j0 + u * 256 < n2 ? cand[j0 + u * 256] : 0u;
+            for (int u = 0; u < 4; ++u) v[u] = j0 + u * NT < n2 ? cand[j0 + u * NT] : 0u;
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                if (j0 + u * 256 < n2) s_cand[j0 + u * 256] = v[u];
+                if (j0 + u * NT < n2) s_cand[j0 + u * NT] = v[u];
         }
         // lane's queries: blockIdx.x * (64 * QPL) + 64 u + lane
         uint32_t qv[QPL];
@@ -2505,8 +2533,8 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
             const int q = blockIdx.x * (64 * QPL) + 64 * u + lane;
             qv[u] = q < n1 ? d.pre[(size_t)m.prev * N + q] : 0u;
         }
-        // quarter of the candidates: [j0, j1), j0 a multiple of 4
-        const int qs = ((n2 + 15) >> 4) << 2;
+        // the wave's share of the candidates: [j0, j1), j0 a multiple of 4
+        const int qs = ((n2 + 4 * NW - 1) / (4 * NW)) * 4;
         const int j0 = min(wave * qs, n2), j1 = min(j0 + qs, n2);
         uint32_t a1[QPL], a2[QPL], b1[QPL], b2[QPL];
 #pragma unroll
@@ -2538,7 +2566,7 @@ __global__ void __launch_bounds__(256) k_match(VoDev d, int stage)
 #pragma unroll
             for (int u = 0; u < QPL; ++u) {
 #pragma unroll
-                for (int w = 0; w < 3; ++w) {
+                for (int w = 0; w < NW - 1; ++w) {
                     const uint2 o = s_top[w][u][lane];
                     top2_merge(a1[u], a2[u], o.x, o.y);
                 }
@@ -4347,8 +4375,16 @@ int select_lds_bytes(int W, int H, int* key_cap)
 void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned publish, hipStream_t s)
 {
     ensure_tables();
-    hipLaunchKernelGGL(k_describe, dim3(xcd_grid((d.N + DS_KPB - 1) / DS_KPB, nb)), dim3(64 * DS_WAVES), 0, s, d, f0,
-                       slot_override, publish, nb);
+    // VO_DS_LDS_TABLE=1: the per-frame call's describe reads the pair table from LDS (measured: describe
+    // 26 -> 30 us, the call 165 -> 168 us, so the scalar-cache path stays the default)
+    static const int lt_env = getenv("VO_DS_LDS_TABLE") ? atoi(getenv("VO_DS_LDS_TABLE")) : 0;
+    const bool lt = lt_env != 0 && nb == 1 && d.single;
+    if (lt)
+        hipLaunchKernelGGL(k_describe<true>, dim3(xcd_grid((d.N + DS_KPB - 1) / DS_KPB, nb)), dim3(64 * DS_WAVES), 0, s, d,
+                           f0, slot_override, publish, nb);
+    else
+        hipLaunchKernelGGL(k_describe<false>, dim3(xcd_grid((d.N + DS_KPB - 1) / DS_KPB, nb)), dim3(64 * DS_WAVES), 0, s,
+                           d, f0, slot_override, publish, nb);
 }
 // the kernel symbol(s) (base names, comma-separated) stage k of the batched path launches for
 // this context -- what a rocprofv3 summary of the same run lists (bench.py profile_row)
@@ -4372,7 +4408,8 @@ void launch_match(const VoDev& d, int stage, hipStream_t s)
     if (d.match_bits == 32) {
         // single-frame calls: one query per lane (4x the workgroups, a quarter of the walk each)
         if (d.single)
-            hipLaunchKernelGGL(k_match<1>, dim3((d.N + 63) / 64, stage ? 1 : d.gridw), dim3(256), 0, s, d, stage);
+            hipLaunchKernelGGL((k_match<1, MT_SINGLE_WAVES>), dim3((d.N + 63) / 64, stage ? 1 : d.gridw),
+                               dim3(64 * MT_SINGLE_WAVES), 0, s, d, stage);
         else
             hipLaunchKernelGGL(k_match<MT_QPL>, dim3(match_blocks(d.N, 32), stage ? 1 : d.gridw), dim3(256), 0, s, d, stage);
     } else {

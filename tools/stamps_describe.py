@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """k_describe anatomy from s_memtime stamps (diagnostic VO_STAMPS build): median cycles per
 phase of a describe wave (32 keypoints), over the waves of a 64-frame batched run.
-usage: VO_LIB_PATH=acs_visual_odometry_amd/libvo_mi355x_stamps.so python tools/stamps_describe.py"""
+usage: VO_LIB_PATH=acs_visual_odometry_amd/libvo_mi355x_stamps.so [PF=1] python tools/stamps_describe.py
+PF=1: one vo_process_frame call per sample (the per-frame path's describe launch)."""
 import ctypes as C
 import os
 import sys
@@ -21,11 +22,17 @@ L.vo_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
 names = ["1 pattern gathers -> LDS", "2 orientation sums (903 terms)", "3 atan2 / sincos",
          "4 rotated gathers -> LDS", "5 512 tests (ballots)"]
 rows, spans = [], []
+PF = int(os.environ.get("PF", "0"))        # PF=1: the per-frame call (vo_process_frame), stamps of each call's describe
 for rep in range(10):
-    df = ctx.device_frames(fr)
-    ctx.reset()
-    ctx.process_frames_device(df)
-    df.free()
+    if PF:
+        if rep == 0:
+            ctx.reset()
+        ctx.process_frame(fr[rep + 1])
+    else:
+        df = ctx.device_frames(fr)
+        ctx.reset()
+        ctx.process_frames_device(df)
+        df.free()
     buf = np.zeros(2000 * 16, np.uint64)
     L.vo_debug_stamps(ctx.h, buf.ctypes.data_as(C.c_void_p), buf.size)
     t = buf[1000 * 16:1900 * 16].reshape(900, 16)[:, :6].astype(np.int64)
