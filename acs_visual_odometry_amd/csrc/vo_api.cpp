@@ -67,6 +67,11 @@ struct vo_ctx {
     uint8_t* dring = nullptr;         // host streaming: VO_HRING device slots of B frames
     uint8_t* hstage = nullptr;        // host streaming: pinned staging ring for pageable sources
     int gt_cap = 0;
+    // GT rows [0] and sequence starts [1]: pinned staging of their asynchronous uploads (upload_meta)
+    void* meta_host[2] = {};
+    size_t meta_cap[2] = {};
+    hipEvent_t ev_meta[2] = {};                       // the last upload from each staging buffer
+    hipEvent_t ev_meta_q[VO_EXT_QUEUES + 2] = {};     // the other queues' work before an upload
     VoFrameOut* out_dev = nullptr;
     int out_cap = 0;
     VoFrameOut* out_host = nullptr;   // pinned
@@ -313,24 +318,29 @@ void timed(vo_ctx* c, EvRec* ev, int k, hipStream_t st, F&& launch)
 // eq: extract queue index (its scratch copy and counters)
 // ev_stencil (optional): recorded on q once the stencil (the only reader of the images) is enqueued
 // q2 (optional): select and describe on a second queue after the stencil (event e_s)
+// scr: the scratch copy (default eq, the queue's); st_nb: frames of the stencil launch -- nb, 0 (the
+// previous batch's paired launch covered this one) or 2 nb (this batch and the next, scratch copies
+// scr and scr + 1, which are contiguous)
 int enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, int nb, bool publish,
                     hipStream_t q, EvRec* ev, int eq, hipEvent_t ev_stencil = nullptr, hipStream_t q2 = nullptr,
-                    hipEvent_t e_s = nullptr, bool single = false)
+                    hipEvent_t e_s = nullptr, bool single = false, int scr = -1, int st_nb = -1)
 {
     VoDev d = c->d;
     d.single = single ? 1 : 0;          // the single-frame call: latency-shaped extract launches
     const size_t B = (size_t)c->B;
+    if (scr < 0) scr = eq;
+    if (st_nb < 0) st_nb = nb;
     d.eq = eq;
     d.diag_f0 = f0;
-    d.blurred += d.bplane * B * eq;
-    d.cand += (size_t)d.cand_cap * B * eq;
-    d.tilerows += (size_t)d.ntiles * 16 * B * eq;
-    d.ckeys += (size_t)d.cand_cap * B * eq;
-    d.selbits += ((size_t)d.cand_cap / 64 + 1) * B * eq;
-    d.selctl += B * eq;
-    d.hist += (size_t)VO_HIST_BINS * B * eq;
-    if (d.tile_ck) d.tile_ck += (size_t)d.ntiles * B * eq;
-    timed(c, ev, 0, q, [&] { vo::launch_stencil(d, img0, frame_bytes, nb, 0, q); });
+    d.blurred += d.bplane * B * scr;
+    d.cand += (size_t)d.cand_cap * B * scr;
+    d.tilerows += (size_t)d.ntiles * 16 * B * scr;
+    d.ckeys += (size_t)d.cand_cap * B * scr;
+    d.selbits += ((size_t)d.cand_cap / 64 + 1) * B * scr;
+    d.selctl += B * scr;
+    d.hist += (size_t)VO_HIST_BINS * B * scr;
+    if (d.tile_ck) d.tile_ck += (size_t)d.ntiles * B * scr;
+    if (st_nb > 0) timed(c, ev, 0, q, [&] { vo::launch_stencil(d, img0, frame_bytes, st_nb, 0, q); });
     if (ev_stencil) HIPCHK(hipEventRecord(ev_stencil, q));
     if (q2) {
         HIPCHK(hipEventRecord(e_s, q));
@@ -493,6 +503,9 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         c->reset_pending = false;
     }
     const std::vector<int> sched = batch_schedule(nf, B, hs ? VO_HOST_FIRST_BATCH : 0);
+    // VO_ST_PAIR=1: one stencil launch per two full batches (device frames, one extract queue)
+    static const bool st_pair = getenv("VO_ST_PAIR") && atoi(getenv("VO_ST_PAIR")) != 0;
+    const bool pair = st_pair && multi && !hs && !c->split && nq == 1 && VO_EXT_QUEUES >= 2;
     // extract batch j on its queue (+ its event in event-wait mode)
     std::vector<int> f0s(sched.size() + 1, 0);
     for (size_t j = 0; j < sched.size(); ++j) f0s[j + 1] = f0s[j] + sched[j];
@@ -525,6 +538,14 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
             HIPCHK(hipStreamWaitEvent(q, e_cp, 0));
             rc = enqueue_extract(c, dimg, (size_t)c->cfg.width * c->cfg.height, base + f0, cnt, publish, q, ev, eq,
                                  e_st, q2, e_s);
+            if (rc) return rc;
+        } else if (pair) {
+            // paired stencils: batches 2i and 2i + 1 (both full) share one stencil launch of 2B frames
+            // into scratch copies 0 and 1; each batch's select and describe read its own copy
+            auto paired = [&](int i) { return i % 2 == 0 && i + 1 < (int)sched.size() && sched[i] == B && sched[i + 1] == B; };
+            const int st_nb = paired(j) ? 2 * cnt : (j % 2 == 1 && paired(j - 1) ? 0 : cnt);
+            int rc = enqueue_extract(c, img0 + (size_t)f0 * frame_bytes, frame_bytes, base + f0, cnt, publish, q, ev,
+                                     eq, nullptr, q2, e_s, host_frame, j % 2, st_nb);
             if (rc) return rc;
         } else {
             int rc = enqueue_extract(c, img0 + (size_t)f0 * frame_bytes, frame_bytes, base + f0, cnt, publish, q, ev,
@@ -903,6 +924,13 @@ void vo_destroy(vo_ctx* c)
     if (c->hstage) (void)hipHostFree(c->hstage);
     if (c->sc) (void)hipStreamDestroy(c->sc);
     if (c->ev_reset) (void)hipEventDestroy(c->ev_reset);
+    for (int i = 0; i < 2; ++i) {
+        if (c->ev_meta[i]) (void)hipEventSynchronize(c->ev_meta[i]);
+        if (c->ev_meta[i]) (void)hipEventDestroy(c->ev_meta[i]);
+        if (c->meta_host[i]) (void)hipHostFree(c->meta_host[i]);
+    }
+    for (hipEvent_t e : c->ev_meta_q)
+        if (e) (void)hipEventDestroy(e);
     for (auto& kv : c->tab_by_p) (void)hipFree(kv.second);
     for (hipStream_t q : c->se)
         if (q) (void)hipStreamDestroy(q);
@@ -933,14 +961,49 @@ int vo_reset(vo_ctx* c)
     return VO_OK;
 }
 
+// Host metadata (which = 0: GT rows, 1: sequence starts) to device memory without a host-device
+// sync: copied into a pinned staging buffer (the caller's array may go away on return) and from
+// there on the pose queue, after every other queue's earlier work.  Every kernel that reads it --
+// k_match's sequence bases (pose queue), the trajectory chain's GT scale (behind the pose queue
+// through the pass events) -- is enqueued later, so it sees the new values; extract kernels read
+// neither.  The staging buffer is rewritten only after its previous upload has run.
+int upload_meta(vo_ctx* c, int which, void* dst, const void* src, size_t bytes)
+{
+    if (!bytes) return VO_OK;
+    if (c->ev_meta[which]) HIPCHK(hipEventSynchronize(c->ev_meta[which]));
+    else HIPCHK(hipEventCreateWithFlags(&c->ev_meta[which], hipEventDisableTiming));
+    if (c->meta_cap[which] < bytes) {
+        if (c->meta_host[which]) (void)hipHostFree(c->meta_host[which]);
+        c->meta_host[which] = nullptr;
+        c->meta_cap[which] = 0;
+        HIPCHK(hipHostMalloc(&c->meta_host[which], bytes, hipHostMallocDefault));
+        c->meta_cap[which] = bytes;
+    }
+    std::memcpy(c->meta_host[which], src, bytes);
+    hipStream_t others[VO_EXT_QUEUES + 2];
+    int no = 0;
+    for (hipStream_t q : c->se) others[no++] = q;
+    others[no++] = c->sf;
+    others[no++] = c->st;
+    for (int i = 0; i < no; ++i) {
+        if (!others[i]) continue;
+        if (!c->ev_meta_q[i]) HIPCHK(hipEventCreateWithFlags(&c->ev_meta_q[i], hipEventDisableTiming));
+        HIPCHK(hipEventRecord(c->ev_meta_q[i], others[i]));
+        HIPCHK(hipStreamWaitEvent(c->s, c->ev_meta_q[i], 0));
+    }
+    HIPCHK(hipMemcpyAsync(dst, c->meta_host[which], bytes, hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipEventRecord(c->ev_meta[which], c->s));
+    return VO_OK;
+}
+
 int vo_set_sequence_starts(vo_ctx* c, const int32_t* starts, int n)
 {
     if (!c || n < 0 || n > VO_MAX_SEQ_STARTS || (n > 0 && !starts)) return VO_ERR_ARG;
     for (int i = 0; i < n; ++i)
         if (starts[i] < 1 || (i > 0 && starts[i] <= starts[i - 1])) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    SYNC_ALL(c);
-    if (n) HIPCHK(hipMemcpy((void*)c->d.seq_starts, starts, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice));
+    const int rc = upload_meta(c, 1, (void*)c->d.seq_starts, starts, sizeof(int32_t) * (size_t)n);
+    if (rc) return rc;
     c->d.n_seq_starts = n;
     return VO_OK;
 }
@@ -993,15 +1056,16 @@ int vo_set_ground_truth(vo_ctx* c, const double* poses12, int n)
 {
     if (!c || n < 0 || (n > 0 && !poses12)) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    SYNC_ALL(c);
     if (n > c->gt_cap) {
+        SYNC_ALL(c);                                   // the old rows may still be read
         if (c->d.gt) (void)hipFree((void*)c->d.gt);
         double* g = nullptr;
         HIPCHK(hipMalloc((void**)&g, sizeof(double) * 12 * (size_t)n));
         c->d.gt = g;
         c->gt_cap = n;
     }
-    if (n) HIPCHK(hipMemcpy((void*)c->d.gt, poses12, sizeof(double) * 12 * (size_t)n, hipMemcpyHostToDevice));
+    const int rc = upload_meta(c, 0, (void*)c->d.gt, poses12, sizeof(double) * 12 * (size_t)n);
+    if (rc) return rc;
     c->d.gt_n = n;
     return VO_OK;
 }

@@ -1977,7 +1977,7 @@ __global__ void k_ext_missing(VoDev d, int slot)
 #endif
 #define DS_KPB (DS_KPW * DS_WAVES)
 #ifndef DS_PKSUB
-#define DS_PKSUB 1             // the orientation sums' sample differences two per v_pk_add_f32
+#define DS_PKSUB 0             // 1: the orientation sums' sample differences two per v_pk_add_f32 (12 % fewer orientation VALU, but KITTI 288-290k vs 293-298k, r4s)
 #endif
 #ifndef DS_UNROLL
 #define DS_UNROLL 0            // 1: the orientation sums fully unrolled from sample registers (describe
@@ -4183,19 +4183,22 @@ __global__ void __launch_bounds__(256) k_traj_range(VoDev d, VoFrameOut* out, in
 
 // vo_reset on the device (VisualOdometry.cpp:50-62 initial state): trajectory state, slot
 // statuses, histograms, window records and cross-queue counters; no host round trip
-// a frame from pinned host memory (read over PCIe by the kernel) into device memory: four
+// a frame from pinned host memory (read over PCIe by the kernel) into device memory: H2D_PT
 // 16-byte loads in flight per thread, the tail bytes by the first thread
+#ifndef H2D_PT
+#define H2D_PT 4
+#endif
 __global__ void __launch_bounds__(256) k_h2d(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, size_t n)
 {
-    const size_t n16 = n / 16, i0 = (size_t)blockIdx.x * 1024 + threadIdx.x;
+    const size_t n16 = n / 16, i0 = (size_t)blockIdx.x * (256 * H2D_PT) + threadIdx.x;
     const uint4* s4 = reinterpret_cast<const uint4*>(src);
     uint4* d4 = reinterpret_cast<uint4*>(dst);
-    uint4 v[4];
+    uint4 v[H2D_PT];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < H2D_PT; ++u)
         if (i0 + 256 * u < n16) v[u] = s4[i0 + 256 * u];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < H2D_PT; ++u)
         if (i0 + 256 * u < n16) d4[i0 + 256 * u] = v[u];
     if (blockIdx.x == 0 && threadIdx.x == 0)
         for (size_t i = n16 * 16; i < n; ++i) dst[i] = src[i];
@@ -4474,7 +4477,7 @@ void launch_traj_range(const VoDev& d, VoFrameOut* out, int out_base, int lo, in
 void launch_h2d(uint8_t* dst, const uint8_t* src, size_t n, hipStream_t s)
 {
     const size_t n16 = n / 16;
-    const int blocks = (int)std::max<size_t>(1, (n16 + 4 * 256 - 1) / (4 * 256));
+    const int blocks = (int)std::max<size_t>(1, (n16 + H2D_PT * 256 - 1) / (H2D_PT * 256));
     hipLaunchKernelGGL(k_h2d, dim3(blocks), dim3(256), 0, s, dst, src, n);
 }
 void launch_reset(const VoDev& d, hipStream_t s)

@@ -55,3 +55,13 @@ def test_algorithmic_bytes_follow_the_survey():
     parts = sum(bench.algorithmic_bytes(k, W, H, info) for k in
                 ("stencil", "select", "describe", "match", "ransac", "trajectory"))
     assert bench.algorithmic_bytes("path", W, H, info) == W * H + 80 * 2000 + 24 * 300 + 96 == parts
+
+
+def test_dominant_kernel_is_on_the_critical_queue():
+    """The roofline kernel is the largest kernel of the busier queue, not the largest of any queue:
+    KITTI at round 4 has the matcher above the stencil but the extract queue ahead of the pose queue."""
+    kitti = {"stencil": 1.49, "select": 0.61, "describe": 0.95, "match": 1.63, "ransac": 1.0, "refit": 0.6,
+             "triangulate": 0.55, "finalize": 0.38, "trajectory": 0.5}
+    assert bench.dominant_kernel(kitti) == "stencil"
+    low_inlier = dict(kitti, ransac=4.2)
+    assert bench.dominant_kernel(low_inlier) == "ransac"
