@@ -567,10 +567,11 @@ def main():
         s0, fr0 = seqs[my_seqs[0]]
         cpu, oracle_rows = cpu_baseline(fr0, s0, args.cpu_seconds, args.max_kpts, workers)
 
-    dist = dist_init(world, local)
+    dev = local if args.device < 0 else args.device     # (--device 0 --backend gloo: ranks sharing one GPU)
+    dist = dist_init(world, dev, backend=args.backend)
     from acs_visual_odometry_amd import Context
 
-    ctx = Context(W, H, K=seqs[my_seqs[0]][0].K, max_kpts=args.max_kpts, device=local, frame_batch=args.batch,
+    ctx = Context(W, H, K=seqs[my_seqs[0]][0].K, max_kpts=args.max_kpts, device=dev, frame_batch=args.batch,
                   match_bits=args.match_bits)
     # the rank's sequences as one frame stream: frames and GT rows concatenated, each sequence's
     # first frame marked (vo_set_sequence_starts), so the next sequence's extract overlaps the
@@ -627,17 +628,18 @@ def main():
     barrier()
     dt = t1 - t0
     frames_rank = args.steps * F * len(my_seqs)
-    dt, value = aggregate(dist, dt, frames_rank, world, local=local)
+    dt, value = aggregate(dist, dt, frames_rank, world, backend=args.backend, local=dev)
     repeat_equal = all(np.array_equal(warm[s][0], last[s][0]) and np.array_equal(warm[s][1], last[s][1])
                        for s in my_seqs)
     rows = {s: np.concatenate([last[s][0].reshape(F, 12), last[s][1].reshape(F, 1).astype(np.float64)], axis=1)
             for s in my_seqs}
-    gathered = gather_poses(dist, rows, owners, F, local=local)
+    gathered = gather_poses(dist, rows, owners, F, backend=args.backend, local=dev)
     # every rank runs each of its sequences alone, as the reference would (one run() each); those
     # rows are gathered too and rank 0 checks every sequence's stream rows against them bit for bit
     gather_ok = None
     if not args.no_check:
-        sep = gather_poses(dist, {s: separate(s, seqs[s][1]) for s in my_seqs}, owners, F, local=local)
+        sep = gather_poses(dist, {s: separate(s, seqs[s][1]) for s in my_seqs}, owners, F, backend=args.backend,
+                           local=dev)
         gather_ok = bool(np.array_equal(sep.view(np.int64), gathered.view(np.int64)))
     # the CPU oracle's rows of the first sequence (the cpu_baseline leg's first complete pass)
     # against the GPU's rows of that sequence in the timed stream, bit for bit
