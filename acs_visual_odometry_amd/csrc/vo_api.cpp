@@ -223,7 +223,8 @@ double now_us()
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride, hipStream_t st)
+// zero_copy: only stage the frame in the pinned buffer; the caller's stencil reads it there over PCIe
+int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride, hipStream_t st, bool zero_copy = false)
 {
     const int W = c->cfg.width, H = c->cfg.height;
     if (stride == 0) stride = (size_t)W;
@@ -242,6 +243,7 @@ int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride, hipStream_t st)
         c->pf_t[0] += t1 - t0;
         c->pf_t[1] += t2 - t1;
     }
+    if (zero_copy) return VO_OK;
     vo::launch_h2d(c->d.frame_in, c->stage_host, (size_t)W * H, st);
     HIPCHK(hipGetLastError());
     return VO_OK;
@@ -1297,14 +1299,17 @@ int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_
     if (!c) return VO_ERR_ARG;
     const double t0 = c->pf_profile ? now_us() : 0.0;
     HIPCHK(hipSetDevice(c->cfg.device));
+    // VO_PF_ZEROCOPY=1: the stencil reads the frame from the pinned staging buffer itself (no upload
+    // kernel); the next call's staging copy waits for this one (upload_frame's sync)
+    static const bool zc = getenv("VO_PF_ZEROCOPY") && atoi(getenv("VO_PF_ZEROCOPY")) != 0;
     if (gray) {
-        int rc = upload_frame(c, gray, stride, c->s);
+        int rc = upload_frame(c, gray, stride, c->s, zc);
         if (rc) return rc;
     }
     const double t1 = c->pf_profile ? now_us() : 0.0;
     const int f = c->fidx;
     // one frame: extract on the pose queue, a window of one (no speculation)
-    int rc = run_chunk(c, gray ? c->d.frame_in : nullptr, 0, 1, c->out_dev, f, nullptr, true);
+    int rc = run_chunk(c, gray ? (zc ? c->stage_host : c->d.frame_in) : nullptr, 0, 1, c->out_dev, f, nullptr, true);
     if (rc) return rc;
     if (c->pf_profile) {
         c->pf_t[2] += c->pf_enq_end - t1;

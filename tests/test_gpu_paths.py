@@ -412,3 +412,36 @@ def test_process_knobs_match_oracle(leak_case, tmp_path, env, batch):
     assert "KNOB_OK" in out.stdout, (out.stdout[-2000:], out.stderr[-2000:])
     if "VO_FORCE_WAIT_REFUSAL" in kv:
         assert "event waits" in out.stderr
+
+
+_PF_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from acs_visual_odometry_amd import Context
+d = np.load(sys.argv[2])
+ctx = Context(int(d["W"]), int(d["H"]), K=d["K"])
+ctx.set_ground_truth(d["gt"])
+rows = [ctx.process_frame(f) for f in d["frames"]]
+ctx.close()
+ok = np.array_equal(np.array([r[1] for r in rows]), d["st"]) and \
+     np.array_equal(np.stack([r[0] for r in rows]), d["poses"]) and \
+     np.array_equal(np.stack([r[2][:6] for r in rows]), d["info"])
+print("PF_OK" if ok else "PF_DIFF")
+"""
+
+
+@pytest.mark.parametrize("env", ["VO_PF_ZEROCOPY=1", "VO_DS_LDS_TABLE=1"])
+def test_per_frame_knobs_match_oracle(leak_case, tmp_path, env):
+    """Per-frame-call knobs read once per process (the stencil reading the frame from the pinned
+    staging buffer, describe's LDS pair table), in a child process over the leak sequence: one
+    vo_process_frame per frame, rows, statuses and counts equal the oracle's."""
+    import sys
+    seq, frames, ref = leak_case
+    npz = tmp_path / "case.npz"
+    np.savez(npz, W=seq.W, H=seq.H, K=seq.K, gt=seq.gt(), frames=frames,
+             st=np.array([r[1] for r in ref]), poses=np.stack([r[0] for r in ref]),
+             info=np.stack([r[2][:6] for r in ref]))
+    kv = dict(e.split("=") for e in env.split(","))
+    out = subprocess.run([sys.executable, "-c", _PF_SCRIPT, ROOT, str(npz)], capture_output=True,
+                         text=True, timeout=240, env={**os.environ, **kv})
+    assert "PF_OK" in out.stdout, (out.stdout[-2000:], out.stderr[-2000:])
