@@ -587,6 +587,9 @@ __device__ __forceinline__ void st_for(F&& f, std::integer_sequence<int, I...>)
 #define ST_DROP_SOFFSET 0
 #endif      // gfx9 buffer descriptor word 3 (raw bytes, no format)
 
+#ifndef ST_HIST_FLUSH
+#define ST_HIST_FLUSH 0   // the general form's histogram counts at the group flush (from the LDS keys)
+#endif
 #ifndef ST_KEYS_LDS
 #define ST_KEYS_LDS 1     // the general form stages a tile pair's keys in LDS and writes them once per
                           // 16-row group, contiguously (0: a divergent 8-byte global store per maximum)
@@ -618,7 +621,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
     const int sxi = g % nsx, seg = g / nsx;
     const int lane = threadIdx.x & 63;
 #if ST_KEYS_LDS
-    __shared__ uint64_t s_keys[4][2 * ST_TCAP];                // this wave's tile pair's keys (general form)
+    // this wave's tile pair's keys (+ 128 lane-private slots: the FLAT form's lanes without a maximum)
+    __shared__ uint64_t s_keys[4][2 * ST_TCAP + (FLAT ? 128 : 0)];
     uint64_t* __restrict__ wkeys = s_keys[threadIdx.x >> 6];
 #endif
     // image rows and blurred rows through buffer descriptors: the row offset is a scalar
@@ -891,14 +895,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             asm("v_writelane_b32 %0, %1, %2" : "+v"(trows) : "s"(cA), "n"(r));
             asm("v_writelane_b32 %0, %1, %2" : "+v"(trows) : "s"(cB), "n"(16 + r));
             if constexpr (FLAT) {
-                // every lane stores; a lane without a maximum gets an out-of-range offset (dropped)
                 const uint32_t pos0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32),
                                       __builtin_amdgcn_mbcnt_lo((uint32_t)b1,
                                       __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32),
                                       __builtin_amdgcn_mbcnt_lo((uint32_t)b0, 0u))));
                 const uint32_t base = (uint32_t)(isB ? ST_TCAP + toffB - cA : toffA) + pos0;
-                const uint32_t slot0 = (uint32_t)((yn / ST_TH) * ntx + 2 * sxi) * ST_TCAP + base;
                 const uint32_t key_lo = ((uint32_t)yn << 16) | (uint32_t)c0;
+#if ST_KEYS_LDS
+                // every lane writes LDS: a lane without a maximum into its own slot past the pair's
+                // (the histogram counts follow from the flushed keys, once per 16-row group)
+                const int s0 = mx0 ? (int)base : 2 * ST_TCAP + lane;
+                const int s1 = mx1 ? (int)(base + (mx0 ? 1u : 0u)) : 2 * ST_TCAP + 64 + lane;
+                wkeys[s0] = ((uint64_t)(uint32_t)rm0 << 32) | key_lo;
+                wkeys[s1] = ((uint64_t)(uint32_t)rm1 << 32) | (key_lo + 1u);
+#else
+                // every lane stores; a lane without a maximum gets an out-of-range offset (dropped)
+                const uint32_t slot0 = (uint32_t)((yn / ST_TH) * ntx + 2 * sxi) * ST_TCAP + base;
                 const int o0 = mx0 ? (int)(slot0 * 8u) : 0x7FFFFFF0;
                 const int o1 = mx1 ? (int)((slot0 + (mx0 ? 1u : 0u)) * 8u) : 0x7FFFFFF0;
                 typedef unsigned int st_u2 __attribute__((ext_vector_type(2)));
@@ -908,6 +920,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                 const int h1 = mx1 ? (int)(min(((uint32_t)rm1 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1)) * 4u) : 0x7FFFFFF0;
                 (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rhist, h0, 0, 0);
                 (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rhist, h1, 0, 0);
+#endif
             } else if (b0 | b1) {
                 // tile-local raster order: rows before this one, then columns before: the lower
                 // lanes' pairs, and c0 before c0 + 1
@@ -925,16 +938,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
 #endif
                 if (mx0) {
                     tk[base] = ((uint64_t)(uint32_t)rm0 << 32) | key_lo;
+#if !(ST_KEYS_LDS && ST_HIST_FLUSH)
                     const uint32_t bin = min(((uint32_t)rm0 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1));
                     atomicAdd(&hist[bin], 1u);
+#endif
 #if ST_DIAG & 2
                     dck += mix64((((uint64_t)(uint32_t)rm0 << 32) | key_lo) ^ ((uint64_t)base << 48));
 #endif
                 }
                 if (mx1) {
                     tk[base + (mx0 ? 1u : 0u)] = ((uint64_t)(uint32_t)rm1 << 32) | (key_lo + 1u);
+#if !(ST_KEYS_LDS && ST_HIST_FLUSH)
                     const uint32_t bin = min(((uint32_t)rm1 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1));
                     atomicAdd(&hist[bin], 1u);
+#endif
 #if ST_DIAG & 2
                     dck += mix64((((uint64_t)(uint32_t)rm1 << 32) | (key_lo + 1u)) ^ ((uint64_t)(base + (mx0 ? 1u : 0u)) << 48));
 #endif
@@ -1003,14 +1020,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         const int tileA = (ys / ST_TH + i) * ntx + 2 * sxi;
         if (lane < (hasB ? 2 * ST_TH : ST_TH)) tilerows[tileA * ST_TH + lane] = (uint8_t)trows;
 #if ST_KEYS_LDS
-        if constexpr (!FLAT) {
+        {
             // the group's keys: tile A's toffA from slot 0, tile B's toffB from ST_TCAP (tile A + 1's
             // region of cand), copied out in order by consecutive lanes.  LDS operations of one wave
             // complete in order, so the next group's writes cannot overtake these reads.
+            // ST_HIST_FLUSH (and always in the FLAT form): each flushed key's histogram count here
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             uint64_t* __restrict__ dst = cand + (size_t)tileA * ST_TCAP;
-            for (int j = lane; j < toffA; j += 64) dst[j] = wkeys[j];
-            for (int j = lane; j < toffB; j += 64) dst[ST_TCAP + j] = wkeys[ST_TCAP + j];
+            constexpr bool hf = FLAT || ST_HIST_FLUSH;
+            for (int j = lane; j < toffA; j += 64) {
+                const uint64_t kv = wkeys[j];
+                dst[j] = kv;
+                if constexpr (hf) atomicAdd(&hist[min(((uint32_t)(kv >> 32) - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1))], 1u);
+            }
+            for (int j = lane; j < toffB; j += 64) {
+                const uint64_t kv = wkeys[ST_TCAP + j];
+                dst[ST_TCAP + j] = kv;
+                if constexpr (hf) atomicAdd(&hist[min(((uint32_t)(kv >> 32) - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1))], 1u);
+            }
         }
 #endif
 #if ST_DIAG & 2

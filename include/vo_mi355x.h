@@ -129,7 +129,10 @@ int  vo_pose(vo_ctx* ctx, const double F[9], const float* p1, const float* p2, i
              double scale, double R[9], double t[3], int32_t* counts4);
 
 /* Ground truth for the trajectory loop's scale (VisualOdometry.cpp:161-162): n rows of
- * 12 doubles (KITTI 3x4 row-major).  Without it the scale is 1. */
+ * 12 doubles (KITTI 3x4 row-major).  Without it the scale is 1.  The rows are copied into a
+ * pinned staging buffer before the call returns (the caller's array may be freed) and reach the
+ * device asynchronously, ahead of every later call's kernels; like vo_set_sequence_starts, the
+ * call does not wait for the GPU unless the row count outgrows the device buffer. */
 int  vo_set_ground_truth(vo_ctx* ctx, const double* poses12, int n);
 
 /* Independent sequences in one frame stream (config 5 on one GPU): frames starts[0..n) (counted
