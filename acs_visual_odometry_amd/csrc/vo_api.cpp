@@ -501,7 +501,8 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     const bool multi = hs || !(c->serial || host_frame || !img0);   // extract on its own queues
     static const int nq = getenv("VO_EXTQ") ? std::max(1, std::min(VO_EXT_QUEUES, atoi(getenv("VO_EXTQ")))) : 1;
     if (multi && c->reset_pending) {
-        for (hipStream_t q : c->se) HIPCHK(hipStreamWaitEvent(q, c->ev_reset, 0));
+        for (hipStream_t q : c->se)
+            if (q) HIPCHK(hipStreamWaitEvent(q, c->ev_reset, 0));
         c->reset_pending = false;
     }
     const std::vector<int> sched = batch_schedule(nf, B, hs ? VO_HOST_FIRST_BATCH : 0);
@@ -809,8 +810,16 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
         if (hip_ok(hipEventCreateWithFlags(&c->ev_rs[i], hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK ||
             hip_ok(hipEventCreateWithFlags(&c->ev_fn[i], hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK)
             return bail(VO_ERR_HIP);
-    for (hipStream_t& q : c->se)
-        if (hip_ok(make_stream(&q, true, p_ext)) != VO_OK) return bail(VO_ERR_HIP);
+    // extract queues: only those a configuration uses (VO_EXTQ / VO_SPLIT / VO_ST_PAIR's scratch
+    // copies need no queue of their own) -- every stream takes one of the process's hardware
+    // queues (GPU_MAX_HW_QUEUES, 4 by default), and a stream past them shares another's and
+    // serialises behind its kernels
+    {
+        const int nq = getenv("VO_EXTQ") ? std::max(1, std::min(VO_EXT_QUEUES, atoi(getenv("VO_EXTQ")))) : 1;
+        const int ne = c->split ? 2 : nq;
+        for (int i = 0; i < ne; ++i)
+            if (hip_ok(make_stream(&c->se[i], true, p_ext)) != VO_OK) return bail(VO_ERR_HIP);
+    }
     if (hip_ok(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming)) != VO_OK) return bail(VO_ERR_HIP);
     d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
     if (d.sel_lds < 0) return bail(VO_ERR_HIP);

@@ -568,6 +568,11 @@ def main():
         cpu, oracle_rows = cpu_baseline(fr0, s0, args.cpu_seconds, args.max_kpts, workers)
 
     dev = local if args.device < 0 else args.device     # (--device 0 --backend gloo: ranks sharing one GPU)
+    if world > 1:
+        # the context's four queues plus RCCL's streams: room for all of them on hardware queues of
+        # their own (HIP's default is 4 per process; a stream past them shares one and serialises
+        # behind its kernels).  Measured neutral at N = 1 (gpurun_out r5g); set before HIP starts.
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     dist = dist_init(world, dev, backend=args.backend)
     from acs_visual_odometry_amd import Context
 
