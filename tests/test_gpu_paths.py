@@ -430,10 +430,10 @@ print("PF_OK" if ok else "PF_DIFF")
 """
 
 
-@pytest.mark.parametrize("env", ["VO_PF_ZEROCOPY=1", "VO_DS_LDS_TABLE=1"])
+@pytest.mark.parametrize("env", ["VO_PF_ZEROCOPY=0", "VO_DS_LDS_TABLE=1"])
 def test_per_frame_knobs_match_oracle(leak_case, tmp_path, env):
-    """Per-frame-call knobs read once per process (the stencil reading the frame from the pinned
-    staging buffer, describe's LDS pair table), in a child process over the leak sequence: one
+    """Per-frame-call knobs read once per process (the upload kernel instead of the stencil reading
+    the frame from the pinned staging buffer, describe's LDS pair table), in a child process over the leak sequence: one
     vo_process_frame per frame, rows, statuses and counts equal the oracle's."""
     import sys
     seq, frames, ref = leak_case
