@@ -445,3 +445,27 @@ def test_per_frame_knobs_match_oracle(leak_case, tmp_path, env):
     out = subprocess.run([sys.executable, "-c", _PF_SCRIPT, ROOT, str(npz)], capture_output=True,
                          text=True, timeout=240, env={**os.environ, **kv})
     assert "PF_OK" in out.stdout, (out.stdout[-2000:], out.stderr[-2000:])
+
+
+def test_per_frame_call_with_row_stride(leak_case):
+    """vo_process_frame on frames inside wider rows (a cv::Mat ROI: stride > W): the rows are
+    gathered into the pinned staging buffer the stencil reads, and every pose row, status and count
+    equals the oracle's (VisualOdometry.cpp:67-190 per frame)."""
+    import ctypes as C
+    seq, frames, ref = leak_case
+    ctx = Context(seq.W, seq.H, K=seq.K)
+    ctx.set_ground_truth(seq.gt())
+    stride = seq.W + 13
+    for f, fr in enumerate(frames):
+        buf = np.full((seq.H, stride), 77, np.uint8)
+        buf[:, :seq.W] = fr
+        pose = np.zeros(12)
+        st = C.c_int()
+        info = np.zeros(8, np.int32)
+        rc = ctx.lib.vo_process_frame(ctx.h, buf.ctypes.data_as(C.c_void_p), stride, pose.ctypes.data_as(C.c_void_p),
+                                      C.byref(st), info.ctypes.data_as(C.c_void_p))
+        assert rc >= 0 or rc == -10, rc          # VO_ERR_DEGENERATE_E: a row still comes back
+        assert st.value == ref[f][1], f
+        assert np.array_equal(pose.reshape(3, 4), ref[f][0]), f
+        assert np.array_equal(info[:6], ref[f][2][:6]), f
+    ctx.close()
