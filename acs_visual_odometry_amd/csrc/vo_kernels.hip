@@ -4394,7 +4394,9 @@ int select_lds_bytes(int W, int H, int* key_cap)
     const int ntiles = ((W + ST_TW - 1) / ST_TW) * ((H + ST_TH - 1) / ST_TH);
     // the whole CU's LDS: keys staged in LDS are read 4 times (a 64 KB request, which lets other
     // kernels share the CU, measured 2-3 % slower end to end)
-    const int bytes = 160 * 1024 - 2048;               // static __shared__ of k_select < 2 KB
+    // VO_SEL_LDS_KB: a smaller request (the keys then stay in global scratch past its capacity)
+    static const int kb = getenv("VO_SEL_LDS_KB") ? std::max(40, std::min(158, atoi(getenv("VO_SEL_LDS_KB")))) : 158;
+    const int bytes = kb == 158 ? 160 * 1024 - 2048 : kb * 1024;   // static __shared__ of k_select < 2 KB
     if (hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
         return -1;
     const SelLayout L = sel_layout(ntiles, bytes);

@@ -392,7 +392,8 @@ print("KNOB_OK" if ok else "KNOB_DIFF")
                                        ("VO_TRI_BPF=0", 64), ("VO_RREPS=4", 16), ("VO_EXTQ=2", 8), ("VO_XCD=0", 64),
                                        ("VO_EVENT_WAIT=0,VO_FORCE_WAIT_REFUSAL=1,VO_EXTQ=2", 8),
                                        ("VO_ST_FLAT=1", 64), ("VO_ST_FLAT=1,VO_STSEG=8", 64), ("VO_ST_FLAT=1", 8),
-                                       ("VO_ST_PAIR=1", 16), ("VO_ST_PAIR=1", 8)])
+                                       ("VO_ST_PAIR=1", 16), ("VO_ST_PAIR=1", 8),
+                                       ("VO_SEL_LDS_KB=48", 64)])
 def test_process_knobs_match_oracle(leak_case, tmp_path, env, batch):
     """Knobs the library reads once per process (stencil segment height, RANSAC cut and loop,
     triangulation grid, alternating extract queues, XCD placement, the branch-free FLAT stencil),
