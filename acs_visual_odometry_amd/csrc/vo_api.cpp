@@ -40,6 +40,7 @@ struct vo_ctx {
     hipStream_t se[VO_EXT_QUEUES] = {};   // extract batches of the device path (batch j on j % n)
     int B = VO_DEFAULT_BATCH;         // frames per extract batch / pose-pass window
     int fidx = 0;                     // frames enqueued since vo_reset
+    int nq = 1;                       // extract queues of this context (VO_EXTQ at vo_create)
     bool serial = false;              // VO_SERIAL=1: every kernel on one queue, no cross-queue
                                       // waits (for profilers that serialize dispatches: PMC passes)
     bool event_wait = true;           // pose queue waits for extract batches on events (default)
@@ -499,7 +500,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     const int base = c->fidx, end = base + nf, B = c->B;
     hipStream_t s = c->s;
     const bool multi = hs || !(c->serial || host_frame || !img0);   // extract on its own queues
-    static const int nq = getenv("VO_EXTQ") ? std::max(1, std::min(VO_EXT_QUEUES, atoi(getenv("VO_EXTQ")))) : 1;
+    const int nq = c->nq;             // the extract queues vo_create made for this context
     if (multi && c->reset_pending) {
         for (hipStream_t q : c->se)
             if (q) HIPCHK(hipStreamWaitEvent(q, c->ev_reset, 0));
@@ -655,7 +656,22 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         // (the host synchronised: every pass is finalized, so these run from the state, in order)
         for (int k = 0; k < (end - lo + B - 1) / B; ++k) enqueue_pass(c, out, out_base, ev, end, false, host_frame);
     }
-    return ev && ev->err ? ev->err : VO_OK;
+    if (ev && ev->err) return ev->err;
+    // a frame the select's consistency check failed (VO_STATUS_INCONSISTENT): a library defect, loud
+    for (int f = base; f < end; ++f)
+        if (c->out_host[f - out_base].status == VO_STATUS_INCONSISTENT || c->out_host[f - out_base].err) {
+            fprintf(stderr, "[vo_mi355x] frame %d: select consistency check failed (VO_STATUS_INCONSISTENT)\n", f);
+            return VO_ERR_INTERNAL;
+        }
+    return VO_OK;
+}
+
+// the context's device consistency failures (ctr[VO_CTR_ERR]) once its queues are idle
+int dev_errors(vo_ctx* c, uint32_t* n)
+{
+    SYNC_ALL(c);
+    HIPCHK(hipMemcpy(n, c->d.ctr + VO_CTR_ERR, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return VO_OK;
 }
 
 int ensure_out(vo_ctx* c, int n)
@@ -703,6 +719,7 @@ const char* vo_strerror(int code)
     case VO_ERR_CAPACITY: return "capacity exceeded";
     case VO_ERR_STATE: return "invalid state";
     case VO_ERR_IO: return "image could not be read";
+    case VO_ERR_INTERNAL: return "device consistency check failed (library defect)";
     case VO_ERR_DEGENERATE_E: return "Degenerate essential matrix";
     default: return "unknown error";
     }
@@ -792,6 +809,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     c->force_wait_refusal = getenv("VO_FORCE_WAIT_REFUSAL") && atoi(getenv("VO_FORCE_WAIT_REFUSAL")) != 0;
     c->split = VO_EXT_QUEUES >= 2 && (getenv("VO_SPLIT") ? atoi(getenv("VO_SPLIT")) != 0 : VO_SPLIT_DEFAULT != 0);
     c->slack = getenv("VO_SLACK") ? std::max(0, std::min(64, atoi(getenv("VO_SLACK")))) : VO_SLACK_DEFAULT;
+    d.fault_inject = getenv("VO_FAULT_INJECT") && atoi(getenv("VO_FAULT_INJECT")) != 0;   // tests only
     // repair windows hold two work records per frame (k_finalize): at most WB / 2 frames
     d.repair_win = std::max(1, std::min(d.WB / 2, getenv("VO_REPAIR_WIN") ? atoi(getenv("VO_REPAIR_WIN")) : VO_REPAIR_WIN_DEFAULT));
     // queue priorities (VO_PRIO): 0 none; 1 the pose and trajectory queues high (the pose queue is the
@@ -815,8 +833,8 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     // queues (GPU_MAX_HW_QUEUES, 4 by default), and a stream past them shares another's and
     // serialises behind its kernels
     {
-        const int nq = getenv("VO_EXTQ") ? std::max(1, std::min(VO_EXT_QUEUES, atoi(getenv("VO_EXTQ")))) : 1;
-        const int ne = c->split ? 2 : nq;
+        c->nq = getenv("VO_EXTQ") ? std::max(1, std::min(VO_EXT_QUEUES, atoi(getenv("VO_EXTQ")))) : 1;
+        const int ne = c->split ? 2 : c->nq;
         for (int i = 0; i < ne; ++i)
             if (hip_ok(make_stream(&c->se[i], true, p_ext)) != VO_OK) return bail(VO_ERR_HIP);
     }
@@ -1094,6 +1112,7 @@ int vo_extract(vo_ctx* c, const uint8_t* gray, size_t stride, vo_kp* kps, uint64
     const size_t stg = (size_t)c->d.ring + 1;
     HIPCHK(hipMemcpy(&nk, &c->d.ext_n[stg], sizeof(int32_t), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(&status, &c->d.ext_st[stg], sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (status == VO_STATUS_INCONSISTENT) return VO_ERR_INTERNAL;
     if (status != VO_STATUS_OK) return VO_ERR_CAPACITY;
     *n = nk;
     const size_t N = (size_t)c->cfg.max_kpts;
@@ -1477,7 +1496,8 @@ int vo_extract_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
             HIPCHK(hipMemcpy(stt.data(), c->d.ext_st, sizeof(int32_t) * nf, hipMemcpyDeviceToHost));
             for (int z = 0; z < nf; ++z) {
                 const size_t f = (size_t)(f0 + z);
-                if (stt[z] != VO_STATUS_OK) return VO_ERR_CAPACITY;      // top-N boundary overflow
+                if (stt[z] == VO_STATUS_INCONSISTENT) return VO_ERR_INTERNAL;
+                if (stt[z] != VO_STATUS_OK) return VO_ERR_CAPACITY;
                 if (n_kps) n_kps[f] = nk[z];
                 if (kps && nk[z])
                     HIPCHK(hipMemcpyAsync(kps + f * N, c->d.kps + (size_t)z * N, sizeof(vo_kp) * nk[z],
@@ -1492,7 +1512,22 @@ int vo_extract_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
     rc = finish_timing(c, evp);
     if (rc) return rc;
     c->last_frames = nframes;
-    return vo_reset(c);              // the ring no longer holds the trajectory's descriptors
+    uint32_t nerr = 0;               // read before the reset clears the counter
+    if ((rc = dev_errors(c, &nerr)) != VO_OK) return rc;
+    rc = vo_reset(c);                // the ring no longer holds the trajectory's descriptors
+    if (rc) return rc;
+    if (nerr) {
+        fprintf(stderr, "[vo_mi355x] %u frames failed the select consistency check\n", nerr);
+        return VO_ERR_INTERNAL;
+    }
+    return VO_OK;
+}
+
+int vo_device_error_count(vo_ctx* c, uint32_t* count)
+{
+    if (!c || !count) return VO_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    return dev_errors(c, count);
 }
 
 int vo_host_alloc(vo_ctx* c, size_t bytes, void** hptr)

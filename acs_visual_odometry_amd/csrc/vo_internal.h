@@ -110,7 +110,8 @@ inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_T
 #define VO_SYNC_EXT 32         // + 16 * queue: frames extracted since vo_reset by that queue
                                // (its batches complete in order; the pose queue waits on it)
 #define VO_CTR_FIN 64          // fused triangulate + finalize: workgroups arrived (the last one finalizes)
-#define VO_CTR_WORDS 80
+#define VO_CTR_ERR 80          // device consistency failures (k_select / k_select_count: VO_STATUS_INCONSISTENT)
+#define VO_CTR_WORDS 96
 // host-frame streaming (vo_process_frames_host): device ring of VO_HRING slots of B frames
 #define VO_HRING 3
 #define VO_HOST_FIRST_BATCH 16 // host streaming: frames in a chunk's first batch (shorter pipeline fill)
@@ -127,6 +128,9 @@ inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_T
 
 struct VoFrameOut {
     int32_t status, n_kps, n_matches, n_inl, best_k, n_eval, fitted, frame;
+    int32_t err;          // the frame's extract failed the select's consistency check (VO_STATUS_INCONSISTENT;
+                          // reported even where the status is FIRST): the call returns VO_ERR_INTERNAL
+    int32_t pad;
     double pose[12];
 };
 
@@ -217,6 +221,8 @@ struct VoSelCtl {
     int32_t pad;
     uint64_t Tb;                     // smallest selected key of the boundary bin
     int32_t base[VO_SEL_BANDS];      // per band: its first keypoint position in raster order
+    int32_t ktot[VO_SEL_BANDS];      // per band: its keys by the stencil's tile row counts (the
+                                     // consistency check: their sum must equal the histogram's total)
 };
 
 // Everything a kernel needs, passed by value.
@@ -276,7 +282,8 @@ struct VoDev {
     VoState* st;
     int ring;             // ring slots (VO_RING)
     int32_t* ext_n;       // x SLOTS: keypoints extracted into the slot
-    int32_t* ext_st;      // x SLOTS: VO_STATUS_OK, VO_STATUS_OVERFLOW (select capacity), VO_STATUS_MISSING
+    int32_t* ext_st;      // x SLOTS: VO_STATUS_OK, VO_STATUS_OVERFLOW (select capacity), VO_STATUS_MISSING,
+                          // VO_STATUS_INCONSISTENT (the select's consistency check failed; ctr[VO_CTR_ERR] counts them)
     const int32_t* seq_starts;   // sorted frame indices (since vo_reset) where a new sequence begins
     int n_seq_starts;
     int origin;           // in-sequence index of frame 0 of the stream's first sequence (a shard of one sequence)
@@ -295,6 +302,8 @@ struct VoDev {
     unsigned long long* diag_resp;   // [f][tile]  stencil: checksum of the responses a wave computed (even tiles)
     unsigned long long* diag_keys;   // [f][VO_DIAG_KEYS] select: the frame's compact key list (first VO_DIAG_KEYS)
     int diag_f0;                     // frame index of batch frame 0 (enqueue_extract)
+    int fault_inject;                // VO_FAULT_INJECT=1 (tests only): launch_stencil adds N counts to each frame's
+                                     // top histogram bin, so the select's consistency check must fire
 };
 
 // launch wrappers (vo_kernels.hip)

@@ -744,9 +744,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                 // last tile, so every output lane stores; rows past the segment (k >= SEG + 10:
                 // the last 4 rows of the segment's last tile row group) are the next segment's
                 // (the same values, stored by its wave), so their store is dropped by an
-                // out-of-range *voffset* (boffq).  The row offset rides in soffset, which gfx950's
-                // range check does not include (tests/hip/buffer_range_probe.hip): round 3 put
-                // the drop there and those stores landed 1 GiB past the plane.
+                // out-of-range *voffset* (boffq).  gfx950's raw-buffer range check covers voffset +
+                // soffset (tests/hip/buffer_range_probe.hip, tests/test_buffer_range.py: a
+                // straddling store keeps its in-range lanes, nothing lands past num_records), so
+                // round 3's drop through soffset was also safe; voffset keeps the row offset in
+                // soffset a plain scalar operand.
 #if ST_DROP_SOFFSET
                 // round 3's form, kept for the A/B evidence run only (tools/gpu_det.sh): the drop in soffset
                 const int brow = k < SEG + 10 ? (ys - 10 + k) * Wb : 0x40000000;
@@ -1297,22 +1299,23 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
             d.diag_keys[(size_t)(f0 + z) * VO_DIAG_KEYS + g] = g < C ? keys[g] : 0ull;
 #endif
     VO_STAMP(d, 1990, 1);
-    // C
+    // C (the histogram is read for every frame: its total must equal C, the consistency check)
     int b = -1;
     uint64_t Tb = 0ull;
-    bool ovf = false;
+    uint32_t h[4], hs = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { h[q] = hist[4 * tid + q]; hs += h[q]; }
+    uint32_t suf = hs;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t v = __shfl_down(suf, off);
+        if (lane + off < 64) suf += v;
+    }
+    if (lane == 0) s_hs[wave] = suf;
+    __syncthreads();
+    uint32_t htot = 0u;                                 // the histogram's total: the keys the stencil counted
+    for (int w = 0; w < 16; ++w) htot += s_hs[w];
     if (C > N) {
-        uint32_t h[4], hs = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) { h[q] = hist[4 * tid + q]; hs += h[q]; }
-        uint32_t suf = hs;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            uint32_t v = __shfl_down(suf, off);
-            if (lane + off < 64) suf += v;
-        }
-        if (lane == 0) s_hs[wave] = suf;
-        __syncthreads();
         uint32_t above = suf - hs;
         for (int w = wave + 1; w < 16; ++w) above += s_hs[w];
         uint32_t run = above;
@@ -1394,7 +1397,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
         return bin > b || (bin == b && key >= Tb);
     };
     // D
-    const int nround = ovf ? 0 : (C + 1023) / 1024;
+    const int nround = (C + 1023) / 1024;
     for (int r0 = 0; r0 < nround; r0 += 4) {
         uint64_t v[4];
 #pragma unroll
@@ -1500,13 +1503,17 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     // select is the histogram's only reader: leave it zeroed for the next frame's stencil
     for (int i = tid; i < VO_HIST_BINS; i += 1024) hist[i] = 0u;
     if (tid == 0) {
-        // the keypoints emitted: min(C, N) by construction; a frame whose count disagrees (inconsistent
-        // stencil output) is marked OVERFLOW, so no later kernel reads a slot entry nobody wrote
+        // consistency: the histogram counts exactly the keys the tiles hold (round 4's r4j stencil
+        // counted margin-row maxima it never stored, tests/test_select_consistency.py), and the
+        // keypoints emitted are min(C, N).  A failure is a library defect, never a capacity limit:
+        // the frame gets 0 keypoints (no later kernel reads a slot entry nobody wrote), its own
+        // status, and the context's error counter, which the host turns into VO_ERR_INTERNAL
         int sel = 0;
         for (int w = 0; w < 16; ++w) sel += s_wsum[w];
-        const bool bad = !ovf && sel != (C < N ? C : N);
-        d.ext_n[slot] = ovf || bad ? 0 : (C < N ? C : N);
-        d.ext_st[slot] = ovf || bad ? VO_STATUS_OVERFLOW : VO_STATUS_OK;
+        const bool bad = htot != (uint32_t)C || sel != (C < N ? C : N);
+        d.ext_n[slot] = bad ? 0 : (C < N ? C : N);
+        d.ext_st[slot] = bad ? VO_STATUS_INCONSISTENT : VO_STATUS_OK;
+        if (bad) atomicAdd(d.ctr + VO_CTR_ERR, 1u);
     }
 }
 
@@ -1770,7 +1777,10 @@ __global__ void __launch_bounds__(SL_T) k_select_count(VoDev d, int f0, int slot
     for (int off = 32; off > 0; off >>= 1) D += __shfl_xor(D, off);
     if (lane == 0) s_w[wave] = (uint32_t)D;
     __syncthreads();
-    if (tid == 0) st_sc1(&ctl->dcount[w], (int)(s_w[0] + s_w[1] + s_w[2] + s_w[3]));
+    if (tid == 0) {
+        st_sc1(&ctl->dcount[w], (int)(s_w[0] + s_w[1] + s_w[2] + s_w[3]));
+        st_sc1(&ctl->ktot[w], total);                    // the band's keys by the tile row counts
+    }
     if (!arrive_last(&ctl->arrive, VO_SEL_BANDS, &s_last)) return;
     // 3. last workgroup of the frame: the threshold key, each band's first position
     const int nbk = (int)__hip_atomic_load((gu32*)&ctl->nbnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1814,7 +1824,11 @@ __global__ void __launch_bounds__(SL_T) k_select_count(VoDev d, int f0, int slot
             Tb = prefix;                                 // one key matches all 64 bits
         }
     }
-    if (tid < VO_SEL_BANDS) s_cnt[tid] = ld_sc1(&ctl->dcount[tid]);
+    __shared__ int s_ktot[VO_SEL_BANDS];
+    if (tid < VO_SEL_BANDS) {
+        s_cnt[tid] = ld_sc1(&ctl->dcount[tid]);
+        s_ktot[tid] = ld_sc1(&ctl->ktot[tid]);
+    }
     __syncthreads();
     if (b >= 0) {
         const int nbr = (nty + VO_SEL_BANDS - 1) / VO_SEL_BANDS;
@@ -1832,11 +1846,16 @@ __global__ void __launch_bounds__(SL_T) k_select_count(VoDev d, int f0, int slot
         ctl->arrive = 0u;                                // for the next launch (the kernel boundary orders it)
         ctl->nbnd = 0u;
         const int slot = ext_slot(d, f0, z, slot_override);
-        // the keypoints the bands will emit (pre) is min(C, N) by construction; an inconsistent
-        // stencil output marks the frame OVERFLOW, so nothing reads a slot entry nobody wrote
-        const bool bad = pre != (C < N ? C : N);
+        // consistency (as k_select): the keys the tiles hold (the bands' totals) equal the histogram's
+        // total C, and the keypoints the bands will emit (pre) are min(C, N).  A failure gives the
+        // frame 0 keypoints (nothing reads a slot entry nobody wrote), VO_STATUS_INCONSISTENT and a
+        // count in the context's error counter (VO_ERR_INTERNAL on the host)
+        int kt = 0;
+        for (int k = 0; k < VO_SEL_BANDS; ++k) kt += s_ktot[k];
+        const bool bad = kt != C || pre != (C < N ? C : N);
         d.ext_n[slot] = bad ? 0 : (C < N ? C : N);
-        d.ext_st[slot] = bad ? VO_STATUS_OVERFLOW : VO_STATUS_OK;
+        d.ext_st[slot] = bad ? VO_STATUS_INCONSISTENT : VO_STATUS_OK;
+        if (bad) atomicAdd(d.ctr + VO_CTR_ERR, 1u);
     }
     // every band has read the histogram: leave it zeroed for the next frame's stencil
     uint4* hp = reinterpret_cast<uint4*>(hist) + 4 * tid;
@@ -2422,7 +2441,7 @@ __device__ __forceinline__ bool match_header(const VoDev& d, int stage, const Vo
         const int base = seq_base(d, f);
         fl = f - base;
         if (fl == 0) status = VO_STATUS_FIRST;                 // VisualOdometry.cpp:58,64-66
-        else if (es != VO_STATUS_OK) status = es;              // MISSING / OVERFLOW
+        else if (es != VO_STATUS_OK) status = es;              // MISSING / INCONSISTENT
         if (base == 0) fl += d.origin;                         // a sequence shard: the sampler's frame index
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -4042,6 +4061,7 @@ __device__ void finalize_body(const VoDev& d, VoFrameOut* out, int out_base)
         VoFrameOut* o = out + (lo + tid - out_base);
         o->status = s;
         o->n_kps = s == VO_STATUS_MISSING ? 0 : d.ext_n[s_cur[tid]];
+        o->err = d.ext_st[s_cur[tid]] == VO_STATUS_INCONSISTENT;
         o->n_matches = w->M;
         o->n_inl = w->n_inl;
         o->best_k = w->bestk;
@@ -4324,6 +4344,13 @@ static const char* g_names[] = {"stencil", "select", "describe", "match", "ransa
 int kernel_count() { return (int)(sizeof(g_names) / sizeof(g_names[0])); }
 const char* kernel_name(int i) { return g_names[i]; }
 
+// tests only (VO_FAULT_INJECT=1): N counts more in each frame's top histogram bin than the stencil
+// stored keys, so the select's consistency check must fire (tests/test_gpu_parity.py
+// test_select_consistency_failure_is_loud)
+__global__ void k_inject_hist(VoDev d, int nb)
+{
+    if (threadIdx.x == 0 && (int)blockIdx.x < nb) d.hist[(size_t)blockIdx.x * VO_HIST_BINS + VO_HIST_BINS - 1] += (uint32_t)d.N;
+}
 void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int nb, int write_response, hipStream_t s)
 {
     ensure_tables();
@@ -4360,6 +4387,7 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
         }
     }
 #undef ST_LAUNCH
+    if (d.fault_inject && !write_response) hipLaunchKernelGGL(k_inject_hist, dim3(nb), dim3(64), 0, s, d, nb);
 }
 void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s)
 {

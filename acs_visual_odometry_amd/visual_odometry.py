@@ -156,6 +156,13 @@ class Context:
     def reset(self):
         check(self.lib.vo_reset(self.h), "vo_reset")
 
+    def device_errors(self) -> int:
+        """Frames that failed the select's consistency check since creation / the last reset
+        (vo_device_error_count; VO_STATUS_INCONSISTENT).  Expected 0."""
+        n = C.c_uint32()
+        check(self.lib.vo_device_error_count(self.h, C.byref(n)), "vo_device_error_count")
+        return n.value
+
     def ring_slots(self) -> int:
         """Frames whose keypoints, descriptors and trajectory records stay resident (vo_ring_slots)."""
         return check(self.lib.vo_ring_slots(self.h), "vo_ring_slots")

@@ -239,6 +239,7 @@ def _cpu_worker(budget_s: float, keep_rows: bool = False):
     import oracle as O
     frames, W, H, K, gt, N = (_CPU[k] for k in ("frames", "W", "H", "K", "gt", "N"))
     cfg = O.config(W, H, K=K.reshape(9), max_kpts=N)
+    O.stage_reset()
     t0 = time.perf_counter()
     done = 0
     rows = None
@@ -256,7 +257,15 @@ def _cpu_worker(budget_s: float, keep_rows: bool = False):
             rows = pas
         if time.perf_counter() - t0 > budget_s and (rows is not None or not keep_rows):
             break
-    return (done, time.perf_counter() - t0, rows) if keep_rows else (done, time.perf_counter() - t0)
+    dt = time.perf_counter() - t0
+    stages = O.stage_times()
+    return (done, dt, rows, stages) if keep_rows else (done, dt, stages)
+
+
+def stage_ms(stages, frames: int):
+    """The oracle's stage timers (VisualOdometry.cpp:85-178) as ms per frame of the run, and the
+    calls behind each (match / RANSAC / pose run only on frames that reach them)."""
+    return {k: {"ms_per_frame": round(1e3 * sec / max(frames, 1), 4), "calls": n} for k, (sec, n) in stages.items()}
 
 
 def cpu_model() -> str:
@@ -276,10 +285,11 @@ def cpu_baseline(frames, seq, budget_s: float, max_kpts: int, procs: int):
     process touches the GPU.  Returns (the JSON object, the single process's first complete pass
     as [(pose 3x4, status)] -- the oracle's rows of the sequence, checked against the GPU's)."""
     _CPU.update(frames=frames, W=seq.W, H=seq.H, K=seq.K, gt=seq.gt(), N=max_kpts)
-    one_done, one_dt, rows = _cpu_worker(budget_s, keep_rows=True)
+    one_done, one_dt, rows, one_st = _cpu_worker(budget_s, keep_rows=True)
     single = {"value": one_done / one_dt, "unit": "frames/s", "cores": 1, "kind": "port",
               "sample": f"{one_done} frames of the {frames.shape[0]}-frame sequence (restarted at frame 0 after "
-                        f"each pass), oracle/vo_oracle.c in one process, {one_dt:.1f} s"}
+                        f"each pass), oracle/vo_oracle.c in one process, {one_dt:.1f} s",
+              "stages": stage_ms(one_st, one_done)}
     if procs <= 1:
         return dict(single, cpu_model=cpu_model()), rows
     pool = mp.get_context("fork").Pool(procs)
@@ -290,9 +300,11 @@ def cpu_baseline(frames, seq, budget_s: float, max_kpts: int, procs: int):
         pool.join()
     done = sum(r[0] for r in res)
     dt = max(r[1] for r in res)
+    tot = {k: (sum(r[2][k][0] for r in res), sum(r[2][k][1] for r in res)) for k in res[0][2]}
     return {"value": done / dt, "unit": "frames/s", "cores": procs, "kind": "port",
             "sample": f"{procs} processes (one per host core), each running oracle/vo_oracle.c over the same "
                       f"{frames.shape[0]}-frame sequence for ~{budget_s:.0f} s: {done} frames in {dt:.1f} s",
+            "stages": stage_ms(tot, done),
             "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "single_thread": single}, rows
 
 

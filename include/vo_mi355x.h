@@ -37,6 +37,9 @@ extern "C" {
 #define VO_ERR_CAPACITY      (-4)
 #define VO_ERR_STATE         (-5)
 #define VO_ERR_IO            (-6)   /* image file missing or not decodable (cv::imread -> empty) */
+#define VO_ERR_INTERNAL      (-7)   /* a device consistency check failed (VO_STATUS_INCONSISTENT
+                                       frames; vo_device_error_count); results of the call are not
+                                       those of the reference.  Sticky until vo_reset. */
 #define VO_ERR_DEGENERATE_E  (-10)  /* PoseUpdate.hpp:71-73 throws "Degenerate essential matrix" */
 
 /* per-frame status (VisualOdometry.cpp:68-189) */
@@ -46,8 +49,12 @@ extern "C" {
 #define VO_STATUS_FEW_MATCHES   3   /* < 8 matches (:108-115), flipZ*T_curr pushed   */
 #define VO_STATUS_FEW_INLIERS   4   /* < 8 model inliers (:147-153)                  */
 #define VO_STATUS_DEGENERATE    5   /* getPose threw (countNonZero(E) < 5)           */
-#define VO_STATUS_OVERFLOW      6   /* top-N boundary bin exceeded the LDS select buffer */
+#define VO_STATUS_OVERFLOW      6   /* (not produced since round 3: boundary bins of any size are ranked) */
 #define VO_STATUS_STALLED       7   /* frame pipeline: this frame's extract never signalled */
+#define VO_STATUS_INCONSISTENT  8   /* the stencil's histogram disagrees with its keys, or the top-N
+                                       select emitted other than min(C, N) keypoints: the frame is
+                                       treated as having 0 keypoints and the call returns
+                                       VO_ERR_INTERNAL (never expected; a library defect) */
 
 typedef struct vo_ctx vo_ctx;
 
@@ -211,6 +218,11 @@ int  vo_host_free(vo_ctx* ctx, void* hptr);
 int  vo_device_alloc(vo_ctx* ctx, size_t bytes, void** dptr);
 int  vo_device_free(vo_ctx* ctx, void* dptr);
 int  vo_device_upload(vo_ctx* ctx, void* dptr, const void* src, size_t bytes);
+
+/* Device consistency failures since vo_create / the last vo_reset (frames marked
+ * VO_STATUS_INCONSISTENT by the top-N select).  Waits for the context's queues.  The bench and the
+ * GPU tests assert it is 0. */
+int  vo_device_error_count(vo_ctx* ctx, uint32_t* count);
 
 /* Reset the trajectory state (frame counter, T_curr, model, prev descriptors). */
 int  vo_reset(vo_ctx* ctx);

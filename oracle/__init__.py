@@ -77,6 +77,10 @@ def lib():
         L.voo_vo_create.restype = P
         L.voo_vo_create.argtypes = [C.POINTER(VooConfig)]
         L.voo_vo_destroy.argtypes = [P]
+        L.voo_stage_reset.argtypes = []
+        L.voo_stage_reset.restype = None
+        L.voo_stage_times.argtypes = [P, P]
+        L.voo_stage_times.restype = None
         L.voo_vo_process.argtypes = [P, P, C.c_size_t, P, C.c_int, P, P, P]
         _lib = L
     return _lib
@@ -275,3 +279,18 @@ class VO:
 
     def __del__(self):
         self.close()
+
+
+STAGES = ("blur", "response", "nms", "describe", "match", "ransac", "pose")
+
+
+def stage_reset():
+    lib().voo_stage_reset()
+
+
+def stage_times():
+    """{stage: (seconds, calls)} since the last stage_reset (the oracle's stage timers)."""
+    sec = np.zeros(len(STAGES))
+    n = np.zeros(len(STAGES), np.int64)
+    lib().voo_stage_times(_p(sec), _p(n))
+    return {k: (float(sec[i]), int(n[i])) for i, k in enumerate(STAGES)}

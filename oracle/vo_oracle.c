@@ -14,6 +14,27 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+
+/* Per-stage CPU time of the trajectory loop, the reference's stage timers (VisualOdometry.cpp:85-178:
+ * "Feature extraction", "Descriptor matching", "RANSAC", "Pose estimation" around the calls, with
+ * get_current_time_fenced, corner_detection_parallel_GPU.h:15-22), extraction split further into its
+ * steps (feature_extraction_parallel_GPU.cpp:200-294).  Process-wide (the bench's CPU leg runs one
+ * process per core); voo_stage_times reads and voo_stage_reset clears them. */
+static double g_stage_s[VOO_NSTAGES];
+static int64_t g_stage_n[VOO_NSTAGES];
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+#define STAGE(k, stmt) do { double _t0 = now_s(); stmt; g_stage_s[k] += now_s() - _t0; g_stage_n[k] += 1; } while (0)
+void voo_stage_reset(void) { memset(g_stage_s, 0, sizeof(g_stage_s)); memset(g_stage_n, 0, sizeof(g_stage_n)); }
+void voo_stage_times(double* seconds, int64_t* calls)
+{
+    for (int k = 0; k < VOO_NSTAGES; ++k) { seconds[k] = g_stage_s[k]; calls[k] = g_stage_n[k]; }
+}
 
 /* ========================================================================== */
 /* deterministic math                                                          */
@@ -777,10 +798,11 @@ int voo_extract(const voo_config* cf, const uint8_t* gray, size_t stride, int32_
     int W = cf->width, H = cf->height;
     uint8_t* bl = (uint8_t*)malloc((size_t)W * H);
     float* R = (float*)malloc(sizeof(float) * W * H);
-    voo_blur7(gray, stride, W, H, bl);
-    voo_response(bl, W, H, cf->resp_thr, R);
-    int n = voo_nms_topn(R, W, H, cf->nms_k, cf->max_kpts, cf->border_row, cf->border_col, kps);
-    voo_describe(bl, W, H, kps, n, desc, NULL);
+    int n;
+    STAGE(VOO_STAGE_BLUR, voo_blur7(gray, stride, W, H, bl));
+    STAGE(VOO_STAGE_RESPONSE, voo_response(bl, W, H, cf->resp_thr, R));
+    STAGE(VOO_STAGE_NMS, n = voo_nms_topn(R, W, H, cf->nms_k, cf->max_kpts, cf->border_row, cf->border_col, kps));
+    STAGE(VOO_STAGE_DESCRIBE, voo_describe(bl, W, H, kps, n, desc, NULL));
     if (blurred_out) memcpy(blurred_out, bl, (size_t)W * H);
     free(bl); free(R);
     return n;
@@ -1341,7 +1363,8 @@ int voo_vo_process(voo_vo* s, const uint8_t* gray, size_t stride, const double* 
     if (!gray) { push_pose(s->Tcurr, 0, pose_out); *status = VO_STATUS_MISSING; return 0; }  /* :77-82 */
     int n = voo_extract(c, gray, stride, s->kps_cur, s->desc_cur, NULL);
     int32_t* pairs = (int32_t*)malloc(sizeof(int32_t) * 2 * (s->n_prev > 0 ? s->n_prev : 1));
-    int m = voo_match(s->desc_prev, s->n_prev, s->desc_cur, n, c->match_bits, c->ratio, pairs);
+    int m;
+    STAGE(VOO_STAGE_MATCH, m = voo_match(s->desc_prev, s->n_prev, s->desc_cur, n, c->match_bits, c->ratio, pairs));
     if (info) { info[0] = n; info[1] = m; }
     if (m < 8) {                                                  /* :108-115 */
         free(pairs);
@@ -1356,8 +1379,8 @@ int voo_vo_process(voo_vo* s, const uint8_t* gray, size_t stride, const double* 
     free(pairs);
     voo_ransac_result rr;
     int32_t* inl = (int32_t*)malloc(sizeof(int32_t) * m);
-    voo_ransac(pts, m, c->ransac_p, c->sampson_thr, c->ransac_chunk_threads, voo_frame_seed(c->seed, fi),
-               NULL, inl, &rr);
+    STAGE(VOO_STAGE_RANSAC, voo_ransac(pts, m, c->ransac_p, c->sampson_thr, c->ransac_chunk_threads,
+                                        voo_frame_seed(c->seed, fi), NULL, inl, &rr));
     if (info) { info[2] = rr.n_inl; info[3] = rr.best_k; info[4] = rr.n_evaluated; info[5] = rr.fitted; }
     if (rr.fitted) {                                              /* model state leak, quirk 9 */
         memcpy(s->model_F, rr.F, sizeof(rr.F));
@@ -1378,7 +1401,8 @@ int voo_vo_process(voo_vo* s, const uint8_t* gray, size_t stride, const double* 
     { uint64_t* t = s->desc_prev; s->desc_prev = s->desc_cur; s->desc_cur = t; }
     s->n_prev = n;
     double R[9], t[3];
-    int rc = voo_pose(s->model_F, c->K, s->model_p1, s->model_p2, s->model_n, scale, R, t, NULL);
+    int rc;
+    STAGE(VOO_STAGE_POSE, rc = voo_pose(s->model_F, c->K, s->model_p1, s->model_p2, s->model_n, scale, R, t, NULL));
     if (rc != VOO_OK) { push_pose(s->Tcurr, 1, pose_out); *status = VO_STATUS_DEGENERATE; return rc; }
     double Trel[16] = {R[0], R[1], R[2], t[0], R[3], R[4], R[5], t[1], R[6], R[7], R[8], t[2], 0, 0, 0, 1};
     mm4(s->Tcurr, Trel, s->Tcurr);                                /* :180 */

@@ -115,6 +115,11 @@ int  voo_pose(const double F[9], const double K[9], const float* p1, const float
 typedef struct voo_vo voo_vo;
 voo_vo* voo_vo_create(const voo_config* c);
 void voo_vo_destroy(voo_vo* s);
+/* per-stage CPU seconds and calls since the last reset (VisualOdometry.cpp:85-178 stage timers) */
+enum { VOO_STAGE_BLUR, VOO_STAGE_RESPONSE, VOO_STAGE_NMS, VOO_STAGE_DESCRIBE, VOO_STAGE_MATCH, VOO_STAGE_RANSAC,
+       VOO_STAGE_POSE, VOO_NSTAGES };
+void voo_stage_reset(void);
+void voo_stage_times(double* seconds, int64_t* calls);
 /* gray == NULL: missing image.  gt: 12 doubles (KITTI row) per frame for the whole
  * sequence (gt_n rows) or NULL (scale 1).  pose_out: 12 doubles (3x4 row-major).
  * info_out (optional, 8 ints): n_kpts, n_matches, n_inliers, best_k, n_evaluated, fitted, 0, 0 */

@@ -97,3 +97,26 @@ def test_matcher_forms_match_oracle(cases):
     bad = [ln for ln in lines if ln.startswith("MATCH_DIFF")]
     assert not bad, bad
     assert len(lines) == 2 * 7 + 3
+
+
+def test_k_match_equals_reference_library():
+    """k_match (stage API, 32 tests) against the REFERENCE's own matchCustomBinaryDescriptorsThreadPool
+    (feature_matching_parallel.cpp:39-113) compiled from /root/reference into oracle/_ref/libref_matcher.so
+    (oracle/ref_matcher.mk): the same pairs, on the factory images and the bench's KITTI-shape frames.
+    The library travels with the tree; skipped where it was never built."""
+    from acs_visual_odometry_amd import Context
+    from test_ref_matcher import LIB, ref_match
+    import ctypes as C
+    if not os.path.exists(LIB):
+        pytest.skip("oracle/_ref/libref_matcher.so not built")
+    L = C.CDLL(LIB)
+    L.ref_match.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_float, C.c_void_p, C.c_int]
+    L.ref_match.restype = C.c_int
+    s = SceneSequence(nframes=3, step=1.0)
+    cfg = O.config(s.W, s.H, K=s.K.reshape(9))
+    desc = [O.extract(f, cfg)[1] for f in s.frames()]
+    ctx = Context(s.W, s.H, K=s.K)
+    for a, b in zip(desc[:-1], desc[1:]):
+        for T in (1, 8):
+            assert np.array_equal(ctx.match(a, b), ref_match(L, a, b, T))
+    ctx.close()

@@ -189,6 +189,44 @@ def test_extract_sizes_bit_exact(W, H, N, kind, sel1, monkeypatch):
     assert np.array_equal(d, dr), "descriptor bits differ"
 
 
+@pytest.mark.parametrize("sel1", ["1", "0"])
+def test_select_consistency_failure_is_loud(sel1, scene, monkeypatch):
+    """An inconsistent stencil output (round 4's r4j: histogram counts without keys,
+    tests/test_select_consistency.py) is reported, not hidden as OVERFLOW: VO_FAULT_INJECT=1 adds N
+    counts to every frame's top histogram bin after the stencil, and each entry point returns
+    VO_ERR_INTERNAL, marks the frames VO_STATUS_INCONSISTENT and counts them in the context's error
+    counter -- through the single-workgroup select (VO_SEL1=1, the batched KITTI path) and the banded
+    one (VO_SEL1=0; the per-frame call always).  A context without the injection counts 0."""
+    seq, frames = scene
+    monkeypatch.setenv("VO_SEL1", sel1)
+    monkeypatch.setenv("VO_FAULT_INJECT", "1")
+    ctx = Context(seq.W, seq.H, K=seq.K)
+    monkeypatch.delenv("VO_FAULT_INJECT")
+    with pytest.raises(RuntimeError, match=r"consistency.*\(-7\)"):
+        ctx.extract(frames[0])
+    assert ctx.device_errors() == 1
+    dfr = ctx.device_frames(frames[:4])
+    with pytest.raises(RuntimeError, match=r"consistency.*\(-7\)"):
+        ctx.process_frames_device(dfr)
+    assert ctx.device_errors() >= 4
+    with pytest.raises(RuntimeError, match=r"consistency.*\(-7\)"):
+        ctx.extract_frames_device(dfr)
+    ctx.reset()
+    assert ctx.device_errors() == 0
+    with pytest.raises(RuntimeError, match=r"consistency.*\(-7\)"):
+        ctx.process_frame(frames[1])
+    dfr.free()
+    ctx.close()
+    good = Context(seq.W, seq.H, K=seq.K)
+    good.set_ground_truth(seq.gt())
+    dfr = good.device_frames(frames)
+    _, st, _ = good.process_frames_device(dfr)
+    assert 8 not in set(np.asarray(st).tolist())
+    assert good.device_errors() == 0
+    dfr.free()
+    good.close()
+
+
 @pytest.mark.parametrize("bits", [32, 512])
 def test_match_bit_exact(bits, scene):
     seq, frames = scene
