@@ -410,6 +410,27 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 static_assert(ST_SW + 2 * ST_HALO <= 128, "strip + halo within one wave of column pairs");
 static_assert(VO_STRIP_XL + ST_TW - 1 == 63, "tile A in lanes 0..31, tile B in lanes 32..63");
 
+#ifndef ST_NOPK
+#define ST_NOPK 1                      // k_stencil without packed FP32 (every v_pk_*_f32 split in two v_*_f32):
+                                       // the instruction class round 4 saw perturbed next to its MFMA matcher
+                                       // (DESIGN.md section 3); four alternating pairs, round 5 (gpurun_out
+                                       // r5c_ab): 289.6k with packed FP32, 291.1k without -- within noise, so
+                                       // the stencil ships without it (0: the packed form, ST_XSUB_ASM)
+#endif
+// ST_NOPK: the stencil and every helper it inlines (to the end of k_stencil) compiled without packed
+// FP32 -- the whole region, so the kernel's callees keep a subset of its target features and inline
+#if ST_NOPK && defined(__HIP_DEVICE_COMPILE__)
+#pragma clang attribute push (__attribute__((target("no-packed-fp32-ops"))), apply_to = function)
+#endif
+// bit casts, popcount and the histogram atomic as the stencil's own inline helpers (the HIP header's
+// are defined outside the ST_NOPK region, so a no-packed-FP32 stencil could not inline them)
+__device__ __forceinline__ int st_popc(unsigned long long v) { return __builtin_popcountll(v); }
+__device__ __forceinline__ int st_f2i(float v) { return __builtin_bit_cast(int, v); }
+__device__ __forceinline__ float st_i2f(int v) { return __builtin_bit_cast(float, v); }
+__device__ __forceinline__ unsigned st_atomic_add(uint32_t* p, uint32_t v)
+{
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ int refl101(int i, int n)
 {
     if (n == 1) return 0;
@@ -508,12 +529,13 @@ typedef float st_f2 __attribute__((ext_vector_type(2)));
 typedef unsigned short st_w2 __attribute__((ext_vector_type(2)));
 // (the box sums add across lanes with hand-written v_add_f32_dpp in k_stencil: the build disables
 // LLVM's DPP combine -- it mis-folded a wave shift into v_subrev_u32_dpp on gfx950, Makefile)
-__device__ __forceinline__ float from_leftf(float v) { return __int_as_float(from_left(__float_as_int(v))); }
-__device__ __forceinline__ float from_rightf(float v) { return __int_as_float(from_right(__float_as_int(v))); }
+__device__ __forceinline__ float from_leftf(float v) { return st_i2f(from_left(st_f2i(v))); }
+__device__ __forceinline__ float from_rightf(float v) { return st_i2f(from_right(st_f2i(v))); }
 // (a.x - b.y, b.x - a.y) in one v_pk_add_f32: cross halves through op_sel, signs through neg
 #ifndef ST_XSUB_ASM
-#define ST_XSUB_ASM 1
+#define ST_XSUB_ASM (!ST_NOPK)         // (the asm form is a v_pk_add_f32)
 #endif
+
 __device__ __forceinline__ st_f2 st_xsub(st_f2 a, st_f2 b)
 {
 #if ST_XSUB_ASM
@@ -538,8 +560,8 @@ __device__ __forceinline__ st_f2 st_response2(st_f2 jx2, st_f2 jy2, st_f2 sxy)
     const st_f2 tr = jx2 + jy2;
     const st_f2 x = st_fma(det, st_f2{-4.0f, -4.0f}, tr * tr);
     const st_f2 s = {__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
-    const st_f2 sm = {__int_as_float(__float_as_int(s.x) - 1), __int_as_float(__float_as_int(s.y) - 1)};
-    const st_f2 sp = {__int_as_float(__float_as_int(s.x) + 1), __int_as_float(__float_as_int(s.y) + 1)};
+    const st_f2 sm = {st_i2f(st_f2i(s.x) - 1), st_i2f(st_f2i(s.y) - 1)};
+    const st_f2 sp = {st_i2f(st_f2i(s.x) + 1), st_i2f(st_f2i(s.y) + 1)};
     const st_f2 rm = st_fma(-sm, s, x), rp = st_fma(-sp, s, x);
     st_f2 r;
 #if ST_RSEL_ASM
@@ -643,8 +665,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
     // wave shifts: pinned against sinking into a masked arm, except in the FLAT form (no masked arm)
     auto shl = [](int v) { if constexpr (FLAT && !ST_SHIFT_BPERM) return __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true); else return from_right(v); };
     auto shr = [](int v) { if constexpr (FLAT && !ST_SHIFT_BPERM) return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true); else return from_left(v); };
-    auto shrf = [&](float v) { return __int_as_float(shr(__float_as_int(v))); };
-    auto shlf = [&](float v) { return __int_as_float(shl(__float_as_int(v))); };
+    auto shrf = [&](float v) { return st_i2f(shr(st_f2i(v))); };
+    auto shlf = [&](float v) { return st_i2f(shl(st_f2i(v))); };
 
     const int xs = sxi * ST_SW, ys = seg * SEG;
     const int c0 = xs - VO_STRIP_XL + 2 * lane;                // this lane's columns: c0, c0 + 1
@@ -846,15 +868,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             const int yr = ys - 13 + k;
             const bool rrow = (unsigned)(yr - 2) <= (unsigned)(H - 5);
             const st_f2 rv = st_response2(SX, SY, SS);
-            const int o0 = ((rv.x > thr0) & rrow) ? __float_as_int(rv.x) : 0;
-            const int o1 = ((rv.y > thr1) & rrow) ? __float_as_int(rv.y) : 0;
+            const int o0 = ((rv.x > thr0) & rrow) ? st_f2i(rv.x) : 0;
+            const int o1 = ((rv.y > thr1) & rrow) ? st_f2i(rv.y) : 0;
             if constexpr (DBG) {
                 if (write_response && yr >= ys && yr < min(ys + SEG, H)) {
                     float* R = d.response + (size_t)yr * W;
                     const float w0 = write_response == 2 ? SX.x : write_response == 3 ? SY.x
-                                   : write_response == 4 ? SS.x : __int_as_float(o0);
+                                   : write_response == 4 ? SS.x : st_i2f(o0);
                     const float w1 = write_response == 2 ? SX.y : write_response == 3 ? SY.y
-                                   : write_response == 4 ? SS.y : __int_as_float(o1);
+                                   : write_response == 4 ? SS.y : st_i2f(o1);
                     if (outc(c0) && c0 >= 0 && c0 < W) R[c0] = w0;
                     if (outc(c0 + 1) && c0 + 1 < W) R[c0 + 1] = w1;
                 }
@@ -892,10 +914,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             const unsigned long long b0 = lt_mask(nb0, rm0) & rokm, b1 = lt_mask(nb1, rm1) & rokm;
             // (rok: the NMS rows; the general form reaches the stores only through b0 | b1, which rok masks)
             const bool mx0 = rok && nb0 < rm0, mx1 = rok && nb1 < rm1;
-            const int cA = __popcll(b0 & mA) + __popcll(b1 & mA);
-            const int cB = __popcll(b0 & mB) + __popcll(b1 & mB);
-            asm("v_writelane_b32 %0, %1, %2" : "+v"(trows) : "s"(cA), "n"(r));
-            asm("v_writelane_b32 %0, %1, %2" : "+v"(trows) : "s"(cB), "n"(16 + r));
+            const int cA = st_popc(b0 & mA) + st_popc(b1 & mA);
+            const int cB = st_popc(b0 & mB) + st_popc(b1 & mB);
+            // (readfirstlane: the counts are wave-uniform SGPR values already -- a no-op -- but the
+            // ST_NOPK build's compiler keeps them in VGPRs without it)
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(trows) : "s"(__builtin_amdgcn_readfirstlane(cA)), "n"(r));
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(trows) : "s"(__builtin_amdgcn_readfirstlane(cB)), "n"(16 + r));
             if constexpr (FLAT) {
                 const uint32_t pos0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32),
                                       __builtin_amdgcn_mbcnt_lo((uint32_t)b1,
@@ -942,7 +966,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                     tk[base] = ((uint64_t)(uint32_t)rm0 << 32) | key_lo;
 #if !(ST_KEYS_LDS && ST_HIST_FLUSH)
                     const uint32_t bin = min(((uint32_t)rm0 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1));
-                    atomicAdd(&hist[bin], 1u);
+                    st_atomic_add(&hist[bin], 1u);
 #endif
 #if ST_DIAG & 2
                     dck += mix64((((uint64_t)(uint32_t)rm0 << 32) | key_lo) ^ ((uint64_t)base << 48));
@@ -952,7 +976,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                     tk[base + (mx0 ? 1u : 0u)] = ((uint64_t)(uint32_t)rm1 << 32) | (key_lo + 1u);
 #if !(ST_KEYS_LDS && ST_HIST_FLUSH)
                     const uint32_t bin = min(((uint32_t)rm1 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1));
-                    atomicAdd(&hist[bin], 1u);
+                    st_atomic_add(&hist[bin], 1u);
 #endif
 #if ST_DIAG & 2
                     dck += mix64((((uint64_t)(uint32_t)rm1 << 32) | (key_lo + 1u)) ^ ((uint64_t)(base + (mx0 ? 1u : 0u)) << 48));
@@ -1033,12 +1057,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             for (int j = lane; j < toffA; j += 64) {
                 const uint64_t kv = wkeys[j];
                 dst[j] = kv;
-                if constexpr (hf) atomicAdd(&hist[min(((uint32_t)(kv >> 32) - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1))], 1u);
+                if constexpr (hf) st_atomic_add(&hist[min(((uint32_t)(kv >> 32) - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1))], 1u);
             }
             for (int j = lane; j < toffB; j += 64) {
                 const uint64_t kv = wkeys[ST_TCAP + j];
                 dst[ST_TCAP + j] = kv;
-                if constexpr (hf) atomicAdd(&hist[min(((uint32_t)(kv >> 32) - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1))], 1u);
+                if constexpr (hf) st_atomic_add(&hist[min(((uint32_t)(kv >> 32) - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1))], 1u);
             }
         }
 #endif
@@ -1076,6 +1100,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
 #endif
     }
 }
+
+#if ST_NOPK && defined(__HIP_DEVICE_COMPILE__)
+#pragma clang attribute pop
+#endif
 
 // ---------------------------------------------------------------------------
 // select: exact top-N of the candidate keys + raster sort (1 workgroup of 1024)

@@ -564,7 +564,11 @@ def main():
     # -- host-side preparation, before anything touches the GPU (forked workers) --
     from acs_visual_odometry_amd.synth import SceneSequence, render_sequences
     workers = max(1, min(16, (os.cpu_count() or 4) // max(world, 1)))
-    specs = [(W, H, F, s, args.motion) for s in my_seqs]
+    # N > 1 with weak scaling: config 5 literally as well (8 sequences in all, sequence s on GPU s mod G),
+    # timed after the weak-scaling line's run and reported beside it (config5_strong)
+    c5_seqs = rank_sequences(8, rank, world, "strong") if world > 1 and args.scaling == "weak" else []
+    specs = [(W, H, F, s, args.motion) for s in my_seqs] + [(W, H, F, s, args.motion) for s in c5_seqs
+                                                            if s not in my_seqs]
     extra_specs = {}
     if lead and not args.no_variants:
         extra_specs = {"motion_0.05": (W, H, F, 0, 0.05), "low_inlier_0.12": (W, H, F, 0, 0.12),
@@ -572,7 +576,8 @@ def main():
     rendered = render_sequences(specs + list(extra_specs.values()), workers)
     seqs = {sp[3]: (SceneSequence(W, H, nframes=F, seq=sp[3], step=args.motion), rendered[i])
             for i, sp in enumerate(specs)}
-    extra = {tag: (rendered[len(specs) + i], SceneSequence(sp[0], sp[1], nframes=sp[2], seq=sp[3], step=sp[4]))
+    n_mine = len(specs)
+    extra = {tag: (rendered[n_mine + i], SceneSequence(sp[0], sp[1], nframes=sp[2], seq=sp[3], step=sp[4]))
              for i, (tag, sp) in enumerate(extra_specs.items())}
     cpu, oracle_rows = None, None
     if lead and not args.no_cpu:
@@ -667,6 +672,36 @@ def main():
                          all(np.array_equal(last[s0][0][f], oracle_rows[f][0]) and int(last[s0][1][f]) == oracle_rows[f][1]
                              for f in range(F)))
 
+    # config 5 literally (N > 1, weak-scaling line): 8 sequences in all, sequence s on GPU s mod G, each
+    # rank's sequences as one stream; the same barrier / max-over-ranks timing
+    c5 = None
+    if c5_seqs:
+        d5 = ctx.device_frames(np.concatenate([seqs[s][1] for s in c5_seqs]))
+        gt5 = np.concatenate([seqs[s][0].gt() for s in c5_seqs])
+        st5 = [F * i for i in range(1, len(c5_seqs))]
+
+        def step5():
+            ctx.reset()
+            ctx.set_ground_truth(gt5)
+            ctx.set_sequence_starts(st5)
+            return ctx.process_frames_device(d5)
+
+        for _ in range(max(args.warmup, 1)):
+            step5()
+        barrier()
+        t5 = time.perf_counter()
+        for _ in range(args.steps):
+            step5()
+        t5 = time.perf_counter() - t5
+        barrier()
+        t5, v5 = aggregate(dist, t5, args.steps * F * len(c5_seqs), world, backend=args.backend, local=dev)
+        c5 = {"value": v5, "unit": "frames/s", "ms_per_step": t5 / args.steps * 1e3, "sequences": 8,
+              "sequences_per_gpu": [len(rank_sequences(8, r, world, "strong")) for r in range(world)],
+              "scaling": "strong", "parallelism": f"config 5: sequence s of 0..7 on GPU s mod {world}"}
+        d5.free()
+        ctx.set_sequence_starts([])
+
+    dev_errors = ctx.device_errors()                 # select consistency failures (expected 0)
     variants = None
     if lead and not args.no_variants:
         s0 = my_seqs[0]
@@ -719,6 +754,7 @@ def main():
                               "frac": path_bytes * value / world / 1e9 / HBM_PEAK_GBS},
             "kernels": kern,
             "determinism": {"timed_rows_equal_warmup_rows": bool(repeat_equal),
+                            "device_errors": dev_errors,
                             "gathered_rows_equal_separate_runs": gather_ok,
                             "gather": "all_gather of raw int64 bits (stream rows and separate-run rows of every "
                                       "sequence)",
@@ -729,6 +765,8 @@ def main():
             "variants": variants,
             "cpu_baseline": cpu,
         }
+        if c5 is not None:
+            line["config5_strong"] = c5
         if args.breakdown:
             for k in KERNELS:
                 if k in ks:

@@ -55,3 +55,12 @@ def test_library_has_no_wait_state_violation(tmp_path):
     assert len(stencils) >= 6 and any("k_describe" in k for k in ks) and any("k_ransac_hyp" in k for k in ks)
     viol = [str(v) for k, lines in ks.items() for v in H.check_stream(k, lines)]
     assert not viol, "\n".join(viol[:20])
+
+
+def test_stencil_has_no_packed_fp32(tmp_path):
+    """Round 4 saw packed-FP32 results in k_stencil's upper half-wave perturbed while its (since deleted)
+    MFMA matcher ran; the stencil now ships without packed FP32 (ST_NOPK, measured within noise:
+    DESIGN.md section 3), so no v_pk_*_f32 is left in any k_stencil instance."""
+    ks = H.disassemble(LIB, str(tmp_path))
+    pk = [(k, l) for k, lines in ks.items() if "k_stencil" in k for l in lines if re.match(r"v_pk_\w+_f32", l)]
+    assert not pk, pk[:5]
