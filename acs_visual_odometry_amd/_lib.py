@@ -13,6 +13,8 @@ LIB_PATH = os.environ.get("VO_LIB_PATH") or os.path.join(_HERE, "libvo_mi355x.so
 VO_OK = 0
 VO_ERR_IO = -6
 VO_ERR_INTERNAL = -7
+VO_RNG_SPLITMIX = 0
+VO_RNG_MT19937 = 1
 VO_ERR_DEGENERATE_E = -10
 STATUS = {0: "OK", 1: "FIRST", 2: "MISSING", 3: "FEW_MATCHES", 4: "FEW_INLIERS", 5: "DEGENERATE",
           6: "OVERFLOW", 7: "STALLED", 8: "INCONSISTENT"}
@@ -22,7 +24,7 @@ EXPORTS = [
     "vo_config_default", "vo_create", "vo_destroy", "vo_strerror", "vo_abi_version", "vo_extract",
     "vo_response", "vo_match", "vo_ransac_F", "vo_ransac_run", "vo_fit_F", "vo_pose", "vo_set_ground_truth", "vo_set_sequence_starts", "vo_set_frame_origin",
     "vo_trajectory_state", "vo_ring_slots", "vo_rechain", "vo_process_frame",
-    "vo_process_frames_device", "vo_process_frames_host", "vo_extract_frames_device", "vo_host_alloc", "vo_host_free", "vo_imread_gray", "vo_device_alloc", "vo_device_free", "vo_device_upload", "vo_device_error_count", "vo_reset",
+    "vo_process_frames_device", "vo_process_frames_host", "vo_extract_frames_device", "vo_host_alloc", "vo_host_free", "vo_imread_gray", "vo_device_alloc", "vo_device_free", "vo_device_upload", "vo_device_error_count", "vo_reference_samples", "vo_reset",
     "vo_last_kernel_times", "vo_last_kernel_stats", "vo_enable_kernel_timing", "vo_kernel_form",
     "vo_unpack_descriptor",
 ]
@@ -34,7 +36,7 @@ class VoConfig(C.Structure):
         ("resp_thr", C.c_float), ("border_row", C.c_int), ("border_col", C.c_int),
         ("ratio", C.c_float), ("match_bits", C.c_int), ("ransac_p", C.c_double),
         ("sampson_thr", C.c_double), ("ransac_chunk_threads", C.c_int), ("seed", C.c_uint64),
-        ("K", C.c_double * 9), ("device", C.c_int), ("frame_batch", C.c_int),
+        ("K", C.c_double * 9), ("device", C.c_int), ("frame_batch", C.c_int), ("rng_mode", C.c_int),
     ]
 
 
@@ -84,6 +86,7 @@ def load():
     L.vo_device_free.argtypes = [P, P]
     L.vo_device_upload.argtypes = [P, P, P, C.c_size_t]
     L.vo_device_error_count.argtypes = [P, C.POINTER(C.c_uint32)]
+    L.vo_reference_samples.argtypes = [C.c_uint32, I, I, P]
     L.vo_reset.argtypes = [P]
     L.vo_last_kernel_times.argtypes = [P, C.POINTER(C.c_char_p), C.POINTER(C.c_float), I]
     L.vo_last_kernel_stats.argtypes = [P, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.POINTER(C.c_float), I]

@@ -24,8 +24,11 @@
 #include <climits>
 #include <map>
 #include <memory>
+#include <iterator>
 #include <mutex>
 #include <new>
+#include <numeric>
+#include <random>
 #include <utility>
 #include <vector>
 
@@ -41,6 +44,7 @@ struct vo_ctx {
     int B = VO_DEFAULT_BATCH;         // frames per extract batch / pose-pass window
     int fidx = 0;                     // frames enqueued since vo_reset
     int nq = 1;                       // extract queues of this context (VO_EXTQ at vo_create)
+    int mt_err = 0;                   // VO_RNG_MT19937: a failed sample upload of a pass (returned by run_chunk)
     bool serial = false;              // VO_SERIAL=1: every kernel on one queue, no cross-queue
                                       // waits (for profilers that serialize dispatches: PMC passes)
     bool event_wait = true;           // pose queue waits for extract batches on events (default)
@@ -76,6 +80,8 @@ struct vo_ctx {
     VoFrameOut* out_dev = nullptr;
     int out_cap = 0;
     VoFrameOut* out_host = nullptr;   // pinned
+    VoFrameOut* out_host_dev = nullptr;   // out_host as the device addresses it (the per-frame call's kernels
+                                          // write its row there directly: no copy kernel behind the pass)
     int32_t* lo_host = nullptr;       // pinned: VoState::lo after a chunk
     hipEvent_t ev_reset = nullptr;    // recorded on s by vo_reset; the extract queue waits on it
     bool reset_pending = false;
@@ -403,6 +409,44 @@ int enqueue_h2d(vo_ctx* c, const HostSrc& hs, int f0, int nb, int j, uint8_t** d
 
 // the window buffers of pass p: set p & 1 (a pipelined pass's match and RANSAC write one set while
 // the previous pass's refit, triangulation and finalize read the other)
+// The reference's sampler (ransac.cpp:137,142): rng = std::mt19937(seed32) once, then per hypothesis
+// k the elements std::sample(data.begin(), data.end(), std::back_inserter(sample), sampleSize, rng)
+// picks, as indices into data (selection sampling keeps data order).  The population is an index
+// vector with random-access iterators like the reference's vector<pair<Point, Point>>, and the size
+// argument an int like its `int sampleSize = 8`, so libstdc++ takes the same code path and draws the
+// same numbers (tests/test_reference_sampler.py compiles the reference's own expression against it).
+void mt_samples(uint32_t seed32, int m, int nhyp, int32_t* out)
+{
+    std::mt19937 rng(seed32);
+    std::vector<int32_t> idx((size_t)m);
+    std::iota(idx.begin(), idx.end(), 0);
+    const int sampleSize = 8;
+    std::vector<int32_t> smp;
+    smp.reserve(8);
+    for (int k = 0; k < nhyp; ++k) {
+        smp.clear();
+        std::sample(idx.begin(), idx.end(), std::back_inserter(smp), sampleSize, rng);
+        for (int i = 0; i < 8; ++i) out[8 * (size_t)k + i] = i < (int)smp.size() ? smp[(size_t)i] : 0;
+    }
+}
+
+// VO_RNG_MT19937: the hypotheses' samples of records [0, nrec) of a pose window, once k_match has
+// written the records (status, M, frame seed) -- a host round trip on the pose queue
+int upload_mt_samples(vo_ctx* c, const VoDev& d, int nrec, hipStream_t s)
+{
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<VoWork> w((size_t)nrec);
+    HIPCHK(hipMemcpy(w.data(), d.work, sizeof(VoWork) * (size_t)nrec, hipMemcpyDeviceToHost));
+    std::vector<int32_t> tab((size_t)d.max_hyp * 8);
+    for (int r = 0; r < nrec; ++r) {
+        if (w[(size_t)r].status != VO_STATUS_OK || w[(size_t)r].M < 8) continue;
+        mt_samples((uint32_t)w[(size_t)r].frame_seed, w[(size_t)r].M, d.max_hyp, tab.data());
+        HIPCHK(hipMemcpy(d.samples + (size_t)r * d.max_hyp * 8, tab.data(), tab.size() * sizeof(int32_t),
+                         hipMemcpyHostToDevice));
+    }
+    return VO_OK;
+}
+
 VoDev pass_dev(const vo_ctx* c, int p)
 {
     VoDev d = c->d;
@@ -436,6 +480,11 @@ void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax,
     hipStream_t sf = pipelined ? c->sf : s;
     if (pipelined) (void)hipStreamWaitEvent(s, c->ev_fn[(p + vo_ctx::kPassEv - 2) % vo_ctx::kPassEv], 0);
     timed(c, ev, 3, s, [&] { vo::launch_match(d, 0, s); });
+    if (d.rng_mode == VO_RNG_MT19937) {
+        const int rc = upload_mt_samples(c, d, d.gridw, s);
+        if (rc && ev && !ev->err) ev->err = rc;
+        if (rc) c->mt_err = rc;
+    }
     timed(c, ev, 4, s, [&] { vo::launch_ransac(d, 0, s); });
     if (pipelined) {
         (void)hipEventRecord(c->ev_rs[p % vo_ctx::kPassEv], s);
@@ -628,8 +677,9 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         // the chunk's output rows (complete once the trajectory queue's last k_traj ran, which
         // waited for the last k_finalize) and the commit point
         hipStream_t tq = c->serial || host_frame ? s : c->st;
-        HIPCHK(hipMemcpyAsync(c->out_host + (base - out_base), out + (base - out_base), sizeof(VoFrameOut) * nf,
-                              hipMemcpyDeviceToHost, tq));
+        if (out != c->out_host_dev)                        // (the per-frame call's kernels wrote out_host itself)
+            HIPCHK(hipMemcpyAsync(c->out_host + (base - out_base), out + (base - out_base), sizeof(VoFrameOut) * nf,
+                                  hipMemcpyDeviceToHost, tq));
         // the commit point after the last finalize (the fit queue's, which the trajectory queue waited
         // for).  A single frame's pass (window of one, no speculation) commits it: its row is read
         // alone and checked to be that frame's
@@ -657,6 +707,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         for (int k = 0; k < (end - lo + B - 1) / B; ++k) enqueue_pass(c, out, out_base, ev, end, false, host_frame);
     }
     if (ev && ev->err) return ev->err;
+    if (c->mt_err) { const int e = c->mt_err; c->mt_err = 0; return e; }
     // a frame the select's consistency check failed (VO_STATUS_INCONSISTENT): a library defect, loud
     for (int f = base; f < end; ++f)
         if (c->out_host[f - out_base].status == VO_STATUS_INCONSISTENT || c->out_host[f - out_base].err) {
@@ -679,9 +730,13 @@ int ensure_out(vo_ctx* c, int n)
     if (n <= c->out_cap) return VO_OK;
     if (c->out_dev) (void)hipFree(c->out_dev);
     if (c->out_host) (void)hipHostFree(c->out_host);
-    c->out_dev = nullptr; c->out_host = nullptr; c->out_cap = 0;
+    c->out_dev = nullptr; c->out_host = nullptr; c->out_host_dev = nullptr; c->out_cap = 0;
     HIPCHK(hipMalloc((void**)&c->out_dev, sizeof(VoFrameOut) * (size_t)n));
     HIPCHK(hipHostMalloc((void**)&c->out_host, sizeof(VoFrameOut) * (size_t)n, hipHostMallocDefault));
+    if (hipHostGetDevicePointer((void**)&c->out_host_dev, c->out_host, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        c->out_host_dev = nullptr;
+    }
     c->out_cap = n;
     return VO_OK;
 }
@@ -756,6 +811,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     if (k.match_bits != 32 && k.match_bits != 512) return VO_ERR_ARG;
     if (!(k.ransac_p > 0.0 && k.ransac_p < 1.0) || k.ransac_chunk_threads < 1) return VO_ERR_ARG;
     if (k.frame_batch < 0 || k.frame_batch > VO_MAX_BATCH) return VO_ERR_ARG;
+    if (k.rng_mode != VO_RNG_SPLITMIX && k.rng_mode != VO_RNG_MT19937) return VO_ERR_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return VO_ERR_NO_DEVICE;
     if (k.device < 0 || k.device >= ndev) return VO_ERR_NO_DEVICE;
@@ -784,6 +840,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     d.ratio = k.ratio; d.match_bits = k.match_bits;
     d.ransac_p = k.ransac_p; d.sampson_thr = k.sampson_thr; d.T = k.ransac_chunk_threads;
     d.seed = k.seed;
+    d.rng_mode = k.rng_mode;                // validated with the other arguments above
     std::memcpy(d.K, k.K, sizeof(d.K));
     {
         double outlierRatio = 0.5;
@@ -810,6 +867,10 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     c->split = VO_EXT_QUEUES >= 2 && (getenv("VO_SPLIT") ? atoi(getenv("VO_SPLIT")) != 0 : VO_SPLIT_DEFAULT != 0);
     c->slack = getenv("VO_SLACK") ? std::max(0, std::min(64, atoi(getenv("VO_SLACK")))) : VO_SLACK_DEFAULT;
     d.fault_inject = getenv("VO_FAULT_INJECT") && atoi(getenv("VO_FAULT_INJECT")) != 0;   // tests only
+    // the per-frame call's select in one launch: measured slower (21.2 us against 9.0 + 9.2 us for the two
+    // kernels, gpurun_out r5e), so opt-in (VO_SEL_FUSED=1)
+    d.sel_fused = getenv("VO_SEL_FUSED") && atoi(getenv("VO_SEL_FUSED")) != 0;
+    d.ransac_fused = !(getenv("VO_RANSAC_FUSED") && atoi(getenv("VO_RANSAC_FUSED")) == 0);
     // repair windows hold two work records per frame (k_finalize): at most WB / 2 frames
     d.repair_win = std::max(1, std::min(d.WB / 2, getenv("VO_REPAIR_WIN") ? atoi(getenv("VO_REPAIR_WIN")) : VO_REPAIR_WIN_DEFAULT));
     // queue priorities (VO_PRIO): 0 none; 1 the pose and trajectory queues high (the pose queue is the
@@ -878,6 +939,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc_rec(c, "inlmask", &d.inlmask, 2 * per[6]);
     rc |= dalloc_rec(c, "model_p", &d.model_p, 2 * per[7]);
     rc |= dalloc_rec(c, "work", &d.work, 2 * per[8]);
+    if (d.rng_mode == VO_RNG_MT19937) rc |= dalloc_rec(c, "samples", &d.samples, (size_t)d.max_hyp * 8 * WB);
     rc |= dalloc_rec(c, "plan", &d.plan, VO_PASS_RING);
     rc |= dalloc_rec(c, "snap", &d.snap, VO_PASS_RING);
     rc |= dalloc_rec(c, "st", &d.st, 1);
@@ -940,7 +1002,7 @@ void vo_destroy(vo_ctx* c)
     void* ptrs[] = {d.frame_in, d.blurred, d.response, d.cand, d.tilerows, d.ckeys, d.selbits, d.hist, d.selctl, d.ext_n, d.ext_st, (void*)d.seq_starts,
                     d.kps, d.desc, d.pre, d.match_j, d.match_pairs, d.pts, d.hypF, d.counts, d.inl, d.inlmask,
                     d.model_p, d.work, d.st, (void*)d.gt, c->tab_dev, c->out_dev, d.ctr, d.trec, d.plog, d.dbg,
-                    d.plan, d.snap, d.tile_ck, d.diag_tile, d.diag_src, d.diag_resp, d.diag_keys};
+                    d.plan, d.snap, d.tile_ck, d.diag_tile, d.diag_src, d.diag_resp, d.diag_keys, d.samples};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->out_host) (void)hipHostFree(c->out_host);
@@ -1187,6 +1249,7 @@ int vo_ransac_F(vo_ctx* c, const double* pts, int m, uint64_t seed, double F[9],
     w.frame_seed = seed;
     int rc = write_work0(c, &w);
     if (rc) return rc;
+    if (c->d.rng_mode == VO_RNG_MT19937 && (rc = upload_mt_samples(c, c->d, 1, c->s)) != VO_OK) return rc;
     vo::launch_ransac(c->d, 1, c->s);
     vo::launch_refit(c->d, 0, 1, c->s);
     HIPCHK(hipGetLastError());
@@ -1241,6 +1304,7 @@ int vo_ransac_run(vo_ctx* c, const double* pts, int m, double probability, doubl
     w.frame_seed = seed;
     int rc = write_work0(c, &w);
     if (rc) return rc;
+    if (d.rng_mode == VO_RNG_MT19937 && (rc = upload_mt_samples(c, d, 1, c->s)) != VO_OK) return rc;
     vo::launch_ransac(d, 1, c->s);
     vo::launch_refit(d, 0, 1, c->s);
     HIPCHK(hipGetLastError());
@@ -1339,7 +1403,10 @@ int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_
     const double t1 = c->pf_profile ? now_us() : 0.0;
     const int f = c->fidx;
     // one frame: extract on the pose queue, a window of one (no speculation)
-    int rc = run_chunk(c, gray ? (zc ? c->stage_host : c->d.frame_in) : nullptr, 0, 1, c->out_dev, f, nullptr, true);
+    // the frame's output row straight into pinned host memory (VO_PF_OUT_ZC=0: a device row and a copy)
+    static const bool out_zc = !(getenv("VO_PF_OUT_ZC") && atoi(getenv("VO_PF_OUT_ZC")) == 0);
+    VoFrameOut* out = out_zc && c->out_host_dev ? c->out_host_dev : c->out_dev;
+    int rc = run_chunk(c, gray ? (zc ? c->stage_host : c->d.frame_in) : nullptr, 0, 1, out, f, nullptr, true);
     if (rc) return rc;
     if (c->pf_profile) {
         c->pf_t[2] += c->pf_enq_end - t1;
@@ -1520,6 +1587,13 @@ int vo_extract_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
         fprintf(stderr, "[vo_mi355x] %u frames failed the select consistency check\n", nerr);
         return VO_ERR_INTERNAL;
     }
+    return VO_OK;
+}
+
+int vo_reference_samples(uint32_t seed32, int m, int nhyp, int32_t* out)
+{
+    if (m < 8 || nhyp < 0 || (nhyp > 0 && !out)) return VO_ERR_ARG;
+    mt_samples(seed32, m, nhyp, out);
     return VO_OK;
 }
 

@@ -153,6 +153,8 @@ struct VoWork {
     int32_t cold;         // refit from x0 = ones instead of the best hypothesis (vo_fit_F, stage only)
     int32_t counts4[4];   // positive-depth counts per (R, t) candidate
     uint32_t ctr[4];      // in-launch arrival counters: [0] match, [1] ransac chunk 1, [2] chunk 2
+    uint32_t ready1;      // k_ransac_fused: the first chunk's replay is written (reset by k_match's header)
+    uint32_t pad1;
     uint64_t frame_seed;
     double F[9];          // refit F (valid iff fitted)
     double R1[9], R2[9], t[3];
@@ -223,6 +225,8 @@ struct VoSelCtl {
     int32_t base[VO_SEL_BANDS];      // per band: its first keypoint position in raster order
     int32_t ktot[VO_SEL_BANDS];      // per band: its keys by the stencil's tile row counts (the
                                      // consistency check: their sum must equal the histogram's total)
+    uint32_t ready;                  // k_select_fused: the threshold and band positions are written
+    uint32_t arrive2;                // k_select_fused: bands done emitting (the last clears ready)
 };
 
 // Everything a kernel needs, passed by value.
@@ -262,6 +266,10 @@ struct VoDev {
     int sel_lds;          // select (single-workgroup form, VO_SEL1=1): dynamic LDS bytes
     int sel_emit_lds;     // banded select: k_select_emit's dynamic LDS bytes (a band's segment counts)
     int sel1;             // VO_SEL1=1: the single-workgroup select (one 1024-thread workgroup per frame)
+    int sel_fused;        // the per-frame call's banded select in one launch (k_select_fused; VO_SEL_FUSED=0: two)
+    int ransac_fused;     // one frame's two RANSAC chunks in one launch (k_ransac_fused; VO_RANSAC_FUSED=0: two)
+    int rng_mode;         // VO_RNG_MT19937: the hypotheses' samples come from `samples` (host-drawn std::sample)
+    int32_t* samples;     // x WB records: max_hyp x 8 indices per record (VO_RNG_MT19937 only)
     VoSelCtl* selctl;     // x B x VO_EXT_QUEUES
     uint32_t* hist;       // x B (scratch of extract queue eq; x VO_EXT_QUEUES allocated)
     int2* kps;            // x SLOTS (N each)

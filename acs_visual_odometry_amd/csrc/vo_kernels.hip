@@ -48,6 +48,9 @@ __constant__ float4 c_orient[DS_ONPAD];
 #define DS_UB 8                // terms per block of the unrolled sum (one table request per block)
 #endif
 __constant__ float4 c_orient_u[VO_FREAK_NPAIRS + DS_UB];
+// the pattern points (x, y) and the pair list (p, q) in pair order (k_describe_pf's loop indices)
+__constant__ short2 c_ppt[VO_FREAK_NPOINTS];
+__constant__ uchar2 c_pair[VO_FREAK_NPAIRS];
 
 static bool g_tables_ready = false;
 static void ensure_tables()
@@ -75,6 +78,12 @@ static void ensure_tables()
     if (o != DS_ONPAD) fprintf(stderr, "[vo_mi355x] orientation table size %d != %d\n", o, DS_ONPAD);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_orient), orient, sizeof(orient));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_orient_u), orient_u, sizeof(orient_u));
+    static short2 ppt[VO_FREAK_NPOINTS];
+    static uchar2 pair[VO_FREAK_NPAIRS];
+    for (int i = 0; i < VO_FREAK_NPOINTS; ++i) ppt[i] = make_short2(px[i], py[i]);
+    for (int t = 0; t < VO_FREAK_NPAIRS; ++t) pair[t] = make_uchar2(pp[t], pq[t]);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_ppt), ppt, sizeof(ppt));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pair), pair, sizeof(pair));
     g_tables_ready = true;
 }
 
@@ -997,7 +1006,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
     // prologue: source rows ys-7 .. ys+6 (blurred rows from ys-4, gradients from ys-3,
     // responses from ys-1: what the segment's first NMS row needs); then the first 8 rows of
     // the main loop are requested
-    constexpr int LA = 8;                                      // source rows in flight ahead of the step
+    // source rows in flight ahead of the step: 8; 16 in the one-tile-row segments of the per-frame
+    // call, so that its whole 30-row walk is requested up front (it reads the frame from pinned host
+    // memory: a second wave of requests paid the PCIe latency again)
+    constexpr int LA = SEGT == 1 ? 16 : 8;
     uint32_t ahead[LA];
     {
         const int rows = row_offsets(0);
@@ -1034,12 +1046,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
 #endif
         st_for([&](auto U) {
             const uint32_t cur = ahead[U % LA];
+            // the row requested here is consumed only if it lies inside the segment: in the last group
+            // the requests of steps U >= ST_TH - LA would read past it (wave-uniform; none for SEGT 1)
+            if (U < ST_TH - LA || (SEGT > 1 && i + 1 < ntl)) {
 #if ST_SOFF_HOIST
-            ahead[U % LA] = load(soff[U]);
+                ahead[U % LA] = load(soff[U]);
 #else
-            (void)soff;
-            ahead[U % LA] = load(__builtin_amdgcn_readlane(rows, U));
+                (void)soff;
+                ahead[U % LA] = load(__builtin_amdgcn_readlane(rows, U));
 #endif
+            }
             step(P5{}, k0 + U, cur, U);
         }, std::make_integer_sequence<int, ST_TH>{});
         // the 16 row counts of tile A (lanes 0..15) and B (16..31) are contiguous
@@ -1713,11 +1729,11 @@ __device__ __forceinline__ int sel_tile_of(int g, int total, int nt, const int* 
     return lo;
 }
 
-__global__ void __launch_bounds__(SL_T) k_select_count(VoDev d, int f0, int slot_override, int nb)
+// fused (the per-frame call's k_select_fused): the last band to arrive also publishes ctl->ready
+// after writing the threshold and the band positions, for the other bands waiting in the same launch
+__device__ __forceinline__ void sel_count_body(const VoDev& d, int f0, int slot_override, int z, int w,
+                                               unsigned char* smem, bool fused)
 {
-    int z, w;
-    if (!xcd_frame(d, VO_SEL_BANDS, nb, z, w)) return;
-    extern __shared__ __align__(16) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int N = d.N;
     const int ntx = (d.W + ST_TW - 1) / ST_TW, nty = (d.H + ST_TH - 1) / ST_TH;
@@ -1884,6 +1900,7 @@ __global__ void __launch_bounds__(SL_T) k_select_count(VoDev d, int f0, int slot
         d.ext_n[slot] = bad ? 0 : (C < N ? C : N);
         d.ext_st[slot] = bad ? VO_STATUS_INCONSISTENT : VO_STATUS_OK;
         if (bad) atomicAdd(d.ctr + VO_CTR_ERR, 1u);
+        if (fused) __hip_atomic_store((gu32*)&ctl->ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
     // every band has read the histogram: leave it zeroed for the next frame's stencil
     uint4* hp = reinterpret_cast<uint4*>(hist) + 4 * tid;
@@ -1891,11 +1908,17 @@ __global__ void __launch_bounds__(SL_T) k_select_count(VoDev d, int f0, int slot
     for (int q = 0; q < 4; ++q) hp[q] = make_uint4(0u, 0u, 0u, 0u);
 }
 
-__global__ void __launch_bounds__(SL_T) k_select_emit(VoDev d, int f0, int slot_override, int nb)
+__global__ void __launch_bounds__(SL_T) k_select_count(VoDev d, int f0, int slot_override, int nb)
 {
     int z, w;
     if (!xcd_frame(d, VO_SEL_BANDS, nb, z, w)) return;
     extern __shared__ __align__(16) unsigned char smem[];
+    sel_count_body(d, f0, slot_override, z, w, smem, false);
+}
+
+__device__ __forceinline__ void sel_emit_body(const VoDev& d, int f0, int slot_override, int z, int w,
+                                              unsigned char* smem)
+{
     __shared__ uint32_t s_w[4];
     const int tid = threadIdx.x, lane = tid & 63;
     const int N = d.N;
@@ -2017,6 +2040,55 @@ __global__ void __launch_bounds__(SL_T) k_select_emit(VoDev d, int f0, int slot_
             if (pos < N) out[pos] = make_int2(col, row);  // < N by construction
         }
     }
+}
+
+__global__ void __launch_bounds__(SL_T) k_select_emit(VoDev d, int f0, int slot_override, int nb)
+{
+    int z, w;
+    if (!xcd_frame(d, VO_SEL_BANDS, nb, z, w)) return;
+    extern __shared__ __align__(16) unsigned char smem[];
+    sel_emit_body(d, f0, slot_override, z, w, smem);
+}
+
+// The per-frame call's select: count and emit in one launch of the frame's VO_SEL_BANDS workgroups
+// (one launch and one dependent-launch gap less than the two kernels).  The bands meet after the
+// count: the last to arrive ranks the boundary keys and publishes ctl->ready (release, agent scope);
+// every band waits for it (acquire) before emitting.  The launch follows its frame's stencil on the
+// same queue, so its eight workgroups find the chip free and run together; the wait is bounded all
+// the same -- a band that times out marks the frame VO_STATUS_INCONSISTENT and counts a device error
+// instead of hanging -- and the last band to finish clears the flag for the next launch.
+#define SEL_FUSED_SPIN (1u << 22)
+__global__ void __launch_bounds__(SL_T) k_select_fused(VoDev d, int f0, int slot_override, int nb)
+{
+    int z, w;
+    if (!xcd_frame(d, VO_SEL_BANDS, nb, z, w)) return;
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ unsigned s_timeout, s_last2;
+    VoSelCtl* ctl = d.selctl + z;
+    sel_count_body(d, f0, slot_override, z, w, smem, true);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned it = 0u;
+        while (__hip_atomic_load((gu32*)&ctl->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u && it < SEL_FUSED_SPIN) {
+            __builtin_amdgcn_s_sleep(2);
+            ++it;
+        }
+        s_timeout = it >= SEL_FUSED_SPIN ? 1u : 0u;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the ranked threshold and band positions
+    if (s_timeout) {
+        if (threadIdx.x == 0) {
+            const int slot = ext_slot(d, f0, z, slot_override);
+            d.ext_n[slot] = 0;
+            d.ext_st[slot] = VO_STATUS_INCONSISTENT;
+            atomicAdd(d.ctr + VO_CTR_ERR, 1u);
+        }
+    } else {
+        sel_emit_body(d, f0, slot_override, z, w, smem);
+    }
+    if (!arrive_last(&ctl->arrive2, VO_SEL_BANDS, &s_last2)) return;
+    if (threadIdx.x == 0) { ctl->ready = 0u; ctl->arrive2 = 0u; }   // for the next launch
 }
 
 // extract side of a missing image (VisualOdometry.cpp:77-82): the slot holds no keypoints
@@ -2312,6 +2384,115 @@ __global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int
 }
 
 // ---------------------------------------------------------------------------
+// The per-frame call's describe (k_describe_pf): one 64-keypoint block per workgroup of DP_WAVES
+// waves instead of one wave, lane = keypoint as in describe_wave, the same arithmetic in the same
+// order.  One wave alone walks 43 gathers, 903 in-order terms, 43 rotated gathers and 512 tests per
+// keypoint -- the per-frame call's longest link (26.5 us).  Here the waves share every phase but
+// the in-order sum: the pattern and rotated gathers (a sample row per wave in turn, into LDS), the
+// orientation terms (fmaf(ic, A, ic * B) per component, exactly describe_wave's term) computed a
+// chunk ahead into an LDS ring by waves 1.., while wave 0 adds each chunk's terms to the running
+// f32 sums in pair order t = 0 .. 902 (so every rounding is the sequential loop's), and the 16
+// test words (two per wave).
+// ---------------------------------------------------------------------------
+#define DP_WAVES 8
+#define DP_CH 64                                     // terms per chunk of the LDS ring (two chunks)
+__global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, int slot_override)
+{
+    constexpr int NP = VO_FREAK_NPOINTS;
+    constexpr int NC = (VO_FREAK_NPAIRS + DP_CH - 1) / DP_CH;
+    __shared__ float s_I[NP][64];                    // pattern samples (then the rotated samples, as u32)
+    __shared__ ds_f2 s_t[2][DP_CH][64];              // orientation terms, a chunk ahead
+    __shared__ float s_c[64], s_s[64];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int cur = ext_slot(d, f0, 0, slot_override);
+    const int n = d.ext_n[cur];
+    const int base = blockIdx.x * 64;
+    if (base >= n) return;                           // workgroup-uniform
+    const int W = d.W, H = d.H, Wb = d.bstride;
+    const uint8_t* __restrict__ img = d.blurred + VO_BLUR_X0;
+    const bool valid = base + lane < n;
+    const int2 kp = valid ? d.kps[(size_t)cur * d.N + base + lane] : make_int2(d.bcol, d.brow);
+    // 1. pattern samples, rows u = wave, wave + DP_WAVES, ...
+    for (int u = wave; u < NP; u += DP_WAVES)
+        s_I[u][lane] = (float)img[(size_t)(kp.y + (int)c_ppt[u].y) * Wb + (kp.x + (int)c_ppt[u].x)];
+    __syncthreads();
+    // 2. terms of chunk c into ring slot c & 1 by waves 1 .. DP_WAVES - 1 (term t of the chunk by wave
+    //    1 + t % (DP_WAVES - 1)); wave 0 sums chunk c - 1 meanwhile
+    auto terms = [&](int c) {
+        for (int j = wave - 1; j < DP_CH; j += DP_WAVES - 1) {
+            const int t = c * DP_CH + j;
+            if (t >= VO_FREAK_NPAIRS) break;
+            const float4 tb = c_orient_u[t];
+            const float ic = s_I[c_pair[t].x][lane] - s_I[c_pair[t].y][lane];
+            const ds_f2 i2 = {ic, ic};
+            s_t[c & 1][j][lane] = __builtin_elementwise_fma(i2, ds_f2{tb.x, tb.y}, i2 * ds_f2{tb.z, tb.w});
+        }
+    };
+    ds_f2 oxy = {0.0f, 0.0f};
+    if (wave > 0) terms(0);
+    __syncthreads();
+    for (int c = 0; c < NC; ++c) {
+        if (wave > 0) {
+            if (c + 1 < NC) terms(c + 1);
+        } else {
+            const int m = min(DP_CH, VO_FREAK_NPAIRS - c * DP_CH);
+#pragma unroll 16
+            for (int j = 0; j < m; ++j) oxy = oxy + s_t[c & 1][j][lane];
+        }
+        __syncthreads();
+    }
+    // 3. angle and rotation (wave 0), as describe_wave
+    if (wave == 0) {
+        const float ox = oxy.x, oy = oxy.y;
+        float angle = 0.0f;
+        if (!(isnan(ox) || isnan(oy))) angle = (float)det_atan2((double)oy, (double)ox);
+        double sd, cd;
+        det_sincos((double)angle, &sd, &cd);
+        s_c[lane] = (float)cd;
+        s_s[lane] = (float)sd;
+    }
+    __syncthreads();
+    // 4. rotated samples (quirk 4), rows u = wave, wave + DP_WAVES, ...
+    {
+        const float c = s_c[lane], s = s_s[lane], ms = -1.0f * s;
+        uint32_t* rot = reinterpret_cast<uint32_t*>(&s_I[0][0]);
+        for (int u = wave; u < NP; u += DP_WAVES) {
+            const int px = c_ppt[u].x, py = c_ppt[u].y;
+            int x = (int)(((float)kp.x + (float)px * c) + (float)py * s);
+            int y = (int)(((float)kp.y + (float)(-1 * px) * ms) + (float)py * c);
+            x = min(max(x, 0), W - 1);
+            y = min(max(y, 0), H - 1);
+            rot[u * 64 + lane] = img[(size_t)y * Wb + x];
+        }
+    }
+    __syncthreads();
+    // 5. the 512 tests: words wave and wave + 8 of 16
+    {
+        const uint32_t* rot = reinterpret_cast<const uint32_t*>(&s_I[0][0]);
+        uint32_t r[NP];
+#pragma unroll
+        for (int u = 0; u < NP; ++u) r[u] = rot[u * 64 + lane];
+        uint32_t w0 = 0u, w1 = 0u;
+        switch (wave) {
+        case 0: w0 = ds_word<0>(r); w1 = ds_word<8>(r); break;
+        case 1: w0 = ds_word<1>(r); w1 = ds_word<9>(r); break;
+        case 2: w0 = ds_word<2>(r); w1 = ds_word<10>(r); break;
+        case 3: w0 = ds_word<3>(r); w1 = ds_word<11>(r); break;
+        case 4: w0 = ds_word<4>(r); w1 = ds_word<12>(r); break;
+        case 5: w0 = ds_word<5>(r); w1 = ds_word<13>(r); break;
+        case 6: w0 = ds_word<6>(r); w1 = ds_word<14>(r); break;
+        default: w0 = ds_word<7>(r); w1 = ds_word<15>(r); break;
+        }
+        if (valid) {
+            uint32_t* dst = reinterpret_cast<uint32_t*>(d.desc + ((size_t)cur * d.N + base + lane) * 8);
+            dst[wave] = w0;
+            dst[wave + 8] = w1;
+            if (wave == 0) d.pre[(size_t)cur * d.N + base + lane] = w0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // match: brute-force Hamming top-2 + Lowe ratio, one query per wave; the last workgroup
 // compacts the accepted queries in ascending order into matches + f64 points.
 // feature_matching_parallel.cpp:39-113; VisualOdometry.cpp:100-123.
@@ -2476,6 +2657,7 @@ __device__ __forceinline__ bool match_header(const VoDev& d, int stage, const Vo
         w->frame = f; w->cur = cur; w->prev = prev;
         w->bestk = -1; w->n_eval = 0; w->n_inl = 0; w->fitted = 0; w->n_fit = 0; w->degenerate = 0;
         w->need_more = 0;
+        w->ready1 = 0u;                                        // k_ransac_fused's hand-off flag
         for (int c = 0; c < 4; ++c) w->counts4[c] = 0;
         if (!stage) w->frame_seed = frame_seed_of(d, fl);
         if (status != VO_STATUS_OK) { w->status = status; w->M = 0; w->scored = 0; }
@@ -3001,8 +3183,7 @@ __device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], in
     nn = sqrt(nn);
 #pragma unroll
     for (int j = 0; j < 9; ++j) f[j] = f[j] / nn;
-    denormalize(f, sc1, mx1, my1, sc2, mx2, my2, F);
-    rank2(F);
+    denormalize(f, sc1, mx1, my1, sc2, mx2, my2, F);   // (rank 2 by the caller: rank2(F))
 }
 
 // inliers of the group's F among the first `scored` matches: lane r tests matches 8 j + r of
@@ -3150,20 +3331,46 @@ __device__ void inv4(const double* M, double* Inv)
 // HPB waves per workgroup, eight hypotheses per wave (lane 8 h + r: hypothesis h, row r).
 // reps: hypothesis blocks per workgroup (strided by the grid), so a later chunk, which usually
 // exits at once, dispatches reps times fewer workgroups
+// One chunk [k0, k1) of the hypotheses on workgroups bx of nbx.  ready (the fused form): the chunk's
+// replay publishes w->ready1 when it is done (k0 == 0), or the chunk waits for it first (k0 > 0).
 template <int HPB>
-__global__ void __launch_bounds__(64 * HPB) k_ransac_hyp(VoDev d, int k0, int k1, int nhyp, int stage, int reps)
+__device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int nhyp, int stage, int reps, int bx,
+                                             int nbx, bool ready)
 {
     const int wf = blockIdx.y;                     // window frame
     if (wf >= vwin_count(d, stage)) return;
     VoWork* w = d.work + wf;
     if (w->status != VO_STATUS_OK) return;
+    if (ready && k0 > 0) {
+        // the fused launch: wait for the first chunk's replay (bounded; its four workgroups and these
+        // run together -- the launch is one frame's 64 workgroups on an otherwise idle queue)
+        __shared__ unsigned s_to;
+        if (threadIdx.x == 0) {
+            unsigned it = 0u;
+            while (__hip_atomic_load((gu32*)&w->ready1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+                   it < (1u << 22)) {
+                __builtin_amdgcn_s_sleep(2);
+                ++it;
+            }
+            s_to = it >= (1u << 22) ? 1u : 0u;
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (s_to) {
+            if (bx == 0 && threadIdx.x == 0) {
+                atomicAdd(d.ctr + VO_CTR_ERR, 1u);
+                w->need_more = 0;                  // the frame's RANSAC stops at [0, k0): loud, never a hang
+            }
+            return;
+        }
+    }
     if (k0 > 0 && !w->need_more) return;           // the replay of [0, k0) already stopped
     __shared__ unsigned s_last;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 3, r = lane & 7;
     const int M = w->M, scored = w->scored;
     const double* pts = d.pts + (size_t)wf * 4 * d.N;
     int32_t* counts = d.counts + (size_t)wf * d.max_hyp;
-    int k = k0 + (blockIdx.x * HPB + wave) * 8 + h;
+    int k = k0 + (bx * HPB + wave) * 8 + h;
     // Hypotheses at or past the previous replay's bound are never evaluated by the sequential
     // loop: once an improvement updated maxIterations (best > 0 and its table entry is not the
     // 'denom == 0: no update' mark) and the loop went on past k0 (maxit > 100), the inlier ratio
@@ -3174,17 +3381,27 @@ __global__ void __launch_bounds__(64 * HPB) k_ransac_hyp(VoDev d, int k0, int k1
     int kbound = k1;
     if (k0 > 0 && w->best > 0 && d.maxit_tab[(size_t)M * (M + 1) / 2 + w->best] != 0xFFFFu)
         kbound = min(w->maxit, k1);
-    for (int rep = 0; rep < reps; ++rep, k += gridDim.x * HPB * 8) {
+    for (int rep = 0; rep < reps; ++rep, k += nbx * HPB * 8) {
         const int kb = k - h;                      // the wave's first hypothesis
         if (kb >= k1) break;                       // wave-uniform
         const bool mine = k < kbound;
         if (__builtin_amdgcn_readfirstlane(kb) < kbound) {   // some group of the wave has work
             VO_STAMP(d, k, 0);
             int s8[8];
-            sample8(w->frame_seed, min(k, nhyp - 1), M, s8);
+            if (d.rng_mode == VO_RNG_MT19937) {
+                // the reference's std::sample draws, drawn on the host for this record (vo_api.cpp)
+                const int4* sp = reinterpret_cast<const int4*>(d.samples + ((size_t)wf * d.max_hyp + min(k, nhyp - 1)) * 8);
+                const int4 lo = sp[0], hi = sp[1];
+                s8[0] = lo.x; s8[1] = lo.y; s8[2] = lo.z; s8[3] = lo.w;
+                s8[4] = hi.x; s8[5] = hi.y; s8[6] = hi.z; s8[7] = hi.w;
+            } else {
+                sample8(w->frame_seed, min(k, nhyp - 1), M, s8);
+            }
             VO_STAMP(d, k, 1);
             double F[9];
             fit_F8_group(pts, s8, r, lane & ~7, F);
+            VO_STAMP(d, k, 2);
+            rank2(F);
             VO_STAMP(d, k, 5);
             if (mine) {
                 double* hf = d.hypF + ((size_t)wf * d.max_hyp + k) * 9;
@@ -3200,7 +3417,7 @@ __global__ void __launch_bounds__(64 * HPB) k_ransac_hyp(VoDev d, int k0, int k1
         if (!mine && k < k1 && r == 0) st_sc1(counts + k, -1);   // skipped: the replay never takes it
     }
     unsigned* ctr = &w->ctr[k0 == 0 ? 1 : (k0 < VO_HYP_CHUNK1 ? 2 : 3)];   // one arrival counter per chunk
-    if (!arrive_last(ctr, gridDim.x, &s_last)) return;
+    if (!arrive_last(ctr, nbx, &s_last)) return;
     if (threadIdx.x >= 64) return;                 // the replay is one wave's
     VO_STAMP(d, 1997 + (k0 > 0), 0);
     // ---- last workgroup (one wave): replay of ransac.cpp:139-190 over [kk, k1) ----
@@ -3237,7 +3454,23 @@ __global__ void __launch_bounds__(64 * HPB) k_ransac_hyp(VoDev d, int k0, int k1
         w->need_more = kk < maxit ? 1 : 0;
         w->n_eval = kk;
         *ctr = 0u;
+        if (ready && k0 == 0) __hip_atomic_store((gu32*)&w->ready1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+template <int HPB>
+__global__ void __launch_bounds__(64 * HPB) k_ransac_hyp(VoDev d, int k0, int k1, int nhyp, int stage, int reps)
+{
+    ransac_chunk<HPB>(d, k0, k1, nhyp, stage, reps, blockIdx.x, gridDim.x, false);
+}
+// one frame's two chunks in one launch (the per-frame call and the stage API: one launch and one
+// dependent-launch gap less): workgroups [0, b0) run [0, c0) and publish its replay; the rest wait
+// for it and run [c0, nhyp) as the second launch would
+template <int HPB>
+__global__ void __launch_bounds__(64 * HPB) k_ransac_fused(VoDev d, int c0, int nhyp, int stage, int b0)
+{
+    if ((int)blockIdx.x < b0) ransac_chunk<HPB>(d, 0, c0, nhyp, stage, 1, blockIdx.x, b0, true);
+    else ransac_chunk<HPB>(d, c0, nhyp, nhyp, stage, 1, blockIdx.x - b0, gridDim.x - b0, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -4424,6 +4657,10 @@ void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_
         return;
     }
     const dim3 g(xcd_grid(VO_SEL_BANDS, nb));
+    if (d.single && nb == 1 && d.sel_fused) {          // the per-frame call: one launch
+        hipLaunchKernelGGL(k_select_fused, g, dim3(SL_T), (size_t)d.sel_emit_lds, s, d, f0, slot_override, nb);
+        return;
+    }
     // the count kernel uses the layout's tile table only (rows, pre, tof)
     const int cnt_lds = sel_band_layout((d.W + ST_TW - 1) / ST_TW, (d.H + ST_TH - 1) / ST_TH).bits;
     hipLaunchKernelGGL(k_select_count, g, dim3(SL_T), (size_t)cnt_lds, s, d, f0, slot_override, nb);
@@ -4436,7 +4673,8 @@ int select_emit_lds_bytes(int W, int H)
     if (bytes > 150 * 1024) return -1;
     if (bytes > 64 * 1024) {
         if (hipFuncSetAttribute((const void*)k_select_emit, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess ||
-            hipFuncSetAttribute((const void*)k_select_count, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
+            hipFuncSetAttribute((const void*)k_select_count, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess ||
+            hipFuncSetAttribute((const void*)k_select_fused, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
             return -1;
     }
     return bytes;
@@ -4467,6 +4705,12 @@ void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned
     // 26 -> 30 us, the call 165 -> 168 us, so the scalar-cache path stays the default)
     static const int lt_env = getenv("VO_DS_LDS_TABLE") ? atoi(getenv("VO_DS_LDS_TABLE")) : 0;
     const bool lt = lt_env != 0 && nb == 1 && d.single;
+    // the per-frame call: eight waves per 64 keypoints (VO_DS_PF=0: one, k_describe)
+    static const int pf_env = getenv("VO_DS_PF") ? atoi(getenv("VO_DS_PF")) : 1;
+    if (pf_env && nb == 1 && d.single && !publish && !lt) {
+        hipLaunchKernelGGL(k_describe_pf, dim3((d.N + 63) / 64), dim3(64 * DP_WAVES), 0, s, d, f0, slot_override);
+        return;
+    }
     if (lt)
         hipLaunchKernelGGL(k_describe<true>, dim3(xcd_grid((d.N + DS_KPB - 1) / DS_KPB, nb)), dim3(64 * DS_WAVES), 0, s, d,
                            f0, slot_override, publish, nb);
@@ -4517,6 +4761,12 @@ void launch_match(const VoDev& d, int stage, hipStream_t s)
 void launch_ransac(const VoDev& d, int stage, hipStream_t s)
 {
     const int nhyp = d.max_hyp, nb = stage ? 1 : d.gridw;
+    // (the per-frame call's window: one frame, two work records -- the repair form's second record)
+    if ((stage || d.single) && nb <= 2 && d.ransac_fused && nhyp > VO_HYP_CHUNK0) {
+        const int b0 = (VO_HYP_CHUNK0 + 31) / 32, b1 = (nhyp - VO_HYP_CHUNK0 + 31) / 32;
+        hipLaunchKernelGGL((k_ransac_fused<4>), dim3(b0 + b1, nb), dim3(256), 0, s, d, VO_HYP_CHUNK0, nhyp, stage, b0);
+        return;
+    }
     // VO_HYP_CUT1: the second cut (VO_HYP_CHUNK1; >= max_hyp merges the last two chunks)
     static const int cut1 = getenv("VO_HYP_CUT1") ? std::max(VO_HYP_CHUNK0, atoi(getenv("VO_HYP_CUT1"))) : VO_HYP_CHUNK1;
     const int cut[3] = {std::min(nhyp, VO_HYP_CHUNK0), std::min(nhyp, cut1), nhyp};

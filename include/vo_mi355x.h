@@ -78,7 +78,19 @@ typedef struct {
     int device;               /* HIP device ordinal                                    */
     int frame_batch;          /* frames per extract batch / pose-pass window (1..128);
                                  0 = default 64.  Results do not depend on it.         */
+    int rng_mode;             /* RANSAC sampler (ransac.cpp:137,142):
+                                 VO_RNG_SPLITMIX (default): Floyd samples from splitmix64, drawn
+                                   on the device per hypothesis (the throughput mode);
+                                 VO_RNG_MT19937: the reference's own sampler, std::sample(data, 8,
+                                   rng) with std::mt19937 rng(seed32) per frame -- seed32 = the low
+                                   32 bits of the frame seed (of `seed` in the stage calls), where
+                                   the reference seeds std::random_device{}() -- drawn on the host
+                                   once the frame's match count is known (a host round trip per
+                                   pose pass).  A reference build seeded with seed32 draws the same
+                                   hypotheses. */
 } vo_config;
+#define VO_RNG_SPLITMIX 0
+#define VO_RNG_MT19937  1
 
 /* Fill the reference defaults for a width x height stream. */
 void vo_config_default(vo_config* cfg, int width, int height);
@@ -218,6 +230,12 @@ int  vo_host_free(vo_ctx* ctx, void* hptr);
 int  vo_device_alloc(vo_ctx* ctx, size_t bytes, void** dptr);
 int  vo_device_free(vo_ctx* ctx, void* dptr);
 int  vo_device_upload(vo_ctx* ctx, void* dptr, const void* src, size_t bytes);
+
+/* The reference's RANSAC sampler, host only (no device needed): for k = 0 .. nhyp-1 the indices
+ * (ascending) that the k-th std::sample(data.begin(), data.end(), std::back_inserter(sample), 8, rng)
+ * of ransac.cpp:142 picks from m elements, rng = std::mt19937(seed32) constructed once
+ * (ransac.cpp:137).  out: nhyp * 8 indices.  What VO_RNG_MT19937 uploads per frame. */
+int  vo_reference_samples(uint32_t seed32, int m, int nhyp, int32_t* out);
 
 /* Device consistency failures since vo_create / the last vo_reset (frames marked
  * VO_STATUS_INCONSISTENT by the top-N select).  Waits for the context's queues.  The bench and the

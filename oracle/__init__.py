@@ -22,7 +22,7 @@ class VooConfig(C.Structure):
         ("resp_thr", C.c_float), ("border_row", C.c_int), ("border_col", C.c_int),
         ("ratio", C.c_float), ("match_bits", C.c_int), ("ransac_p", C.c_double),
         ("sampson_thr", C.c_double), ("ransac_chunk_threads", C.c_int), ("seed", C.c_uint64),
-        ("K", C.c_double * 9),
+        ("K", C.c_double * 9), ("rng_mode", C.c_int),
     ]
 
 
@@ -73,6 +73,9 @@ def lib():
         L.voo_sampson.argtypes = [P, P]
         L.voo_ransac.argtypes = [P, C.c_int, C.c_double, C.c_double, C.c_int, C.c_uint64, P, P,
                                  C.POINTER(VooRansacResult)]
+        L.voo_ransac_ex.argtypes = [P, C.c_int, C.c_double, C.c_double, C.c_int, C.c_uint64, C.c_int, P, P, P]
+        L.voo_mt_samples.argtypes = [C.c_uint32, C.c_int, C.c_int, P]
+        L.voo_mt_samples.restype = None
         L.voo_pose.argtypes = [P, P, P, P, C.c_int, C.c_double, P, P, P]
         L.voo_vo_create.restype = P
         L.voo_vo_create.argtypes = [C.POINTER(VooConfig)]
@@ -229,13 +232,14 @@ def sampson(F, p):
     return lib().voo_sampson(_p(F), _p(p))
 
 
-def ransac(pts, prob=0.99, thr=1.0, T=8, seed=1):
+def ransac(pts, prob=0.99, thr=1.0, T=8, seed=1, rng_mode=0):
+    """rng_mode 1: the reference's sampler (std::mt19937(low 32 bits of seed) + std::sample)."""
     pts = np.ascontiguousarray(pts, dtype=np.float64).reshape(-1, 4)
     m = pts.shape[0]
     counts = np.zeros(2000, np.int32)
     inl = np.zeros(max(m, 1), np.int32)
     res = VooRansacResult()
-    rc = lib().voo_ransac(_p(pts), m, prob, thr, T, seed, _p(counts), _p(inl), C.byref(res))
+    rc = lib().voo_ransac_ex(_p(pts), m, prob, thr, T, seed, rng_mode, _p(counts), _p(inl), C.byref(res))
     return dict(rc=rc, F=np.array(res.F[:]).reshape(3, 3), fitted=res.fitted, best_k=res.best_k,
                 best_count=res.best_count, n_evaluated=res.n_evaluated, n_inl=res.n_inl,
                 counts=counts[:res.n_evaluated].copy(), inliers=inl[:res.n_inl].copy())
@@ -294,3 +298,10 @@ def stage_times():
     n = np.zeros(len(STAGES), np.int64)
     lib().voo_stage_times(_p(sec), _p(n))
     return {k: (float(sec[i]), int(n[i])) for i, k in enumerate(STAGES)}
+
+
+def mt_samples(seed32, m, nhyp):
+    """The reference's std::sample draws of std::mt19937(seed32): (nhyp, 8) indices."""
+    out = np.zeros((max(nhyp, 1), 8), np.int32)
+    lib().voo_mt_samples(seed32 & 0xFFFFFFFF, m, nhyp, _p(out))
+    return out[:nhyp]

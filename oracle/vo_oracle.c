@@ -981,9 +981,25 @@ int voo_refit_normal(const double* pts, const int32_t* idx, int n, double AtA_ou
 int voo_ransac(const double* pts, int m, double prob, double thr, int T, uint64_t seed,
                int32_t* counts, int32_t* inl_idx, voo_ransac_result* res)
 {
+    return voo_ransac_ex(pts, m, prob, thr, T, seed, 0, counts, inl_idx, res);
+}
+
+/* rng_mode 1: hypothesis k's sample is the k-th std::sample(data, 8, rng) of rng = std::mt19937(seed32),
+ * seed32 = the low 32 bits of seed (ransac.cpp:137,142; vo_oracle_mt.cpp) */
+int voo_ransac_ex(const double* pts, int m, double prob, double thr, int T, uint64_t seed, int rng_mode,
+                  int32_t* counts, int32_t* inl_idx, voo_ransac_result* res)
+{
     memset(res, 0, sizeof(*res));
     res->best_k = -1;
     if (m < 8 || T < 1) return -1;
+    int32_t* tab = NULL;
+    if (rng_mode == 1) {
+        const int mi = voo_ransac_maxit_initial(prob), ntab = mi > 2000 ? mi : 2000;   /* clamp: <= 2000 later */
+        tab = (int32_t*)malloc(sizeof(int32_t) * 8 * (size_t)ntab);
+        voo_mt_samples((uint32_t)seed, m, ntab, tab);
+    }
+#define SAMPLE8(k, s8) do { if (tab) memcpy((s8), tab + 8 * (size_t)(k), 8 * sizeof(int32_t)); \
+                            else voo_sample8(seed, (k), m, (s8)); } while (0)
     int chunk = m / T;
     int scored = chunk * T;
     int maxIt = voo_ransac_maxit_initial(prob);
@@ -991,7 +1007,7 @@ int voo_ransac(const double* pts, int m, double prob, double thr, int T, uint64_
     double F[9];
     for (it = 0; it < maxIt; ++it) {
         int32_t s8[8];
-        voo_sample8(seed, it, m, s8);
+        SAMPLE8(it, s8);
         voo_fit_F8(pts, s8, F);
         int c = 0;
         for (int i = 0; i < scored; ++i)
@@ -1006,9 +1022,11 @@ int voo_ransac(const double* pts, int m, double prob, double thr, int T, uint64_
     res->n_evaluated = it;
     res->best_k = bestk;
     res->best_count = best;
-    if (bestk < 0) { res->n_inl = 0; res->fitted = 0; return 0; }
+    if (bestk < 0) { res->n_inl = 0; res->fitted = 0; free(tab); return 0; }
     int32_t s8[8];
-    voo_sample8(seed, bestk, m, s8);
+    SAMPLE8(bestk, s8);
+    free(tab);
+#undef SAMPLE8
     voo_fit_F8(pts, s8, F);
     int32_t* idx = (int32_t*)malloc(sizeof(int32_t) * m);
     int n = 0;
@@ -1379,8 +1397,8 @@ int voo_vo_process(voo_vo* s, const uint8_t* gray, size_t stride, const double* 
     free(pairs);
     voo_ransac_result rr;
     int32_t* inl = (int32_t*)malloc(sizeof(int32_t) * m);
-    STAGE(VOO_STAGE_RANSAC, voo_ransac(pts, m, c->ransac_p, c->sampson_thr, c->ransac_chunk_threads,
-                                        voo_frame_seed(c->seed, fi), NULL, inl, &rr));
+    STAGE(VOO_STAGE_RANSAC, voo_ransac_ex(pts, m, c->ransac_p, c->sampson_thr, c->ransac_chunk_threads,
+                                           voo_frame_seed(c->seed, fi), c->rng_mode, NULL, inl, &rr));
     if (info) { info[2] = rr.n_inl; info[3] = rr.best_k; info[4] = rr.n_evaluated; info[5] = rr.fitted; }
     if (rr.fitted) {                                              /* model state leak, quirk 9 */
         memcpy(s->model_F, rr.F, sizeof(rr.F));

@@ -45,7 +45,10 @@ typedef struct {
     int ransac_chunk_threads;/* T      ransac.cpp:152-157 (CLI thread count)        */
     uint64_t seed;           /* RANSAC sampler seed (replaces std::random_device)   */
     double K[9];             /* PoseUpdate.hpp:36-39                                */
+    int rng_mode;            /* 0: Floyd / splitmix64 samples; 1: std::mt19937 + std::sample (ransac.cpp:137,142) */
 } voo_config;
+/* the reference's sampler (vo_oracle_mt.cpp): hypotheses k = 0 .. nhyp-1 of std::mt19937(seed32) */
+void voo_mt_samples(uint32_t seed32, int m, int nhyp, int32_t* out);
 
 void voo_config_default(voo_config* c, int width, int height);
 
@@ -97,6 +100,8 @@ double voo_sampson(const double F[9], const double* p);
 int  voo_ransac(const double* pts /* m*4: x1,y1,x2,y2 */, int m, double prob, double thr,
                 int T, uint64_t seed, int32_t* counts /* >=2000 or NULL */,
                 int32_t* inl_idx /* m or NULL */, voo_ransac_result* res);
+int  voo_ransac_ex(const double* pts, int m, double prob, double thr, int T, uint64_t seed, int rng_mode,
+                   int32_t* counts, int32_t* inl_idx, voo_ransac_result* res);
 
 /* ---- pose (PoseUpdate::getPose, PoseUpdate.hpp:61-179) ---- */
 #define VOO_OK 0
