@@ -1396,9 +1396,24 @@ int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_
     // pairs, gpurun_out pf_a / pf_z); the next call's staging copy waits for this one (upload_frame's
     // sync).  VO_PF_ZEROCOPY=0: the upload kernel
     static const bool zc = !(getenv("VO_PF_ZEROCOPY") && atoi(getenv("VO_PF_ZEROCOPY")) == 0);
-    if (gray) {
+    // a caller frame already in pinned host memory (vo_host_alloc / hipHostRegister) with rows
+    // packed: the stencil reads it where it lies, no staging copy (VO_PF_PINNED_DIRECT=0: staged)
+    static const bool direct_ok = !(getenv("VO_PF_PINNED_DIRECT") && atoi(getenv("VO_PF_PINNED_DIRECT")) == 0);
+    const uint8_t* src = nullptr;
+    if (gray && zc && direct_ok && (stride == 0 || stride == (size_t)c->cfg.width)) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, gray) == hipSuccess) {
+            if (a.type == hipMemoryTypeHost && a.devicePointer) src = static_cast<const uint8_t*>(a.devicePointer);
+        } else {
+            (void)hipGetLastError();
+        }
+    }
+    if (src) {
+        SYNC_ALL(c);                  // nothing of an earlier batched call still in flight
+    } else if (gray) {
         int rc = upload_frame(c, gray, stride, c->s, zc);
         if (rc) return rc;
+        src = zc ? c->stage_host : c->d.frame_in;
     }
     const double t1 = c->pf_profile ? now_us() : 0.0;
     const int f = c->fidx;
@@ -1406,7 +1421,7 @@ int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_
     // the frame's output row straight into pinned host memory (VO_PF_OUT_ZC=0: a device row and a copy)
     static const bool out_zc = !(getenv("VO_PF_OUT_ZC") && atoi(getenv("VO_PF_OUT_ZC")) == 0);
     VoFrameOut* out = out_zc && c->out_host_dev ? c->out_host_dev : c->out_dev;
-    int rc = run_chunk(c, gray ? (zc ? c->stage_host : c->d.frame_in) : nullptr, 0, 1, out, f, nullptr, true);
+    int rc = run_chunk(c, src, 0, 1, out, f, nullptr, true);
     if (rc) return rc;
     if (c->pf_profile) {
         c->pf_t[2] += c->pf_enq_end - t1;

@@ -51,6 +51,13 @@ __constant__ float4 c_orient_u[VO_FREAK_NPAIRS + DS_UB];
 // the pattern points (x, y) and the pair list (p, q) in pair order (k_describe_pf's loop indices)
 __constant__ short2 c_ppt[VO_FREAK_NPOINTS];
 __constant__ uchar2 c_pair[VO_FREAK_NPAIRS];
+// k_describe_pf's term tables, padded to whole 64-term chunks (padding: both rows 0, weights 0):
+// each entry one scalar load -- the pair as the two sample rows' LDS byte offsets (p * 256 |
+// q * 256 << 16), the weights as in c_orient_u
+#define DP_CHUNK 64
+#define DP_NPAD (((VO_FREAK_NPAIRS + DP_CHUNK - 1) / DP_CHUNK) * DP_CHUNK)
+__constant__ uint32_t c_pairoff[DP_NPAD];
+__constant__ float4 c_orient_pf[DP_NPAD];
 
 static bool g_tables_ready = false;
 static void ensure_tables()
@@ -84,6 +91,14 @@ static void ensure_tables()
     for (int t = 0; t < VO_FREAK_NPAIRS; ++t) pair[t] = make_uchar2(pp[t], pq[t]);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_ppt), ppt, sizeof(ppt));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pair), pair, sizeof(pair));
+    static uint32_t pairoff[DP_NPAD];
+    static float4 orient_pf[DP_NPAD];
+    for (int t = 0; t < DP_NPAD; ++t) {
+        pairoff[t] = t < VO_FREAK_NPAIRS ? (uint32_t)pp[t] * 256u | ((uint32_t)pq[t] * 256u) << 16 : 0u;
+        orient_pf[t] = t < VO_FREAK_NPAIRS ? orient_u[t] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pairoff), pairoff, sizeof(pairoff));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_orient_pf), orient_pf, sizeof(orient_pf));
     g_tables_ready = true;
 }
 
@@ -2069,7 +2084,9 @@ __global__ void __launch_bounds__(SL_T) k_select_fused(VoDev d, int f0, int slot
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned it = 0u;
-        while (__hip_atomic_load((gu32*)&ctl->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u && it < SEL_FUSED_SPIN) {
+        // relaxed polls (a device-coherent load each), one acquire after the loop: an acquire poll
+        // invalidates the XCD's L2 (buffer_inv sc1) on every iteration, under the working waves
+        while (__hip_atomic_load((gu32*)&ctl->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u && it < SEL_FUSED_SPIN) {
             __builtin_amdgcn_s_sleep(2);
             ++it;
         }
@@ -2410,22 +2427,37 @@ __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, 
     if (base >= n) return;                           // workgroup-uniform
     const int W = d.W, H = d.H, Wb = d.bstride;
     const uint8_t* __restrict__ img = d.blurred + VO_BLUR_X0;
+    [[maybe_unused]] const int sslot = 1000 + blockIdx.x * DP_WAVES + wave;
+    VO_STAMP(d, sslot, 0);
     const bool valid = base + lane < n;
     const int2 kp = valid ? d.kps[(size_t)cur * d.N + base + lane] : make_int2(d.bcol, d.brow);
     // 1. pattern samples, rows u = wave, wave + DP_WAVES, ...
     for (int u = wave; u < NP; u += DP_WAVES)
         s_I[u][lane] = (float)img[(size_t)(kp.y + (int)c_ppt[u].y) * Wb + (kp.x + (int)c_ppt[u].x)];
     __syncthreads();
+    VO_STAMP(d, sslot, 1);
     // 2. terms of chunk c into ring slot c & 1 by waves 1 .. DP_WAVES - 1 (term t of the chunk by wave
     //    1 + t % (DP_WAVES - 1)); wave 0 sums chunk c - 1 meanwhile
+    //    A wave's terms of a chunk are a fixed unrolled run (j = wave - 1 + 7 i) over the padded
+    //    tables, so its scalar loads and LDS reads are all in flight at once (the loop with a
+    //    data-dependent exit and a byte table in global memory left wave 0 waiting at every chunk
+    //    barrier: 47k of the wave's 62k cycles)
+    static_assert(DP_CH == DP_CHUNK, "k_describe_pf's chunk is its tables' padding unit");
+    const unsigned char* sIb = reinterpret_cast<const unsigned char*>(&s_I[0][0]) + 4 * lane;
     auto terms = [&](int c) {
-        for (int j = wave - 1; j < DP_CH; j += DP_WAVES - 1) {
-            const int t = c * DP_CH + j;
-            if (t >= VO_FREAK_NPAIRS) break;
-            const float4 tb = c_orient_u[t];
-            const float ic = s_I[c_pair[t].x][lane] - s_I[c_pair[t].y][lane];
-            const ds_f2 i2 = {ic, ic};
-            s_t[c & 1][j][lane] = __builtin_elementwise_fma(i2, ds_f2{tb.x, tb.y}, i2 * ds_f2{tb.z, tb.w});
+        constexpr int TPW = (DP_CH + DP_WAVES - 2) / (DP_WAVES - 1);
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            const int j = wave - 1 + (DP_WAVES - 1) * i;
+            if (j < DP_CH) {
+                const int t = c * DP_CH + j;
+                const float4 tb = c_orient_pf[t];
+                const uint32_t po = c_pairoff[t];
+                const float ic = *reinterpret_cast<const float*>(sIb + (po & 0xFFFFu)) -
+                                 *reinterpret_cast<const float*>(sIb + (po >> 16));
+                const ds_f2 i2 = {ic, ic};
+                s_t[c & 1][j][lane] = __builtin_elementwise_fma(i2, ds_f2{tb.x, tb.y}, i2 * ds_f2{tb.z, tb.w});
+            }
         }
     };
     ds_f2 oxy = {0.0f, 0.0f};
@@ -2441,6 +2473,7 @@ __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, 
         }
         __syncthreads();
     }
+    VO_STAMP(d, sslot, 2);
     // 3. angle and rotation (wave 0), as describe_wave
     if (wave == 0) {
         const float ox = oxy.x, oy = oxy.y;
@@ -2452,6 +2485,7 @@ __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, 
         s_s[lane] = (float)sd;
     }
     __syncthreads();
+    VO_STAMP(d, sslot, 3);
     // 4. rotated samples (quirk 4), rows u = wave, wave + DP_WAVES, ...
     {
         const float c = s_c[lane], s = s_s[lane], ms = -1.0f * s;
@@ -2466,6 +2500,7 @@ __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, 
         }
     }
     __syncthreads();
+    VO_STAMP(d, sslot, 4);
     // 5. the 512 tests: words wave and wave + 8 of 16
     {
         const uint32_t* rot = reinterpret_cast<const uint32_t*>(&s_I[0][0]);
@@ -2490,6 +2525,7 @@ __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, 
             if (wave == 0) d.pre[(size_t)cur * d.N + base + lane] = w0;
         }
     }
+    VO_STAMP(d, sslot, 5);
 }
 
 // ---------------------------------------------------------------------------
@@ -3036,7 +3072,8 @@ __device__ __forceinline__ double sel9(const double (&a)[9], int c)
 // computeFundamentalMatrix on a minimal sample (ransac.cpp:63-93) for the lane group's
 // hypothesis: Gauss-Jordan with complete pivoting exactly as oracle nullvec_8x9 (pivot = max
 // |a| over unused rows/cols, ties to the first in row-major order), lane r holding row r.
-__device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], int r, int gbase, double F[9])
+__device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], int r, int gbase, double F[9],
+                             [[maybe_unused]] const VoDev* sd = nullptr, [[maybe_unused]] int sk = 0)
 {
     double P[8][4];
 #pragma unroll
@@ -3058,6 +3095,9 @@ __device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], in
     }
     sc1 = sqrt(2.0) / sqrt(sc1 / 8.0);
     sc2 = sqrt(2.0) / sqrt(sc2 / 8.0);
+#ifdef VO_STAMPS
+    if (sd) { __builtin_amdgcn_s_waitcnt(0); VO_STAMP(*sd, sk, 3); }   // points loaded, normalisation done
+#endif
     const double o1x = -(sc1 * mx1), o1y = -(sc1 * my1), o2x = -(sc2 * mx2), o2y = -(sc2 * my2);
     double x1 = 0, y1 = 0, x2 = 0, y2 = 0;
 #pragma unroll
@@ -3133,6 +3173,9 @@ __device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], in
             }
         }
     }
+#ifdef VO_STAMPS
+    if (sd) VO_STAMP(*sd, sk, 4);                   // Gauss-Jordan done
+#endif
     int fc = 0;
 #pragma unroll
     for (int j = 8; j >= 0; --j) if (!((used_c >> j) & 1u)) fc = j;
@@ -3189,6 +3232,99 @@ __device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], in
 // inliers of the group's F among the first `scored` matches: lane r tests matches 8 j + r of
 // each 64-match word, the group's byte of each ballot is shifted into the word (bit i = match
 // i); the words go to `mask` (k_refit compacts the best set from it)
+#ifndef RS_COUNT_ILP
+#define RS_COUNT_ILP 1
+#endif
+// Two forms by register budget: the batched launches (k_ransac_hyp: many waves per SIMD) take four
+// chains and no prefetch (152 VGPRs, 3 waves per SIMD); the latency launches (k_ransac_fused: the
+// per-frame call and the stage API, about one wave per SIMD) take eight chains and the prefetch.
+#ifndef RS_HYP_J
+#define RS_HYP_J 4                     // Sampson chains in flight per lane
+#endif
+#ifndef RS_HYP_PF
+#define RS_HYP_PF 0                    // the next word's points loaded before this word's tests
+#endif
+#ifndef RS_FUSED_J
+#define RS_FUSED_J 8
+#endif
+#ifndef RS_FUSED_PF
+#define RS_FUSED_PF 1
+#endif
+#if RS_COUNT_ILP
+// The word's eight Sampson tests as one branch-free stream (each step over j = 0..7, so eight
+// independent f64 chains are in flight), the threshold form hoisted out of the loop, and the next
+// word's points loaded before this word's tests.  The per-match arithmetic is sampson_inlier's,
+// operation for operation (computeSampsonError, ransac.cpp:12-23): the same values, the same
+// roundings.  (The single-chain form, RS_COUNT_ILP=0, issued one Sampson at a time behind two
+// exec-mask branches: 4.3k cycles per word for a lone wave.)
+template <bool ONE, int RS_COUNT_J, bool RS_COUNT_PREFETCH>
+__device__ __forceinline__ int count_words(const double* __restrict__ pts, int scored, const double* F, double thr,
+                                           int h, int r, bool store, uint64_t* __restrict__ mask)
+{
+    const int nw = (scored + 63) >> 6;
+    const bool deg_in = 1.7976931348623157e308 < thr;     // sampson() of a degenerate match
+    const double F0 = F[0], F1 = F[1], F2 = F[2], F3 = F[3], F4 = F[4], F5 = F[5], F6 = F[6], F7 = F[7], F8 = F[8];
+    int cnt = 0;
+    double2 a[8], c[8];
+    auto ld = [&](int w) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int i = min(w * 64 + j * 8 + r, scored - 1);   // in range; lanes past scored test nothing
+            const double2* p = reinterpret_cast<const double2*>(pts + 4 * (size_t)i);
+            a[j] = p[0]; c[j] = p[1];
+        }
+    };
+    if (RS_COUNT_PREFETCH && nw > 0) ld(0);
+    for (int w = 0; w < nw; ++w) {
+        if (!RS_COUNT_PREFETCH) ld(w);
+        double x[8], y[8], xp[8], yp[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { x[j] = a[j].x; y[j] = a[j].y; xp[j] = c[j].x; yp[j] = c[j].y; }
+        if (RS_COUNT_PREFETCH && w + 1 < nw) ld(w + 1);
+        uint64_t word = 0ull;
+#pragma unroll
+        for (int q = 0; q < 8; q += RS_COUNT_J) {          // RS_COUNT_J chains in flight
+            double Fx0[RS_COUNT_J], Fx1[RS_COUNT_J], Ft0[RS_COUNT_J], Ft1[RS_COUNT_J], Ft2[RS_COUNT_J], v[RS_COUNT_J];
+#pragma unroll
+            for (int u = 0; u < RS_COUNT_J; ++u) Fx0[u] = (F0 * x[q + u] + F1 * y[q + u]) + F2 * 1.0;
+#pragma unroll
+            for (int u = 0; u < RS_COUNT_J; ++u) Fx1[u] = (F3 * x[q + u] + F4 * y[q + u]) + F5 * 1.0;
+#pragma unroll
+            for (int u = 0; u < RS_COUNT_J; ++u) Ft0[u] = (F0 * xp[q + u] + F3 * yp[q + u]) + F6 * 1.0;
+#pragma unroll
+            for (int u = 0; u < RS_COUNT_J; ++u) Ft1[u] = (F1 * xp[q + u] + F4 * yp[q + u]) + F7 * 1.0;
+#pragma unroll
+            for (int u = 0; u < RS_COUNT_J; ++u) Ft2[u] = (F2 * xp[q + u] + F5 * yp[q + u]) + F8 * 1.0;
+#pragma unroll
+            for (int u = 0; u < RS_COUNT_J; ++u) v[u] = (Ft0[u] * x[q + u] + Ft1[u] * y[q + u]) + Ft2[u] * 1.0;
+#pragma unroll
+            for (int u = 0; u < RS_COUNT_J; ++u) {
+                const int j = q + u;
+                const double num = v[u] * v[u];
+                const double den = ((Fx0[u] * Fx0[u] + Fx1[u] * Fx1[u]) + Ft0[u] * Ft0[u]) + Ft1[u] * Ft1[u];
+                bool in;
+                if constexpr (ONE) in = num < den;         // num / den < 1.0 exactly when num < den
+                else in = num / den < thr;
+                in = den < 1e-12 ? deg_in : in;
+                in = in && w * 64 + j * 8 + r < scored;
+                const unsigned long long bal = ballot64(in);
+                word |= ((bal >> (8 * h)) & 0xFFull) << (8 * j);
+            }
+        }
+        cnt += __popcll(word);
+        if (store && r == (w & 7)) mask[w] = word;
+    }
+    return cnt;
+}
+template <int J, bool PF>
+__device__ __forceinline__ int count_inliers_group(const double* __restrict__ pts, int scored, const double* F, double thr,
+                                                   int h, int r, bool store, uint64_t* __restrict__ mask)
+{
+    return thr == 1.0 ? count_words<true, J, PF>(pts, scored, F, thr, h, r, store, mask)
+                      : count_words<false, J, PF>(pts, scored, F, thr, h, r, store, mask);
+}
+#else
+template <int J, bool PF>
 __device__ int count_inliers_group(const double* __restrict__ pts, int scored, const double* F, double thr,
                                    int h, int r, bool store, uint64_t* __restrict__ mask)
 {
@@ -3218,6 +3354,7 @@ __device__ int count_inliers_group(const double* __restrict__ pts, int scored, c
     }
     return cnt;
 }
+#endif
 
 // SVD of a 3x3 A (mirror of oracle svd3): min_eigvec3 + one 2x2 Jacobi rotation
 __device__ void svd3(const double* A, double* U, double* S, double* Vt)
@@ -3333,7 +3470,7 @@ __device__ void inv4(const double* M, double* Inv)
 // exits at once, dispatches reps times fewer workgroups
 // One chunk [k0, k1) of the hypotheses on workgroups bx of nbx.  ready (the fused form): the chunk's
 // replay publishes w->ready1 when it is done (k0 == 0), or the chunk waits for it first (k0 > 0).
-template <int HPB>
+template <int HPB, int CJ, bool CPF>
 __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int nhyp, int stage, int reps, int bx,
                                              int nbx, bool ready)
 {
@@ -3347,7 +3484,9 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
         __shared__ unsigned s_to;
         if (threadIdx.x == 0) {
             unsigned it = 0u;
-            while (__hip_atomic_load((gu32*)&w->ready1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+            // relaxed polls, one acquire fence after the barrier (an acquire poll invalidates the
+            // XCD's L2 on every iteration, under the first chunk's waves: 31.7 us vs 2 x 5.5 us)
+            while (__hip_atomic_load((gu32*)&w->ready1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
                    it < (1u << 22)) {
                 __builtin_amdgcn_s_sleep(2);
                 ++it;
@@ -3399,7 +3538,7 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
             }
             VO_STAMP(d, k, 1);
             double F[9];
-            fit_F8_group(pts, s8, r, lane & ~7, F);
+            fit_F8_group(pts, s8, r, lane & ~7, F, &d, k);
             VO_STAMP(d, k, 2);
             rank2(F);
             VO_STAMP(d, k, 5);
@@ -3409,7 +3548,7 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
                 for (int j = 0; j < 9; ++j)
                     if (j == r || (j == 8 && r == 0)) hf[j] = F[j];   // lane r: F[r]; lane 0 also F[8]
             }
-            const int cnt = count_inliers_group(pts, scored, F, d.sampson_thr, h, r, mine,
+            const int cnt = count_inliers_group<CJ, CPF>(pts, scored, F, d.sampson_thr, h, r, mine,
                                                 d.inlmask + ((size_t)wf * d.max_hyp + min(k, nhyp - 1)) * d.mask_words);
             if (mine && r == 0) st_sc1(counts + k, cnt);
             VO_STAMP(d, k, 6);
@@ -3458,19 +3597,27 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
     }
 }
 
+#ifndef RS_WAVES_EU
+#define RS_WAVES_EU 0                  // 0: the compiler's register budget
+#endif
+#if RS_WAVES_EU
+#define RS_OCC __attribute__((amdgpu_waves_per_eu(RS_WAVES_EU)))
+#else
+#define RS_OCC
+#endif
 template <int HPB>
-__global__ void __launch_bounds__(64 * HPB) k_ransac_hyp(VoDev d, int k0, int k1, int nhyp, int stage, int reps)
+__global__ void __launch_bounds__(64 * HPB) RS_OCC k_ransac_hyp(VoDev d, int k0, int k1, int nhyp, int stage, int reps)
 {
-    ransac_chunk<HPB>(d, k0, k1, nhyp, stage, reps, blockIdx.x, gridDim.x, false);
+    ransac_chunk<HPB, RS_HYP_J, RS_HYP_PF>(d, k0, k1, nhyp, stage, reps, blockIdx.x, gridDim.x, false);
 }
 // one frame's two chunks in one launch (the per-frame call and the stage API: one launch and one
 // dependent-launch gap less): workgroups [0, b0) run [0, c0) and publish its replay; the rest wait
 // for it and run [c0, nhyp) as the second launch would
 template <int HPB>
-__global__ void __launch_bounds__(64 * HPB) k_ransac_fused(VoDev d, int c0, int nhyp, int stage, int b0)
+__global__ void __launch_bounds__(64 * HPB) RS_OCC k_ransac_fused(VoDev d, int c0, int nhyp, int stage, int b0)
 {
-    if ((int)blockIdx.x < b0) ransac_chunk<HPB>(d, 0, c0, nhyp, stage, 1, blockIdx.x, b0, true);
-    else ransac_chunk<HPB>(d, c0, nhyp, nhyp, stage, 1, blockIdx.x - b0, gridDim.x - b0, true);
+    if ((int)blockIdx.x < b0) ransac_chunk<HPB, RS_FUSED_J, RS_FUSED_PF>(d, 0, c0, nhyp, stage, 1, blockIdx.x, b0, true);
+    else ransac_chunk<HPB, RS_FUSED_J, RS_FUSED_PF>(d, c0, nhyp, nhyp, stage, 1, blockIdx.x - b0, gridDim.x - b0, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -4619,8 +4766,17 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
     static const int segt = getenv("VO_STSEG") ? atoi(getenv("VO_STSEG")) : ST_SEGT_DEFAULT;
     // one frame (the per-frame call): segments of one tile row, so the frame's waves (4x 8-tile
     // segments' count) each walk 30 source rows instead of 142 -- the latency of the launch
-    const int st = write_response ? 4 : nb == 1 && d.single ? 1
-                 : segt == 4 || segt == 5 || segt == 6 || segt == 8 ? segt : ST_SEGT_DEFAULT;
+    int st = write_response ? 4 : nb == 1 && d.single ? 1
+           : segt == 4 || segt == 5 || segt == 6 || segt == 8 ? segt : ST_SEGT_DEFAULT;
+    // a small batch (a sequence's ragged last batch): shorter segments until the launch has two
+    // waves per SIMD, since its latency is one wave's walk down its segment (8 frames at 6-tile
+    // segments: 352 waves of 110 rows, 89 us; at one-tile segments 2112 waves of 30 rows)
+    static const bool seg_adapt = !(getenv("VO_STSEG_ADAPT") && atoi(getenv("VO_STSEG_ADAPT")) == 0);
+    if (seg_adapt && !write_response && st > 1) {
+        const int steps[4] = {6, 5, 4, 1};
+        for (int i = 0; i < 4 && (size_t)nb * nsx * ((nty + st - 1) / st) < 2048; ++i)
+            if (steps[i] < st) st = steps[i];
+    }
     // the FLAT form for NMS margins of 5+ (the reference's 35 / 37; VO_ST_FLAT=1 turns it on); the
     // general form keeps the border masks (small margins, the response map)
     static const int flat_env = getenv("VO_ST_FLAT") ? atoi(getenv("VO_ST_FLAT")) : ST_FLAT_DEFAULT;

@@ -406,7 +406,19 @@ def run_variants(args, ctx, W, H, frames0, gt0, extra, Context) -> dict:
         for f in range(nf):
             ctx.process_frame(frames0[f])
     out["process_frame"] = {"fps": timed_rate(per_frame, nf, 2), "frames": nf,
-                            "note": "one vo_process_frame call per frame (H2D + extract + pose + D2H, host sync)"}
+                            "note": "one vo_process_frame call per frame from pageable numpy frames (staging copy "
+                                    "+ extract + pose + pose row back, host sync)"}
+    hpf = ctx.host_frames(frames0[:nf])
+
+    def per_frame_pinned():
+        ctx.reset()
+        for f in range(nf):
+            ctx.process_frame(hpf.array[f])
+    out["process_frame"]["pinned_source_fps"] = timed_rate(per_frame_pinned, nf, 2)
+    out["process_frame"]["pinned_source_note"] = ("the same calls with the frames in pinned host memory "
+                                                  "(vo_host_alloc): the stencil reads each frame over PCIe "
+                                                  "where it lies, no staging copy")
+    hpf.free()
     # config 4: 1920x1080, N = 4096, 32-test and 512-test matching
     if "x1080" in extra:
         fr, seq = extra["x1080"]

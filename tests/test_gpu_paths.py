@@ -422,7 +422,12 @@ from acs_visual_odometry_amd import Context
 d = np.load(sys.argv[2])
 ctx = Context(int(d["W"]), int(d["H"]), K=d["K"])
 ctx.set_ground_truth(d["gt"])
-rows = [ctx.process_frame(f) for f in d["frames"]]
+import os
+hf = ctx.host_frames(d["frames"]) if "VO_PF_PINNED_DIRECT" in os.environ else None
+src = hf.array if hf is not None else d["frames"]
+rows = [ctx.process_frame(f) for f in src]
+if hf is not None:
+    hf.free()
 ctx.close()
 ok = np.array_equal(np.array([r[1] for r in rows]), d["st"]) and \
      np.array_equal(np.stack([r[0] for r in rows]), d["poses"]) and \
@@ -432,12 +437,12 @@ print("PF_OK" if ok else "PF_DIFF")
 
 
 @pytest.mark.parametrize("env", ["VO_PF_ZEROCOPY=0", "VO_DS_LDS_TABLE=1", "VO_DS_PF=0", "VO_RANSAC_FUSED=0",
-                                 "VO_SEL_FUSED=1", "VO_PF_OUT_ZC=0"])
+                                 "VO_SEL_FUSED=1", "VO_PF_OUT_ZC=0", "VO_PF_PINNED_DIRECT=0"])
 def test_per_frame_knobs_match_oracle(leak_case, tmp_path, env):
     """Per-frame-call knobs read once per process (the upload kernel instead of the stencil reading
     the frame from the pinned staging buffer, describe's LDS pair table, the one-wave describe instead
     of k_describe_pf, the two RANSAC launches instead of k_ransac_fused, the one-launch select, the
-    output row through a device copy), in a child process over the leak sequence: one
+    output row through a device copy, pinned caller frames staged instead of read in place), in a child process over the leak sequence: one
     vo_process_frame per frame, rows, statuses and counts equal the oracle's."""
     import sys
     seq, frames, ref = leak_case
@@ -449,6 +454,25 @@ def test_per_frame_knobs_match_oracle(leak_case, tmp_path, env):
     out = subprocess.run([sys.executable, "-c", _PF_SCRIPT, ROOT, str(npz)], capture_output=True,
                          text=True, timeout=240, env={**os.environ, **kv})
     assert "PF_OK" in out.stdout, (out.stdout[-2000:], out.stderr[-2000:])
+
+
+def test_per_frame_call_from_pinned_frames(leak_case):
+    """vo_process_frame on frames that already lie in pinned host memory (vo_host_alloc, one block
+    holding the whole sequence, each frame at its offset): the stencil reads each frame in place,
+    no staging copy, and every pose row, status and count equals the oracle's."""
+    seq, frames, ref = leak_case
+    ctx = Context(seq.W, seq.H, K=seq.K)
+    ctx.set_ground_truth(seq.gt())
+    hf = ctx.host_frames(frames)
+    for f in range(len(frames)):
+        pose, st, info = ctx.process_frame(hf.array[f])
+        assert st == ref[f][1], f
+        assert np.array_equal(pose, ref[f][0]), f
+        assert np.array_equal(info[:6], ref[f][2][:6]), f
+    hf.array[0] = 0                                # the block still belongs to the caller
+    hf.free()
+    assert ctx.device_errors() == 0
+    ctx.close()
 
 
 def test_per_frame_call_with_row_stride(leak_case):

@@ -17,13 +17,17 @@ seq = SceneSequence(nframes=n, step=1.0)
 frames = seq.frames()
 ctx = Context(seq.W, seq.H, K=seq.K)
 ctx.set_ground_truth(seq.gt())
+hf = ctx.host_frames(frames) if os.environ.get("PF_PINNED") == "1" else None   # frames in pinned memory
+src = hf.array if hf is not None else frames
 for rep in range(2):
     ctx.reset()
     ts = []
     for f in range(n):
         t0 = time.perf_counter()
-        ctx.process_frame(frames[f])
+        ctx.process_frame(src[f])
         ts.append(time.perf_counter() - t0)
     ts = np.array(ts[5:]) * 1e6
-    print(f"rep {rep}: per call median {np.median(ts):.1f} us, mean {ts.mean():.1f} us, min {ts.min():.1f} us")
+    print(f"{'pinned' if hf is not None else 'pageable'} rep {rep}: per call median {np.median(ts):.1f} us, mean {ts.mean():.1f} us, min {ts.min():.1f} us")
+if hf is not None:
+    hf.free()
 ctx.close()

@@ -2,7 +2,8 @@
 """k_describe anatomy from s_memtime stamps (diagnostic VO_STAMPS build): median cycles per
 phase of a describe wave (32 keypoints), over the waves of a 64-frame batched run.
 usage: VO_LIB_PATH=acs_visual_odometry_amd/libvo_mi355x_stamps.so [PF=1] python tools/stamps_describe.py
-PF=1: one vo_process_frame call per sample (the per-frame path's describe launch)."""
+PF=1: one vo_process_frame call per sample (the per-frame path's k_describe_pf launch, wave 0 of
+each 8-wave workgroup: its phase 2 is the in-order sum of the terms the other waves computed)."""
 import ctypes as C
 import os
 import sys
@@ -36,6 +37,8 @@ for rep in range(10):
     buf = np.zeros(2000 * 16, np.uint64)
     L.vo_debug_stamps(ctx.h, buf.ctypes.data_as(C.c_void_p), buf.size)
     t = buf[1000 * 16:1900 * 16].reshape(900, 16)[:, :6].astype(np.int64)
+    if PF:
+        t = t[:256:8]         # k_describe_pf: wave 0 of each workgroup (slot 1000 + 8 b + wave)
     t = t[(t > 0).all(axis=1)]
     rows.append(np.diff(t, axis=1))
     spans.append(t[:, 5].max() - t[:, 0].min())

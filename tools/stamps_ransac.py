@@ -23,8 +23,8 @@ ctx = Context(seq.W, seq.H, K=seq.K)
 ctx.set_ground_truth(seq.gt())
 L = load()
 L.vo_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
-names = ["sample8", "fit (normalize, Gauss-Jordan, denormalize)", "rank 2 (3x3 min eigenvector)", "hypF store + Sampson count"]
-idx = [0, 1, 2, 5, 6]
+names = ["sample8", "point loads + normalisation", "Gauss-Jordan (8 steps)", "back substitution + denormalize", "rank 2 (3x3 min eigenvector)", "hypF store + Sampson count"]
+idx = [0, 1, 3, 4, 2, 5, 6]
 rows = []
 if STAGE:
     import oracle as O
@@ -49,8 +49,9 @@ for rep in range(10):
     nk = 2000 if STAGE else 100
     t = buf[:nk * 16].reshape(nk, 16)[:, idx].astype(np.int64)
     t = t[(t > 0).all(axis=1)]
-    # order: 0 entry, 1 after sample8, 2 after the fit, 5 after rank 2, 6 after the count (a wave = 8 hypotheses)
-    d = np.stack([t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2], t[:, 4] - t[:, 3]], 1)
+    # order: 0 entry, 1 after sample8, 3 after the normalisation, 4 after Gauss-Jordan, 2 after the fit,
+    # 5 after rank 2, 6 after the count (a wave = 8 hypotheses)
+    d = np.diff(t, axis=1)
     rows.append(d)
 R = np.concatenate(rows)
 print(f"hypothesis waves sampled: {len(R)}")
