@@ -22,4 +22,6 @@ python3 -c "import json; d=json.load(open('$O/b.json')); print('0.12', round(d['
 done
 VO_SERIAL=1 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_LDS --output-format csv -d $O/stall -o stall -- python3 bench.py --steps 1 --warmup 1 --no-cpu --no-variants --sequences 1 --motion 0.12 > $O/stall.json 2> $O/stall.err || { echo PMC_FAIL; tail -5 $O/stall.err; exit 1; }
 python3 tools/pmc_stall.py $(ls $O/stall/*counter_collection.csv | head -1)
+
+timeout -k 10 60 ./tools/f64_lat > $O/f64_lat.txt 2>&1 && cat $O/f64_lat.txt
 echo DONE
