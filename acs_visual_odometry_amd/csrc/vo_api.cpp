@@ -485,11 +485,17 @@ void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax,
         if (rc && ev && !ev->err) ev->err = rc;
         if (rc) c->mt_err = rc;
     }
-    timed(c, ev, 4, s, [&] { vo::launch_ransac(d, 0, s); });
+    // pipelined: the later hypothesis chunks run on the fit queue, after the first chunk's replay,
+    // so the next pass's match and first chunk overlap them (the pass's buffer set is its own; the
+    // reference-sampler mode's sample table is not, so it keeps every chunk on the pose queue)
+    static const bool split_env = !(getenv("VO_RANSAC_SPLIT") && atoi(getenv("VO_RANSAC_SPLIT")) == 0);
+    const bool split = pipelined && split_env && d.rng_mode != VO_RNG_MT19937;
+    timed(c, ev, 4, s, [&] { vo::launch_ransac(d, 0, s, split ? 1 : 0); });
     if (pipelined) {
         (void)hipEventRecord(c->ev_rs[p % vo_ctx::kPassEv], s);
         (void)hipStreamWaitEvent(sf, c->ev_rs[p % vo_ctx::kPassEv], 0);
     }
+    if (split) timed(c, ev, 4, sf, [&] { vo::launch_ransac(d, 0, sf, 2); });
     timed(c, ev, 5, sf, [&] { vo::launch_refit(d, 1, 0, sf); });
     if (single) {
         // one frame: triangulation, finalize and the trajectory chain in one launch (its last
@@ -867,9 +873,10 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     c->split = VO_EXT_QUEUES >= 2 && (getenv("VO_SPLIT") ? atoi(getenv("VO_SPLIT")) != 0 : VO_SPLIT_DEFAULT != 0);
     c->slack = getenv("VO_SLACK") ? std::max(0, std::min(64, atoi(getenv("VO_SLACK")))) : VO_SLACK_DEFAULT;
     d.fault_inject = getenv("VO_FAULT_INJECT") && atoi(getenv("VO_FAULT_INJECT")) != 0;   // tests only
-    // the per-frame call's select in one launch: measured slower (21.2 us against 9.0 + 9.2 us for the two
-    // kernels, gpurun_out r5e), so opt-in (VO_SEL_FUSED=1)
-    d.sel_fused = getenv("VO_SEL_FUSED") && atoi(getenv("VO_SEL_FUSED")) != 0;
+    // the per-frame call's select in one launch (VO_SEL_FUSED=0: two launches).  With acquire polls it
+    // was slower (21.2 us against 9.0 + 9.2 us, gpurun_out r5e: each poll invalidated the XCD's L2);
+    // with relaxed polls the call is 1.5-1.9 us faster per frame (two alternating pairs, r5i)
+    d.sel_fused = !(getenv("VO_SEL_FUSED") && atoi(getenv("VO_SEL_FUSED")) == 0);
     d.ransac_fused = !(getenv("VO_RANSAC_FUSED") && atoi(getenv("VO_RANSAC_FUSED")) == 0);
     // repair windows hold two work records per frame (k_finalize): at most WB / 2 frames
     d.repair_win = std::max(1, std::min(d.WB / 2, getenv("VO_REPAIR_WIN") ? atoi(getenv("VO_REPAIR_WIN")) : VO_REPAIR_WIN_DEFAULT));

@@ -328,7 +328,8 @@ void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned
 void launch_ext_missing(const VoDev& d, int slot, hipStream_t s);   // extract side of a missing image
 // pose pass over the window (stage = 0) or over work[0] prepared by a stage API (stage = 1)
 void launch_match(const VoDev& d, int stage, hipStream_t s);        // + ordered compaction per frame
-void launch_ransac(const VoDev& d, int stage, hipStream_t s);       // all hypotheses + replay per frame
+void launch_ransac(const VoDev& d, int stage, hipStream_t s, int part = 0);   // all hypotheses + replay per frame
+// (part 1: only the first chunk [0, VO_HYP_CHUNK0) and its replay; part 2: only the later chunks)
 void launch_refit(const VoDev& d, int with_pose, int stage, hipStream_t s);
 // fin: the pass's finalize in the last workgroup of the launch (out / out_base as launch_finalize)
 void launch_triangulate(const VoDev& d, int stage, hipStream_t s, VoFrameOut* out = nullptr, int out_base = 0, int fin = 0);

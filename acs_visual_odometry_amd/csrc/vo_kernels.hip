@@ -2418,8 +2418,10 @@ __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, 
     constexpr int NP = VO_FREAK_NPOINTS;
     constexpr int NC = (VO_FREAK_NPAIRS + DP_CH - 1) / DP_CH;
     __shared__ float s_I[NP][64];                    // pattern samples (then the rotated samples, as u32)
-    __shared__ ds_f2 s_t[2][DP_CH][64];              // orientation terms, a chunk ahead
+    __shared__ ds_f2 s_t[2][DP_CH + 1][64];          // orientation terms, a chunk ahead (+ a spare row)
     __shared__ float s_c[64], s_s[64];
+    __shared__ float4 s_orient[DP_NPAD];
+    __shared__ uint32_t s_pairoff[DP_NPAD];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int cur = ext_slot(d, f0, 0, slot_override);
     const int n = d.ext_n[cur];
@@ -2431,6 +2433,11 @@ __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, 
     VO_STAMP(d, sslot, 0);
     const bool valid = base + lane < n;
     const int2 kp = valid ? d.kps[(size_t)cur * d.N + base + lane] : make_int2(d.bcol, d.brow);
+    // 0. the term tables into LDS
+    for (int t = threadIdx.x; t < DP_NPAD; t += 64 * DP_WAVES) {
+        s_orient[t] = c_orient_pf[t];
+        s_pairoff[t] = c_pairoff[t];
+    }
     // 1. pattern samples, rows u = wave, wave + DP_WAVES, ...
     for (int u = wave; u < NP; u += DP_WAVES)
         s_I[u][lane] = (float)img[(size_t)(kp.y + (int)c_ppt[u].y) * Wb + (kp.x + (int)c_ppt[u].x)];
@@ -2442,22 +2449,36 @@ __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, 
     //    tables, so its scalar loads and LDS reads are all in flight at once (the loop with a
     //    data-dependent exit and a byte table in global memory left wave 0 waiting at every chunk
     //    barrier: 47k of the wave's 62k cycles)
+    //    The tables come from LDS (copied at entry): scalar loads share lgkmcnt with the LDS
+    //    reads, so every term waited for its scalar load's full latency (54k cycles at wave 0)
     static_assert(DP_CH == DP_CHUNK, "k_describe_pf's chunk is its tables' padding unit");
     const unsigned char* sIb = reinterpret_cast<const unsigned char*>(&s_I[0][0]) + 4 * lane;
     auto terms = [&](int c) {
         constexpr int TPW = (DP_CH + DP_WAVES - 2) / (DP_WAVES - 1);
+        // branch-free (a wave's run past the chunk writes the spare row DP_CH), so the compiler
+        // issues the run's LDS reads together instead of three dependent round trips per term
+        // (in three sweeps -- the run's pair offsets, then its samples and weights, then the terms
+        // -- so each sweep's reads are in flight together)
+        uint32_t po[TPW];
+        float4 tb[TPW];
+        float ia[TPW], ib[TPW];
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
-            const int j = wave - 1 + (DP_WAVES - 1) * i;
-            if (j < DP_CH) {
-                const int t = c * DP_CH + j;
-                const float4 tb = c_orient_pf[t];
-                const uint32_t po = c_pairoff[t];
-                const float ic = *reinterpret_cast<const float*>(sIb + (po & 0xFFFFu)) -
-                                 *reinterpret_cast<const float*>(sIb + (po >> 16));
-                const ds_f2 i2 = {ic, ic};
-                s_t[c & 1][j][lane] = __builtin_elementwise_fma(i2, ds_f2{tb.x, tb.y}, i2 * ds_f2{tb.z, tb.w});
-            }
+            const int t = c * DP_CH + min(wave - 1 + (DP_WAVES - 1) * i, DP_CH - 1);
+            po[i] = s_pairoff[t];
+            tb[i] = s_orient[t];
+        }
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            ia[i] = *reinterpret_cast<const float*>(sIb + (po[i] & 0xFFFFu));
+            ib[i] = *reinterpret_cast<const float*>(sIb + (po[i] >> 16));
+        }
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            const int j = min(wave - 1 + (DP_WAVES - 1) * i, DP_CH);
+            const float ic = ia[i] - ib[i];
+            const ds_f2 i2 = {ic, ic};
+            s_t[c & 1][j][lane] = __builtin_elementwise_fma(i2, ds_f2{tb[i].x, tb[i].y}, i2 * ds_f2{tb[i].z, tb[i].w});
         }
     };
     ds_f2 oxy = {0.0f, 0.0f};
@@ -3244,6 +3265,9 @@ __device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], in
 #ifndef RS_HYP_PF
 #define RS_HYP_PF 0                    // the next word's points loaded before this word's tests
 #endif
+#ifndef RS_EARLY
+#define RS_EARLY 1                     // later chunks: a wave's count stops once it cannot pass the best
+#endif
 #ifndef RS_FUSED_J
 #define RS_FUSED_J 8
 #endif
@@ -3257,9 +3281,13 @@ __device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], in
 // operation for operation (computeSampsonError, ransac.cpp:12-23): the same values, the same
 // roundings.  (The single-chain form, RS_COUNT_ILP=0, issued one Sampson at a time behind two
 // exec-mask branches: 4.3k cycles per word for a lone wave.)
+// bound >= 0 (a later chunk of the pose pass): the count stops once no hypothesis of the wave can
+// end above `bound`, the previous replay's best -- the sequential loop only takes a count above its
+// running best, which is at least that.  Such a count is left partial (still <= bound, so the
+// replay decides the same) and so are its mask words (k_refit reads only the best hypothesis').
 template <bool ONE, int RS_COUNT_J, bool RS_COUNT_PREFETCH>
 __device__ __forceinline__ int count_words(const double* __restrict__ pts, int scored, const double* F, double thr,
-                                           int h, int r, bool store, uint64_t* __restrict__ mask)
+                                           int h, int r, bool store, uint64_t* __restrict__ mask, int bound)
 {
     const int nw = (scored + 63) >> 6;
     const bool deg_in = 1.7976931348623157e308 < thr;     // sampson() of a degenerate match
@@ -3281,7 +3309,11 @@ __device__ __forceinline__ int count_words(const double* __restrict__ pts, int s
 #pragma unroll
         for (int j = 0; j < 8; ++j) { x[j] = a[j].x; y[j] = a[j].y; xp[j] = c[j].x; yp[j] = c[j].y; }
         if (RS_COUNT_PREFETCH && w + 1 < nw) ld(w + 1);
-        uint64_t word = 0ull;
+        // the word's bits as lane masks (each test one v_cmp into SGPRs, combined by the scalar
+        // unit), then the group's byte of each mask into byte j of the lane's word: a per-lane
+        // 64-bit shift and one v_perm_b32 per j
+        uint32_t wlo = 0u, whi = 0u;
+        const unsigned sh = 8u * (unsigned)h;
 #pragma unroll
         for (int q = 0; q < 8; q += RS_COUNT_J) {          // RS_COUNT_J chains in flight
             double Fx0[RS_COUNT_J], Fx1[RS_COUNT_J], Ft0[RS_COUNT_J], Ft1[RS_COUNT_J], Ft2[RS_COUNT_J], v[RS_COUNT_J];
@@ -3302,32 +3334,41 @@ __device__ __forceinline__ int count_words(const double* __restrict__ pts, int s
                 const int j = q + u;
                 const double num = v[u] * v[u];
                 const double den = ((Fx0[u] * Fx0[u] + Fx1[u] * Fx1[u]) + Ft0[u] * Ft0[u]) + Ft1[u] * Ft1[u];
-                bool in;
-                if constexpr (ONE) in = num < den;         // num / den < 1.0 exactly when num < den
-                else in = num / den < thr;
-                in = den < 1e-12 ? deg_in : in;
-                in = in && w * 64 + j * 8 + r < scored;
-                const unsigned long long bal = ballot64(in);
-                word |= ((bal >> (8 * h)) & 0xFFull) << (8 * j);
+                const unsigned long long dg = ballot64(den < 1e-12);          // sampson() = DBL_MAX
+                unsigned long long bal;
+                if constexpr (ONE) bal = ballot64(num < den) & ~dg;      // num / den < 1.0 exactly when num < den
+                else bal = (ballot64(num / den < thr) & ~dg) | (deg_in ? dg : 0ull);
+                bal &= ballot64(w * 64 + j * 8 + r < scored);
+                const uint32_t b = (uint32_t)(bal >> sh);                    // byte 0: this group's tests
+                // byte j of the half-word from b's byte 0, the other bytes kept (selector 4 + k: byte k of
+                // the first operand; 0: byte 0 of the second)
+                constexpr uint32_t keep = 0x07060504u;
+                const uint32_t sel = keep & ~(0xFFu << (8 * (j & 3)));
+                if (j < 4) wlo = __builtin_amdgcn_perm(wlo, b, sel);
+                else whi = __builtin_amdgcn_perm(whi, b, sel);
             }
         }
+        const uint64_t word = (uint64_t)wlo | ((uint64_t)whi << 32);
         cnt += __popcll(word);
         if (store && r == (w & 7)) mask[w] = word;
+        if (bound >= 0 && ballot64(store && cnt + max(scored - (w + 1) * 64, 0) > bound) == 0ull) break;
     }
     return cnt;
 }
 template <int J, bool PF>
 __device__ __forceinline__ int count_inliers_group(const double* __restrict__ pts, int scored, const double* F, double thr,
-                                                   int h, int r, bool store, uint64_t* __restrict__ mask)
+                                                   int h, int r, bool store, uint64_t* __restrict__ mask,
+                                                   int bound = -1)
 {
-    return thr == 1.0 ? count_words<true, J, PF>(pts, scored, F, thr, h, r, store, mask)
-                      : count_words<false, J, PF>(pts, scored, F, thr, h, r, store, mask);
+    return thr == 1.0 ? count_words<true, J, PF>(pts, scored, F, thr, h, r, store, mask, bound)
+                      : count_words<false, J, PF>(pts, scored, F, thr, h, r, store, mask, bound);
 }
 #else
 template <int J, bool PF>
 __device__ int count_inliers_group(const double* __restrict__ pts, int scored, const double* F, double thr,
-                                   int h, int r, bool store, uint64_t* __restrict__ mask)
+                                   int h, int r, bool store, uint64_t* __restrict__ mask, int bound = -1)
 {
+    (void)bound;
     const bool one = thr == 1.0;
     const int nw = (scored + 63) >> 6;
     int cnt = 0;
@@ -3520,6 +3561,9 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
     int kbound = k1;
     if (k0 > 0 && w->best > 0 && d.maxit_tab[(size_t)M * (M + 1) / 2 + w->best] != 0xFFFFu)
         kbound = min(w->maxit, k1);
+    // counts past the previous replay's best only matter to the loop: a later chunk stops a wave's
+    // count once none of its hypotheses can pass it (not the stage API, which returns every count)
+    const int cbound = (RS_EARLY && k0 > 0 && !stage) ? w->best : -1;
     for (int rep = 0; rep < reps; ++rep, k += nbx * HPB * 8) {
         const int kb = k - h;                      // the wave's first hypothesis
         if (kb >= k1) break;                       // wave-uniform
@@ -3549,7 +3593,8 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
                     if (j == r || (j == 8 && r == 0)) hf[j] = F[j];   // lane r: F[r]; lane 0 also F[8]
             }
             const int cnt = count_inliers_group<CJ, CPF>(pts, scored, F, d.sampson_thr, h, r, mine,
-                                                d.inlmask + ((size_t)wf * d.max_hyp + min(k, nhyp - 1)) * d.mask_words);
+                                                d.inlmask + ((size_t)wf * d.max_hyp + min(k, nhyp - 1)) * d.mask_words,
+                                                cbound);
             if (mine && r == 0) st_sc1(counts + k, cnt);
             VO_STAMP(d, k, 6);
         }
@@ -4766,7 +4811,10 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
     static const int segt = getenv("VO_STSEG") ? atoi(getenv("VO_STSEG")) : ST_SEGT_DEFAULT;
     // one frame (the per-frame call): segments of one tile row, so the frame's waves (4x 8-tile
     // segments' count) each walk 30 source rows instead of 142 -- the latency of the launch
-    int st = write_response ? 4 : nb == 1 && d.single ? 1
+    // the per-frame call's segment (VO_PF_SEGT: 1 or 2 tile rows; 2 reads 1.44x the frame's rows over
+    // PCIe instead of 1.88x, in half as many waves of 46 source rows)
+    static const int pf_segt = getenv("VO_PF_SEGT") && atoi(getenv("VO_PF_SEGT")) == 2 ? 2 : 1;
+    int st = write_response ? 4 : nb == 1 && d.single ? pf_segt
            : segt == 4 || segt == 5 || segt == 6 || segt == 8 ? segt : ST_SEGT_DEFAULT;
     // a small batch (a sequence's ragged last batch): shorter segments until the launch has two
     // waves per SIMD, since its latency is one wave's walk down its segment (8 frames at 6-tile
@@ -4789,6 +4837,7 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
     else if (!flat) {
         switch (st) {
         case 1: ST_LAUNCH(1, false); break;
+        case 2: ST_LAUNCH(2, false); break;
         case 4: ST_LAUNCH(4, false); break;
         case 5: ST_LAUNCH(5, false); break;
         case 6: ST_LAUNCH(6, false); break;
@@ -4797,6 +4846,7 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
     } else {
         switch (st) {
         case 1: ST_LAUNCH(1, true); break;
+        case 2: ST_LAUNCH(2, true); break;
         case 4: ST_LAUNCH(4, true); break;
         case 5: ST_LAUNCH(5, true); break;
         case 6: ST_LAUNCH(6, true); break;
@@ -4808,7 +4858,20 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
 }
 void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s)
 {
-    if (d.sel1 && !(d.single && d.sel_emit_lds >= 0)) {   // single frames: always banded (8 workgroups, not 1)
+    // single frames always banded (8 workgroups, not 1); small batches too (a sequence's ragged last
+    // batch, VO_SEL_SMALL frames or fewer): the one-workgroup select asks for a whole CU's LDS, so
+    // under the pose queue's kernels it waits for a CU to drain (8 frames: 118 us against 25 us
+    // for 64 frames alone, gpurun_out r5j), while the banded kernels' 256-thread workgroups
+    // co-run.  (Whole batches keep the one-workgroup form: KITTI within noise either way.)
+    static const int sel_small = getenv("VO_SEL_SMALL") ? atoi(getenv("VO_SEL_SMALL")) : 16;
+    if (d.sel1 && d.sel_emit_lds >= 0 && nb <= sel_small && !d.single) {
+        const dim3 g(xcd_grid(VO_SEL_BANDS, nb));
+        const int cnt_lds = sel_band_layout((d.W + ST_TW - 1) / ST_TW, (d.H + ST_TH - 1) / ST_TH).bits;
+        hipLaunchKernelGGL(k_select_count, g, dim3(SL_T), (size_t)cnt_lds, s, d, f0, slot_override, nb);
+        hipLaunchKernelGGL(k_select_emit, g, dim3(SL_T), (size_t)d.sel_emit_lds, s, d, f0, slot_override, nb);
+        return;
+    }
+    if (d.sel1 && !(d.single && d.sel_emit_lds >= 0)) {
         hipLaunchKernelGGL(k_select, dim3(nb), dim3(1024), (size_t)d.sel_lds, s, d, f0, slot_override);
         return;
     }
@@ -4914,11 +4977,11 @@ void launch_match(const VoDev& d, int stage, hipStream_t s)
 // once when its replay has already stopped (ransac.cpp:139 adaptive bound; 100 hypotheses for
 // most frames).  One wave per hypothesis, four per workgroup: with B frames per launch there
 // are enough hypotheses to fill the chip, so no wave repeats another's 8-point fit.
-void launch_ransac(const VoDev& d, int stage, hipStream_t s)
+void launch_ransac(const VoDev& d, int stage, hipStream_t s, int part)
 {
     const int nhyp = d.max_hyp, nb = stage ? 1 : d.gridw;
     // (the per-frame call's window: one frame, two work records -- the repair form's second record)
-    if ((stage || d.single) && nb <= 2 && d.ransac_fused && nhyp > VO_HYP_CHUNK0) {
+    if (part == 0 && (stage || d.single) && nb <= 2 && d.ransac_fused && nhyp > VO_HYP_CHUNK0) {
         const int b0 = (VO_HYP_CHUNK0 + 31) / 32, b1 = (nhyp - VO_HYP_CHUNK0 + 31) / 32;
         hipLaunchKernelGGL((k_ransac_fused<4>), dim3(b0 + b1, nb), dim3(256), 0, s, d, VO_HYP_CHUNK0, nhyp, stage, b0);
         return;
@@ -4930,6 +4993,7 @@ void launch_ransac(const VoDev& d, int stage, hipStream_t s)
     for (int c = 0; c < 3; ++c) {
         const int k1 = cut[c];
         if (k1 <= k0) continue;
+        if ((part == 1 && c > 0) || (part == 2 && c == 0)) { k0 = k1; continue; }
         static const int r2 = getenv("VO_RREPS") ? std::max(1, atoi(getenv("VO_RREPS"))) : VO_HYP_REPS;
         const int reps = c == 0 ? 1 : (c == 1 ? std::max(1, r2 / 2) : r2);
         const int blocks = ((k1 - k0 + 31) / 32 + reps - 1) / reps;      // 32 hypotheses per workgroup
