@@ -464,7 +464,10 @@ VoDev pass_dev(const vo_ctx* c, int p)
 // triangulation and finalize on the fit queue, so the next pass's match overlaps them; the pass
 // first waits for pass p - 2's finalize (its buffer set and its state snapshot).  Otherwise every
 // kernel on the pose queue and the window comes from the state (every earlier pass finalized).
-void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax, bool pipelined, bool single = false)
+// first: the chunk's first pass (every earlier pass finalized: its window comes from the state,
+// d.nospec) -- pipelined or not, its own window needs no speculation
+void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax, bool pipelined, bool single = false,
+                  bool first = false)
 {
     hipStream_t s = c->s;
     const int p = c->npass++;
@@ -476,7 +479,7 @@ void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax,
         d.gridw = std::min(2, d.WB);
     }
     d.pass = p;
-    d.nospec = pipelined ? 0 : 1;
+    d.nospec = pipelined && !first ? 0 : 1;
     hipStream_t sf = pipelined ? c->sf : s;
     if (pipelined) (void)hipStreamWaitEvent(s, c->ev_fn[(p + vo_ctx::kPassEv - 2) % vo_ctx::kPassEv], 0);
     timed(c, ev, 3, s, [&] { vo::launch_match(d, 0, s); });
@@ -652,8 +655,13 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
             }
         }
         // the chunk's first pass sees every earlier pass finalized (the last call synchronised):
-        // its window comes from the state; later passes are pipelined
-        enqueue_pass(c, out, out_base, ev, base + f0s[k + 1], multi && c->pipeline && k > 0, host_frame);
+        // its window comes from the state.  Its refit, triangulation and finalize go to the fit
+        // queue like every later pass's (the next pass speculates on its window as on any
+        // pipelined one's), so pass 1's match need not wait for them (VO_PIPE_FIRST=0: the whole
+        // first pass on the pose queue)
+        static const bool pipe_first = !(getenv("VO_PIPE_FIRST") && atoi(getenv("VO_PIPE_FIRST")) == 0);
+        enqueue_pass(c, out, out_base, ev, base + f0s[k + 1], multi && c->pipeline && (k > 0 || pipe_first), host_frame,
+                     k == 0);
         return VO_OK;
     };
     if (!img0 && !hs) {

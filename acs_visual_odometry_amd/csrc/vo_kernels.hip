@@ -3253,9 +3253,6 @@ __device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], in
 // inliers of the group's F among the first `scored` matches: lane r tests matches 8 j + r of
 // each 64-match word, the group's byte of each ballot is shifted into the word (bit i = match
 // i); the words go to `mask` (k_refit compacts the best set from it)
-#ifndef RS_COUNT_ILP
-#define RS_COUNT_ILP 1
-#endif
 // Two forms by register budget: the batched launches (k_ransac_hyp: many waves per SIMD) take four
 // chains and no prefetch (152 VGPRs, 3 waves per SIMD); the latency launches (k_ransac_fused: the
 // per-frame call and the stage API, about one wave per SIMD) take eight chains and the prefetch.
@@ -3274,20 +3271,20 @@ __device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], in
 #ifndef RS_FUSED_PF
 #define RS_FUSED_PF 1
 #endif
-#if RS_COUNT_ILP
 // The word's eight Sampson tests as one branch-free stream (each step over j = 0..7, so eight
 // independent f64 chains are in flight), the threshold form hoisted out of the loop, and the next
 // word's points loaded before this word's tests.  The per-match arithmetic is sampson_inlier's,
 // operation for operation (computeSampsonError, ransac.cpp:12-23): the same values, the same
-// roundings.  (The single-chain form, RS_COUNT_ILP=0, issued one Sampson at a time behind two
-// exec-mask branches: 4.3k cycles per word for a lone wave.)
+// roundings.  (The single-chain form it replaced issued one Sampson at a time behind two exec-mask
+// branches: 4.3k cycles per word for a lone wave.)  w0, ws: the words w0, w0 + ws, ... (a split count)
 // bound >= 0 (a later chunk of the pose pass): the count stops once no hypothesis of the wave can
 // end above `bound`, the previous replay's best -- the sequential loop only takes a count above its
 // running best, which is at least that.  Such a count is left partial (still <= bound, so the
 // replay decides the same) and so are its mask words (k_refit reads only the best hypothesis').
 template <bool ONE, int RS_COUNT_J, bool RS_COUNT_PREFETCH>
 __device__ __forceinline__ int count_words(const double* __restrict__ pts, int scored, const double* F, double thr,
-                                           int h, int r, bool store, uint64_t* __restrict__ mask, int bound)
+                                           int h, int r, bool store, uint64_t* __restrict__ mask, int bound,
+                                           int w0 = 0, int ws = 1)
 {
     const int nw = (scored + 63) >> 6;
     const bool deg_in = 1.7976931348623157e308 < thr;     // sampson() of a degenerate match
@@ -3302,13 +3299,13 @@ __device__ __forceinline__ int count_words(const double* __restrict__ pts, int s
             a[j] = p[0]; c[j] = p[1];
         }
     };
-    if (RS_COUNT_PREFETCH && nw > 0) ld(0);
-    for (int w = 0; w < nw; ++w) {
+    if (RS_COUNT_PREFETCH && w0 < nw) ld(w0);
+    for (int w = w0; w < nw; w += ws) {
         if (!RS_COUNT_PREFETCH) ld(w);
         double x[8], y[8], xp[8], yp[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) { x[j] = a[j].x; y[j] = a[j].y; xp[j] = c[j].x; yp[j] = c[j].y; }
-        if (RS_COUNT_PREFETCH && w + 1 < nw) ld(w + 1);
+        if (RS_COUNT_PREFETCH && w + ws < nw) ld(w + ws);
         // the word's bits as lane masks (each test one v_cmp into SGPRs, combined by the scalar
         // unit), then the group's byte of each mask into byte j of the lane's word: a per-lane
         // 64-bit shift and one v_perm_b32 per j
@@ -3358,44 +3355,11 @@ __device__ __forceinline__ int count_words(const double* __restrict__ pts, int s
 template <int J, bool PF>
 __device__ __forceinline__ int count_inliers_group(const double* __restrict__ pts, int scored, const double* F, double thr,
                                                    int h, int r, bool store, uint64_t* __restrict__ mask,
-                                                   int bound = -1)
+                                                   int bound = -1, int w0 = 0, int ws = 1)
 {
-    return thr == 1.0 ? count_words<true, J, PF>(pts, scored, F, thr, h, r, store, mask, bound)
-                      : count_words<false, J, PF>(pts, scored, F, thr, h, r, store, mask, bound);
+    return thr == 1.0 ? count_words<true, J, PF>(pts, scored, F, thr, h, r, store, mask, bound, w0, ws)
+                      : count_words<false, J, PF>(pts, scored, F, thr, h, r, store, mask, bound, w0, ws);
 }
-#else
-template <int J, bool PF>
-__device__ int count_inliers_group(const double* __restrict__ pts, int scored, const double* F, double thr,
-                                   int h, int r, bool store, uint64_t* __restrict__ mask, int bound = -1)
-{
-    (void)bound;
-    const bool one = thr == 1.0;
-    const int nw = (scored + 63) >> 6;
-    int cnt = 0;
-    for (int w = 0; w < nw; ++w) {
-        double2 a[8], c[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int i = w * 64 + j * 8 + r;
-            if (i < scored) {
-                const double2* p = reinterpret_cast<const double2*>(pts + 4 * (size_t)i);
-                a[j] = p[0]; c[j] = p[1];
-            }
-        }
-        uint64_t word = 0ull;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int i = w * 64 + j * 8 + r;
-            const bool in = i < scored && sampson_inlier(F, a[j].x, a[j].y, c[j].x, c[j].y, thr, one);
-            const unsigned long long bal = ballot64(in);
-            word |= ((bal >> (8 * h)) & 0xFFull) << (8 * j);
-        }
-        cnt += __popcll(word);
-        if (store && r == (w & 7)) mask[w] = word;
-    }
-    return cnt;
-}
-#endif
 
 // SVD of a 3x3 A (mirror of oracle svd3): min_eigvec3 + one 2x2 Jacobi rotation
 __device__ void svd3(const double* A, double* U, double* S, double* Vt)
@@ -3511,10 +3475,14 @@ __device__ void inv4(const double* M, double* Inv)
 // exits at once, dispatches reps times fewer workgroups
 // One chunk [k0, k1) of the hypotheses on workgroups bx of nbx.  ready (the fused form): the chunk's
 // replay publishes w->ready1 when it is done (k0 == 0), or the chunk waits for it first (k0 > 0).
-template <int HPB, int CJ, bool CPF>
+// SP: waves per hypothesis set (1, or HPB: the latency form -- the workgroup's waves fit the same
+// eight hypotheses and split their count by words, the partial counts summed through LDS)
+template <int HPB, int CJ, bool CPF, int SP = 1>
 __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int nhyp, int stage, int reps, int bx,
                                              int nbx, bool ready)
 {
+    static_assert(SP == 1 || SP == HPB, "a split set is the whole workgroup (its barrier)");
+    constexpr int SETS = HPB / SP;                 // hypothesis sets (eight hypotheses each) per workgroup
     const int wf = blockIdx.y;                     // window frame
     if (wf >= vwin_count(d, stage)) return;
     VoWork* w = d.work + wf;
@@ -3550,7 +3518,8 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
     const int M = w->M, scored = w->scored;
     const double* pts = d.pts + (size_t)wf * 4 * d.N;
     int32_t* counts = d.counts + (size_t)wf * d.max_hyp;
-    int k = k0 + (bx * HPB + wave) * 8 + h;
+    const int set = wave / SP, sub = wave % SP;
+    int k = k0 + (bx * SETS + set) * 8 + h;
     // Hypotheses at or past the previous replay's bound are never evaluated by the sequential
     // loop: once an improvement updated maxIterations (best > 0 and its table entry is not the
     // 'denom == 0: no update' mark) and the loop went on past k0 (maxit > 100), the inlier ratio
@@ -3563,8 +3532,8 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
         kbound = min(w->maxit, k1);
     // counts past the previous replay's best only matter to the loop: a later chunk stops a wave's
     // count once none of its hypotheses can pass it (not the stage API, which returns every count)
-    const int cbound = (RS_EARLY && k0 > 0 && !stage) ? w->best : -1;
-    for (int rep = 0; rep < reps; ++rep, k += nbx * HPB * 8) {
+    const int cbound = (RS_EARLY && SP == 1 && k0 > 0 && !stage) ? w->best : -1;
+    for (int rep = 0; rep < reps; ++rep, k += nbx * SETS * 8) {
         const int kb = k - h;                      // the wave's first hypothesis
         if (kb >= k1) break;                       // wave-uniform
         const bool mine = k < kbound;
@@ -3586,19 +3555,29 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
             VO_STAMP(d, k, 2);
             rank2(F);
             VO_STAMP(d, k, 5);
-            if (mine) {
+            if (mine && sub == 0) {
                 double* hf = d.hypF + ((size_t)wf * d.max_hyp + k) * 9;
 #pragma unroll
                 for (int j = 0; j < 9; ++j)
                     if (j == r || (j == 8 && r == 0)) hf[j] = F[j];   // lane r: F[r]; lane 0 also F[8]
             }
-            const int cnt = count_inliers_group<CJ, CPF>(pts, scored, F, d.sampson_thr, h, r, mine,
+            int cnt = count_inliers_group<CJ, CPF>(pts, scored, F, d.sampson_thr, h, r, mine,
                                                 d.inlmask + ((size_t)wf * d.max_hyp + min(k, nhyp - 1)) * d.mask_words,
-                                                cbound);
-            if (mine && r == 0) st_sc1(counts + k, cnt);
+                                                cbound, sub, SP);
+            if constexpr (SP > 1) {
+                __shared__ int s_pc[HPB][64];
+                s_pc[wave][lane] = cnt;
+                __syncthreads();
+                if (sub == 0) {
+#pragma unroll
+                    for (int u = 1; u < SP; ++u) cnt += s_pc[wave + u][lane];
+                }
+                __syncthreads();                   // s_pc is rewritten by the next rep
+            }
+            if (mine && sub == 0 && r == 0) st_sc1(counts + k, cnt);
             VO_STAMP(d, k, 6);
         }
-        if (!mine && k < k1 && r == 0) st_sc1(counts + k, -1);   // skipped: the replay never takes it
+        if (!mine && k < k1 && sub == 0 && r == 0) st_sc1(counts + k, -1);   // skipped: the replay never takes it
     }
     unsigned* ctr = &w->ctr[k0 == 0 ? 1 : (k0 < VO_HYP_CHUNK1 ? 2 : 3)];   // one arrival counter per chunk
     if (!arrive_last(ctr, nbx, &s_last)) return;
@@ -3658,11 +3637,11 @@ __global__ void __launch_bounds__(64 * HPB) RS_OCC k_ransac_hyp(VoDev d, int k0,
 // one frame's two chunks in one launch (the per-frame call and the stage API: one launch and one
 // dependent-launch gap less): workgroups [0, b0) run [0, c0) and publish its replay; the rest wait
 // for it and run [c0, nhyp) as the second launch would
-template <int HPB>
+template <int HPB, int SP>
 __global__ void __launch_bounds__(64 * HPB) RS_OCC k_ransac_fused(VoDev d, int c0, int nhyp, int stage, int b0)
 {
-    if ((int)blockIdx.x < b0) ransac_chunk<HPB, RS_FUSED_J, RS_FUSED_PF>(d, 0, c0, nhyp, stage, 1, blockIdx.x, b0, true);
-    else ransac_chunk<HPB, RS_FUSED_J, RS_FUSED_PF>(d, c0, nhyp, nhyp, stage, 1, blockIdx.x - b0, gridDim.x - b0, true);
+    if ((int)blockIdx.x < b0) ransac_chunk<HPB, RS_FUSED_J, RS_FUSED_PF, SP>(d, 0, c0, nhyp, stage, 1, blockIdx.x, b0, true);
+    else ransac_chunk<HPB, RS_FUSED_J, RS_FUSED_PF, SP>(d, c0, nhyp, nhyp, stage, 1, blockIdx.x - b0, gridDim.x - b0, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -4982,8 +4961,14 @@ void launch_ransac(const VoDev& d, int stage, hipStream_t s, int part)
     const int nhyp = d.max_hyp, nb = stage ? 1 : d.gridw;
     // (the per-frame call's window: one frame, two work records -- the repair form's second record)
     if (part == 0 && (stage || d.single) && nb <= 2 && d.ransac_fused && nhyp > VO_HYP_CHUNK0) {
-        const int b0 = (VO_HYP_CHUNK0 + 31) / 32, b1 = (nhyp - VO_HYP_CHUNK0 + 31) / 32;
-        hipLaunchKernelGGL((k_ransac_fused<4>), dim3(b0 + b1, nb), dim3(256), 0, s, d, VO_HYP_CHUNK0, nhyp, stage, b0);
+        // VO_RANSAC_SPLIT_COUNT=1: the workgroup's four waves fit the same eight hypotheses and split
+        // their count (8 hypotheses per workgroup) instead of one wave per eight (32 per workgroup):
+        // measured slower, 138-140 vs 136.7 us per call (two alternating pairs, gpurun_out r5m)
+        static const bool spc = getenv("VO_RANSAC_SPLIT_COUNT") && atoi(getenv("VO_RANSAC_SPLIT_COUNT")) != 0;
+        const int hpw = spc ? 8 : 32;
+        const int b0 = (VO_HYP_CHUNK0 + hpw - 1) / hpw, b1 = (nhyp - VO_HYP_CHUNK0 + hpw - 1) / hpw;
+        if (spc) hipLaunchKernelGGL((k_ransac_fused<4, 4>), dim3(b0 + b1, nb), dim3(256), 0, s, d, VO_HYP_CHUNK0, nhyp, stage, b0);
+        else hipLaunchKernelGGL((k_ransac_fused<4, 1>), dim3(b0 + b1, nb), dim3(256), 0, s, d, VO_HYP_CHUNK0, nhyp, stage, b0);
         return;
     }
     // VO_HYP_CUT1: the second cut (VO_HYP_CHUNK1; >= max_hyp merges the last two chunks)

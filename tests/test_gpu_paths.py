@@ -393,7 +393,8 @@ print("KNOB_OK" if ok else "KNOB_DIFF")
                                        ("VO_EVENT_WAIT=0,VO_FORCE_WAIT_REFUSAL=1,VO_EXTQ=2", 8),
                                        ("VO_ST_FLAT=1", 64), ("VO_ST_FLAT=1,VO_STSEG=8", 64), ("VO_ST_FLAT=1", 8),
                                        ("VO_ST_PAIR=1", 16), ("VO_ST_PAIR=1", 8),
-                                       ("VO_SEL_LDS_KB=48", 64)])
+                                       ("VO_SEL_LDS_KB=48", 64), ("VO_PIPE_FIRST=0", 16), ("VO_RANSAC_SPLIT=0", 16),
+                                       ("VO_SEL_SMALL=0", 8), ("VO_STSEG_ADAPT=0", 8)])
 def test_process_knobs_match_oracle(leak_case, tmp_path, env, batch):
     """Knobs the library reads once per process (stencil segment height, RANSAC cut and loop,
     triangulation grid, alternating extract queues, XCD placement, the branch-free FLAT stencil),
@@ -438,13 +439,13 @@ print("PF_OK" if ok else "PF_DIFF")
 
 @pytest.mark.parametrize("env", ["VO_PF_ZEROCOPY=0", "VO_DS_LDS_TABLE=1", "VO_DS_PF=0", "VO_RANSAC_FUSED=0",
                                  "VO_SEL_FUSED=0", "VO_PF_OUT_ZC=0", "VO_PF_PINNED_DIRECT=0",
-                                 "VO_PF_SEGT=2"])
+                                 "VO_PF_SEGT=2", "VO_RANSAC_SPLIT_COUNT=1"])
 def test_per_frame_knobs_match_oracle(leak_case, tmp_path, env):
     """Per-frame-call knobs read once per process (the upload kernel instead of the stencil reading
     the frame from the pinned staging buffer, describe's LDS pair table, the one-wave describe instead
     of k_describe_pf, the two RANSAC launches instead of k_ransac_fused, the two-launch select, the
     output row through a device copy, pinned caller frames staged instead of read in place, stencil
-    segments of two tile rows), in a child process over the leak sequence: one
+    segments of two tile rows, the RANSAC count split over a workgroup's waves), in a child process over the leak sequence: one
     vo_process_frame per frame, rows, statuses and counts equal the oracle's."""
     import sys
     seq, frames, ref = leak_case
