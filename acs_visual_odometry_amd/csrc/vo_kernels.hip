@@ -2990,14 +2990,17 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) { return __shfl_xo
 // row_half_mirror, row_mirror), then the 4 row maxima via readlane.  No LDS round trips.
 __device__ __forceinline__ double dpp_f64(double v, int ctrl_sel)
 {
+    // every lane of every row is written by these patterns (quad_perm, row_half_mirror, row_mirror),
+    // so the moves need no old value: mov_dpp lets the compiler drop the copy (and fold the move
+    // into its consumer where it can)
     long long x = __double_as_longlong(v);
     int lo = (int)(x & 0xFFFFFFFFll), hi = (int)(x >> 32);
     int lo2, hi2;
     switch (ctrl_sel) {
-    case 0: lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0xB1, 0xF, 0xF, false); hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0xB1, 0xF, 0xF, false); break;
-    case 1: lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0x4E, 0xF, 0xF, false); hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0x4E, 0xF, 0xF, false); break;
-    case 2: lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0x141, 0xF, 0xF, false); hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0x141, 0xF, 0xF, false); break;
-    default: lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0x140, 0xF, 0xF, false); hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0x140, 0xF, 0xF, false); break;
+    case 0: lo2 = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, true); hi2 = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, true); break;
+    case 1: lo2 = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xF, 0xF, true); hi2 = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xF, 0xF, true); break;
+    case 2: lo2 = __builtin_amdgcn_mov_dpp(lo, 0x141, 0xF, 0xF, true); hi2 = __builtin_amdgcn_mov_dpp(hi, 0x141, 0xF, 0xF, true); break;
+    default: lo2 = __builtin_amdgcn_mov_dpp(lo, 0x140, 0xF, 0xF, true); hi2 = __builtin_amdgcn_mov_dpp(hi, 0x140, 0xF, 0xF, true); break;
     }
     return __longlong_as_double(((long long)hi2 << 32) | (unsigned)lo2);
 }
@@ -3049,9 +3052,9 @@ __device__ __forceinline__ bool sampson_inlier(const double* F, double x, double
 __device__ __forceinline__ int dpp_g8(int v, int step)
 {
     switch (step) {
-    case 0: return __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);
-    case 1: return __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);
-    default: return __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false);
+    case 0: return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);
+    case 1: return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);
+    default: return __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true);
     }
 }
 // lane q of each 8-lane group -> every lane of the group (ds_swizzle bitmask mode:
@@ -3090,6 +3093,13 @@ __device__ __forceinline__ double sel9(const double (&a)[9], int c)
 #endif
 }
 
+#ifndef RS_FASTRED
+#define RS_FASTRED 1                   // Gauss-Jordan pivot: group max, then min index among the maxima
+#endif
+#ifndef RS_LDSPIV
+#define RS_LDSPIV 1                    // Gauss-Jordan pivot row through LDS (else lane shuffles)
+#endif
+#define RS_ROWSTRIDE 10                // doubles per lane row in LDS (16-byte aligned rows)
 // computeFundamentalMatrix on a minimal sample (ransac.cpp:63-93) for the lane group's
 // hypothesis: Gauss-Jordan with complete pivoting exactly as oracle nullvec_8x9 (pivot = max
 // |a| over unused rows/cols, ties to the first in row-major order), lane r holding row r.
@@ -3156,18 +3166,36 @@ __device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], in
             win(w0, i0, w1, i1); win(w2, i2, w3, i3);
             win(w0, i0, w2, i2);
             win(w0, i0, mv[8], 8);
-            if (!((used_r >> r) & 1u) && w0 > 0.0) { bv = w0; bi = r * 9 + i0; }
+            if (!((used_r >> r) & 1u) && w0 > 0.0) { bv = w0; bi = r * 16 + i0; }
         }
 #else
         if (!((used_r >> r) & 1u)) {
 #pragma unroll
             for (int c = 0; c < 9; ++c) {
                 const double v = fabs(a[c]);
-                if (!((used_c >> c) & 1u) && v > 0.0 && v > bv) { bv = v; bi = r * 9 + c; }
+                if (!((used_c >> c) & 1u) && v > 0.0 && v > bv) { bv = v; bi = r * 16 + c; }
             }
         }
 #endif
-        // group maximum, ties to the smaller flat index
+        // group maximum, ties to the smaller flat index: the maximum value first (three DPP max
+        // steps; candidates are positive or -1, never NaN), then the smallest index among the lanes
+        // holding it (three DPP min steps) -- the same pivot as the pairwise (value, index) reduction
+        // with its compare / select chains
+#if RS_FASTRED
+        {
+            double gm = bv;
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const double o = dpp_f64(gm, t);
+                asm volatile("v_max_f64 %0, %1, %2" : "=v"(gm) : "v"(gm), "v"(o));   // no NaN: no canonicalising max
+            }
+            int ci = bv == gm ? bi : (1 << 30);
+#pragma unroll
+            for (int t = 0; t < 3; ++t) ci = min(ci, dpp_g8(ci, t));
+            bv = gm;
+            bi = ci;
+        }
+#else
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
             const double ov = dpp_f64(bv, t);
@@ -3176,14 +3204,46 @@ __device__ void fit_F8_group(const double* __restrict__ pts, const int s8[8], in
             bv = take ? ov : bv;
             bi = take ? oi : bi;
         }
+#endif
         live = live && bv > 0.0;                    // rank deficient: remaining columns free
-        const int pr = bi / 9, pc = bi - (bi / 9) * 9;
+        // (flat index r * 16 + c: the same order as r * 9 + c, row and column by shift and mask)
+        const int pr = bi >> 4, pc = bi & 15;
+#if RS_LDSPIV
+        // the pivot row, A[r][pc] and the pivot through LDS: each lane stores its row, then reads
+        // the group's pivot row and its own entry in column pc (12 LDS instructions instead of 20
+        // lane shuffles and a nine-way select).  One wave's lanes only, ordered by wave barriers.
+        double prow[9], arpc, piv;
+        {
+            __shared__ __attribute__((aligned(16))) double s_row[RS_GROUPS_MAX * 8][RS_ROWSTRIDE];
+            double* mine = s_row[threadIdx.x];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();              // the previous step's reads are done
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) *reinterpret_cast<double2*>(mine + c) = make_double2(a[c], a[c + 1]);
+            mine[8] = a[8];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const double* prw = s_row[(threadIdx.x & ~7u) + (live ? pr : 0)];
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+                const double2 v2 = *reinterpret_cast<const double2*>(prw + c);
+                prow[c] = v2.x; prow[c + 1] = v2.y;
+            }
+            prow[8] = prw[8];
+            const int pcc = live ? pc : 0;
+            arpc = mine[pcc];
+            piv = prw[pcc];
+        }
+#else
         const double arpc = sel9(a, live ? pc : 0);   // A[r][pc]
         const int src = gbase + (live ? pr : 0);
         const double piv = __shfl(arpc, src);
         double prow[9];
 #pragma unroll
         for (int c = 0; c < 9; ++c) prow[c] = __shfl(a[c], src);
+#endif
         if (live) {
             used_r |= 1u << pr; used_c |= 1u << pc;
             if (r == pr) my_pc = pc;
