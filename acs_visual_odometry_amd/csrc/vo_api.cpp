@@ -616,7 +616,10 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         }
         hipStream_t qd = q2 ? q2 : q;
         if (split) HIPCHK(hipEventRecord(e_d, qd));
-        if (multi) {
+        // VO_EV_SKIP=1 (wait-value mode only): no batch events; a refused packet records them then,
+        // at the tails of the queues (below)
+        static const bool ev_skip = getenv("VO_EV_SKIP") && atoi(getenv("VO_EV_SKIP")) != 0;
+        if (multi && !(ev_skip && !c->event_wait)) {
             // recorded in both wait modes: if the runtime refuses a wait-value packet, the passes
             // fall back to these events, and every batch enqueued so far -- on any extract queue --
             // already has its own
@@ -644,6 +647,19 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
                             we != hipSuccess ? hipGetErrorString(we) : "refusal forced by VO_FORCE_WAIT_REFUSAL");
                     (void)hipGetLastError();
                     c->event_wait = true;
+                    static const bool ev_skip = getenv("VO_EV_SKIP") && atoi(getenv("VO_EV_SKIP")) != 0;
+                    if (ev_skip) {
+                        // batches k and k + 1 (the extract queue runs one batch ahead) have no event:
+                        // record theirs now, at the tails of their queues (later than their describe:
+                        // a conservative wait); later batches record their own
+                        for (int j = k; j <= k + 1 && j < (int)sched.size(); ++j) {
+                            hipEvent_t ej;
+                            int rc = batch_event(c, VO_EV_WAIT, (size_t)j, &ej);
+                            if (rc) return rc;
+                            hipStream_t qj = c->split ? c->se[1] : c->se[j % nq];
+                            HIPCHK(hipEventRecord(ej, qj));
+                        }
+                    }
                     int rc = batch_event(c, VO_EV_WAIT, (size_t)k, &e);
                     if (rc) return rc;
                     HIPCHK(hipStreamWaitEvent(s, e, 0));

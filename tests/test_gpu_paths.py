@@ -391,6 +391,8 @@ print("KNOB_OK" if ok else "KNOB_DIFF")
 @pytest.mark.parametrize("env,batch", [("VO_STSEG=4", 16), ("VO_STSEG=5", 64), ("VO_STSEG=8", 64), ("VO_HYP_CUT1=512", 16),
                                        ("VO_TRI_BPF=0", 64), ("VO_RREPS=4", 16), ("VO_EXTQ=2", 8), ("VO_XCD=0", 64),
                                        ("VO_EVENT_WAIT=0,VO_FORCE_WAIT_REFUSAL=1,VO_EXTQ=2", 8),
+                                       ("VO_EVENT_WAIT=0,VO_EV_SKIP=1", 16),
+                                       ("VO_EVENT_WAIT=0,VO_EV_SKIP=1,VO_FORCE_WAIT_REFUSAL=1,VO_EXTQ=2", 8),
                                        ("VO_ST_FLAT=1", 64), ("VO_ST_FLAT=1,VO_STSEG=8", 64), ("VO_ST_FLAT=1", 8),
                                        ("VO_ST_PAIR=1", 16), ("VO_ST_PAIR=1", 8),
                                        ("VO_SEL_LDS_KB=48", 64), ("VO_PIPE_FIRST=0", 16), ("VO_RANSAC_SPLIT=0", 16),
