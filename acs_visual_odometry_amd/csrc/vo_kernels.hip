@@ -54,7 +54,9 @@ __constant__ uchar2 c_pair[VO_FREAK_NPAIRS];
 // k_describe_pf's term tables, padded to whole 64-term chunks (padding: both rows 0, weights 0):
 // each entry one scalar load -- the pair as the two sample rows' LDS byte offsets (p * 256 |
 // q * 256 << 16), the weights as in c_orient_u
-#define DP_CHUNK 64
+#ifndef DP_CHUNK
+#define DP_CHUNK 64                    // k_describe_pf: terms per chunk of its LDS ring
+#endif
 #define DP_NPAD (((VO_FREAK_NPAIRS + DP_CHUNK - 1) / DP_CHUNK) * DP_CHUNK)
 __constant__ uint32_t c_pairoff[DP_NPAD];
 __constant__ float4 c_orient_pf[DP_NPAD];
@@ -2412,7 +2414,7 @@ __global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int
 // test words (two per wave).
 // ---------------------------------------------------------------------------
 #define DP_WAVES 8
-#define DP_CH 64                                     // terms per chunk of the LDS ring (two chunks)
+#define DP_CH DP_CHUNK                               // terms per chunk of the LDS ring (two chunks)
 __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, int slot_override)
 {
     constexpr int NP = VO_FREAK_NPOINTS;
@@ -3412,6 +3414,57 @@ __device__ __forceinline__ int count_words(const double* __restrict__ pts, int s
     }
     return cnt;
 }
+// One hypothesis per wave (the latency form): lane L tests match 64 w + L, four words in flight, and
+// the ballot is the mask word itself.  The same per-match arithmetic as count_words.
+template <bool ONE>
+__device__ __forceinline__ int count_wave(const double* __restrict__ pts, int scored, const double* F, double thr,
+                                          int lane, bool store, uint64_t* __restrict__ mask, int bound)
+{
+    const int nw = (scored + 63) >> 6;
+    const bool deg_in = 1.7976931348623157e308 < thr;
+    const double F0 = F[0], F1 = F[1], F2 = F[2], F3 = F[3], F4 = F[4], F5 = F[5], F6 = F[6], F7 = F[7], F8 = F[8];
+    int cnt = 0;
+    for (int w0 = 0; w0 < nw; w0 += 4) {
+        double x[4], y[4], xp[4], yp[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = min((w0 + u) * 64 + lane, scored - 1);
+            const double2* p = reinterpret_cast<const double2*>(pts + 4 * (size_t)i);
+            const double2 a = p[0], c = p[1];
+            x[u] = a.x; y[u] = a.y; xp[u] = c.x; yp[u] = c.y;
+        }
+        double Fx0[4], Fx1[4], Ft0[4], Ft1[4], Ft2[4], v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) Fx0[u] = (F0 * x[u] + F1 * y[u]) + F2 * 1.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) Fx1[u] = (F3 * x[u] + F4 * y[u]) + F5 * 1.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) Ft0[u] = (F0 * xp[u] + F3 * yp[u]) + F6 * 1.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) Ft1[u] = (F1 * xp[u] + F4 * yp[u]) + F7 * 1.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) Ft2[u] = (F2 * xp[u] + F5 * yp[u]) + F8 * 1.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = (Ft0[u] * x[u] + Ft1[u] * y[u]) + Ft2[u] * 1.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int w = w0 + u;
+            if (w < nw) {                                  // wave-uniform
+                const double num = v[u] * v[u];
+                const double den = ((Fx0[u] * Fx0[u] + Fx1[u] * Fx1[u]) + Ft0[u] * Ft0[u]) + Ft1[u] * Ft1[u];
+                const unsigned long long dg = ballot64(den < 1e-12);
+                unsigned long long bal;
+                if constexpr (ONE) bal = ballot64(num < den) & ~dg;
+                else bal = (ballot64(num / den < thr) & ~dg) | (deg_in ? dg : 0ull);
+                bal &= ballot64(w * 64 + lane < scored);
+                cnt += __popcll(bal);
+                if (store && lane == 0) mask[w] = bal;
+            }
+        }
+        if (bound >= 0 && !(store && cnt + max(scored - (w0 + 4) * 64, 0) > bound)) break;   // wave-uniform
+    }
+    return cnt;
+}
 template <int J, bool PF>
 __device__ __forceinline__ int count_inliers_group(const double* __restrict__ pts, int scored, const double* F, double thr,
                                                    int h, int r, bool store, uint64_t* __restrict__ mask,
@@ -3535,14 +3588,13 @@ __device__ void inv4(const double* M, double* Inv)
 // exits at once, dispatches reps times fewer workgroups
 // One chunk [k0, k1) of the hypotheses on workgroups bx of nbx.  ready (the fused form): the chunk's
 // replay publishes w->ready1 when it is done (k0 == 0), or the chunk waits for it first (k0 > 0).
-// SP: waves per hypothesis set (1, or HPB: the latency form -- the workgroup's waves fit the same
-// eight hypotheses and split their count by words, the partial counts summed through LDS)
-template <int HPB, int CJ, bool CPF, int SP = 1>
+// W1: one hypothesis per wave (the latency form: every lane group fits the same hypothesis, the
+// wave's 64 lanes split its count) instead of eight
+template <int HPB, int CJ, bool CPF, bool W1 = false>
 __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int nhyp, int stage, int reps, int bx,
                                              int nbx, bool ready)
 {
-    static_assert(SP == 1 || SP == HPB, "a split set is the whole workgroup (its barrier)");
-    constexpr int SETS = HPB / SP;                 // hypothesis sets (eight hypotheses each) per workgroup
+    constexpr int HPW = W1 ? 1 : 8;                // hypotheses per wave
     const int wf = blockIdx.y;                     // window frame
     if (wf >= vwin_count(d, stage)) return;
     VoWork* w = d.work + wf;
@@ -3578,8 +3630,7 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
     const int M = w->M, scored = w->scored;
     const double* pts = d.pts + (size_t)wf * 4 * d.N;
     int32_t* counts = d.counts + (size_t)wf * d.max_hyp;
-    const int set = wave / SP, sub = wave % SP;
-    int k = k0 + (bx * SETS + set) * 8 + h;
+    int k = k0 + (bx * HPB + wave) * HPW + (W1 ? 0 : h);
     // Hypotheses at or past the previous replay's bound are never evaluated by the sequential
     // loop: once an improvement updated maxIterations (best > 0 and its table entry is not the
     // 'denom == 0: no update' mark) and the loop went on past k0 (maxit > 100), the inlier ratio
@@ -3592,9 +3643,9 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
         kbound = min(w->maxit, k1);
     // counts past the previous replay's best only matter to the loop: a later chunk stops a wave's
     // count once none of its hypotheses can pass it (not the stage API, which returns every count)
-    const int cbound = (RS_EARLY && SP == 1 && k0 > 0 && !stage) ? w->best : -1;
-    for (int rep = 0; rep < reps; ++rep, k += nbx * SETS * 8) {
-        const int kb = k - h;                      // the wave's first hypothesis
+    const int cbound = (RS_EARLY && k0 > 0 && !stage) ? w->best : -1;
+    for (int rep = 0; rep < reps; ++rep, k += nbx * HPB * HPW) {
+        const int kb = W1 ? k : k - h;             // the wave's first hypothesis
         if (kb >= k1) break;                       // wave-uniform
         const bool mine = k < kbound;
         if (__builtin_amdgcn_readfirstlane(kb) < kbound) {   // some group of the wave has work
@@ -3615,29 +3666,23 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
             VO_STAMP(d, k, 2);
             rank2(F);
             VO_STAMP(d, k, 5);
-            if (mine && sub == 0) {
+            if (mine && (!W1 || h == 0)) {
                 double* hf = d.hypF + ((size_t)wf * d.max_hyp + k) * 9;
 #pragma unroll
                 for (int j = 0; j < 9; ++j)
                     if (j == r || (j == 8 && r == 0)) hf[j] = F[j];   // lane r: F[r]; lane 0 also F[8]
             }
-            int cnt = count_inliers_group<CJ, CPF>(pts, scored, F, d.sampson_thr, h, r, mine,
-                                                d.inlmask + ((size_t)wf * d.max_hyp + min(k, nhyp - 1)) * d.mask_words,
-                                                cbound, sub, SP);
-            if constexpr (SP > 1) {
-                __shared__ int s_pc[HPB][64];
-                s_pc[wave][lane] = cnt;
-                __syncthreads();
-                if (sub == 0) {
-#pragma unroll
-                    for (int u = 1; u < SP; ++u) cnt += s_pc[wave + u][lane];
-                }
-                __syncthreads();                   // s_pc is rewritten by the next rep
-            }
-            if (mine && sub == 0 && r == 0) st_sc1(counts + k, cnt);
+            uint64_t* msk = d.inlmask + ((size_t)wf * d.max_hyp + min(k, nhyp - 1)) * d.mask_words;
+            int cnt;
+            if constexpr (W1)
+                cnt = d.sampson_thr == 1.0 ? count_wave<true>(pts, scored, F, d.sampson_thr, lane, mine, msk, cbound)
+                                           : count_wave<false>(pts, scored, F, d.sampson_thr, lane, mine, msk, cbound);
+            else
+                cnt = count_inliers_group<CJ, CPF>(pts, scored, F, d.sampson_thr, h, r, mine, msk, cbound);
+            if (mine && (W1 ? lane == 0 : r == 0)) st_sc1(counts + k, cnt);
             VO_STAMP(d, k, 6);
         }
-        if (!mine && k < k1 && sub == 0 && r == 0) st_sc1(counts + k, -1);   // skipped: the replay never takes it
+        if (!mine && k < k1 && (W1 ? lane == 0 : r == 0)) st_sc1(counts + k, -1);   // skipped: the replay never takes it
     }
     unsigned* ctr = &w->ctr[k0 == 0 ? 1 : (k0 < VO_HYP_CHUNK1 ? 2 : 3)];   // one arrival counter per chunk
     if (!arrive_last(ctr, nbx, &s_last)) return;
@@ -3697,11 +3742,11 @@ __global__ void __launch_bounds__(64 * HPB) RS_OCC k_ransac_hyp(VoDev d, int k0,
 // one frame's two chunks in one launch (the per-frame call and the stage API: one launch and one
 // dependent-launch gap less): workgroups [0, b0) run [0, c0) and publish its replay; the rest wait
 // for it and run [c0, nhyp) as the second launch would
-template <int HPB, int SP>
+template <int HPB, bool W1>
 __global__ void __launch_bounds__(64 * HPB) RS_OCC k_ransac_fused(VoDev d, int c0, int nhyp, int stage, int b0)
 {
-    if ((int)blockIdx.x < b0) ransac_chunk<HPB, RS_FUSED_J, RS_FUSED_PF, SP>(d, 0, c0, nhyp, stage, 1, blockIdx.x, b0, true);
-    else ransac_chunk<HPB, RS_FUSED_J, RS_FUSED_PF, SP>(d, c0, nhyp, nhyp, stage, 1, blockIdx.x - b0, gridDim.x - b0, true);
+    if ((int)blockIdx.x < b0) ransac_chunk<HPB, RS_FUSED_J, RS_FUSED_PF, W1>(d, 0, c0, nhyp, stage, 1, blockIdx.x, b0, true);
+    else ransac_chunk<HPB, RS_FUSED_J, RS_FUSED_PF, W1>(d, c0, nhyp, nhyp, stage, 1, blockIdx.x - b0, gridDim.x - b0, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -5021,14 +5066,15 @@ void launch_ransac(const VoDev& d, int stage, hipStream_t s, int part)
     const int nhyp = d.max_hyp, nb = stage ? 1 : d.gridw;
     // (the per-frame call's window: one frame, two work records -- the repair form's second record)
     if (part == 0 && (stage || d.single) && nb <= 2 && d.ransac_fused && nhyp > VO_HYP_CHUNK0) {
-        // VO_RANSAC_SPLIT_COUNT=1: the workgroup's four waves fit the same eight hypotheses and split
-        // their count (8 hypotheses per workgroup) instead of one wave per eight (32 per workgroup):
-        // measured slower, 138-140 vs 136.7 us per call (two alternating pairs, gpurun_out r5m)
-        static const bool spc = getenv("VO_RANSAC_SPLIT_COUNT") && atoi(getenv("VO_RANSAC_SPLIT_COUNT")) != 0;
-        const int hpw = spc ? 8 : 32;
-        const int b0 = (VO_HYP_CHUNK0 + hpw - 1) / hpw, b1 = (nhyp - VO_HYP_CHUNK0 + hpw - 1) / hpw;
-        if (spc) hipLaunchKernelGGL((k_ransac_fused<4, 4>), dim3(b0 + b1, nb), dim3(256), 0, s, d, VO_HYP_CHUNK0, nhyp, stage, b0);
-        else hipLaunchKernelGGL((k_ransac_fused<4, 1>), dim3(b0 + b1, nb), dim3(256), 0, s, d, VO_HYP_CHUNK0, nhyp, stage, b0);
+        // one hypothesis per wave (4 per workgroup), the wave's lanes splitting its count: the count's
+        // latency is 7 Sampson tests per lane instead of 52 (VO_RANSAC_WAVE_HYP=0: eight hypotheses per
+        // wave, 32 per workgroup).  (Round 5 also measured four waves splitting one eight-hypothesis
+        // set's count through LDS: slower, 138-140 vs 136.7 us per call.)
+        static const bool w1 = !(getenv("VO_RANSAC_WAVE_HYP") && atoi(getenv("VO_RANSAC_WAVE_HYP")) == 0);
+        const int hpg = w1 ? 4 : 32;
+        const int b0 = (VO_HYP_CHUNK0 + hpg - 1) / hpg, b1 = (nhyp - VO_HYP_CHUNK0 + hpg - 1) / hpg;
+        if (w1) hipLaunchKernelGGL((k_ransac_fused<4, true>), dim3(b0 + b1, nb), dim3(256), 0, s, d, VO_HYP_CHUNK0, nhyp, stage, b0);
+        else hipLaunchKernelGGL((k_ransac_fused<4, false>), dim3(b0 + b1, nb), dim3(256), 0, s, d, VO_HYP_CHUNK0, nhyp, stage, b0);
         return;
     }
     // VO_HYP_CUT1: the second cut (VO_HYP_CHUNK1; >= max_hyp merges the last two chunks)
