@@ -55,7 +55,7 @@ __constant__ uchar2 c_pair[VO_FREAK_NPAIRS];
 // each entry one scalar load -- the pair as the two sample rows' LDS byte offsets (p * 256 |
 // q * 256 << 16), the weights as in c_orient_u
 #ifndef DP_CHUNK
-#define DP_CHUNK 64                    // k_describe_pf: terms per chunk of its LDS ring
+#define DP_CHUNK 96                    // k_describe_pf: terms per chunk of its LDS ring (64: 1.3-2.6 us slower per call, r5q)
 #endif
 #define DP_NPAD (((VO_FREAK_NPAIRS + DP_CHUNK - 1) / DP_CHUNK) * DP_CHUNK)
 __constant__ uint32_t c_pairoff[DP_NPAD];
@@ -3743,10 +3743,10 @@ __global__ void __launch_bounds__(64 * HPB) RS_OCC k_ransac_hyp(VoDev d, int k0,
 // dependent-launch gap less): workgroups [0, b0) run [0, c0) and publish its replay; the rest wait
 // for it and run [c0, nhyp) as the second launch would
 template <int HPB, bool W1>
-__global__ void __launch_bounds__(64 * HPB) RS_OCC k_ransac_fused(VoDev d, int c0, int nhyp, int stage, int b0)
+__global__ void __launch_bounds__(64 * HPB) RS_OCC k_ransac_fused(VoDev d, int c0, int nhyp, int stage, int b0, int reps1)
 {
     if ((int)blockIdx.x < b0) ransac_chunk<HPB, RS_FUSED_J, RS_FUSED_PF, W1>(d, 0, c0, nhyp, stage, 1, blockIdx.x, b0, true);
-    else ransac_chunk<HPB, RS_FUSED_J, RS_FUSED_PF, W1>(d, c0, nhyp, nhyp, stage, 1, blockIdx.x - b0, gridDim.x - b0, true);
+    else ransac_chunk<HPB, RS_FUSED_J, RS_FUSED_PF, W1>(d, c0, nhyp, nhyp, stage, reps1, blockIdx.x - b0, gridDim.x - b0, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -5073,8 +5073,12 @@ void launch_ransac(const VoDev& d, int stage, hipStream_t s, int part)
         static const bool w1 = !(getenv("VO_RANSAC_WAVE_HYP") && atoi(getenv("VO_RANSAC_WAVE_HYP")) == 0);
         const int hpg = w1 ? 4 : 32;
         const int b0 = (VO_HYP_CHUNK0 + hpg - 1) / hpg, b1 = (nhyp - VO_HYP_CHUNK0 + hpg - 1) / hpg;
-        if (w1) hipLaunchKernelGGL((k_ransac_fused<4, true>), dim3(b0 + b1, nb), dim3(256), 0, s, d, VO_HYP_CHUNK0, nhyp, stage, b0);
-        else hipLaunchKernelGGL((k_ransac_fused<4, false>), dim3(b0 + b1, nb), dim3(256), 0, s, d, VO_HYP_CHUNK0, nhyp, stage, b0);
+        // the later chunk on at most 60 workgroups (hypothesis blocks strided by the grid): its
+        // workgroups wait for the first chunk's replay, and hundreds of pollers slowed it
+        static const int wg1 = getenv("VO_RANSAC_WG1") ? std::max(1, atoi(getenv("VO_RANSAC_WG1"))) : 60;
+        const int n1 = std::min(b1, wg1), reps1 = (b1 + n1 - 1) / n1;
+        if (w1) hipLaunchKernelGGL((k_ransac_fused<4, true>), dim3(b0 + n1, nb), dim3(256), 0, s, d, VO_HYP_CHUNK0, nhyp, stage, b0, reps1);
+        else hipLaunchKernelGGL((k_ransac_fused<4, false>), dim3(b0 + n1, nb), dim3(256), 0, s, d, VO_HYP_CHUNK0, nhyp, stage, b0, reps1);
         return;
     }
     // VO_HYP_CUT1: the second cut (VO_HYP_CHUNK1; >= max_hyp merges the last two chunks)
