@@ -312,14 +312,17 @@ int batch_event(vo_ctx* c, int pool, size_t k, hipEvent_t* e)
     return VO_OK;
 }
 
+constexpr int kContSpan = 1000;    // EvRec span tag of a continuation launch (timed, cont)
+// cont: the rest of the previous launch of kernel k (a pass's later RANSAC chunks on another
+// queue): its time adds to that launch's, which stays one launch in the counts
 template <typename F>
-void timed(vo_ctx* c, EvRec* ev, int k, hipStream_t st, F&& launch)
+void timed(vo_ctx* c, EvRec* ev, int k, hipStream_t st, F&& launch, bool cont = false)
 {
-    const int nth = c->klaunch[k]++;
+    const int nth = cont ? c->klaunch[k] - 1 : c->klaunch[k]++;
     const bool on = ev && ev->err == VO_OK && (ev->only < 0 || (ev->only == k && nth % VO_TIMING_STRIDE == 0));
     size_t b = on ? ev_mark(ev, st) : 0;
     launch();
-    if (on && b != SIZE_MAX && ev_mark(ev, st) != SIZE_MAX) ev->spans.emplace_back(k, b);
+    if (on && b != SIZE_MAX && ev_mark(ev, st) != SIZE_MAX) ev->spans.emplace_back(cont ? k + kContSpan : k, b);
 }
 
 // extract of nb frames f0.. (device images img0 + z * frame_bytes) on stream q; publish:
@@ -498,7 +501,7 @@ void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax,
         (void)hipEventRecord(c->ev_rs[p % vo_ctx::kPassEv], s);
         (void)hipStreamWaitEvent(sf, c->ev_rs[p % vo_ctx::kPassEv], 0);
     }
-    if (split) timed(c, ev, 4, sf, [&] { vo::launch_ransac(d, 0, sf, 2); });
+    if (split) timed(c, ev, 4, sf, [&] { vo::launch_ransac(d, 0, sf, 2); }, true);
     timed(c, ev, 5, sf, [&] { vo::launch_refit(d, 1, 0, sf); });
     if (single) {
         // one frame: triangulation, finalize and the trajectory chain in one launch (its last
@@ -782,8 +785,9 @@ int finish_timing(vo_ctx* c, EvRec* ev)
     for (const auto& sp : ev->spans) {
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, c->ev_pool[sp.second], c->ev_pool[sp.second + 1]);
-        c->ktime_ms[sp.first] += ms;
-        c->kcount[sp.first] += 1;
+        const bool cont = sp.first >= kContSpan;
+        c->ktime_ms[cont ? sp.first - kContSpan : sp.first] += ms;
+        if (!cont) c->kcount[sp.first] += 1;
     }
     return VO_OK;
 }
