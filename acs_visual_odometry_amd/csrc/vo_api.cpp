@@ -719,22 +719,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         if (!host_frame)
             HIPCHK(hipMemcpyAsync(c->lo_host, &c->d.st->lo, sizeof(int32_t), hipMemcpyDeviceToHost, tq));
         if (c->pf_profile && host_frame) c->pf_enq_end = now_us();
-        // the per-frame call with its row in pinned host memory: the last kernel stores the row's
-        // `done` field last (after a system-scope release), so the host polls it instead of waiting
-        // for the stream's completion signal (VO_PF_POLL=0: the stream wait).  The kernels' exit
-        // is not waited for here; the next call's synchronisation covers it.
-        static const bool pf_poll = !(getenv("VO_PF_POLL") && atoi(getenv("VO_PF_POLL")) == 0);
-        bool polled = false;
-        if (pf_poll && host_frame && nf == 1 && out == c->out_host_dev) {
-            volatile const int32_t* done = &c->out_host[base - out_base].done;
-            const double tp = now_us();
-            while (*done != base + 1) {
-                if (now_us() - tp > 2e5) break;        // 200 ms: fall back to the stream wait (an error surfaces there)
-                __builtin_ia32_pause();
-            }
-            polled = *done == base + 1;
-        }
-        if (!polled) HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipStreamSynchronize(s));
         if (c->pf_profile && host_frame) c->pf_wait_end = now_us();
         if (c->sf && !host_frame) HIPCHK(hipStreamSynchronize(c->sf));
         if (tq != s) HIPCHK(hipStreamSynchronize(tq));
@@ -1471,7 +1456,6 @@ int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_
     // the frame's output row straight into pinned host memory (VO_PF_OUT_ZC=0: a device row and a copy)
     static const bool out_zc = !(getenv("VO_PF_OUT_ZC") && atoi(getenv("VO_PF_OUT_ZC")) == 0);
     VoFrameOut* out = out_zc && c->out_host_dev ? c->out_host_dev : c->out_dev;
-    if (out == c->out_host_dev) c->out_host[0].done = 0;   // the last kernel stores f + 1 (run_chunk polls it)
     int rc = run_chunk(c, src, 0, 1, out, f, nullptr, true);
     if (rc) return rc;
     if (c->pf_profile) {

@@ -130,7 +130,7 @@ struct VoFrameOut {
     int32_t status, n_kps, n_matches, n_inl, best_k, n_eval, fitted, frame;
     int32_t err;          // the frame's extract failed the select's consistency check (VO_STATUS_INCONSISTENT;
                           // reported even where the status is FIRST): the call returns VO_ERR_INTERNAL
-    int32_t done;         // the per-frame call: frame + 1 once the row is complete (stored last)
+    int32_t pad;
     double pose[12];
 };
 

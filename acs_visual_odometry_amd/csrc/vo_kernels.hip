@@ -4748,14 +4748,6 @@ __device__ void traj_chain(const VoDev& d, VoFrameOut* out, int out_base, int lo
     } else if (tid == 255) {
         for (int i = 0; i < 16; ++i) st->Tcurr[i] = s_T[i];
     }
-    if (d.single) {
-        // the per-frame call: the row is in pinned host memory, and its `done` field, stored last
-        // after a system-scope release by every thread, tells the waiting host the row is complete
-        // (it polls the field instead of waiting for the stream)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        __syncthreads();
-        if (tid < nc) __hip_atomic_store(&out[lo + tid - out_base].done, lo + tid + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
 }
 
 __global__ void __launch_bounds__(256) k_traj(VoDev d, VoFrameOut* out, int out_base)
