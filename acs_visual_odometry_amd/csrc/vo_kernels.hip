@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
+#include <utility>
 #include <cstdio>
 
 #include "vo_internal.h"
@@ -2413,8 +2414,52 @@ __global__ void __launch_bounds__(64 * DS_WAVES) k_describe(VoDev d, int f0, int
 // f32 sums in pair order t = 0 .. 902 (so every rounding is the sequential loop's), and the 16
 // test words (two per wave).
 // ---------------------------------------------------------------------------
+// pair (p, q) of orientation term t, p < q in the pattern's pair order (compile-time: the term
+// waves of k_describe_pf generate one straight-line block per term)
+__host__ __device__ constexpr int dp_pair_p(int t)
+{
+    int p = 0;
+    for (int cnt = VO_FREAK_NPOINTS - 1; t >= cnt; --cnt) { t -= cnt; ++p; }
+    return p;
+}
+__host__ __device__ constexpr int dp_pair_q(int t)
+{
+    int p = 0, cnt = VO_FREAK_NPOINTS - 1;
+    for (; t >= cnt; --cnt) { t -= cnt; ++p; }
+    return p + 1 + t;
+}
+static_assert(dp_pair_p(0) == 0 && dp_pair_q(0) == 1 && dp_pair_p(42) == 1 && dp_pair_q(42) == 2, "pair order");
 #define DP_WAVES 8
+#ifndef DP_CT_TERMS
+#define DP_CT_TERMS 1                  // term waves with compile-time pairs and samples in registers
+#endif
 #define DP_CH DP_CHUNK                               // terms per chunk of the LDS ring (two chunks)
+// k_describe_pf's term wave W (1 .. DP_WAVES - 1): the terms t = W - 1 (mod DP_WAVES - 1) of each
+// chunk, generated at compile time (pairs as register indices into the wave's 43 samples, weights by
+// scalar loads at fixed offsets), a barrier after each chunk as the sum wave expects
+template <int W, int T, int J>
+__device__ __forceinline__ void dp_one_term(const float* I, ds_f2 (*slot)[64], int lane)
+{
+    if constexpr (T < VO_FREAK_NPAIRS && T % (DP_WAVES - 1) == W - 1) {
+        constexpr int P = dp_pair_p(T), Q = dp_pair_q(T);
+        const float4 tb = c_orient_u[T];
+        const float ic = I[P] - I[Q];
+        const ds_f2 i2 = {ic, ic};
+        slot[J][lane] = __builtin_elementwise_fma(i2, ds_f2{tb.x, tb.y}, i2 * ds_f2{tb.z, tb.w});
+    }
+}
+template <int W, int C, int... J>
+__device__ __forceinline__ void dp_chunk_terms(const float* I, ds_f2 (*slot)[64], int lane, std::integer_sequence<int, J...>)
+{
+    (dp_one_term<W, C * DP_CH + J, J>(I, slot, lane), ...);
+}
+template <int W, int... C>
+__device__ __forceinline__ void dp_term_wave(const float* I, ds_f2 (*s_t)[DP_CH + 1][64], int lane,
+                                             std::integer_sequence<int, C...>)
+{
+    ((dp_chunk_terms<W, C>(I, s_t[C & 1], lane, std::make_integer_sequence<int, DP_CH>{}), __syncthreads()), ...);
+    __syncthreads();                                 // the sum wave's last chunk
+}
 __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, int slot_override)
 {
     constexpr int NP = VO_FREAK_NPOINTS;
@@ -2422,8 +2467,10 @@ __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, 
     __shared__ float s_I[NP][64];                    // pattern samples (then the rotated samples, as u32)
     __shared__ ds_f2 s_t[2][DP_CH + 1][64];          // orientation terms, a chunk ahead (+ a spare row)
     __shared__ float s_c[64], s_s[64];
+#if !DP_CT_TERMS
     __shared__ float4 s_orient[DP_NPAD];
     __shared__ uint32_t s_pairoff[DP_NPAD];
+#endif
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int cur = ext_slot(d, f0, 0, slot_override);
     const int n = d.ext_n[cur];
@@ -2435,11 +2482,13 @@ __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, 
     VO_STAMP(d, sslot, 0);
     const bool valid = base + lane < n;
     const int2 kp = valid ? d.kps[(size_t)cur * d.N + base + lane] : make_int2(d.bcol, d.brow);
+#if !DP_CT_TERMS
     // 0. the term tables into LDS
     for (int t = threadIdx.x; t < DP_NPAD; t += 64 * DP_WAVES) {
         s_orient[t] = c_orient_pf[t];
         s_pairoff[t] = c_pairoff[t];
     }
+#endif
     // 1. pattern samples, rows u = wave, wave + DP_WAVES, ...
     for (int u = wave; u < NP; u += DP_WAVES)
         s_I[u][lane] = (float)img[(size_t)(kp.y + (int)c_ppt[u].y) * Wb + (kp.x + (int)c_ppt[u].x)];
@@ -2453,6 +2502,7 @@ __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, 
     //    barrier: 47k of the wave's 62k cycles)
     //    The tables come from LDS (copied at entry): scalar loads share lgkmcnt with the LDS
     //    reads, so every term waited for its scalar load's full latency (54k cycles at wave 0)
+#if !DP_CT_TERMS
     static_assert(DP_CH == DP_CHUNK, "k_describe_pf's chunk is its tables' padding unit");
     const unsigned char* sIb = reinterpret_cast<const unsigned char*>(&s_I[0][0]) + 4 * lane;
     auto terms = [&](int c) {
@@ -2483,7 +2533,37 @@ __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, 
             s_t[c & 1][j][lane] = __builtin_elementwise_fma(i2, ds_f2{tb[i].x, tb[i].y}, i2 * ds_f2{tb[i].z, tb[i].w});
         }
     };
+#endif
     ds_f2 oxy = {0.0f, 0.0f};
+#if DP_CT_TERMS
+    // term wave W (1 .. DP_WAVES - 1) computes the terms t = W - 1 (mod DP_WAVES - 1) with
+    // compile-time pairs: its 43 samples in registers, the weights by scalar loads, no table or
+    // sample reads through LDS (those made the term waves LDS-bound: 25-29k cycles per block)
+    float I[NP];
+    if (wave > 0) {
+#pragma unroll
+        for (int u = 0; u < NP; ++u) I[u] = s_I[u][lane];
+    }
+    switch (wave) {
+    case 0: {
+        __syncthreads();                             // chunk 0 written
+        for (int c = 0; c < NC; ++c) {
+            const int m = min(DP_CH, VO_FREAK_NPAIRS - c * DP_CH);
+#pragma unroll 16
+            for (int j = 0; j < m; ++j) oxy = oxy + s_t[c & 1][j][lane];
+            __syncthreads();
+        }
+        break;
+    }
+    case 1: dp_term_wave<1>(I, s_t, lane, std::make_integer_sequence<int, NC>{}); break;
+    case 2: dp_term_wave<2>(I, s_t, lane, std::make_integer_sequence<int, NC>{}); break;
+    case 3: dp_term_wave<3>(I, s_t, lane, std::make_integer_sequence<int, NC>{}); break;
+    case 4: dp_term_wave<4>(I, s_t, lane, std::make_integer_sequence<int, NC>{}); break;
+    case 5: dp_term_wave<5>(I, s_t, lane, std::make_integer_sequence<int, NC>{}); break;
+    case 6: dp_term_wave<6>(I, s_t, lane, std::make_integer_sequence<int, NC>{}); break;
+    default: dp_term_wave<7>(I, s_t, lane, std::make_integer_sequence<int, NC>{}); break;
+    }
+#else
     if (wave > 0) terms(0);
     __syncthreads();
     for (int c = 0; c < NC; ++c) {
@@ -2496,6 +2576,7 @@ __global__ void __launch_bounds__(64 * DP_WAVES) k_describe_pf(VoDev d, int f0, 
         }
         __syncthreads();
     }
+#endif
     VO_STAMP(d, sslot, 2);
     // 3. angle and rotation (wave 0), as describe_wave
     if (wave == 0) {

@@ -22,7 +22,7 @@ between two instructions are the instructions issued between them, an ``s_nop N`
     VALU writes VGPR                DPP reads it as src0                       2
     VALU writes VGPR                v_readlane / v_readfirstlane src0          1
     v_pk_*_f32 writes VGPR          VALU reads it                              1
-      (not after a producer with a cross-half op_sel: hipcc pads none there)
+      (not after a producer with a cross-half op_sel / op_sel_hi: hipcc pads none there)
     v_writelane writes VGPR         VALU reads it                              1
     transcendental writes VGPR      non-transcendental VALU reads it           1
     v_dot* writes VGPR              VALU (other than a v_dot* srcC) or VMEM    3
@@ -45,7 +45,9 @@ _REG = re.compile(r"\b(v|s)\[(\d+):(\d+)\]|\b(v|s)(\d+)\b|\b(vcc_lo|vcc_hi|vcc|e
 _TRANS = re.compile(r"^v_(sqrt|rsq|rcp|log|exp|sin|cos)(_iflag)?_(f16|f32|f64|bf16)")
 _PKF32 = re.compile(r"^v_pk_(add|mul|fma|mov)_(f32|b32)")
 _DOT = re.compile(r"^v_dot\d")
-_OPSEL_LO = re.compile(r"\bop_sel:\[[^\]]*1")     # a packed op whose lanes read across halves
+# a packed op whose lanes read across halves: a 1 in op_sel, or a 0 in op_sel_hi (the high lane reads
+# a low half, e.g. a scalar broadcast from an SGPR pair); hipcc pads neither form
+_OPSEL_LO = re.compile(r"\bop_sel:\[[^\]]*1|\bop_sel_hi:\[[^\]]*0")
 _VMEM = re.compile(r"^(buffer|global|flat|scratch)_")
 _DPP_MOD = re.compile(r"\b(quad_perm|row_shl|row_shr|row_ror|wave_shl|wave_shr|wave_rol|wave_ror|row_mirror|"
                       r"row_half_mirror|row_bcast|row_newbcast)\b")
