@@ -1258,7 +1258,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
         s_nbnd = 0; s_b = -1; s_above = 0;
         s_slot = ext_slot(d, f0, z, slot_override);
     }
-    VO_STAMP(d, 1990, 0);
+    VO_STAMP(d, 1900 + (int)blockIdx.x, 0);
     // A
     const int tpt = (ntiles + 1023) / 1024;            // tiles per thread (<= 3)
     int tt[3] = {0, 0, 0};
@@ -1360,7 +1360,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
         for (int g = tid; g < VO_DIAG_KEYS; g += 1024)
             d.diag_keys[(size_t)(f0 + z) * VO_DIAG_KEYS + g] = g < C ? keys[g] : 0ull;
 #endif
-    VO_STAMP(d, 1990, 1);
+    VO_STAMP(d, 1900 + (int)blockIdx.x, 1);
     // C (the histogram is read for every frame: its total must equal C, the consistency check)
     int b = -1;
     uint64_t Tb = 0ull;
@@ -1387,7 +1387,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
         }
         __syncthreads();
         b = s_b;
-        VO_STAMP(d, 1990, 2);
+        VO_STAMP(d, 1900 + (int)blockIdx.x, 2);
         for (int g0 = tid; g0 < C; g0 += 4 * 1024) {
             uint64_t v[4];
 #pragma unroll
@@ -1401,7 +1401,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
             }
         }
         __syncthreads();
-        VO_STAMP(d, 1990, 3);
+        VO_STAMP(d, 1900 + (int)blockIdx.x, 3);
         const int nb = s_nbnd;
         // the need-th largest boundary key: the one with exactly need-1 larger keys
         const int need = N - s_above;
@@ -1452,7 +1452,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     __syncthreads();                                    // s_bnd aliases the segment counts
     for (int w = tid; w < (nseg + 3) / 4; w += 1024) s_segw[w] = 0u;
     __syncthreads();
-    VO_STAMP(d, 1990, 4);
+    VO_STAMP(d, 1900 + (int)blockIdx.x, 4);
     auto selected = [&](uint64_t key) -> bool {
         if (b < 0) return true;
         const int bin = (int)sel_bin(key, d.thr_bits);
@@ -1509,7 +1509,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
         }
     }
     __syncthreads();
-    VO_STAMP(d, 1990, 5);
+    VO_STAMP(d, 1900 + (int)blockIdx.x, 5);
     // F
     const int slot = s_slot;
     int2* out = d.kps + (size_t)slot * N;
@@ -1561,7 +1561,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
             if (pos < N) out[pos] = make_int2(col, row);  // < N by construction (corrupt input: no stray store)
         }
     }
-    VO_STAMP(d, 1990, 6);
+    VO_STAMP(d, 1900 + (int)blockIdx.x, 6);
     // select is the histogram's only reader: leave it zeroed for the next frame's stencil
     for (int i = tid; i < VO_HIST_BINS; i += 1024) hist[i] = 0u;
     if (tid == 0) {
