@@ -4978,7 +4978,8 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
     // segments' count) each walk 30 source rows instead of 142 -- the latency of the launch
     // the per-frame call's segment (VO_PF_SEGT: 1 or 2 tile rows; 2 reads 1.44x the frame's rows over
     // PCIe instead of 1.88x, in half as many waves of 46 source rows)
-    static const int pf_segt = getenv("VO_PF_SEGT") && atoi(getenv("VO_PF_SEGT")) == 2 ? 2 : 1;
+    static const int pf_segt = getenv("VO_PF_SEGT") && (atoi(getenv("VO_PF_SEGT")) == 2 || atoi(getenv("VO_PF_SEGT")) == 4)
+                                   ? atoi(getenv("VO_PF_SEGT")) : 1;
     int st = write_response ? 4 : nb == 1 && d.single ? pf_segt
            : segt == 4 || segt == 5 || segt == 6 || segt == 8 ? segt : ST_SEGT_DEFAULT;
     // a small batch (a sequence's ragged last batch): shorter segments until the launch has two
