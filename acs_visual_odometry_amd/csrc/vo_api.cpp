@@ -62,6 +62,8 @@ struct vo_ctx {
     static constexpr int kPassEv = 8;
     hipEvent_t ev_rs[kPassEv] = {};   // pass p's RANSAC done (the fit queue waits on it), p % 8
     hipEvent_t ev_fn[kPassEv] = {};   // pass p's finalize done (pass p + 2 and the trajectory queue wait on it)
+    hipEvent_t ev_r2[kPassEv] = {};   // pass p's later RANSAC chunks done (rq: the fit queue waits on it)
+    bool rq = false;                  // later RANSAC chunks on the trajectory queue, k_traj on the fit queue
     bool pipeline = true;             // VO_PIPELINE=0: every pass on the pose queue, one after the other
     size_t set_off[9] = {};           // element offsets of window buffer set 1 (pass p uses set p & 1)
     int npass = 0;                    // pose passes enqueued (their pass-log entries)
@@ -497,11 +499,20 @@ void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax,
     static const bool split_env = !(getenv("VO_RANSAC_SPLIT") && atoi(getenv("VO_RANSAC_SPLIT")) == 0);
     const bool split = pipelined && split_env && d.rng_mode != VO_RNG_MT19937;
     timed(c, ev, 4, s, [&] { vo::launch_ransac(d, 0, s, split ? 1 : 0); });
+    // c->rq: the later chunks on the trajectory queue instead (the trajectory chain moves to the fit
+    // queue), so the next pass's later chunks overlap this pass's refit, triangulation and finalize
+    const bool rq = split && c->rq;
     if (pipelined) {
         (void)hipEventRecord(c->ev_rs[p % vo_ctx::kPassEv], s);
-        (void)hipStreamWaitEvent(sf, c->ev_rs[p % vo_ctx::kPassEv], 0);
+        (void)hipStreamWaitEvent(rq ? c->st : sf, c->ev_rs[p % vo_ctx::kPassEv], 0);
     }
-    if (split) timed(c, ev, 4, sf, [&] { vo::launch_ransac(d, 0, sf, 2); }, true);
+    if (rq) {
+        timed(c, ev, 4, c->st, [&] { vo::launch_ransac(d, 0, c->st, 2); }, true);
+        (void)hipEventRecord(c->ev_r2[p % vo_ctx::kPassEv], c->st);
+        (void)hipStreamWaitEvent(sf, c->ev_r2[p % vo_ctx::kPassEv], 0);
+    } else if (split) {
+        timed(c, ev, 4, sf, [&] { vo::launch_ransac(d, 0, sf, 2); }, true);
+    }
     timed(c, ev, 5, sf, [&] { vo::launch_refit(d, 1, 0, sf); });
     if (single) {
         // one frame: triangulation, finalize and the trajectory chain in one launch (its last
@@ -517,7 +528,7 @@ void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax,
     }
     // the T_curr chain and the pose rows on the trajectory queue (serial mode and the single-frame
     // call: the pose queue, no cross-queue event)
-    hipStream_t q = c->serial || single ? s : c->st;
+    hipStream_t q = c->serial || single ? s : (c->rq ? sf : c->st);
     hipEvent_t ef = pipelined ? c->ev_fn[p % vo_ctx::kPassEv] : c->ev_fin;
     if (q != sf || pipelined) {
         (void)hipEventRecord(ef, sf);
@@ -709,7 +720,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         HIPCHK(hipGetLastError());
         // the chunk's output rows (complete once the trajectory queue's last k_traj ran, which
         // waited for the last k_finalize) and the commit point
-        hipStream_t tq = c->serial || host_frame ? s : c->st;
+        hipStream_t tq = c->serial || host_frame ? s : (c->rq ? c->sf : c->st);
         if (out != c->out_host_dev)                        // (the per-frame call's kernels wrote out_host itself)
             HIPCHK(hipMemcpyAsync(c->out_host + (base - out_base), out + (base - out_base), sizeof(VoFrameOut) * nf,
                                   hipMemcpyDeviceToHost, tq));
@@ -723,6 +734,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         if (c->pf_profile && host_frame) c->pf_wait_end = now_us();
         if (c->sf && !host_frame) HIPCHK(hipStreamSynchronize(c->sf));
         if (tq != s) HIPCHK(hipStreamSynchronize(tq));
+        if (c->rq && c->st && !host_frame) HIPCHK(hipStreamSynchronize(c->st));
         if (host_frame && nf == 1 && c->out_host[base - out_base].frame != base) {
             fprintf(stderr, "[vo_mi355x] single-frame pass did not commit frame %d\n", base);
             return VO_ERR_STATE;
@@ -906,6 +918,10 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     // with relaxed polls the call is 1.5-1.9 us faster per frame (two alternating pairs, r5i)
     d.sel_fused = !(getenv("VO_SEL_FUSED") && atoi(getenv("VO_SEL_FUSED")) == 0);
     d.ransac_fused = !(getenv("VO_RANSAC_FUSED") && atoi(getenv("VO_RANSAC_FUSED")) == 0);
+    // a pipelined pass's later RANSAC chunks on the trajectory queue and the trajectory chain on the
+    // fit queue (VO_RANSAC_Q=0: the chunks on the fit queue, the chain on its own queue): 0.12
+    // m/frame 168.0-168.6k -> 177.6-186.1k, KITTI within noise (three alternating pairs, r5z)
+    c->rq = !(getenv("VO_RANSAC_Q") && atoi(getenv("VO_RANSAC_Q")) == 0);
     // repair windows hold two work records per frame (k_finalize): at most WB / 2 frames
     d.repair_win = std::max(1, std::min(d.WB / 2, getenv("VO_REPAIR_WIN") ? atoi(getenv("VO_REPAIR_WIN")) : VO_REPAIR_WIN_DEFAULT));
     // queue priorities (VO_PRIO): 0 none; 1 the pose and trajectory queues high (the pose queue is the
@@ -922,7 +938,8 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     if (hip_ok(make_stream(&c->sf, false, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
     for (int i = 0; i < vo_ctx::kPassEv; ++i)
         if (hip_ok(hipEventCreateWithFlags(&c->ev_rs[i], hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK ||
-            hip_ok(hipEventCreateWithFlags(&c->ev_fn[i], hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK)
+            hip_ok(hipEventCreateWithFlags(&c->ev_fn[i], hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK ||
+            hip_ok(hipEventCreateWithFlags(&c->ev_r2[i], hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK)
             return bail(VO_ERR_HIP);
     // extract queues: only those a configuration uses (VO_EXTQ / VO_SPLIT / VO_ST_PAIR's scratch
     // copies need no queue of their own) -- every stream takes one of the process's hardware
@@ -1067,6 +1084,7 @@ void vo_destroy(vo_ctx* c)
     for (int i = 0; i < vo_ctx::kPassEv; ++i) {
         if (c->ev_rs[i]) (void)hipEventDestroy(c->ev_rs[i]);
         if (c->ev_fn[i]) (void)hipEventDestroy(c->ev_fn[i]);
+        if (c->ev_r2[i]) (void)hipEventDestroy(c->ev_r2[i]);
     }
     delete c;
 }

@@ -361,12 +361,14 @@ def test_sequence_shards_two_processes(leak_case):
 
 
 # -- execution knobs: every measured-and-kept-off alternative still gives the oracle's rows ------
-@pytest.mark.parametrize("env", ["VO_SPLIT=1", "VO_PRIO=1", "VO_PRIO=-1", "VO_FUSE_FIN=1", "VO_PIPELINE=0", "VO_SEL1=0"])
+@pytest.mark.parametrize("env", ["VO_SPLIT=1", "VO_PRIO=1", "VO_PRIO=-1", "VO_FUSE_FIN=1", "VO_PIPELINE=0", "VO_SEL1=0",
+                                 "VO_RANSAC_Q=0"])
 def test_queue_knobs_match_oracle(leak_case, monkeypatch, env):
     """Per-context queue layouts (read by vo_create): select + describe on a second extract queue
     (VO_SPLIT), pose or extract queues at high priority (VO_PRIO), the pass's finalize in the last
     workgroup of k_triangulate (VO_FUSE_FIN), every pass on the pose queue without cross-pass
-    pipelining (VO_PIPELINE=0), the banded select below its default frame size (VO_SEL1=0)."""
+    pipelining (VO_PIPELINE=0), the banded select below its default frame size (VO_SEL1=0), the later
+    RANSAC chunks on the fit queue and the trajectory chain on its own queue (VO_RANSAC_Q=0)."""
     seq, frames, ref = leak_case
     k, v = env.split("=")
     monkeypatch.setenv(k, v)
