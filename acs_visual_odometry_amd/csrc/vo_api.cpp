@@ -721,7 +721,13 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         // the chunk's output rows (complete once the trajectory queue's last k_traj ran, which
         // waited for the last k_finalize) and the commit point
         hipStream_t tq = c->serial || host_frame ? s : (c->rq ? c->sf : c->st);
-        if (out != c->out_host_dev)                        // (the per-frame call's kernels wrote out_host itself)
+        // (c->rq: a non-pipelined pass runs its trajectory chain on the pose queue, which the fit
+        // queue does not otherwise follow — the re-pass rounds, a missing frame's pass)
+        if (c->rq && tq != s) {
+            HIPCHK(hipEventRecord(c->ev_fin, s));
+            HIPCHK(hipStreamWaitEvent(tq, c->ev_fin, 0));
+        }
+        if (out != c->out_host_dev)                       // (the per-frame call's kernels wrote out_host itself)
             HIPCHK(hipMemcpyAsync(c->out_host + (base - out_base), out + (base - out_base), sizeof(VoFrameOut) * nf,
                                   hipMemcpyDeviceToHost, tq));
         // the commit point after the last finalize (the fit queue's, which the trajectory queue waited
