@@ -233,6 +233,14 @@ double now_us()
 }
 
 // zero_copy: only stage the frame in the pinned buffer; the caller's stencil reads it there over PCIe
+// pinned frame memory the kernels read in place (the per-frame call's staging buffer, vo_host_alloc):
+// VO_HOST_NC=1 non-coherent, 2 coherent, else hipHostMallocDefault
+unsigned frame_host_flags()
+{
+    static const int m = getenv("VO_HOST_NC") ? atoi(getenv("VO_HOST_NC")) : 0;
+    return m == 1 ? hipHostMallocNonCoherent : m == 2 ? hipHostMallocCoherent : hipHostMallocDefault;
+}
+
 int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride, hipStream_t st, bool zero_copy = false)
 {
     const int W = c->cfg.width, H = c->cfg.height;
@@ -1024,7 +1032,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     if (hip_ok(hipMemcpy(c->tab_dev, tab.data(), tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice)) != VO_OK)
         return bail(VO_ERR_HIP);
     d.maxit_tab = c->tab_dev;
-    if (hip_ok(hipHostMalloc((void**)&c->stage_host, np, hipHostMallocDefault)) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(hipHostMalloc((void**)&c->stage_host, np, frame_host_flags())) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipHostMalloc((void**)&c->lo_host, sizeof(int32_t), hipHostMallocDefault)) != VO_OK)
         return bail(VO_ERR_HIP);
     // deterministic contents before first use
@@ -1682,7 +1690,7 @@ int vo_host_alloc(vo_ctx* c, size_t bytes, void** hptr)
 {
     if (!c || !hptr) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    HIPCHK(hipHostMalloc(hptr, std::max<size_t>(bytes, 1), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(hptr, std::max<size_t>(bytes, 1), frame_host_flags()));
     return VO_OK;
 }
 

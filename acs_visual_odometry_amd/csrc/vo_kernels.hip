@@ -426,6 +426,9 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #ifndef ST_DPP_ADD
 #define ST_DPP_ADD 1                   // box sums with v_add_f32_dpp (0: v_mov_b32_dpp + packed adds)
 #endif
+#ifndef ST_LD16
+#define ST_LD16 0                      // one 2-byte source load per lane and row where the columns are not reflected
+#endif
 #define ST_HALO 7                      // blur 3 + gradient 1 + window 2 + nms 1
 #define ST_TCAP VO_TILE_CAP            // candidates per tile (strict maxima: at most one per 2x2 cell)
 #ifndef ST_SEGT_DEFAULT
@@ -750,6 +753,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         return y * W;                                          // frames < 2^31 px
     };
     auto load = [&](int soff) -> uint32_t {
+#if ST_LD16
+        // away from the image's outer columns (no reflection) the pair is one 2-byte load
+        if (!colfix) {
+            const uint32_t v = __builtin_amdgcn_raw_buffer_load_b16(rimg, xl0, soff, 0);
+            return __builtin_amdgcn_perm(0u, v, 0x0c010c00u);
+        }
+#endif
         const uint32_t a = __builtin_amdgcn_raw_buffer_load_b8(rimg, xl0, soff, 0);
         const uint32_t b = __builtin_amdgcn_raw_buffer_load_b8(rimg, xl1, soff, 0);
         return a | (b << 16);
@@ -1774,6 +1784,7 @@ __device__ __forceinline__ void sel_count_body(const VoDev& d, int f0, int slot_
     int ty0, ty1;
     sel_band(nty, w, ty0, ty1);
     const int t0 = ty0 * ntx, nt = (ty1 - ty0) * ntx;
+    VO_STAMP(d, 1960 + w, 0);                            // (stamps: the per-frame select's band w)
     // 1. boundary bin: thread tid holds bins 16 tid .. 16 tid + 15 (loads issued with the band table's)
     uint32_t h[16], hs = 0u;
     {
@@ -1787,6 +1798,7 @@ __device__ __forceinline__ void sel_count_body(const VoDev& d, int f0, int slot_
         for (int q = 0; q < 16; ++q) hs += h[q];
     }
     const int total = sel_band_table(tilerows, t0, nt, s_rows, s_pre, s_tof, s_w);
+    VO_STAMP(d, 1960 + w, 1);
     if (tid == 0) { s_b = -1; s_above = 0; }
     const uint32_t suf = sel_suffix(hs, s_w);            // keys in bins >= 16 tid
     if (tid == 0) s_C = (int)suf;
@@ -1802,6 +1814,7 @@ __device__ __forceinline__ void sel_count_body(const VoDev& d, int f0, int slot_
     }
     __syncthreads();
     const int b = s_b;
+    VO_STAMP(d, 1960 + w, 2);
     // 2. the band's keys above bin b, and its keys of bin b appended to the frame's boundary list
     int D = 0;
     if (b < 0) {
@@ -1843,6 +1856,7 @@ __device__ __forceinline__ void sel_count_body(const VoDev& d, int f0, int slot_
         st_sc1(&ctl->dcount[w], (int)(s_w[0] + s_w[1] + s_w[2] + s_w[3]));
         st_sc1(&ctl->ktot[w], total);                    // the band's keys by the tile row counts
     }
+    VO_STAMP(d, 1960 + w, 3);
     if (!arrive_last(&ctl->arrive, VO_SEL_BANDS, &s_last)) return;
     // 3. last workgroup of the frame: the threshold key, each band's first position
     const int nbk = (int)__hip_atomic_load((gu32*)&ctl->nbnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1920,6 +1934,7 @@ __device__ __forceinline__ void sel_count_body(const VoDev& d, int f0, int slot_
         if (bad) atomicAdd(d.ctr + VO_CTR_ERR, 1u);
         if (fused) __hip_atomic_store((gu32*)&ctl->ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
+    VO_STAMP(d, 1968, 0);                                // the last band: ranked and published
     // every band has read the histogram: leave it zeroed for the next frame's stencil
     uint4* hp = reinterpret_cast<uint4*>(hist) + 4 * tid;
 #pragma unroll
@@ -1957,8 +1972,10 @@ __device__ __forceinline__ void sel_emit_body(const VoDev& d, int f0, int slot_o
     sel_band(nty, w, ty0, ty1);
     const int t0 = ty0 * ntx, nt = (ty1 - ty0) * ntx, r0 = ty0 * ST_TH, nseg = (ty1 - ty0) * ST_TH * ntx;
     if (nt <= 0) return;
+    VO_STAMP(d, 1960 + w, 5);
     for (int s = tid; s < (nseg + 1) / 2; s += SL_T) s_seg32[s] = 0u;
     const int total = sel_band_table(tilerows, t0, nt, s_rows, s_pre, s_tof, s_w);
+    VO_STAMP(d, 1960 + w, 6);
     auto selected = [&](uint64_t key) -> bool {
         if (b < 0) return true;
         const int bin = (int)sel_bin(key, d.thr_bits);
@@ -1993,6 +2010,7 @@ __device__ __forceinline__ void sel_emit_body(const VoDev& d, int f0, int slot_o
         }
     }
     __syncthreads();
+    VO_STAMP(d, 1960 + w, 7);
     // 2. exclusive scan of the segments in raster order: thread tid owns [tid cw, tid cw + cw)
     {
         const int cw = (nseg + SL_T - 1) / SL_T;
@@ -2011,6 +2029,7 @@ __device__ __forceinline__ void sel_emit_body(const VoDev& d, int f0, int slot_o
         }
     }
     __syncthreads();
+    VO_STAMP(d, 1960 + w, 8);
     // 3. each selected key at base + its segment's start + the selected keys before it in the
     //    segment (contiguous compact indices: a segment is one row of one tile)
     const int slot = ext_slot(d, f0, z, slot_override);
@@ -2058,6 +2077,7 @@ __device__ __forceinline__ void sel_emit_body(const VoDev& d, int f0, int slot_o
             if (pos < N) out[pos] = make_int2(col, row);  // < N by construction
         }
     }
+    VO_STAMP(d, 1960 + w, 9);
 }
 
 __global__ void __launch_bounds__(SL_T) k_select_emit(VoDev d, int f0, int slot_override, int nb)
