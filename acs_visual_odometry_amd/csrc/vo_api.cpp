@@ -233,14 +233,6 @@ double now_us()
 }
 
 // zero_copy: only stage the frame in the pinned buffer; the caller's stencil reads it there over PCIe
-// pinned frame memory the kernels read in place (the per-frame call's staging buffer, vo_host_alloc):
-// VO_HOST_NC=1 non-coherent, 2 coherent, else hipHostMallocDefault
-unsigned frame_host_flags()
-{
-    static const int m = getenv("VO_HOST_NC") ? atoi(getenv("VO_HOST_NC")) : 0;
-    return m == 1 ? hipHostMallocNonCoherent : m == 2 ? hipHostMallocCoherent : hipHostMallocDefault;
-}
-
 int upload_frame(vo_ctx* c, const uint8_t* gray, size_t stride, hipStream_t st, bool zero_copy = false)
 {
     const int W = c->cfg.width, H = c->cfg.height;
@@ -975,6 +967,10 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     d.sel_emit_lds = vo::select_emit_lds_bytes(W, H);
     d.sel1 = getenv("VO_SEL1") ? atoi(getenv("VO_SEL1")) != 0 : ntiles < VO_SEL_BANDED_TILES;
     if (d.sel_emit_lds < 0) d.sel1 = 1;
+    // the fused select with its band's keys staged in LDS (VO_SEL_EARLY=0: the emit after the wait)
+    if (d.sel_fused && !(getenv("VO_SEL_EARLY") && atoi(getenv("VO_SEL_EARLY")) == 0) && d.sel_emit_lds >= 0 &&
+        vo::select_fused_lds_bytes(W, H) > 0)
+        d.sel_fused = 2;
     const size_t np = (size_t)W * H;
     rc |= dalloc_rec(c, "frame_in", &d.frame_in, np);
     d.bstride = vo_blur_stride(W);
@@ -1032,7 +1028,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     if (hip_ok(hipMemcpy(c->tab_dev, tab.data(), tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice)) != VO_OK)
         return bail(VO_ERR_HIP);
     d.maxit_tab = c->tab_dev;
-    if (hip_ok(hipHostMalloc((void**)&c->stage_host, np, frame_host_flags())) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(hipHostMalloc((void**)&c->stage_host, np, hipHostMallocDefault)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipHostMalloc((void**)&c->lo_host, sizeof(int32_t), hipHostMallocDefault)) != VO_OK)
         return bail(VO_ERR_HIP);
     // deterministic contents before first use
@@ -1475,6 +1471,7 @@ int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_
             (void)hipGetLastError();
         }
     }
+    const bool gray_staged = gray && !src;
     if (src) {
         SYNC_ALL(c);                  // nothing of an earlier batched call still in flight
     } else if (gray) {
@@ -1483,6 +1480,7 @@ int vo_process_frame(vo_ctx* c, const uint8_t* gray, size_t stride, double pose_
         src = zc ? c->stage_host : c->d.frame_in;
     }
     const double t1 = c->pf_profile ? now_us() : 0.0;
+    if (c->pf_profile && !gray_staged) c->pf_t[0] += t1 - t0;   // (direct: the pointer query and the sync)
     const int f = c->fidx;
     // one frame: extract on the pose queue, a window of one (no speculation)
     // the frame's output row straight into pinned host memory (VO_PF_OUT_ZC=0: a device row and a copy)
@@ -1690,7 +1688,7 @@ int vo_host_alloc(vo_ctx* c, size_t bytes, void** hptr)
 {
     if (!c || !hptr) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    HIPCHK(hipHostMalloc(hptr, std::max<size_t>(bytes, 1), frame_host_flags()));
+    HIPCHK(hipHostMalloc(hptr, std::max<size_t>(bytes, 1), hipHostMallocDefault));
     return VO_OK;
 }
 

@@ -266,7 +266,8 @@ struct VoDev {
     int sel_lds;          // select (single-workgroup form, VO_SEL1=1): dynamic LDS bytes
     int sel_emit_lds;     // banded select: k_select_emit's dynamic LDS bytes (a band's segment counts)
     int sel1;             // VO_SEL1=1: the single-workgroup select (one 1024-thread workgroup per frame)
-    int sel_fused;        // the per-frame call's banded select in one launch (k_select_fused; VO_SEL_FUSED=0: two)
+    int sel_fused;        // the per-frame call's banded select in one launch (k_select_fused; VO_SEL_FUSED=0: two);
+                          // 2: keys staged in LDS, the bitmap built before the wait (VO_SEL_EARLY=0: 1)
     int ransac_fused;     // one frame's two RANSAC chunks in one launch (k_ransac_fused; VO_RANSAC_FUSED=0: two)
     int rng_mode;         // VO_RNG_MT19937: the hypotheses' samples come from `samples` (host-drawn std::sample)
     int32_t* samples;     // x WB records: max_hyp x 8 indices per record (VO_RNG_MT19937 only)
@@ -324,6 +325,7 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
 void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s);
 int select_lds_bytes(int W, int H, int* key_cap);     // sets the kernel attribute; <0 on failure
 int select_emit_lds_bytes(int W, int H);              // banded select: sets the attribute; <0 if the band does not fit
+int select_fused_lds_bytes(int W, int H);             // k_select_fused with staged keys: sets the attribute; <0: no fit
 void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned publish, hipStream_t s);
 void launch_ext_missing(const VoDev& d, int slot, hipStream_t s);   // extract side of a missing image
 // pose pass over the window (stage = 0) or over work[0] prepared by a stage API (stage = 1)

@@ -426,9 +426,6 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #ifndef ST_DPP_ADD
 #define ST_DPP_ADD 1                   // box sums with v_add_f32_dpp (0: v_mov_b32_dpp + packed adds)
 #endif
-#ifndef ST_LD16
-#define ST_LD16 0                      // one 2-byte source load per lane and row where the columns are not reflected
-#endif
 #define ST_HALO 7                      // blur 3 + gradient 1 + window 2 + nms 1
 #define ST_TCAP VO_TILE_CAP            // candidates per tile (strict maxima: at most one per 2x2 cell)
 #ifndef ST_SEGT_DEFAULT
@@ -753,13 +750,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         return y * W;                                          // frames < 2^31 px
     };
     auto load = [&](int soff) -> uint32_t {
-#if ST_LD16
-        // away from the image's outer columns (no reflection) the pair is one 2-byte load
-        if (!colfix) {
-            const uint32_t v = __builtin_amdgcn_raw_buffer_load_b16(rimg, xl0, soff, 0);
-            return __builtin_amdgcn_perm(0u, v, 0x0c010c00u);
-        }
-#endif
         const uint32_t a = __builtin_amdgcn_raw_buffer_load_b8(rimg, xl0, soff, 0);
         const uint32_t b = __builtin_amdgcn_raw_buffer_load_b8(rimg, xl1, soff, 0);
         return a | (b << 16);
@@ -1687,6 +1677,10 @@ __host__ __device__ inline SelBandLayout sel_band_layout(int ntx, int nty)
     L.total = L.seg + al(2 * (nbr * ST_TH * ntx + 1));
     return L;
 }
+// the fused select's LDS past the band layout: the band's keys (u64, SL_TOF_CAP) and its boundary-bin
+// keys' compact indices (int, SL_TOF_CAP)
+__host__ __device__ inline int sel_fused_kbuf(int ntx, int nty) { return (sel_band_layout(ntx, nty).total + 15) & ~15; }
+__host__ __device__ inline int sel_fused_lds(int ntx, int nty) { return sel_fused_kbuf(ntx, nty) + 12 * SL_TOF_CAP; }
 __device__ __forceinline__ int row_bytes(uint4 rc)
 {
     uint32_t s = 0u;
@@ -1759,8 +1753,13 @@ __device__ __forceinline__ int sel_tile_of(int g, int total, int nt, const int* 
 
 // fused (the per-frame call's k_select_fused): the last band to arrive also publishes ctl->ready
 // after writing the threshold and the band positions, for the other bands waiting in the same launch
-__device__ __forceinline__ void sel_count_body(const VoDev& d, int f0, int slot_override, int z, int w,
-                                               unsigned char* smem, bool fused)
+// kbuf (the fused select, a band of at most SL_TOF_CAP keys): the band's keys are kept in LDS as they
+// are read (kbuf[g], compact index g), for the emit in the same launch.  Returns whether this band
+// arrived last (ranked the boundary keys and published); *total_out / *b_out: the band's key count
+// and the boundary bin
+__device__ __forceinline__ bool sel_count_body(const VoDev& d, int f0, int slot_override, int z, int w,
+                                               unsigned char* smem, bool fused, uint64_t* kbuf = nullptr,
+                                               int* total_out = nullptr, int* b_out = nullptr)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int N = d.N;
@@ -1814,6 +1813,8 @@ __device__ __forceinline__ void sel_count_body(const VoDev& d, int f0, int slot_
     }
     __syncthreads();
     const int b = s_b;
+    if (total_out) { *total_out = total; *b_out = b; }
+    if (total > SL_TOF_CAP) kbuf = nullptr;
     VO_STAMP(d, 1960 + w, 2);
     // 2. the band's keys above bin b, and its keys of bin b appended to the frame's boundary list
     int D = 0;
@@ -1834,6 +1835,7 @@ __device__ __forceinline__ void sel_count_body(const VoDev& d, int f0, int slot_
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int g = g0 + u * SL_T + tid;
+                if (kbuf && g < total) kbuf[g] = key[u];
                 const int bin = g < total ? (int)sel_bin(key[u], d.thr_bits) : -1;
                 D += bin > b ? 1 : 0;
                 const unsigned long long m = ballot64(bin == b);
@@ -1857,7 +1859,7 @@ __device__ __forceinline__ void sel_count_body(const VoDev& d, int f0, int slot_
         st_sc1(&ctl->ktot[w], total);                    // the band's keys by the tile row counts
     }
     VO_STAMP(d, 1960 + w, 3);
-    if (!arrive_last(&ctl->arrive, VO_SEL_BANDS, &s_last)) return;
+    if (!arrive_last(&ctl->arrive, VO_SEL_BANDS, &s_last)) return false;
     // 3. last workgroup of the frame: the threshold key, each band's first position
     const int nbk = (int)__hip_atomic_load((gu32*)&ctl->nbnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int need = N - s_above;                        // boundary keys to select (b >= 0)
@@ -1939,6 +1941,7 @@ __device__ __forceinline__ void sel_count_body(const VoDev& d, int f0, int slot_
     uint4* hp = reinterpret_cast<uint4*>(hist) + 4 * tid;
 #pragma unroll
     for (int q = 0; q < 4; ++q) hp[q] = make_uint4(0u, 0u, 0u, 0u);
+    return true;
 }
 
 __global__ void __launch_bounds__(SL_T) k_select_count(VoDev d, int f0, int slot_override, int nb)
@@ -2080,6 +2083,131 @@ __device__ __forceinline__ void sel_emit_body(const VoDev& d, int f0, int slot_o
     VO_STAMP(d, 1960 + w, 9);
 }
 
+// The fused select's emit for a band of at most SL_TOF_CAP keys (sel_count_body staged them in kbuf and
+// left the band table in LDS): the selection bitmap and segment counts of every key outside the
+// boundary bin b are known before the threshold key Tb is, so they are built while the last band
+// ranks; after the wait only the band's boundary-bin keys (their compact indices in s_bl) are added
+// against Tb.  Then the segment scan and the emission as sel_emit_body, keys from LDS.
+// wait(): blocks until ctl->ready (false: timed out)
+template <typename Wait>
+__device__ __forceinline__ void sel_emit_fused(const VoDev& d, int f0, int slot_override, int z, int w,
+                                               unsigned char* smem, int total, int b, Wait&& wait)
+{
+    __shared__ uint32_t s_w[4];
+    __shared__ int s_nbl;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int N = d.N;
+    const int ntx = (d.W + ST_TW - 1) / ST_TW, nty = (d.H + ST_TH - 1) / ST_TH;
+    const SelBandLayout L = sel_band_layout(ntx, nty);
+    uint4* s_rows = reinterpret_cast<uint4*>(smem + L.rows);
+    int* s_pre = reinterpret_cast<int*>(smem + L.pre);
+    uint16_t* s_tof = reinterpret_cast<uint16_t*>(smem + L.tof);
+    uint64_t* s_bits = reinterpret_cast<uint64_t*>(smem + L.bits);
+    uint16_t* s_seg = reinterpret_cast<uint16_t*>(smem + L.seg);
+    uint32_t* s_seg32 = reinterpret_cast<uint32_t*>(smem + L.seg);
+    const uint64_t* kbuf = reinterpret_cast<const uint64_t*>(smem + sel_fused_kbuf(ntx, nty));
+    int* s_bl = reinterpret_cast<int*>(smem + sel_fused_kbuf(ntx, nty) + 8 * SL_TOF_CAP);
+    const uint64_t* cand = d.cand + (size_t)z * d.cand_cap;
+    const VoSelCtl* ctl = d.selctl + z;
+    int ty0, ty1;
+    sel_band(nty, w, ty0, ty1);
+    const int t0 = ty0 * ntx, nt = (ty1 - ty0) * ntx, r0 = ty0 * ST_TH, nseg = (ty1 - ty0) * ST_TH * ntx;
+    // (b < 0: sel_count_body read no key; every key is selected, from the tiles)
+    auto key_of = [&](int g, int k) { return b >= 0 ? kbuf[g] : cand[(size_t)(t0 + k) * ST_TCAP + (g - s_pre[k])]; };
+    auto seg_of = [&](uint64_t key, int k) { return ((int)((key >> 16) & 0xFFFF) - r0) * ntx + (t0 + k) % ntx; };
+    VO_STAMP(d, 1960 + w, 5);
+    if (nt > 0) {
+        for (int s = tid; s < (nseg + 1) / 2; s += SL_T) s_seg32[s] = 0u;
+        if (tid == 0) s_nbl = 0;
+        __syncthreads();
+        VO_STAMP(d, 1960 + w, 6);
+        // 1. bitmap and segment counts of the keys above bin b; bin b's keys listed
+        for (int g0 = 0; g0 < total; g0 += SL_T) {
+            const int g = g0 + tid;
+            bool sel = false;
+            if (g < total) {
+                const int k = s_tof[g];
+                const uint64_t key = key_of(g, k);
+                const int bin = b >= 0 ? (int)sel_bin(key, d.thr_bits) : 0;
+                sel = b < 0 || bin > b;
+                if (sel) {
+                    const int sg = seg_of(key, k);
+                    atomicAdd(&s_seg32[sg >> 1], 1u << (16 * (sg & 1)));
+                } else if (bin == b) {
+                    s_bl[atomicAdd(&s_nbl, 1)] = g;
+                }
+            }
+            const unsigned long long m = ballot64(sel);
+            if (lane == 0 && g < total) s_bits[g >> 6] = m;
+        }
+    }
+    // 2. the threshold key and the band's first position
+    if (!wait()) return;
+    const int base = ctl->base[w];
+    const uint64_t Tb = ctl->Tb;
+    if (nt <= 0) return;
+    VO_STAMP(d, 1960 + w, 7);
+    // 3. bin b's keys at or above Tb
+    for (int i = tid; i < s_nbl; i += SL_T) {
+        const int g = s_bl[i];
+        const uint64_t key = kbuf[g];
+        if (key >= Tb) {
+            atomicOr(&s_bits[g >> 6], 1ull << (g & 63));
+            const int sg = seg_of(key, s_tof[g]);
+            atomicAdd(&s_seg32[sg >> 1], 1u << (16 * (sg & 1)));
+        }
+    }
+    __syncthreads();
+    // 4. exclusive scan of the segments in raster order: thread tid owns [tid cw, tid cw + cw)
+    {
+        const int cw = (nseg + SL_T - 1) / SL_T;
+        const int s0 = min(tid * cw, nseg), s1 = min(s0 + cw, nseg);
+        uint32_t mine = 0u;
+        for (int s = s0; s < s1; ++s) mine += s_seg[s];
+        const uint32_t after = sel_suffix(mine, s_w);
+        __shared__ uint32_t s_sum;
+        if (tid == 0) s_sum = after;
+        __syncthreads();
+        uint32_t pre = s_sum - after;
+        for (int s = s0; s < s1; ++s) {
+            const uint32_t v = s_seg[s];
+            s_seg[s] = (uint16_t)pre;
+            pre += v;
+        }
+    }
+    __syncthreads();
+    VO_STAMP(d, 1960 + w, 8);
+    // 5. each selected key at base + its segment's start + the selected keys before it in the segment
+    const int slot = ext_slot(d, f0, z, slot_override);
+    int2* out = d.kps + (size_t)slot * N;
+    for (int g = tid; g < total; g += SL_T) {
+        if (!((s_bits[g >> 6] >> (g & 63)) & 1ull)) continue;
+        const int k = s_tof[g];
+        const uint64_t key = key_of(g, k);
+        const int row = (int)((key >> 16) & 0xFFFF), col = (int)(key & 0xFFFF);
+        const int r = row & (ST_TH - 1);
+        const uint4 rc = s_rows[k];
+        const uint32_t w4[4] = {rc.x, rc.y, rc.z, rc.w};
+        int start = s_pre[k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int sh = 8 * min(max(r - 4 * q, 0), 4);
+            const uint32_t msk = (uint32_t)(0xFFFFFFFFull >> (32 - sh));
+            start = (int)__builtin_amdgcn_udot4(w4[q] & msk, 0x01010101u, (uint32_t)start, false);
+        }
+        int within = 0;
+        for (int wi = start >> 6; wi <= (g >> 6); ++wi) {
+            uint64_t m = s_bits[wi];
+            if (wi == (start >> 6)) m &= ~0ull << (start & 63);
+            if (wi == (g >> 6)) m &= (g & 63) ? (~0ull >> (64 - (g & 63))) : 0ull;
+            within += __popcll(m);
+        }
+        const int pos = base + (int)s_seg[seg_of(key, k)] + within;
+        if (pos < N) out[pos] = make_int2(col, row);
+    }
+    VO_STAMP(d, 1960 + w, 9);
+}
+
 __global__ void __launch_bounds__(SL_T) k_select_emit(VoDev d, int f0, int slot_override, int nb)
 {
     int z, w;
@@ -2103,28 +2231,49 @@ __global__ void __launch_bounds__(SL_T) k_select_fused(VoDev d, int f0, int slot
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ unsigned s_timeout, s_last2;
     VoSelCtl* ctl = d.selctl + z;
-    sel_count_body(d, f0, slot_override, z, w, smem, true);
+    const int ntx = (d.W + ST_TW - 1) / ST_TW, nty = (d.H + ST_TH - 1) / ST_TH;
+    int total = 0, b = -1;
+    // d.sel_fused == 2: bands of at most SL_TOF_CAP keys keep them in LDS and build the bitmap before
+    // the wait (sel_emit_fused); 1 (VO_SEL_EARLY=0, or a frame whose fused LDS does not fit): the
+    // emit after the wait (sel_emit_body)
+    const bool early = d.sel_fused == 2;
+    const bool last = sel_count_body(d, f0, slot_override, z, w, smem, true,
+                                     early ? reinterpret_cast<uint64_t*>(smem + sel_fused_kbuf(ntx, nty)) : nullptr,
+                                     &total, &b);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned it = 0u;
-        // relaxed polls (a device-coherent load each), one acquire after the loop: an acquire poll
-        // invalidates the XCD's L2 (buffer_inv sc1) on every iteration, under the working waves
-        while (__hip_atomic_load((gu32*)&ctl->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u && it < SEL_FUSED_SPIN) {
-            __builtin_amdgcn_s_sleep(2);
-            ++it;
+    // wait for the last band's threshold and positions (the last band itself published them)
+    auto wait = [&]() -> bool {
+        if (!last) {
+            if (threadIdx.x == 0) {
+                unsigned it = 0u;
+                // relaxed polls (a device-coherent load each), one acquire after the loop: an acquire poll
+                // invalidates the XCD's L2 (buffer_inv sc1) on every iteration, under the working waves
+                while (__hip_atomic_load((gu32*)&ctl->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+                       it < SEL_FUSED_SPIN) {
+                    __builtin_amdgcn_s_sleep(2);
+                    ++it;
+                }
+                s_timeout = it >= SEL_FUSED_SPIN ? 1u : 0u;
+            }
+            __syncthreads();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the ranked threshold and band positions
+            if (s_timeout) {
+                if (threadIdx.x == 0) {
+                    const int slot = ext_slot(d, f0, z, slot_override);
+                    d.ext_n[slot] = 0;
+                    d.ext_st[slot] = VO_STATUS_INCONSISTENT;
+                    atomicAdd(d.ctr + VO_CTR_ERR, 1u);
+                }
+                return false;
+            }
+        } else {
+            __syncthreads();
         }
-        s_timeout = it >= SEL_FUSED_SPIN ? 1u : 0u;
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the ranked threshold and band positions
-    if (s_timeout) {
-        if (threadIdx.x == 0) {
-            const int slot = ext_slot(d, f0, z, slot_override);
-            d.ext_n[slot] = 0;
-            d.ext_st[slot] = VO_STATUS_INCONSISTENT;
-            atomicAdd(d.ctr + VO_CTR_ERR, 1u);
-        }
-    } else {
+        return true;
+    };
+    if (early && total <= SL_TOF_CAP) {
+        sel_emit_fused(d, f0, slot_override, z, w, smem, total, b, wait);
+    } else if (wait()) {
         sel_emit_body(d, f0, slot_override, z, w, smem);
     }
     if (!arrive_last(&ctl->arrive2, VO_SEL_BANDS, &s_last2)) return;
@@ -5063,7 +5212,8 @@ void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_
     }
     const dim3 g(xcd_grid(VO_SEL_BANDS, nb));
     if (d.single && nb == 1 && d.sel_fused) {          // the per-frame call: one launch
-        hipLaunchKernelGGL(k_select_fused, g, dim3(SL_T), (size_t)d.sel_emit_lds, s, d, f0, slot_override, nb);
+        const int fl = d.sel_fused == 2 ? sel_fused_lds((d.W + ST_TW - 1) / ST_TW, (d.H + ST_TH - 1) / ST_TH) : d.sel_emit_lds;
+        hipLaunchKernelGGL(k_select_fused, g, dim3(SL_T), (size_t)fl, s, d, f0, slot_override, nb);
         return;
     }
     // the count kernel uses the layout's tile table only (rows, pre, tof)
@@ -5083,6 +5233,16 @@ int select_emit_lds_bytes(int W, int H)
             return -1;
     }
     return bytes;
+}
+int select_fused_lds_bytes(int W, int H)
+{
+    const int ntx = (W + ST_TW - 1) / ST_TW, nty = (H + ST_TH - 1) / ST_TH;
+    const int fbytes = sel_fused_lds(ntx, nty);      // the band layout + its staged keys (96 KB)
+    if (fbytes > 150 * 1024) return -1;
+    if (fbytes > 64 * 1024 &&
+        hipFuncSetAttribute((const void*)k_select_fused, hipFuncAttributeMaxDynamicSharedMemorySize, fbytes) != hipSuccess)
+        return -1;
+    return fbytes;
 }
 void launch_ext_missing(const VoDev& d, int slot, hipStream_t s)
 {

@@ -442,12 +442,13 @@ print("PF_OK" if ok else "PF_DIFF")
 
 
 @pytest.mark.parametrize("env", ["VO_PF_ZEROCOPY=0", "VO_DS_LDS_TABLE=1", "VO_DS_PF=0", "VO_RANSAC_FUSED=0",
-                                 "VO_SEL_FUSED=0", "VO_PF_OUT_ZC=0", "VO_PF_PINNED_DIRECT=0",
+                                 "VO_SEL_FUSED=0", "VO_SEL_EARLY=0", "VO_PF_OUT_ZC=0", "VO_PF_PINNED_DIRECT=0",
                                  "VO_PF_SEGT=2", "VO_RANSAC_WAVE_HYP=0"])
 def test_per_frame_knobs_match_oracle(leak_case, tmp_path, env):
     """Per-frame-call knobs read once per process (the upload kernel instead of the stencil reading
     the frame from the pinned staging buffer, describe's LDS pair table, the one-wave describe instead
-    of k_describe_pf, the two RANSAC launches instead of k_ransac_fused, the two-launch select, the
+    of k_describe_pf, the two RANSAC launches instead of k_ransac_fused, the two-launch select, the fused select emitting
+    after its wait with keys from the tiles, the
     output row through a device copy, pinned caller frames staged instead of read in place, stencil
     segments of two tile rows, eight RANSAC hypotheses per wave), in a child process over the leak sequence: one
     vo_process_frame per frame, rows, statuses and counts equal the oracle's."""

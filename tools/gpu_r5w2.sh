@@ -9,6 +9,8 @@ VO_LIB_PATH=acs_visual_odometry_amd/libvo_mi355x_ld16.so timeout -k 10 600 pytho
 tail -1 $O/pytest.log
 VO_LIB_PATH=acs_visual_odometry_amd/libvo_mi355x_stamps.so timeout -k 10 200 python3 tools/stamps_select_pf.py > $O/stamps_select_pf.txt 2>&1 || { echo STAMPS_FAIL; tail $O/stamps_select_pf.txt; exit 1; }
 cat $O/stamps_select_pf.txt
+VO_PF_PROFILE=1 PF_PINNED=1 timeout -k 10 200 python3 tools/pf_loop.py 60 > $O/pfprof.txt 2>&1 || { echo PFPROF_FAIL; tail $O/pfprof.txt; exit 1; }
+tail -3 $O/pfprof.txt
 for nc in 0 1 2; do for lib in libvo_mi355x.so libvo_mi355x_ld16.so; do
   VO_HOST_NC=$nc VO_LIB_PATH=acs_visual_odometry_amd/$lib PF_PINNED=1 timeout -k 10 200 python3 tools/pf_loop.py 60 > $O/pf.txt 2>&1 || { echo PF_FAIL; tail $O/pf.txt; exit 1; }
   echo "NC=$nc $lib $(tail -1 $O/pf.txt)"

@@ -1,0 +1,19 @@
+# the fused select with the band's keys staged in LDS and the bitmap built before the wait
+# (d.sel_fused == 2) against the emit after the wait (VO_SEL_EARLY=0): parity, stamps, per-call A/B
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r5w3}; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_paths.py tests/test_gpu_parity.py tests/test_select_consistency.py tests/test_gpu_matchers.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for e in 1 0; do
+  VO_SEL_EARLY=$e VO_LIB_PATH=acs_visual_odometry_amd/libvo_mi355x_stamps.so timeout -k 10 200 python3 tools/stamps_select_pf.py > $O/stamps_select_pf_$e.txt 2>&1 || { echo STAMPS_FAIL; tail $O/stamps_select_pf_$e.txt; exit 1; }
+  echo "VO_SEL_EARLY=$e"; cat $O/stamps_select_pf_$e.txt
+done
+for rep in 1 2; do for e in 1 0; do
+  VO_SEL_EARLY=$e PF_PINNED=1 timeout -k 10 200 python3 tools/pf_loop.py 60 > $O/pf.txt 2>&1 || { echo PF_FAIL; tail $O/pf.txt; exit 1; }
+  echo "VO_SEL_EARLY=$e $(tail -1 $O/pf.txt)"
+done; done
+PF_PINNED=1 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/tr -o pf -- python3 tools/pf_loop.py 30 > $O/tr.txt 2>&1 || { echo PFTRACE_FAIL; tail $O/tr.txt; exit 1; }
+python3 tools/pf_timeline.py $O/tr > $O/pf_timeline.txt 2>&1; cat $O/pf_timeline.txt
+echo DONE
