@@ -426,6 +426,10 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #ifndef ST_DPP_ADD
 #define ST_DPP_ADD 1                   // box sums with v_add_f32_dpp (0: v_mov_b32_dpp + packed adds)
 #endif
+#ifndef ST_PF_BPERM
+#define ST_PF_BPERM 1                  // one-tile-row segments: a row's 128 source bytes by two 64-byte loads and
+                                       // two ds_bpermute (instead of two overlapping 128-byte loads)
+#endif
 #define ST_HALO 7                      // blur 3 + gradient 1 + window 2 + nms 1
 #define ST_TCAP VO_TILE_CAP            // candidates per tile (strict maxima: at most one per 2x2 cell)
 #ifndef ST_SEGT_DEFAULT
@@ -749,7 +753,31 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         const int y = refl101(ys - ST_HALO + k0 + (lane & 15), H);
         return y * W;                                          // frames < 2^31 px
     };
+#if ST_PF_BPERM
+    constexpr bool BP = SEGT == 1;
+#else
+    constexpr bool BP = false;
+#endif
+    // BP: lane l loads window columns l and 64 + l (one 64-byte span per load), packed as bytes 0 / 1;
+    // its pair (window columns 2l, 2l + 1) comes back by two ds_bpermute and a byte select
+    const int xa = refl101(xs - VO_STRIP_XL + lane, W), xb = refl101(xs - VO_STRIP_XL + 64 + lane, W);
+    const int bpi0 = ((2 * lane) & 63) << 2, bpi1 = ((2 * lane + 1) & 63) << 2;
+    const uint32_t bsel = lane >= 32 ? 0x0c050c01u : 0x0c040c00u;
+    auto unpack = [&](uint32_t P) -> uint32_t {
+        if constexpr (BP) {
+            const uint32_t r0 = (uint32_t)__builtin_amdgcn_ds_bpermute(bpi0, (int)P);
+            const uint32_t r1 = (uint32_t)__builtin_amdgcn_ds_bpermute(bpi1, (int)P);
+            return __builtin_amdgcn_perm(r1, r0, bsel);
+        } else {
+            return P;
+        }
+    };
     auto load = [&](int soff) -> uint32_t {
+        if constexpr (BP) {
+            const uint32_t a = __builtin_amdgcn_raw_buffer_load_b8(rimg, xa, soff, 0);
+            const uint32_t b = __builtin_amdgcn_raw_buffer_load_b8(rimg, xb, soff, 0);
+            return a | (b << 8);
+        }
         const uint32_t a = __builtin_amdgcn_raw_buffer_load_b8(rimg, xl0, soff, 0);
         const uint32_t b = __builtin_amdgcn_raw_buffer_load_b8(rimg, xl1, soff, 0);
         return a | (b << 16);
@@ -1035,6 +1063,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         st_for([&](auto U) { src[U] = load(__builtin_amdgcn_readlane(rows, U)); }, std::make_integer_sequence<int, 14>{});
         const int rows2 = row_offsets(14);
         st_for([&](auto U) { ahead[U] = load(__builtin_amdgcn_readlane(rows2, U)); }, std::make_integer_sequence<int, LA>{});
+        if constexpr (BP) st_for([&](auto U) { src[U] = unpack(src[U]); }, std::make_integer_sequence<int, 14>{});
         st_for([&](auto U) { step(P0{}, U, src[U], R0{}); }, std::make_integer_sequence<int, 6>{});
         step(P1{}, 6, src[6], R0{});
         step(P1{}, 7, src[7], R0{});
@@ -1045,6 +1074,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         step(P4{}, 12, src[12], R0{});
         step(P4{}, 13, src[13], R0{});
     }
+    // BP: row k0 + U's pair unpacked one row ahead of its step (the ds_bpermute latency under the step)
+    uint32_t nxt = BP ? unpack(ahead[0]) : 0u;
     // one tile row group (16 rows) per iteration; the last segment may hold fewer tiles.  Row
     // k0 + u + LA is requested as row k0 + u is consumed (the last group's requests past the
     // segment read rows that are never used)
@@ -1063,7 +1094,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         st_for([&](auto U) { soff[U] = __builtin_amdgcn_readlane(rows, U); }, std::make_integer_sequence<int, ST_TH>{});
 #endif
         st_for([&](auto U) {
-            const uint32_t cur = ahead[U % LA];
+            uint32_t cur = ahead[U % LA];
+            if constexpr (BP) {
+                cur = nxt;
+                if (U + 1 < ST_TH) nxt = unpack(ahead[(U + 1) % LA]);
+            }
             // the row requested here is consumed only if it lies inside the segment: in the last group
             // the requests of steps U >= ST_TH - LA would read past it (wave-uniform; none for SEGT 1)
             if (U < ST_TH - LA || (SEGT > 1 && i + 1 < ntl)) {
