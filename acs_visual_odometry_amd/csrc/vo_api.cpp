@@ -953,9 +953,12 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     // serialises behind its kernels
     {
         c->nq = getenv("VO_EXTQ") ? std::max(1, std::min(VO_EXT_QUEUES, atoi(getenv("VO_EXTQ")))) : 1;
-        const int ne = c->split ? 2 : c->nq;
+        // VO_SPLIT=2: the second split queue is the trajectory queue (no fifth stream)
+        const bool split_st = c->split && getenv("VO_SPLIT") && atoi(getenv("VO_SPLIT")) == 2;
+        const int ne = c->split ? (split_st ? 1 : 2) : c->nq;
         for (int i = 0; i < ne; ++i)
             if (hip_ok(make_stream(&c->se[i], true, p_ext)) != VO_OK) return bail(VO_ERR_HIP);
+        if (split_st) c->se[1] = c->st;
     }
     if (hip_ok(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming)) != VO_OK) return bail(VO_ERR_HIP);
     d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
@@ -1086,7 +1089,7 @@ void vo_destroy(vo_ctx* c)
         if (e) (void)hipEventDestroy(e);
     for (auto& kv : c->tab_by_p) (void)hipFree(kv.second);
     for (hipStream_t q : c->se)
-        if (q) (void)hipStreamDestroy(q);
+        if (q && q != c->st) (void)hipStreamDestroy(q);
     if (c->s) (void)hipStreamDestroy(c->s);
     if (c->st) (void)hipStreamDestroy(c->st);
     if (c->ev_fin) (void)hipEventDestroy(c->ev_fin);

@@ -361,7 +361,7 @@ def test_sequence_shards_two_processes(leak_case):
 
 
 # -- execution knobs: every measured-and-kept-off alternative still gives the oracle's rows ------
-@pytest.mark.parametrize("env", ["VO_SPLIT=1", "VO_PRIO=1", "VO_PRIO=-1", "VO_FUSE_FIN=1", "VO_PIPELINE=0", "VO_SEL1=0",
+@pytest.mark.parametrize("env", ["VO_SPLIT=1", "VO_SPLIT=2", "VO_PRIO=1", "VO_PRIO=-1", "VO_FUSE_FIN=1", "VO_PIPELINE=0", "VO_SEL1=0",
                                  "VO_RANSAC_Q=0"])
 def test_queue_knobs_match_oracle(leak_case, monkeypatch, env):
     """Per-context queue layouts (read by vo_create): select + describe on a second extract queue
