@@ -154,6 +154,9 @@ def test_extract_bit_exact(which, ctx_kitti, scene, factory):
     (640, 480, 64, "scene"),        # tiny N: the boundary bin holds most of the ranking
     (1280, 720, 500, "periodic"),   # identical blobs: thousands of equal responses in the boundary bin
     (1280, 720, 1500, "periodic"),  #   (ranked by the radix select over the boundary list)
+    (1920, 768, 4096, "mixed"),     # dense blobs over noise: the fused select's upper bands hold more
+                                    # than SL_TOF_CAP keys (emit after the wait), its lower bands fewer
+                                    # (keys staged in LDS, bitmap before the wait), in one frame
 ])
 @pytest.mark.parametrize("sel1", ["", "0", "1"])
 def test_extract_sizes_bit_exact(W, H, N, kind, sel1, monkeypatch):
@@ -165,6 +168,12 @@ def test_extract_sizes_bit_exact(W, H, N, kind, sel1, monkeypatch):
         img = SceneSequence(W, H, nframes=2, step=0.05).frames()[1]
     elif kind == "noise":
         img = noise_frames(W, H, 1)[0]
+    elif kind == "mixed":
+        img = noise_frames(W, H, 1)[0].copy()
+        img[:H // 2] = 60
+        for y in range(0, H // 2, 6):
+            for x in range(0, W, 6):
+                img[y:y + 3, x:x + 3] = 200
     elif kind == "periodic":
         img = np.full((H, W), 60, np.uint8)
         for y in range(40, H - 48, 12):
