@@ -10,6 +10,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VO_LIB_PATH") or os.path.join(_HERE, "libvo_mi355x.so")   # override: diagnostic builds
 
+VO_ABI_VERSION = 2        # include/vo_mi355x.h; VoConfig below mirrors that version's vo_config
 VO_OK = 0
 VO_ERR_IO = -6
 VO_ERR_INTERNAL = -7
@@ -97,6 +98,8 @@ def load():
     L.vo_unpack_descriptor.restype = None
     L.vo_selftest_arith.argtypes = [P, P, P, P, P, P, I, I]
     L.vo_selftest_nullvec9.argtypes = [P, P, P, P, I, I]
+    if L.vo_abi_version() != VO_ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH}: ABI version {L.vo_abi_version()}, this binding is {VO_ABI_VERSION}")
     _lib = L
     return L
 

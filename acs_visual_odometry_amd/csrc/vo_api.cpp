@@ -205,6 +205,13 @@ int read_work0(vo_ctx* c, VoWork* w)
 {
     SYNC_ALL(c);
     HIPCHK(hipMemcpy(w, c->d.work, sizeof(VoWork), hipMemcpyDeviceToHost));
+    // a bounded in-kernel wait that timed out (k_ransac_fused, k_select_fused) counts in ctr[VO_CTR_ERR]
+    uint32_t nerr = 0;
+    HIPCHK(hipMemcpy(&nerr, c->d.ctr + VO_CTR_ERR, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (nerr) {
+        fprintf(stderr, "[vo_mi355x] device error counter is %u (a consistency check or bounded wait failed)\n", nerr);
+        return VO_ERR_INTERNAL;
+    }
     return VO_OK;
 }
 
@@ -762,7 +769,10 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     // a frame the select's consistency check failed (VO_STATUS_INCONSISTENT): a library defect, loud
     for (int f = base; f < end; ++f)
         if (c->out_host[f - out_base].status == VO_STATUS_INCONSISTENT || c->out_host[f - out_base].err) {
-            fprintf(stderr, "[vo_mi355x] frame %d: select consistency check failed (VO_STATUS_INCONSISTENT)\n", f);
+            // err bit 0: the frame's select failed its consistency check; bit 1: the context's device
+            // error counter was set when the frame was committed (a bounded in-kernel wait timed out)
+            fprintf(stderr, "[vo_mi355x] frame %d: device consistency check failed (err %d)\n", f,
+                    c->out_host[f - out_base].err);
             return VO_ERR_INTERNAL;
         }
     return VO_OK;
@@ -919,6 +929,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     c->split = VO_EXT_QUEUES >= 2 && (getenv("VO_SPLIT") ? atoi(getenv("VO_SPLIT")) != 0 : VO_SPLIT_DEFAULT != 0);
     c->slack = getenv("VO_SLACK") ? std::max(0, std::min(64, atoi(getenv("VO_SLACK")))) : VO_SLACK_DEFAULT;
     d.fault_inject = getenv("VO_FAULT_INJECT") && atoi(getenv("VO_FAULT_INJECT")) != 0;   // tests only
+    d.spin_limit = getenv("VO_SPIN_LIMIT") ? (unsigned)atoi(getenv("VO_SPIN_LIMIT")) : (1u << 22);   // tests only
     // the per-frame call's select in one launch (VO_SEL_FUSED=0: two launches).  With acquire polls it
     // was slower (21.2 us against 9.0 + 9.2 us, gpurun_out r5e: each poll invalidated the XCD's L2);
     // with relaxed polls the call is 1.5-1.9 us faster per frame (two alternating pairs, r5i)

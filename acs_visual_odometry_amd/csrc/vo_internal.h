@@ -227,6 +227,9 @@ struct VoSelCtl {
                                      // consistency check: their sum must equal the histogram's total)
     uint32_t ready;                  // k_select_fused: the threshold and band positions are written
     uint32_t arrive2;                // k_select_fused: bands done emitting (the last clears ready)
+    uint32_t timeout;                // k_select_fused: a band timed out waiting for ready (the last band
+                                     // to finish emitting marks the slot INCONSISTENT after the ranker's
+                                     // OK store, then clears it)
 };
 
 // Everything a kernel needs, passed by value.
@@ -313,6 +316,8 @@ struct VoDev {
     int diag_f0;                     // frame index of batch frame 0 (enqueue_extract)
     int fault_inject;                // VO_FAULT_INJECT=1 (tests only): launch_stencil adds N counts to each frame's
                                      // top histogram bin, so the select's consistency check must fire
+    unsigned spin_limit;             // polls of the fused select's / fused RANSAC's bounded waits (1 << 22;
+                                     // VO_SPIN_LIMIT=0, tests only: every wait times out at once)
 };
 
 // launch wrappers (vo_kernels.hip)

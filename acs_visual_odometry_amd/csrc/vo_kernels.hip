@@ -2258,7 +2258,6 @@ __global__ void __launch_bounds__(SL_T) k_select_emit(VoDev d, int f0, int slot_
 // same queue, so its eight workgroups find the chip free and run together; the wait is bounded all
 // the same -- a band that times out marks the frame VO_STATUS_INCONSISTENT and counts a device error
 // instead of hanging -- and the last band to finish clears the flag for the next launch.
-#define SEL_FUSED_SPIN (1u << 22)
 __global__ void __launch_bounds__(SL_T) k_select_fused(VoDev d, int f0, int slot_override, int nb)
 {
     int z, w;
@@ -2284,11 +2283,11 @@ __global__ void __launch_bounds__(SL_T) k_select_fused(VoDev d, int f0, int slot
                 // relaxed polls (a device-coherent load each), one acquire after the loop: an acquire poll
                 // invalidates the XCD's L2 (buffer_inv sc1) on every iteration, under the working waves
                 while (__hip_atomic_load((gu32*)&ctl->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
-                       it < SEL_FUSED_SPIN) {
+                       it < d.spin_limit) {
                     __builtin_amdgcn_s_sleep(2);
                     ++it;
                 }
-                s_timeout = it >= SEL_FUSED_SPIN ? 1u : 0u;
+                s_timeout = it >= d.spin_limit ? 1u : 0u;
             }
             __syncthreads();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the ranked threshold and band positions
@@ -2298,6 +2297,7 @@ __global__ void __launch_bounds__(SL_T) k_select_fused(VoDev d, int f0, int slot
                     d.ext_n[slot] = 0;
                     d.ext_st[slot] = VO_STATUS_INCONSISTENT;
                     atomicAdd(d.ctr + VO_CTR_ERR, 1u);
+                    atomicOr(&ctl->timeout, 1u);   // the ranker may still store OK: re-marked below
                 }
                 return false;
             }
@@ -2312,7 +2312,16 @@ __global__ void __launch_bounds__(SL_T) k_select_fused(VoDev d, int f0, int slot
         sel_emit_body(d, f0, slot_override, z, w, smem);
     }
     if (!arrive_last(&ctl->arrive2, VO_SEL_BANDS, &s_last2)) return;
-    if (threadIdx.x == 0) { ctl->ready = 0u; ctl->arrive2 = 0u; }   // for the next launch
+    if (threadIdx.x == 0) {
+        // every band (the ranker included) has stored: a timed-out band's INCONSISTENT is final
+        if (__hip_atomic_load((gu32*)&ctl->timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            const int slot = ext_slot(d, f0, z, slot_override);
+            d.ext_n[slot] = 0;
+            d.ext_st[slot] = VO_STATUS_INCONSISTENT;
+            ctl->timeout = 0u;
+        }
+        ctl->ready = 0u; ctl->arrive2 = 0u;       // for the next launch
+    }
 }
 
 // extract side of a missing image (VisualOdometry.cpp:77-82): the slot holds no keypoints
@@ -3002,6 +3011,9 @@ __device__ __forceinline__ bool match_header(const VoDev& d, int stage, const Vo
         w->bestk = -1; w->n_eval = 0; w->n_inl = 0; w->fitted = 0; w->n_fit = 0; w->degenerate = 0;
         w->need_more = 0;
         w->ready1 = 0u;                                        // k_ransac_fused's hand-off flag
+        // the RANSAC chunks' arrival counters (each chunk's last arriver clears its own; a timed-out
+        // fused wait leaves one short)
+        w->ctr[1] = 0u; w->ctr[2] = 0u; w->ctr[3] = 0u;
         for (int c = 0; c < 4; ++c) w->counts4[c] = 0;
         if (!stage) w->frame_seed = frame_seed_of(d, fl);
         if (status != VO_STATUS_OK) { w->status = status; w->M = 0; w->scored = 0; }
@@ -3893,19 +3905,19 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
             // relaxed polls, one acquire fence after the barrier (an acquire poll invalidates the
             // XCD's L2 on every iteration, under the first chunk's waves: 31.7 us vs 2 x 5.5 us)
             while (__hip_atomic_load((gu32*)&w->ready1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
-                   it < (1u << 22)) {
+                   it < d.spin_limit) {
                 __builtin_amdgcn_s_sleep(2);
                 ++it;
             }
-            s_to = it >= (1u << 22) ? 1u : 0u;
+            s_to = it >= d.spin_limit ? 1u : 0u;
         }
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (s_to) {
-            if (bx == 0 && threadIdx.x == 0) {
-                atomicAdd(d.ctr + VO_CTR_ERR, 1u);
-                w->need_more = 0;                  // the frame's RANSAC stops at [0, k0): loud, never a hang
-            }
+            // loud, never a hang: the chunk's arrival count stays short, so no replay runs over
+            // counts nobody wrote; every row from here carries err (k_finalize reads the counter) and
+            // the call returns VO_ERR_INTERNAL.  The record's counters are reset by the next header
+            if (threadIdx.x == 0) atomicAdd(d.ctr + VO_CTR_ERR, 1u);
             return;
         }
     }
@@ -4883,7 +4895,10 @@ __device__ void finalize_body(const VoDev& d, VoFrameOut* out, int out_base)
         VoFrameOut* o = out + (lo + tid - out_base);
         o->status = s;
         o->n_kps = s == VO_STATUS_MISSING ? 0 : d.ext_n[s_cur[tid]];
-        o->err = d.ext_st[s_cur[tid]] == VO_STATUS_INCONSISTENT;
+        // bit 0: this frame's select failed its check; bit 1: the context's error counter is set
+        // (a bounded wait timed out somewhere: sticky until vo_reset)
+        o->err = (d.ext_st[s_cur[tid]] == VO_STATUS_INCONSISTENT ? 1 : 0) |
+                 (__hip_atomic_load((gu32*)(d.ctr + VO_CTR_ERR), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 2 : 0);
         o->n_matches = w->M;
         o->n_inl = w->n_inl;
         o->best_k = w->bestk;

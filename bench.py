@@ -28,8 +28,11 @@ Also on the JSON line:
                 (config 2), host-frame streaming from pinned memory (H2D inside the timing), the
                 per-frame vo_process_frame rate, and 1920x1080 / N=4096 (config 4) with the 32-test
                 and the 512-test matcher
-  cpu_baseline  the CPU oracle (plain-C restatement of the reference path) on the host's cores:
-                one process per core over the same sequence (cores stated), plus one core
+  cpu_baseline  the CPU oracle (plain-C restatement of the reference path) on the host's cores,
+                timed by rank 0 at every world size before the GPU is touched: one process per
+                usable core (the affinity set, capped by the box's CPU share when OMP_NUM_THREADS /
+                VO_CPU_SHARE states one; logical and physical counts on the line) over the same
+                sequence, plus one process alone; its rows of sequence 0 are checked against the GPU's
 """
 from __future__ import annotations
 
@@ -268,6 +271,38 @@ def stage_ms(stages, frames: int):
     return {k: {"ms_per_frame": round(1e3 * sec / max(frames, 1), 4), "calls": n} for k, (sec, n) in stages.items()}
 
 
+def cpu_share() -> dict:
+    """The host cores the CPU baseline may use: the process's affinity set (logical CPUs), capped
+    by the CPU share the box states (VO_CPU_SHARE, else OMP_NUM_THREADS: a gpurun box shows the whole
+    machine's CPUs but gives one GPU's job 16), with the physical cores behind those logical CPUs
+    (distinct (package, core) pairs in /proc/cpuinfo)."""
+    aff = sorted(os.sched_getaffinity(0))
+    share, src = None, None
+    for k in ("VO_CPU_SHARE", "OMP_NUM_THREADS"):
+        v = os.environ.get(k, "")
+        if v.isdigit() and int(v) > 0:
+            share, src = int(v), k
+            break
+    cores = {}
+    try:
+        cpu = pkg = None
+        for line in open("/proc/cpuinfo"):
+            key, _, val = line.partition(":")
+            key, val = key.strip(), val.strip()
+            if key == "processor":
+                cpu, pkg = int(val), None
+            elif key == "physical id":
+                pkg = val
+            elif key == "core id" and cpu is not None:
+                cores[cpu] = (pkg, val)
+    except (OSError, ValueError):
+        pass
+    phys = len({cores[c] for c in aff if c in cores}) or None
+    workers = min(len(aff), share) if share else len(aff)
+    return {"workers": workers, "affinity_logical_cpus": len(aff), "affinity_physical_cores": phys,
+            "host_logical_cpus": os.cpu_count(), "share": share, "share_source": src}
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -278,12 +313,14 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(frames, seq, budget_s: float, max_kpts: int, procs: int):
+def cpu_baseline(frames, seq, budget_s: float, max_kpts: int, share: dict):
     """The CPU oracle over the bench sequence (restarted at frame 0 after each pass) for about
-    budget_s seconds: `procs` forked processes, one per host core, each running the sequence
-    (throughput = all frames / the slowest process), and one process alone.  Runs before the
-    process touches the GPU.  Returns (the JSON object, the single process's first complete pass
-    as [(pose 3x4, status)] -- the oracle's rows of the sequence, checked against the GPU's)."""
+    budget_s seconds: share["workers"] forked processes, one per usable logical CPU (cpu_share),
+    each running the sequence (throughput = all frames / the slowest process), and one process
+    alone.  Runs before the process touches the GPU.  Returns (the JSON object, the single
+    process's first complete pass as [(pose 3x4, status)] -- the oracle's rows of the sequence,
+    checked against the GPU's)."""
+    procs = share["workers"]
     _CPU.update(frames=frames, W=seq.W, H=seq.H, K=seq.K, gt=seq.gt(), N=max_kpts)
     one_done, one_dt, rows, one_st = _cpu_worker(budget_s, keep_rows=True)
     single = {"value": one_done / one_dt, "unit": "frames/s", "cores": 1, "kind": "port",
@@ -291,7 +328,7 @@ def cpu_baseline(frames, seq, budget_s: float, max_kpts: int, procs: int):
                         f"each pass), oracle/vo_oracle.c in one process, {one_dt:.1f} s",
               "stages": stage_ms(one_st, one_done)}
     if procs <= 1:
-        return dict(single, cpu_model=cpu_model()), rows
+        return dict(single, cpu_model=cpu_model(), host=share), rows
     pool = mp.get_context("fork").Pool(procs)
     try:
         res = pool.map(_cpu_worker, [budget_s] * procs)
@@ -301,11 +338,16 @@ def cpu_baseline(frames, seq, budget_s: float, max_kpts: int, procs: int):
     done = sum(r[0] for r in res)
     dt = max(r[1] for r in res)
     tot = {k: (sum(r[2][k][0] for r in res), sum(r[2][k][1] for r in res)) for k in res[0][2]}
+    lim = (f"capped at the box's CPU share {share['share_source']}={share['share']}" if share["share"]
+           and share["share"] < share["affinity_logical_cpus"] else "the whole affinity set")
     return {"value": done / dt, "unit": "frames/s", "cores": procs, "kind": "port",
-            "sample": f"{procs} processes (one per host core), each running oracle/vo_oracle.c over the same "
-                      f"{frames.shape[0]}-frame sequence for ~{budget_s:.0f} s: {done} frames in {dt:.1f} s",
+            "cores_note": f"{procs} logical CPUs used ({lim}; affinity set {share['affinity_logical_cpus']} logical "
+                          f"CPUs on {share['affinity_physical_cores']} physical cores, host "
+                          f"{share['host_logical_cpus']} logical CPUs)",
+            "sample": f"{procs} processes (one per usable logical CPU), each running oracle/vo_oracle.c over the "
+                      f"same {frames.shape[0]}-frame sequence for ~{budget_s:.0f} s: {done} frames in {dt:.1f} s",
             "stages": stage_ms(tot, done),
-            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "single_thread": single}, rows
+            "cpu_model": cpu_model(), "host": share, "host_cpus": os.cpu_count(), "single_thread": single}, rows
 
 
 # -- GPU measurement helpers ---------------------------------------------------------------
@@ -449,6 +491,18 @@ def run_variants(args, ctx, W, H, frames0, gt0, extra, Context) -> dict:
     return out
 
 
+def context_class():
+    """The engine: the HIP library's Context (no other; tests/test_multirank.py substitutes a stand-in
+    here to run the N > 1 harness end to end on CPU-only machines)."""
+    from acs_visual_odometry_amd import Context
+    return Context
+
+
+def render_workers(world: int) -> int:
+    """Forked processes rendering the synthetic frames: the rank's part of the CPU share."""
+    return max(1, min(16, cpu_share()["workers"]) // max(world, 1))
+
+
 def shard_main(args, world: int, rank: int, local: int):
     """--shard-sequence: ONE sequence of sequences x frames frames split into G contiguous shards
     (acs_visual_odometry_amd/shard.py).  Each rank holds the frames up to the end of
@@ -460,13 +514,13 @@ def shard_main(args, world: int, rank: int, local: int):
     W, H = args.width, args.height
     F = args.frames * args.sequences
     a, b = shard.partition(F, world)[rank]
-    workers = max(1, min(16, (os.cpu_count() or 4) // max(world, 1)))
+    workers = render_workers(world)
     seq = SceneSequence(W, H, nframes=F, seq=0, step=args.motion)
     need = F if rank == 0 else b                      # rank 0 also runs the unsplit check
     frames = render_sequences([(W, H, F, 0, args.motion)], workers)[0][:need]
     dev = local if args.device < 0 else args.device
     dist = dist_init(world, dev, backend=args.backend)
-    from acs_visual_odometry_amd import Context
+    Context = context_class()
     ctx = Context(W, H, K=seq.K, max_kpts=args.max_kpts, device=dev, frame_batch=args.batch,
                   match_bits=args.match_bits)
     dall = ctx.device_frames(frames)
@@ -571,11 +625,13 @@ def main():
     my_seqs = rank_sequences(S, rank, world, args.scaling)
     owners = [rank_sequences(S, r, world, args.scaling) for r in range(world)]
     n_total = sum(len(o) for o in owners)
-    lead = rank == 0 and world == 1
+    lead = rank == 0 and world == 1                      # the N = 1 variants
+    # the CPU baseline and its oracle-row check run on rank 0 at every world size (north_star: the
+    # reference CPU path timed on the same box in the same run)
 
     # -- host-side preparation, before anything touches the GPU (forked workers) --
     from acs_visual_odometry_amd.synth import SceneSequence, render_sequences
-    workers = max(1, min(16, (os.cpu_count() or 4) // max(world, 1)))
+    workers = render_workers(world)
     # N > 1 with weak scaling: config 5 literally as well (8 sequences in all, sequence s on GPU s mod G),
     # timed after the weak-scaling line's run and reported beside it (config5_strong)
     c5_seqs = rank_sequences(8, rank, world, "strong") if world > 1 and args.scaling == "weak" else []
@@ -592,9 +648,9 @@ def main():
     extra = {tag: (rendered[n_mine + i], SceneSequence(sp[0], sp[1], nframes=sp[2], seq=sp[3], step=sp[4]))
              for i, (tag, sp) in enumerate(extra_specs.items())}
     cpu, oracle_rows = None, None
-    if lead and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
         s0, fr0 = seqs[my_seqs[0]]
-        cpu, oracle_rows = cpu_baseline(fr0, s0, args.cpu_seconds, args.max_kpts, workers)
+        cpu, oracle_rows = cpu_baseline(fr0, s0, args.cpu_seconds, args.max_kpts, cpu_share())
 
     dev = local if args.device < 0 else args.device     # (--device 0 --backend gloo: ranks sharing one GPU)
     if world > 1:
@@ -603,7 +659,7 @@ def main():
         # behind its kernels).  Measured neutral at N = 1 (gpurun_out r5g); set before HIP starts.
         os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     dist = dist_init(world, dev, backend=args.backend)
-    from acs_visual_odometry_amd import Context
+    Context = context_class()
 
     ctx = Context(W, H, K=seqs[my_seqs[0]][0].K, max_kpts=args.max_kpts, device=dev, frame_batch=args.batch,
                   match_bits=args.match_bits)
@@ -692,24 +748,39 @@ def main():
         gt5 = np.concatenate([seqs[s][0].gt() for s in c5_seqs])
         st5 = [F * i for i in range(1, len(c5_seqs))]
 
-        def step5():
+        res5 = {}
+
+        def step5(timing=0, stats=None):
             ctx.reset()
             ctx.set_ground_truth(gt5)
             ctx.set_sequence_starts(st5)
-            return ctx.process_frames_device(d5)
+            res5["out"] = ctx.process_frames_device(d5, timing=timing)
+            if stats is not None:
+                stats.append(ctx.kernel_stats())
 
         for _ in range(max(args.warmup, 1)):
             step5()
+        # its own critical-path kernel (one untimed call with every launch timed), then timed live
+        # inside the timed region as the headline's is
+        bd5 = []
+        step5(timing=1, stats=bd5)
+        ks5 = {k: (float(np.mean([b[k][0] for b in bd5 if k in b])), float(np.mean([b[k][1] for b in bd5 if k in b])))
+               for k in KERNELS if any(k in b for b in bd5)}
+        dom5 = dominant_kernel({k: ks5[k][0] / ks5[k][1] if k in ks5 and ks5[k][1] > 0 else 0.0 for k in KERNELS})
+        live5 = []
         barrier()
         t5 = time.perf_counter()
         for _ in range(args.steps):
-            step5()
+            step5(timing=100 + KERNELS.index(dom5), stats=live5)
         t5 = time.perf_counter() - t5
         barrier()
         t5, v5 = aggregate(dist, t5, args.steps * F * len(c5_seqs), world, backend=args.backend, local=dev)
+        info5 = res5["out"][2]
         c5 = {"value": v5, "unit": "frames/s", "ms_per_step": t5 / args.steps * 1e3, "sequences": 8,
               "sequences_per_gpu": [len(rank_sequences(8, r, world, "strong")) for r in range(world)],
-              "scaling": "strong", "parallelism": f"config 5: sequence s of 0..7 on GPU s mod {world}"}
+              "scaling": "strong", "parallelism": f"config 5: sequence s of 0..7 on GPU s mod {world}",
+              "roofline": roofline_entry(dom5, live5, info5, W, H, *load_profile(W, H, args.match_bits),
+                                         ctx.kernel_forms())}
         d5.free()
         ctx.set_sequence_starts([])
 

@@ -27,7 +27,8 @@
 extern "C" {
 #endif
 
-#define VO_ABI_VERSION 1
+#define VO_ABI_VERSION 2   /* 2: vo_config gained rng_mode (round 5); a binary built against
+                              version 1 has a shorter vo_config and must be rebuilt */
 
 /* error codes */
 #define VO_OK                 0

@@ -32,6 +32,22 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
+def test_vo_config_layout_matches_the_binding(tmp_path):
+    """sizeof / offsetof of the header's vo_config (gcc) equal the ctypes mirror's, so a binding of
+    the wrong ABI version cannot silently under-allocate the struct (rng_mode grew it)."""
+    from acs_visual_odometry_amd import _lib
+    fields = [f for f, _ in _lib.VoConfig._fields_]
+    src = tmp_path / "cfg.c"
+    body = "".join(f'printf("%zu\\n", offsetof(vo_config, {f}));' for f in fields)
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "vo_mi355x.h"\n'
+                   f'int main(void){{printf("%zu\\n", sizeof(vo_config));{body}return 0;}}\n')
+    exe = tmp_path / "cfg"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert got[0] == C.sizeof(_lib.VoConfig)
+    assert got[1:] == [getattr(_lib.VoConfig, f).offset for f in fields]
+
+
 def test_python_binding_lists_every_export():
     from acs_visual_odometry_amd import _lib
     assert sorted(_lib.EXPORTS) == declared_symbols()
@@ -41,7 +57,7 @@ def test_host_only_entry_points():
     """Entry points that need no device: strerror, config defaults, descriptor unpack."""
     from acs_visual_odometry_amd import _lib
     L = _lib.load()
-    assert L.vo_abi_version() == 1
+    assert L.vo_abi_version() == 2 == _lib.VO_ABI_VERSION
     assert L.vo_strerror(-10) == b"Degenerate essential matrix"
     cfg = _lib.default_config(1241, 376)
     assert (cfg.max_kpts, cfg.nms_k, cfg.border_row, cfg.border_col, cfg.match_bits) == (2000, 3, 35, 37, 32)

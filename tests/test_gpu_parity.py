@@ -236,6 +236,39 @@ def test_select_consistency_failure_is_loud(sel1, scene, monkeypatch):
     good.close()
 
 
+def test_bounded_wait_timeout_is_loud(scene, monkeypatch):
+    """The fused select's and the fused RANSAC's in-kernel waits are bounded; a wait that times out
+    (forced: VO_SPIN_LIMIT=0, every wait gives up at once) is a library defect and must be loud
+    (ADVICE r5): the stage RANSAC call and the per-frame call return VO_ERR_INTERNAL, the rows carry
+    err, the counter reads nonzero.  The timed-out chunk leaves its work record's arrival counter
+    short; the next match header clears it, so the same record (work[0]) then gives the batched
+    path's exact rows on the same context after vo_reset (that path has no in-kernel waits)."""
+    seq, frames = scene
+    cfg = O.config(seq.W, seq.H, K=seq.K.reshape(9))
+    pts = _matched_points(frames, cfg)
+    monkeypatch.setenv("VO_SPIN_LIMIT", "0")
+    ctx = Context(seq.W, seq.H, K=seq.K)
+    monkeypatch.delenv("VO_SPIN_LIMIT")
+    with pytest.raises(RuntimeError, match=r"\(-7\)"):
+        ctx.ransac(pts, seed=5)
+    assert ctx.device_errors() >= 1
+    ctx.reset()
+    with pytest.raises(RuntimeError, match=r"\(-7\)"):
+        ctx.process_frame(frames[0])              # the fused select's bands time out
+    ctx.reset()
+    assert ctx.device_errors() == 0
+    ctx.set_ground_truth(seq.gt())
+    dfr = ctx.device_frames(frames)
+    pg, sg, ig = ctx.process_frames_device(dfr)
+    vo = O.VO(cfg, gt=seq.gt())
+    for f in range(len(frames)):
+        pr, sr, ir = vo.process(frames[f])
+        assert sg[f] == sr and np.array_equal(pg[f], pr), f
+    assert ctx.device_errors() == 0
+    dfr.free()
+    ctx.close()
+
+
 @pytest.mark.parametrize("bits", [32, 512])
 def test_match_bit_exact(bits, scene):
     seq, frames = scene
