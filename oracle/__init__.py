@@ -12,7 +12,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(_HERE, "build", "liboracle.so")
+# VO_ORACLE_LIB: another build of the same sources (tests/test_sanitizers.py: the ASan/UBSan build)
+_LIB = os.environ.get("VO_ORACLE_LIB") or os.path.join(_HERE, "build", "liboracle.so")
 _lib = None
 
 

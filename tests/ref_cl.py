@@ -31,8 +31,29 @@ P = C.c_void_p
 SZ = C.c_size_t
 
 
-def freak_tables():
-    """(test_cases int32[903,4], patch uint64[512]) from include/vo_freak_tables.h."""
+REF_FREAK_HEADER = "/root/reference/feature_extraction_parallel_GPU/FREAK_feature_descriptor_parallel_GPU.h"
+
+
+def parse_reference_freak_header(path: str = REF_FREAK_HEADER):
+    """The reference header's tables, read as text: (43 points, 512 patch indices, the text of
+    generate_tests) -- FREAK_feature_descriptor_parallel_GPU.h:47-56, :58-81, :87-123."""
+    src = re.sub(r"//[^\n]*", "", open(path).read())
+    blk = src.split("predefined_point_for_matching", 1)[1].split("}};", 1)[0]
+    pts = [(int(a), int(b)) for a, b in re.findall(r"\{\s*(-?\d+)\s*,\s*(-?\d+)\s*\}", blk)]
+    body = src.split("generate_tests()", 1)[1].split("return result;", 1)[0]
+    pat = src.split("PATCH_DESCRIPTION_POINTS", 1)[1].split("};", 1)[0]
+    patch = [int(v) for v in re.findall(r"\b(\d+)\b", pat.split("=", 1)[1])]
+    return pts, patch, body
+
+
+def freak_tables(source: str = "reference"):
+    """(test_cases int32[903,4], patch uint64[512]): the reference header's own tables where the
+    reference sources are mounted (the reference kernels then run on the reference's tables), else
+    include/vo_freak_tables.h (tests/test_freak_tables.py pins the two equal)."""
+    if source == "reference" and os.path.exists(REF_FREAK_HEADER):
+        pts, patch, _ = parse_reference_freak_header(REF_FREAK_HEADER)
+        tc = [(pts[i][0], pts[i][1], pts[j][0], pts[j][1]) for i in range(43) for j in range(i + 1, 43)]
+        return np.array(tc, np.int32), np.array(patch, np.uint64)
     src = open(os.path.join(ROOT, "include", "vo_freak_tables.h")).read()
     pts_blk = src.split("#define VO_FREAK_POINTS_LIST")[1].split("#define")[0]
     pts = [(int(a), int(b)) for a, b in re.findall(r"\{\s*(-?\d+),\s*(-?\d+)\s*\}", pts_blk)]

@@ -125,19 +125,33 @@ def test_ref_stock_build_differences(images):
         assert bits < 1e-2
 
 
-def a6_agreement(variant):
+def a6_workload(name):
+    """(frame pair, max_kpts) of an A.6 workload: the factory pair (752x480), consecutive frames of the
+    bench's synthetic KITTI sequence 0 at 1.0 and 0.12 m/frame (1241x376, N = 2000), and of the
+    config-4 1920x1080 stream (N = 4096)."""
+    if name == "factory":
+        return [read_gray(os.path.join(GOLD, f"factory{i}.png")) for i in (1, 2)], 2000
+    if name == "x1080":
+        seq = SceneSequence(1920, 1080, nframes=12, seq=0, step=1.0)
+        return [seq.frame(10), seq.frame(11)], 4096
+    step = {"kitti_1.0": 1.0, "kitti_0.12": 0.12}[name]
+    seq = SceneSequence(1241, 376, nframes=12, seq=0, step=step)
+    return [seq.frame(10), seq.frame(11)], 2000
+
+
+def a6_agreement(variant, workload="factory"):
     """SURVEY A.6 secondary numbers: the reference's own compute_all_orientations (CAS-atomic
     order) and merge_all_orientations (OCML f32 atan2/cos/sin), compiled `variant`, drive its
-    compute_all_descriptors on the oracle's keypoints and blurred images of factory1 -> factory2;
-    returns the descriptor-bit agreement with the oracle (whose f64 det-math rotations the HIP
+    compute_all_descriptors on the oracle's keypoints and blurred images of the workload's frame
+    pair; returns the descriptor-bit agreement with the oracle (whose f64 det-math rotations the HIP
     path reproduces bit for bit) and the agreement of the 32-test match pairs."""
-    imgs = [read_gray(os.path.join(GOLD, f"factory{i}.png")) for i in (1, 2)]
-    out = {"variant": variant.name}
+    imgs, N = a6_workload(workload)
+    out = {"variant": variant.name, "workload": workload, "size": f"{imgs[0].shape[1]}x{imgs[0].shape[0]}"}
     descs_ref, descs_our = [], []
     bits_total = bits_same = 0
     for k, img in enumerate(imgs):
         H, W = img.shape
-        kps, desc, bl = O.extract(img, O.config(W, H))
+        kps, desc, bl = O.extract(img, O.config(W, H, max_kpts=N))
         _, _, rot_cl, dcl = variant.orient_describe(bl, kps)
         ours = unpack_descriptor(desc)
         bits_total += ours.size
@@ -145,9 +159,9 @@ def a6_agreement(variant):
         descs_ref.append(np.packbits(dcl.astype(np.uint8), axis=1, bitorder="little").view(np.uint64))
         descs_our.append(desc)
         _, rot_or = O.describe(bl, kps, with_rot=True)
-        out[f"factory{k + 1}_keypoints"] = int(kps.shape[0])
-        out[f"factory{k + 1}_rotation_max_abs_diff"] = float(np.abs(rot_cl - rot_or).max())
-        out[f"factory{k + 1}_descriptors_identical"] = float(np.mean((dcl == ours).all(1)))
+        out[f"frame{k + 1}_keypoints"] = int(kps.shape[0])
+        out[f"frame{k + 1}_rotation_max_abs_diff"] = float(np.abs(rot_cl - rot_or).max())
+        out[f"frame{k + 1}_descriptors_identical"] = float(np.mean((dcl == ours).all(1)))
     out["descriptor_bit_agreement"] = bits_same / bits_total
     m_ref = O.match(descs_ref[0], descs_ref[1])
     m_our = O.match(descs_our[0], descs_our[1])
@@ -159,10 +173,16 @@ def a6_agreement(variant):
     return out
 
 
+@pytest.mark.parametrize("workload", ["factory", "kitti_1.0", "kitti_0.12", "x1080"])
 @pytest.mark.parametrize("name", ["strict", "stock"])
-def test_a6_reference_driven_descriptor_agreement(name):
+def test_a6_reference_driven_descriptor_agreement(name, workload):
     v = _variant(name)
-    out = a6_agreement(v)
+    out = a6_agreement(v, workload)
     print("A.6", out)
+    if os.environ.get("VO_REPORT_DIR"):            # the figures DESIGN.md section 4 quotes
+        import json
+        os.makedirs(os.environ["VO_REPORT_DIR"], exist_ok=True)
+        with open(os.path.join(os.environ["VO_REPORT_DIR"], "a6_agreement.jsonl"), "a") as fh:
+            fh.write(json.dumps(out) + "\n")
     assert out["descriptor_bit_agreement"] > 0.99
     assert out["match_pair_agreement"] > 0.9
