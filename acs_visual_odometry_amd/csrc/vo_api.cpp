@@ -40,10 +40,9 @@ struct vo_ctx {
     vo_config cfg;
     VoDev d;
     hipStream_t s = nullptr;          // pose passes, stage APIs, the single-frame path
-    hipStream_t se[VO_EXT_QUEUES] = {};   // extract batches of the device path (batch j on j % n)
+    hipStream_t se[VO_EXT_QUEUES] = {};   // the extract queue of the device path (se[0])
     int B = VO_DEFAULT_BATCH;         // frames per extract batch / pose-pass window
     int fidx = 0;                     // frames enqueued since vo_reset
-    int nq = 1;                       // extract queues of this context (VO_EXTQ at vo_create)
     int mt_err = 0;                   // VO_RNG_MT19937: a failed sample upload of a pass (returned by run_chunk)
     bool serial = false;              // VO_SERIAL=1: every kernel on one queue, no cross-queue
                                       // waits (for profilers that serialize dispatches: PMC passes)
@@ -52,9 +51,6 @@ struct vo_ctx {
                                       // again after the runtime refused a wait-value packet)
     bool force_wait_refusal = false;  // VO_FORCE_WAIT_REFUSAL=1 (tests): treat the first wait-value packet as
                                       // refused, so the event fallback path runs
-    bool fuse_fin = false;            // VO_FUSE_FIN=1: the pass's finalize in k_triangulate's last workgroup
-                                      // (measured slower: 246-259k vs 257-272k frames/s KITTI)
-    bool split = false;               // VO_SPLIT: stencil and select/describe of a batch on two extract queues
     int slack = 0;                    // VO_SLACK: extra passes enqueued per chunk (misses re-run without a host round trip)
     hipStream_t st = nullptr;         // trajectory queue: k_traj of each pass (T_curr chain, pose rows)
     hipEvent_t ev_fin = nullptr;      // a pass's k_finalize done (the trajectory queue waits on it)
@@ -65,7 +61,7 @@ struct vo_ctx {
     hipEvent_t ev_r2[kPassEv] = {};   // pass p's later RANSAC chunks done (rq: the fit queue waits on it)
     bool rq = false;                  // later RANSAC chunks on the trajectory queue, k_traj on the fit queue
     bool pipeline = true;             // VO_PIPELINE=0: every pass on the pose queue, one after the other
-    size_t set_off[9] = {};           // element offsets of window buffer set 1 (pass p uses set p & 1)
+    size_t set_off[10] = {};           // element offsets of window buffer set 1 (pass p uses set p & 1)
     int npass = 0;                    // pose passes enqueued (their pass-log entries)
     // per-batch event pools of a chunk: [VO_EV_WAIT] extract done (event_wait mode),
     // [VO_EV_COPY] H2D copy done, [VO_EV_STENCIL] stencil done (host streaming)
@@ -233,6 +229,28 @@ void stage_work(VoWork* w, int ring)
     w->cur = ring + 2;
 }
 
+// the stage RANSAC calls' points: f64 as given, their f32 copy in the count's word layout, and the
+// coordinate bounds of the f32 Sampson certificate (rounded up; +inf disables it for the call)
+int upload_stage_pts(vo_ctx* c, const VoDev& d, const double* pts, int m, VoWork* w)
+{
+    HIPCHK(hipMemcpy(d.pts, pts, sizeof(double) * 4 * (size_t)m, hipMemcpyHostToDevice));
+    std::vector<float> p32(VO_PTS32_PER(c->cfg.max_kpts), 0.0f);
+    double mx[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = 0; i < m; ++i)
+        for (int k = 0; k < 4; ++k) {
+            const double v = pts[4 * (size_t)i + k];
+            p32[vo_pts32_index(i, k)] = (float)v;
+            mx[k] = std::isfinite(v) ? std::max(mx[k], std::fabs(v)) : HUGE_VAL;
+        }
+    for (int k = 0; k < 4; ++k) {
+        float f = (float)mx[k];
+        if ((double)f < mx[k]) f = std::nextafter(f, HUGE_VALF);
+        w->cmax[k] = f;
+    }
+    HIPCHK(hipMemcpy(d.pts32, p32.data(), sizeof(float) * p32.size(), hipMemcpyHostToDevice));
+    return VO_OK;
+}
+
 // host frame (any stride) -> frame_in on stream `st`, via the pinned staging buffer
 double now_us()
 {
@@ -343,14 +361,13 @@ void timed(vo_ctx* c, EvRec* ev, int k, hipStream_t st, F&& launch, bool cont = 
 // previous batch's paired launch covered this one) or 2 nb (this batch and the next, scratch copies
 // scr and scr + 1, which are contiguous)
 int enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, int nb, bool publish,
-                    hipStream_t q, EvRec* ev, int eq, hipEvent_t ev_stencil = nullptr, hipStream_t q2 = nullptr,
-                    hipEvent_t e_s = nullptr, bool single = false, int scr = -1, int st_nb = -1)
+                    hipStream_t q, EvRec* ev, int eq, hipEvent_t ev_stencil = nullptr, bool single = false)
 {
     VoDev d = c->d;
     d.single = single ? 1 : 0;          // the single-frame call: latency-shaped extract launches
     const size_t B = (size_t)c->B;
-    if (scr < 0) scr = eq;
-    if (st_nb < 0) st_nb = nb;
+    const int scr = eq;                 // scratch copy
+    const int st_nb = nb;
     d.eq = eq;
     d.diag_f0 = f0;
     d.blurred += d.bplane * B * scr;
@@ -363,11 +380,6 @@ int enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, 
     if (d.tile_ck) d.tile_ck += (size_t)d.ntiles * B * scr;
     if (st_nb > 0) timed(c, ev, 0, q, [&] { vo::launch_stencil(d, img0, frame_bytes, st_nb, 0, q); });
     if (ev_stencil) HIPCHK(hipEventRecord(ev_stencil, q));
-    if (q2) {
-        HIPCHK(hipEventRecord(e_s, q));
-        HIPCHK(hipStreamWaitEvent(q2, e_s, 0));
-        q = q2;
-    }
     timed(c, ev, 1, q, [&] { vo::launch_select(d, f0, nb, -1, q); });
     timed(c, ev, 2, q, [&] { vo::launch_describe(d, f0, nb, -1, publish ? (unsigned)(f0 + nb) : 0u, q); });
     return VO_OK;
@@ -465,7 +477,7 @@ VoDev pass_dev(const vo_ctx* c, int p)
     if (p & 1) {
         const size_t* o = c->set_off;
         d.match_j += o[0]; d.match_pairs += o[1]; d.pts += o[2]; d.hypF += o[3]; d.counts += o[4];
-        d.inl += o[5]; d.inlmask += o[6]; d.model_p += o[7]; d.work += o[8];
+        d.inl += o[5]; d.inlmask += o[6]; d.model_p += o[7]; d.work += o[8]; d.pts32 += o[9];
     }
     return d;
 }
@@ -527,12 +539,8 @@ void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax,
         timed(c, ev, 6, sf, [&] { vo::launch_triangulate(d, 0, sf, out, out_base, 2); });
         return;
     }
-    if (c->fuse_fin) {
-        timed(c, ev, 6, sf, [&] { vo::launch_triangulate(d, 0, sf, out, out_base, 1); });
-    } else {
-        timed(c, ev, 6, sf, [&] { vo::launch_triangulate(d, 0, sf); });
-        timed(c, ev, 7, sf, [&] { vo::launch_finalize(d, out, out_base, sf); });
-    }
+    timed(c, ev, 6, sf, [&] { vo::launch_triangulate(d, 0, sf); });
+    timed(c, ev, 7, sf, [&] { vo::launch_finalize(d, out, out_base, sf); });
     // the T_curr chain and the pose rows on the trajectory queue (serial mode and the single-frame
     // call: the pose queue, no cross-queue event)
     hipStream_t q = c->serial || single ? s : (c->rq ? sf : c->st);
@@ -579,16 +587,12 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     const int base = c->fidx, end = base + nf, B = c->B;
     hipStream_t s = c->s;
     const bool multi = hs || !(c->serial || host_frame || !img0);   // extract on its own queues
-    const int nq = c->nq;             // the extract queues vo_create made for this context
     if (multi && c->reset_pending) {
         for (hipStream_t q : c->se)
             if (q) HIPCHK(hipStreamWaitEvent(q, c->ev_reset, 0));
         c->reset_pending = false;
     }
     const std::vector<int> sched = batch_schedule(nf, B, hs ? VO_HOST_FIRST_BATCH : 0);
-    // VO_ST_PAIR=1: one stencil launch per two full batches (device frames, one extract queue)
-    static const bool st_pair = getenv("VO_ST_PAIR") && atoi(getenv("VO_ST_PAIR")) != 0;
-    const bool pair = st_pair && multi && !hs && !c->split && nq == 1 && VO_EXT_QUEUES >= 2;
     // extract batch j on its queue (+ its event in event-wait mode)
     std::vector<int> f0s(sched.size() + 1, 0);
     for (size_t j = 0; j < sched.size(); ++j) f0s[j + 1] = f0s[j] + sched[j];
@@ -596,21 +600,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         const int f0 = f0s[j], cnt = sched[j];
         // describe publishes the extracted-frame count only for the wait-value packet
         const bool publish = multi && !c->event_wait;
-        const bool split = multi && c->split;
-        const int eq = split ? j % 2 : (multi ? j % nq : 0);
-        hipStream_t q = split ? c->se[0] : (multi ? c->se[eq] : s);
-        hipStream_t q2 = split ? c->se[1] : nullptr;      // the queue whose last kernel is describe
-        hipEvent_t e_s = nullptr, e_d = nullptr;
-        if (split) {
-            int rc = batch_event(c, VO_EV_SPLIT_S, (size_t)j, &e_s);
-            if (rc == VO_OK) rc = batch_event(c, VO_EV_SPLIT_D, (size_t)j, &e_d);
-            if (rc) return rc;
-            if (j >= 2) {                                 // scratch copy eq: describe of batch j - 2 read it last
-                hipEvent_t e_prev;
-                if ((rc = batch_event(c, VO_EV_SPLIT_D, (size_t)(j - 2), &e_prev)) != VO_OK) return rc;
-                HIPCHK(hipStreamWaitEvent(q, e_prev, 0));
-            }
-        }
+        hipStream_t q = multi ? c->se[0] : s;
         if (hs) {
             uint8_t* dimg = nullptr;
             hipEvent_t e_cp, e_st;
@@ -619,46 +609,31 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
             if (rc == VO_OK) rc = batch_event(c, VO_EV_STENCIL, (size_t)j, &e_st);
             if (rc) return rc;
             HIPCHK(hipStreamWaitEvent(q, e_cp, 0));
-            rc = enqueue_extract(c, dimg, (size_t)c->cfg.width * c->cfg.height, base + f0, cnt, publish, q, ev, eq,
-                                 e_st, q2, e_s);
-            if (rc) return rc;
-        } else if (pair) {
-            // paired stencils: batches 2i and 2i + 1 (both full) share one stencil launch of 2B frames
-            // into scratch copies 0 and 1; each batch's select and describe read its own copy
-            auto paired = [&](int i) { return i % 2 == 0 && i + 1 < (int)sched.size() && sched[i] == B && sched[i + 1] == B; };
-            const int st_nb = paired(j) ? 2 * cnt : (j % 2 == 1 && paired(j - 1) ? 0 : cnt);
-            int rc = enqueue_extract(c, img0 + (size_t)f0 * frame_bytes, frame_bytes, base + f0, cnt, publish, q, ev,
-                                     eq, nullptr, q2, e_s, host_frame, j % 2, st_nb);
+            rc = enqueue_extract(c, dimg, (size_t)c->cfg.width * c->cfg.height, base + f0, cnt, publish, q, ev, 0,
+                                 e_st);
             if (rc) return rc;
         } else {
             int rc = enqueue_extract(c, img0 + (size_t)f0 * frame_bytes, frame_bytes, base + f0, cnt, publish, q, ev,
-                                     eq, nullptr, q2, e_s, host_frame);
+                                     0, nullptr, host_frame);
             if (rc) return rc;
         }
-        hipStream_t qd = q2 ? q2 : q;
-        if (split) HIPCHK(hipEventRecord(e_d, qd));
-        // VO_EV_SKIP=1 (wait-value mode only): no batch events; a refused packet records them then,
-        // at the tails of the queues (below)
-        static const bool ev_skip = getenv("VO_EV_SKIP") && atoi(getenv("VO_EV_SKIP")) != 0;
-        if (multi && !(ev_skip && !c->event_wait)) {
+        if (multi) {
             // recorded in both wait modes: if the runtime refuses a wait-value packet, the passes
             // fall back to these events, and every batch enqueued so far -- on any extract queue --
             // already has its own
             hipEvent_t e;
             int rc = batch_event(c, VO_EV_WAIT, (size_t)j, &e);
             if (rc) return rc;
-            HIPCHK(hipEventRecord(e, qd));
+            HIPCHK(hipEventRecord(e, q));
         }
         return VO_OK;
     };
-    // pass k waits for batch k on its queue; batch k-1 (the other queue) was waited for by pass
-    // k-1, which precedes pass k on the pose queue
+    // pass k waits for batch k (the extract queue runs batches in order)
     auto pass = [&](int k) -> int {
         if (multi) {
-            const int eq = c->split ? k % 2 : k % nq;          // describe's counter copy (d.eq)
             hipEvent_t e;
             if (!c->event_wait) {
-                const hipError_t we = hipStreamWaitValue32(s, c->d.ctr + VO_SYNC_EXT + 16 * eq,
+                const hipError_t we = hipStreamWaitValue32(s, c->d.ctr + VO_SYNC_EXT,
                                                            (uint32_t)(base + f0s[k + 1]), hipStreamWaitValueGte,
                                                            0xFFFFFFFFu);
                 if (we != hipSuccess || c->force_wait_refusal) {
@@ -668,19 +643,6 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
                             we != hipSuccess ? hipGetErrorString(we) : "refusal forced by VO_FORCE_WAIT_REFUSAL");
                     (void)hipGetLastError();
                     c->event_wait = true;
-                    static const bool ev_skip = getenv("VO_EV_SKIP") && atoi(getenv("VO_EV_SKIP")) != 0;
-                    if (ev_skip) {
-                        // batches k and k + 1 (the extract queue runs one batch ahead) have no event:
-                        // record theirs now, at the tails of their queues (later than their describe:
-                        // a conservative wait); later batches record their own
-                        for (int j = k; j <= k + 1 && j < (int)sched.size(); ++j) {
-                            hipEvent_t ej;
-                            int rc = batch_event(c, VO_EV_WAIT, (size_t)j, &ej);
-                            if (rc) return rc;
-                            hipStream_t qj = c->split ? c->se[1] : c->se[j % nq];
-                            HIPCHK(hipEventRecord(ej, qj));
-                        }
-                    }
                     int rc = batch_event(c, VO_EV_WAIT, (size_t)k, &e);
                     if (rc) return rc;
                     HIPCHK(hipStreamWaitEvent(s, e, 0));
@@ -922,11 +884,9 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     // counter, which ROCm runs as a polling blit kernel (measured equal or slightly slower)
     c->event_wait = !(getenv("VO_EVENT_WAIT") && atoi(getenv("VO_EVENT_WAIT")) == 0);
     d.xcd_map = getenv("VO_XCD") ? atoi(getenv("VO_XCD")) : 1;
-    c->fuse_fin = getenv("VO_FUSE_FIN") && atoi(getenv("VO_FUSE_FIN")) != 0;
     c->pf_profile = getenv("VO_PF_PROFILE") && atoi(getenv("VO_PF_PROFILE")) != 0;
     c->pipeline = !c->serial && !(getenv("VO_PIPELINE") && atoi(getenv("VO_PIPELINE")) == 0);
     c->force_wait_refusal = getenv("VO_FORCE_WAIT_REFUSAL") && atoi(getenv("VO_FORCE_WAIT_REFUSAL")) != 0;
-    c->split = VO_EXT_QUEUES >= 2 && (getenv("VO_SPLIT") ? atoi(getenv("VO_SPLIT")) != 0 : VO_SPLIT_DEFAULT != 0);
     c->slack = getenv("VO_SLACK") ? std::max(0, std::min(64, atoi(getenv("VO_SLACK")))) : VO_SLACK_DEFAULT;
     d.fault_inject = getenv("VO_FAULT_INJECT") && atoi(getenv("VO_FAULT_INJECT")) != 0;   // tests only
     d.spin_limit = getenv("VO_SPIN_LIMIT") ? (unsigned)atoi(getenv("VO_SPIN_LIMIT")) : (1u << 22);   // tests only
@@ -941,36 +901,20 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     c->rq = !(getenv("VO_RANSAC_Q") && atoi(getenv("VO_RANSAC_Q")) == 0);
     // repair windows hold two work records per frame (k_finalize): at most WB / 2 frames
     d.repair_win = std::max(1, std::min(d.WB / 2, getenv("VO_REPAIR_WIN") ? atoi(getenv("VO_REPAIR_WIN")) : VO_REPAIR_WIN_DEFAULT));
-    // queue priorities (VO_PRIO): 0 none; 1 the pose and trajectory queues high (the pose queue is the
-    // serial critical path; the extract queue has slack); -1 the extract queues high
-    const int prio = getenv("VO_PRIO") ? atoi(getenv("VO_PRIO")) : VO_PRIO_DEFAULT;
-    int p_lo = 0, p_hi = 0;
-    if (prio) (void)hipDeviceGetStreamPriorityRange(&p_lo, &p_hi);
-    const int p_pose = prio > 0 ? p_hi : p_lo, p_ext = prio < 0 ? p_hi : p_lo;
-    auto make_stream = [&](hipStream_t* q, bool, int prio_) { return hipStreamCreateWithPriority(q, hipStreamNonBlocking, prio_); };
-    if (hip_ok(make_stream(&c->s, false, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
-    if (hip_ok(make_stream(&c->st, false, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
+    // four queues: pose (c->s), trajectory (c->st), fit (c->sf), extract (c->se[0]) -- a process has four
+    // hardware queues (GPU_MAX_HW_QUEUES); a fifth stream would share one and serialise behind its kernels
+    auto make_stream = [&](hipStream_t* q) { return hipStreamCreateWithFlags(q, hipStreamNonBlocking); };
+    if (hip_ok(make_stream(&c->s)) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(make_stream(&c->st)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK)
         return bail(VO_ERR_HIP);
-    if (hip_ok(make_stream(&c->sf, false, p_pose)) != VO_OK) return bail(VO_ERR_HIP);
+    if (hip_ok(make_stream(&c->sf)) != VO_OK) return bail(VO_ERR_HIP);
     for (int i = 0; i < vo_ctx::kPassEv; ++i)
         if (hip_ok(hipEventCreateWithFlags(&c->ev_rs[i], hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK ||
             hip_ok(hipEventCreateWithFlags(&c->ev_fn[i], hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK ||
             hip_ok(hipEventCreateWithFlags(&c->ev_r2[i], hipEventDisableTiming | hipEventReleaseToDevice)) != VO_OK)
             return bail(VO_ERR_HIP);
-    // extract queues: only those a configuration uses (VO_EXTQ / VO_SPLIT / VO_ST_PAIR's scratch
-    // copies need no queue of their own) -- every stream takes one of the process's hardware
-    // queues (GPU_MAX_HW_QUEUES, 4 by default), and a stream past them shares another's and
-    // serialises behind its kernels
-    {
-        c->nq = getenv("VO_EXTQ") ? std::max(1, std::min(VO_EXT_QUEUES, atoi(getenv("VO_EXTQ")))) : 1;
-        // VO_SPLIT=2: the second split queue is the trajectory queue (no fifth stream)
-        const bool split_st = c->split && getenv("VO_SPLIT") && atoi(getenv("VO_SPLIT")) == 2;
-        const int ne = c->split ? (split_st ? 1 : 2) : c->nq;
-        for (int i = 0; i < ne; ++i)
-            if (hip_ok(make_stream(&c->se[i], true, p_ext)) != VO_OK) return bail(VO_ERR_HIP);
-        if (split_st) c->se[1] = c->st;
-    }
+    if (hip_ok(make_stream(&c->se[0])) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming)) != VO_OK) return bail(VO_ERR_HIP);
     d.sel_lds = vo::select_lds_bytes(W, H, nullptr);
     if (d.sel_lds < 0) return bail(VO_ERR_HIP);
@@ -1002,13 +946,14 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc_rec(c, "pre", &d.pre, (size_t)N * VO_SLOTS);
     const int WB = d.WB;                                       // pose window buffers: two sets (pass p uses set p & 1)
     d.mask_words = (N + 63) / 64;
-    const size_t per[9] = {(size_t)N * WB, (size_t)N * WB, (size_t)N * 4 * WB, (size_t)d.max_hyp * 9 * WB,
-                           (size_t)d.max_hyp * WB, (size_t)N * WB, (size_t)d.max_hyp * d.mask_words * WB,
-                           (size_t)N * 4 * WB, (size_t)WB};
+    const size_t per[10] = {(size_t)N * WB, (size_t)N * WB, (size_t)N * 4 * WB, (size_t)d.max_hyp * 9 * WB,
+                            (size_t)d.max_hyp * WB, (size_t)N * WB, (size_t)d.max_hyp * d.mask_words * WB,
+                            (size_t)N * 4 * WB, (size_t)WB, VO_PTS32_PER(N) * WB};
     std::memcpy(c->set_off, per, sizeof(per));
     rc |= dalloc_rec(c, "match_j", &d.match_j, 2 * per[0]);
     rc |= dalloc_rec(c, "match_pairs", &d.match_pairs, 2 * per[1]);
     rc |= dalloc_rec(c, "pts", &d.pts, 2 * per[2]);
+    rc |= dalloc_rec(c, "pts32", &d.pts32, 2 * per[9]);
     rc |= dalloc_rec(c, "hypF", &d.hypF, 2 * per[3]);
     rc |= dalloc_rec(c, "counts", &d.counts, 2 * per[4]);
     rc |= dalloc_rec(c, "inl", &d.inl, 2 * per[5]);
@@ -1318,13 +1263,14 @@ int vo_ransac_F(vo_ctx* c, const double* pts, int m, uint64_t seed, double F[9],
     if (!c || !pts || m < 8 || m > c->cfg.max_kpts) return VO_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
     SYNC_ALL(c);
-    HIPCHK(hipMemcpy(c->d.pts, pts, sizeof(double) * 4 * (size_t)m, hipMemcpyHostToDevice));
     VoWork w;
     stage_work(&w, c->d.ring);
+    int rc = upload_stage_pts(c, c->d, pts, m, &w);
+    if (rc) return rc;
     w.M = m;
     w.scored = (m / c->cfg.ransac_chunk_threads) * c->cfg.ransac_chunk_threads;
     w.frame_seed = seed;
-    int rc = write_work0(c, &w);
+    rc = write_work0(c, &w);
     if (rc) return rc;
     if (c->d.rng_mode == VO_RNG_MT19937 && (rc = upload_mt_samples(c, c->d, 1, c->s)) != VO_OK) return rc;
     vo::launch_ransac(c->d, 1, c->s);
@@ -1373,13 +1319,14 @@ int vo_ransac_run(vo_ctx* c, const double* pts, int m, double probability, doubl
         }
         d.maxit_tab = it->second;
     }
-    HIPCHK(hipMemcpy(d.pts, pts, sizeof(double) * 4 * (size_t)m, hipMemcpyHostToDevice));
     VoWork w;
     stage_work(&w, d.ring);
+    int rc = upload_stage_pts(c, d, pts, m, &w);
+    if (rc) return rc;
     w.M = m;
     w.scored = (m / num_threads) * num_threads;        // ransac.cpp:152-157 (quirk 7)
     w.frame_seed = seed;
-    int rc = write_work0(c, &w);
+    rc = write_work0(c, &w);
     if (rc) return rc;
     if (d.rng_mode == VO_RNG_MT19937 && (rc = upload_mt_samples(c, d, 1, c->s)) != VO_OK) return rc;
     vo::launch_ransac(d, 1, c->s);

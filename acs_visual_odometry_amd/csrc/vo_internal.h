@@ -29,6 +29,7 @@
 //   match_j     i32 N        x B   best cur index per prev query, -1 if rejected
 //   match_pairs int2 N       x B   (prev, cur) matches, ascending prev index
 //   pts         f64 4N       x B   matched (x1,y1,x2,y2)
+//   pts32       f32 4N       x B   the same in f32, word-swizzled (vo_pts32_index): the Sampson certificate's input
 //   hypF        f64 9*H      x B   per-hypothesis F (kept for the refit)
 //   counts      i32 H        x B   per-hypothesis inlier counts
 //   inlmask     u64 H*N/64   x B   per-hypothesis Sampson inlier bits
@@ -98,13 +99,9 @@ inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_T
 #define VO_SLACK_DEFAULT 1        // extra passes per chunk of >= 4 batches (VO_SLACK; 0 / 1 / 4 measured within noise)
 // ctr words: cross-queue counters on lines of their own
 #ifndef VO_EXT_QUEUES
-#define VO_EXT_QUEUES 2        // extract queues and scratch copies (VO_EXTQ: batch j on queue j % n; 2 measured no faster)
-#endif
-#ifndef VO_PRIO_DEFAULT
-#define VO_PRIO_DEFAULT 0      // VO_PRIO: 1 pose / trajectory queues at high priority, -1 extract queues
-#endif
-#ifndef VO_SPLIT_DEFAULT
-#define VO_SPLIT_DEFAULT 0     // VO_SPLIT=1: stencils on extract queue 0, select + describe on queue 1 (batch j in scratch j % 2)
+#define VO_EXT_QUEUES 1        // extract queues and scratch copies: one (two queues, stencil and select + describe
+                               // split over them, queue priorities and paired stencil launches were measured and
+                               // removed in round 6: none was faster, each multiplied the cross-queue orderings)
 #endif
 #define VO_CTR_DESCRIBE 0      // + 16 * queue: describe's in-launch arrival counter
 #define VO_SYNC_EXT 32         // + 16 * queue: frames extracted since vo_reset by that queue
@@ -156,6 +153,8 @@ struct VoWork {
     uint32_t ready1;      // k_ransac_fused: the first chunk's replay is written (reset by k_match's header)
     uint32_t pad1;
     uint64_t frame_seed;
+    float cmax[4];        // bounds of |x|, |y|, |x'|, |y'| over the scored matches (the f32 Sampson
+                          // certificate's magnitudes, vo_sampson32.h): W, H, W, H for a pose pass
     double F[9];          // refit F (valid iff fitted)
     double R1[9], R2[9], t[3];
 };
@@ -282,6 +281,8 @@ struct VoDev {
     int32_t* match_j;     // x B
     int2* match_pairs;    // x B
     double* pts;          // x B
+    float* pts32;         // x B: the same points in f32, per 64-match word [component][j / 4][r][j % 4]
+                          // (match 64 w + 8 j + r; vo_pts32_index), for the f32 Sampson certificate
     double* hypF;         // x B
     int32_t* counts;      // x B
     int32_t* inl;         // x B
@@ -322,6 +323,17 @@ struct VoDev {
 
 // launch wrappers (vo_kernels.hip)
 #include <hip/hip_runtime.h>
+// f32 copy of match i's component c (0..3: x, y, x', y') in a frame's pts32 block: lane r of the
+// RANSAC count's lane groups reads components of its matches 64 w + 8 j + r, j = 4 q .. 4 q + 3, as
+// one float4 (vo_kernels.hip count_words32)
+__host__ __device__ inline size_t vo_pts32_index(int i, int c)
+{
+    const int w = i >> 6, j = (i >> 3) & 7, r = i & 7;
+    return (size_t)w * 256 + (size_t)c * 64 + (size_t)(j >> 2) * 32 + (size_t)r * 4 + (size_t)(j & 3);
+}
+// pts32 entries per frame record: whole words
+#define VO_PTS32_PER(N) ((size_t)(((N) + 63) / 64) * 256)
+
 namespace vo {
 // extract of nb frames: frame f0 + z reads img0 + z * frame_bytes into slot
 // (slot_override >= 0 ? slot_override : (f0 + z) % VO_RING), scratch z.  publish > 0: the

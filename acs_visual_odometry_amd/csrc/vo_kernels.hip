@@ -15,6 +15,7 @@
 #include <cstdio>
 
 #include "vo_internal.h"
+#include "vo_sampson32.h"
 #include "../../include/vo_freak_tables.h"
 #include "../../include/vo_mi355x.h"
 
@@ -640,6 +641,14 @@ __device__ __forceinline__ void st_for(F&& f, std::integer_sequence<int, I...>)
 #define ST_DROP_SOFFSET 0
 #endif      // gfx9 buffer descriptor word 3 (raw bytes, no format)
 
+#ifndef ST_LHIST
+#define ST_LHIST 1                     // k_select builds the histogram from its keys; the stencil writes none
+#endif
+// WRITE_SIZE attribution probes (diagnostic builds only, tools/stencil_write_probe.py): the stencil
+// without its blurred-plane stores (1), its key and tile-row stores (2), its histogram atomics (4)
+#ifndef ST_PROBE_NOSTORE
+#define ST_PROBE_NOSTORE 0
+#endif
 #ifndef ST_HIST_FLUSH
 #define ST_HIST_FLUSH 0   // the general form's histogram counts at the group flush (from the LDS keys)
 #endif
@@ -658,7 +667,10 @@ __device__ __forceinline__ void st_for(F&& f, std::integer_sequence<int, I...>)
 // keys and histogram counts are stored through buffer descriptors whose out-of-range offset drops
 // the lanes that hold no maximum (tests/test_buffer_range.py).  A 16-row group is then one basic
 // block with no branch, and the scheduler overlaps consecutive rows' dependency chains.
-template <int SEGT, bool DBG, bool FLAT>
+// NH: no histogram -- the batch's select is the one-workgroup k_select, which builds the histogram
+// in LDS from the keys it stages (the stencil's agent-scope histogram atomics go to memory: 232 KB of
+// WRITE per KITTI frame against a 16 KB histogram, tools/stencil_write_probe.py, r6c)
+template <int SEGT, bool DBG, bool FLAT, bool NH = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAVES_PER_EU))) k_stencil(VoDev d, const uint8_t* __restrict__ img0, size_t frame_bytes,
                                                   int write_response, int nb)
 {
@@ -833,7 +845,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                                                       brow, 0);
                 (void)boffq;
 #else
-                if constexpr (P == 5 && r >= ST_TH - 4) {
+                if constexpr (ST_PROBE_NOSTORE & 1) {
+                } else if constexpr (P == 5 && r >= ST_TH - 4) {
                     __builtin_amdgcn_raw_buffer_store_b16((unsigned short)__builtin_amdgcn_perm(hb, ha, 0x0c0c0602u), rblur,
                                                           boffq, (ys - 10 + k) * Wb, 0);
                 } else {
@@ -999,8 +1012,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                 __builtin_amdgcn_raw_buffer_store_b64(st_u2{key_lo + 1u, (uint32_t)rm1}, rcand, o1, 0, 0);
                 const int h0 = mx0 ? (int)(min(((uint32_t)rm0 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1)) * 4u) : 0x7FFFFFF0;
                 const int h1 = mx1 ? (int)(min(((uint32_t)rm1 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1)) * 4u) : 0x7FFFFFF0;
-                (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rhist, h0, 0, 0);
-                (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rhist, h1, 0, 0);
+                if constexpr (!NH) {
+                    (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rhist, h0, 0, 0);
+                    (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rhist, h1, 0, 0);
+                }
 #endif
             } else if (b0 | b1) {
                 // tile-local raster order: rows before this one, then columns before: the lower
@@ -1021,7 +1036,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                     tk[base] = ((uint64_t)(uint32_t)rm0 << 32) | key_lo;
 #if !(ST_KEYS_LDS && ST_HIST_FLUSH)
                     const uint32_t bin = min(((uint32_t)rm0 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1));
-                    st_atomic_add(&hist[bin], 1u);
+                    if (!(ST_PROBE_NOSTORE & 4) && !NH) st_atomic_add(&hist[bin], 1u);
 #endif
 #if ST_DIAG & 2
                     dck += mix64((((uint64_t)(uint32_t)rm0 << 32) | key_lo) ^ ((uint64_t)base << 48));
@@ -1031,7 +1046,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                     tk[base + (mx0 ? 1u : 0u)] = ((uint64_t)(uint32_t)rm1 << 32) | (key_lo + 1u);
 #if !(ST_KEYS_LDS && ST_HIST_FLUSH)
                     const uint32_t bin = min(((uint32_t)rm1 - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1));
-                    st_atomic_add(&hist[bin], 1u);
+                    if (!(ST_PROBE_NOSTORE & 4) && !NH) st_atomic_add(&hist[bin], 1u);
 #endif
 #if ST_DIAG & 2
                     dck += mix64((((uint64_t)(uint32_t)rm1 << 32) | (key_lo + 1u)) ^ ((uint64_t)(base + (mx0 ? 1u : 0u)) << 48));
@@ -1113,7 +1128,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
         }, std::make_integer_sequence<int, ST_TH>{});
         // the 16 row counts of tile A (lanes 0..15) and B (16..31) are contiguous
         const int tileA = (ys / ST_TH + i) * ntx + 2 * sxi;
-        if (lane < (hasB ? 2 * ST_TH : ST_TH)) tilerows[tileA * ST_TH + lane] = (uint8_t)trows;
+        if (lane < (hasB ? 2 * ST_TH : ST_TH) && !(ST_PROBE_NOSTORE & 2)) tilerows[tileA * ST_TH + lane] = (uint8_t)trows;
 #if ST_KEYS_LDS
         {
             // the group's keys: tile A's toffA from slot 0, tile B's toffB from ST_TCAP (tile A + 1's
@@ -1122,15 +1137,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             // ST_HIST_FLUSH (and always in the FLAT form): each flushed key's histogram count here
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             uint64_t* __restrict__ dst = cand + (size_t)tileA * ST_TCAP;
-            constexpr bool hf = FLAT || ST_HIST_FLUSH;
+            constexpr bool hf = (FLAT || ST_HIST_FLUSH) && !NH;
             for (int j = lane; j < toffA; j += 64) {
                 const uint64_t kv = wkeys[j];
-                dst[j] = kv;
+                if (!(ST_PROBE_NOSTORE & 2)) dst[j] = kv;
                 if constexpr (hf) st_atomic_add(&hist[min(((uint32_t)(kv >> 32) - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1))], 1u);
             }
             for (int j = lane; j < toffB; j += 64) {
                 const uint64_t kv = wkeys[ST_TCAP + j];
-                dst[ST_TCAP + j] = kv;
+                if (!(ST_PROBE_NOSTORE & 2)) dst[ST_TCAP + j] = kv;
                 if constexpr (hf) st_atomic_add(&hist[min(((uint32_t)(kv >> 32) - thr_bits) >> 15, (uint32_t)(VO_HIST_BINS - 1))], 1u);
             }
         }
@@ -1208,7 +1223,7 @@ __device__ void bitonic_lds(T* a, int n_pow2)
 
 // Dynamic LDS layout of k_select (bytes; host and device derive it from the tile count).
 struct SelLayout {
-    int rows, tpre, segw, bits, chunk, keys, key_cap, total;
+    int rows, tpre, segw, bits, chunk, keys, key_cap, hist, total;
 };
 __host__ __device__ inline SelLayout sel_layout(int ntiles, int lds_bytes)
 {
@@ -1222,7 +1237,8 @@ __host__ __device__ inline SelLayout sel_layout(int ntiles, int lds_bytes)
     L.bits = L.segw + segb;
     L.chunk = L.bits + SEL_LDS_BITS / 8;                      // u16 prefix per 4 segments
     L.keys = L.chunk + al(((nseg + 3) / 4) * 2);
-    L.key_cap = (lds_bytes - L.keys) / 8;
+    L.hist = lds_bytes - VO_HIST_BINS * 4;                     // the LDS histogram (lhist launches)
+    L.key_cap = (L.hist - L.keys) / 8;
     L.total = lds_bytes;
     return L;
 }
@@ -1248,7 +1264,9 @@ __device__ __forceinline__ int ext_slot(const VoDev& d, int f0, int z, int slot_
     return slot_override >= 0 ? slot_override : (f0 + z) % VO_RING;
 }
 
-__global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_override)
+// lhist: the batch's stencil wrote no histogram (k_stencil NH): it is built here, in LDS, from the keys
+// as phase B stages them (one LDS atomic per key), and the global one is neither read nor cleared
+__global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_override, int lhist)
 {
     // frame z of the batch: its scratch copy (written by k_stencil's z-slice)
     const int z = blockIdx.x;
@@ -1275,6 +1293,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     uint64_t* s_bitsl = reinterpret_cast<uint64_t*>(smem + L.bits);
     uint16_t* s_wpre = reinterpret_cast<uint16_t*>(smem + L.chunk);   // selected keys before 4-segment word w
     uint64_t* s_keys = reinterpret_cast<uint64_t*>(smem + L.keys);
+    uint32_t* s_lh = reinterpret_cast<uint32_t*>(smem + L.hist);
     const size_t TCAP = ST_TCAP;
 #if LDS_POISON
     // diagnostic build: the whole dynamic LDS and the static words filled with a launch-varying
@@ -1333,6 +1352,8 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     const bool bits_lds = C <= SEL_LDS_BITS;
     uint64_t* bits = bits_lds ? s_bitsl : d.selbits + (size_t)z * (d.cand_cap / 64 + 1);
     for (int w = tid; w < (C + 63) / 64; w += 1024) bits[w] = 0ull;
+    if (lhist)
+        for (int i = tid; i < VO_HIST_BINS; i += 1024) s_lh[i] = 0u;
     __syncthreads();
     // B
     const bool staged = C <= L.key_cap;
@@ -1354,7 +1375,10 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
             for (int u = 0; u < 4; ++u) v[u] = i + u < n ? src[i + u] : 0ull;
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                if (i + u < n) keys[b + i + u] = v[u];
+                if (i + u < n) {
+                    keys[b + i + u] = v[u];
+                    if (lhist) atomicAdd(&s_lh[sel_bin(v[u], d.thr_bits)], 1u);
+                }
 #if ST_DIAG
 #pragma unroll
             for (int u = 0; u < 4; ++u)
@@ -1389,6 +1413,9 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
         }
 #endif
     }
+    // tests only (VO_FAULT_INJECT=1): N counts more in the top bin than the tiles hold keys, as
+    // k_inject_hist adds to a stencil-built histogram -- the consistency check below must fire
+    if (lhist && d.fault_inject && tid == 0) atomicAdd(&s_lh[VO_HIST_BINS - 1], (uint32_t)N);
     __syncthreads();
 #if ST_DIAG
     if (d.diag_keys && f0 + z < VO_DIAG_FRAMES)
@@ -1401,7 +1428,7 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     uint64_t Tb = 0ull;
     uint32_t h[4], hs = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) { h[q] = hist[4 * tid + q]; hs += h[q]; }
+    for (int q = 0; q < 4; ++q) { h[q] = lhist ? s_lh[4 * tid + q] : hist[4 * tid + q]; hs += h[q]; }
     uint32_t suf = hs;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -1598,7 +1625,8 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     }
     VO_STAMP(d, 1900 + (int)blockIdx.x, 6);
     // select is the histogram's only reader: leave it zeroed for the next frame's stencil
-    for (int i = tid; i < VO_HIST_BINS; i += 1024) hist[i] = 0u;
+    if (!lhist)
+        for (int i = tid; i < VO_HIST_BINS; i += 1024) hist[i] = 0u;
     if (tid == 0) {
         // consistency: the histogram counts exactly the keys the tiles hold (round 4's r4j stencil
         // counted margin-row maxima it never stored, tests/test_select_consistency.py), and the
@@ -3041,6 +3069,7 @@ __device__ void match_compact(const VoDev& d, int wf, const MatchFrame& m, int* 
     const int2* kp2 = d.kps + (size_t)m.cur * N;
     int2* match_pairs = d.match_pairs + (size_t)wf * N;
     double* pts = d.pts + (size_t)wf * 4 * N;
+    float* pts32 = d.pts32 + (size_t)wf * VO_PTS32_PER(N);
     VO_STAMP(d, 1993, 2);
     int pos0 = 0;                                 // matches of the earlier passes
     for (int r0 = 0; r0 * 256 < n1; r0 += RC) {
@@ -3080,6 +3109,10 @@ __device__ void match_compact(const VoDev& d, int wf, const MatchFrame& m, int* 
                 double2* pp = reinterpret_cast<double2*>(pts + 4 * (size_t)p);
                 pp[0] = make_double2((double)a.x, (double)a.y);
                 pp[1] = make_double2((double)b.x, (double)b.y);
+                pts32[vo_pts32_index(p, 0)] = (float)a.x;        // exact: pixel coordinates
+                pts32[vo_pts32_index(p, 1)] = (float)a.y;
+                pts32[vo_pts32_index(p, 2)] = (float)b.x;
+                pts32[vo_pts32_index(p, 3)] = (float)b.y;
             }
             pos += total;
         }
@@ -3093,6 +3126,8 @@ __device__ void match_compact(const VoDev& d, int wf, const MatchFrame& m, int* 
         w->scored = (M / d.T) * d.T;
         w->status = M < 8 ? VO_STATUS_FEW_MATCHES : VO_STATUS_OK;   // VisualOdometry.cpp:108-115
         w->ctr[0] = 0u;
+        w->cmax[0] = (float)d.W; w->cmax[1] = (float)d.H;        // keypoints lie inside the frame
+        w->cmax[2] = (float)d.W; w->cmax[3] = (float)d.H;
     }
     VO_STAMP(d, 1993, 3);
 }
@@ -3762,13 +3797,142 @@ __device__ __forceinline__ int count_wave(const double* __restrict__ pts, int sc
     }
     return cnt;
 }
+// The same count through the f32 certificate (vo_sampson32.h; thr == 1): each match's decision is
+// taken in f32 where the error bound proves it equal to the f64 test's, two matches per packed
+// instruction, and by sampson_inlier's f64 arithmetic for the rest (a word's undecided matches,
+// wave-uniform branch; a hypothesis whose constants are not finite sends all its matches there).
+// Lane r reads components of its matches 64 w + 8 j + r from the word-swizzled pts32 block as
+// float4s (j = 4 q .. 4 q + 3), so a packed pair is a register pair as loaded.  The word's bits, the
+// mask store and the early stop are count_words'.
+typedef float vo_f2 __attribute__((ext_vector_type(2)));
+#ifndef RS_S32
+#define RS_S32 1                       // 0: the f64 count for every match (the certificate off)
+#endif
+__device__ __forceinline__ int count_words32(const double* __restrict__ pts, const float* __restrict__ pts32, int scored,
+                                             const double* F, const float* cmax, int h, int r, bool store,
+                                             uint64_t* __restrict__ mask, int bound, int w0, int ws)
+{
+    const int nw = (scored + 63) >> 6;
+    VoS32 s;
+    vo_s32_setup(F, cmax, &s);
+    const auto fma2 = [](vo_f2 a, vo_f2 b, vo_f2 c) { return __builtin_elementwise_fma(a, b, c); };
+    const auto abs2 = [](vo_f2 a) { return __builtin_elementwise_abs(a); };
+    int cnt = 0;
+    for (int w = w0; w < nw; w += ws) {
+        float4 L[4][2];                                // [component][q]: matches j = 4 q .. 4 q + 3
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                L[c][q] = *reinterpret_cast<const float4*>(pts32 + (size_t)w * 256 + c * 64 + q * 32 + r * 4);
+        int dec[8];
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {              // the pair j = 4 q + 2 e, + 1
+                const vo_f2 x = e ? vo_f2{L[0][q].z, L[0][q].w} : vo_f2{L[0][q].x, L[0][q].y};
+                const vo_f2 y = e ? vo_f2{L[1][q].z, L[1][q].w} : vo_f2{L[1][q].x, L[1][q].y};
+                const vo_f2 xp = e ? vo_f2{L[2][q].z, L[2][q].w} : vo_f2{L[2][q].x, L[2][q].y};
+                const vo_f2 yp = e ? vo_f2{L[3][q].z, L[3][q].w} : vo_f2{L[3][q].x, L[3][q].y};
+                vo_f2 diff, bnd, den;
+                vo_s32_eval(s, x, y, xp, yp, fma2, abs2, &diff, &bnd, &den);
+                dec[4 * q + 2 * e] = vo_s32_decide(diff.x, bnd.x, den.x);
+                dec[4 * q + 2 * e + 1] = vo_s32_decide(diff.y, bnd.y, den.y);
+            }
+        bool und = false;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const bool valid = w * 64 + j * 8 + r < scored;
+            if (!s.ok || !RS_S32) dec[j] = -1;
+            und |= valid && dec[j] < 0;
+        }
+        if (ballot64(und) != 0ull) {                   // wave-uniform: the f64 test where f32 cannot decide
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int i = w * 64 + j * 8 + r;
+                if (dec[j] < 0 && i < scored) {
+                    const double2* p = reinterpret_cast<const double2*>(pts + 4 * (size_t)i);
+                    const double2 a = p[0], c = p[1];
+                    dec[j] = sampson_inlier(F, a.x, a.y, c.x, c.y, 1.0, true) ? 1 : 0;
+                }
+            }
+        }
+        uint32_t wlo = 0u, whi = 0u;
+        const unsigned sh = 8u * (unsigned)h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const unsigned long long bal = ballot64(dec[j] == 1 && w * 64 + j * 8 + r < scored);
+            const uint32_t b = (uint32_t)(bal >> sh);
+            constexpr uint32_t keep = 0x07060504u;
+            const uint32_t sel = keep & ~(0xFFu << (8 * (j & 3)));
+            if (j < 4) wlo = __builtin_amdgcn_perm(wlo, b, sel);
+            else whi = __builtin_amdgcn_perm(whi, b, sel);
+        }
+        const uint64_t word = (uint64_t)wlo | ((uint64_t)whi << 32);
+        cnt += __popcll(word);
+        if (store && r == (w & 7)) mask[w] = word;
+        if (bound >= 0 && ballot64(store && cnt + max(scored - (w + 1) * 64, 0) > bound) == 0ull) break;
+    }
+    return cnt;
+}
+// count_wave through the f32 certificate (thr == 1): lane L tests match 64 w + L of four words in
+// flight, each an f32 chain (scalar: the latency form), the f64 test where f32 cannot decide
+__device__ __forceinline__ int count_wave32(const double* __restrict__ pts, const float* __restrict__ pts32, int scored,
+                                            const double* F, const float* cmax, int lane, bool store,
+                                            uint64_t* __restrict__ mask, int bound)
+{
+    const int nw = (scored + 63) >> 6;
+    VoS32 s;
+    vo_s32_setup(F, cmax, &s);
+    const auto fma1 = [](float a, float b, float c) { return __builtin_fmaf(a, b, c); };
+    const auto abs1 = [](float a) { return __builtin_fabsf(a); };
+    const int j = lane >> 3, r = lane & 7;
+    const int lo = (j >> 2) * 32 + r * 4 + (j & 3);           // vo_pts32_index of match 64 w + lane, less 256 w
+    int cnt = 0;
+    for (int w0 = 0; w0 < nw; w0 += 4) {
+        int dec[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float* q = pts32 + (size_t)min(w0 + u, nw - 1) * 256 + lo;
+            float diff, bnd, den;
+            vo_s32_eval(s, q[0], q[64], q[128], q[192], fma1, abs1, &diff, &bnd, &den);
+            dec[u] = (s.ok && RS_S32) ? vo_s32_decide(diff, bnd, den) : -1;
+        }
+        bool und = false;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) und |= (w0 + u) * 64 + lane < scored && dec[u] < 0;
+        if (ballot64(und) != 0ull) {                   // wave-uniform
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = (w0 + u) * 64 + lane;
+                if (dec[u] < 0 && i < scored) {
+                    const double2* p = reinterpret_cast<const double2*>(pts + 4 * (size_t)i);
+                    const double2 a = p[0], c = p[1];
+                    dec[u] = sampson_inlier(F, a.x, a.y, c.x, c.y, 1.0, true) ? 1 : 0;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int w = w0 + u;
+            if (w < nw) {                                  // wave-uniform
+                const unsigned long long bal = ballot64(dec[u] == 1 && w * 64 + lane < scored);
+                cnt += __popcll(bal);
+                if (store && lane == 0) mask[w] = bal;
+            }
+        }
+        if (bound >= 0 && !(store && cnt + max(scored - (w0 + 4) * 64, 0) > bound)) break;   // wave-uniform
+    }
+    return cnt;
+}
 template <int J, bool PF>
-__device__ __forceinline__ int count_inliers_group(const double* __restrict__ pts, int scored, const double* F, double thr,
+__device__ __forceinline__ int count_inliers_group(const double* __restrict__ pts, const float* __restrict__ pts32,
+                                                   const float* cmax, int scored, const double* F, double thr,
                                                    int h, int r, bool store, uint64_t* __restrict__ mask,
                                                    int bound = -1, int w0 = 0, int ws = 1)
 {
-    return thr == 1.0 ? count_words<true, J, PF>(pts, scored, F, thr, h, r, store, mask, bound, w0, ws)
-                      : count_words<false, J, PF>(pts, scored, F, thr, h, r, store, mask, bound, w0, ws);
+    if (thr == 1.0) return count_words32(pts, pts32, scored, F, cmax, h, r, store, mask, bound, w0, ws);
+    return count_words<false, J, PF>(pts, scored, F, thr, h, r, store, mask, bound, w0, ws);
 }
 
 // SVD of a 3x3 A (mirror of oracle svd3): min_eigvec3 + one 2x2 Jacobi rotation
@@ -3972,10 +4136,12 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
             uint64_t* msk = d.inlmask + ((size_t)wf * d.max_hyp + min(k, nhyp - 1)) * d.mask_words;
             int cnt;
             if constexpr (W1)
-                cnt = d.sampson_thr == 1.0 ? count_wave<true>(pts, scored, F, d.sampson_thr, lane, mine, msk, cbound)
+                cnt = d.sampson_thr == 1.0 ? count_wave32(pts, d.pts32 + (size_t)wf * VO_PTS32_PER(d.N), scored, F, w->cmax,
+                                                          lane, mine, msk, cbound)
                                            : count_wave<false>(pts, scored, F, d.sampson_thr, lane, mine, msk, cbound);
             else
-                cnt = count_inliers_group<CJ, CPF>(pts, scored, F, d.sampson_thr, h, r, mine, msk, cbound);
+                cnt = count_inliers_group<CJ, CPF>(pts, d.pts32 + (size_t)wf * VO_PTS32_PER(d.N), w->cmax, scored, F,
+                                                   d.sampson_thr, h, r, mine, msk, cbound);
             if (mine && (W1 ? lane == 0 : r == 0)) st_sc1(counts + k, cnt);
             VO_STAMP(d, k, 6);
         }
@@ -5188,6 +5354,19 @@ __global__ void k_inject_hist(VoDev d, int nb)
 {
     if (threadIdx.x == 0 && (int)blockIdx.x < nb) d.hist[(size_t)blockIdx.x * VO_HIST_BINS + VO_HIST_BINS - 1] += (uint32_t)d.N;
 }
+// the FLAT stencil form (VO_ST_FLAT=1, NMS margins of 5+)
+static bool stencil_flat(const VoDev& d)
+{
+    static const int flat_env = getenv("VO_ST_FLAT") ? atoi(getenv("VO_ST_FLAT")) : ST_FLAT_DEFAULT;
+    return flat_env && d.brow >= 5 && d.bcol >= 5;
+}
+// the batch's select is the one-workgroup k_select (launch_select's choice, shared so the two agree)
+static bool select_single_wg(const VoDev& d, int nb)
+{
+    static const int sel_small = getenv("VO_SEL_SMALL") ? atoi(getenv("VO_SEL_SMALL")) : 16;
+    if (d.sel1 && d.sel_emit_lds >= 0 && nb <= sel_small && !d.single) return false;
+    return d.sel1 && !(d.single && d.sel_emit_lds >= 0);
+}
 void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int nb, int write_response, hipStream_t s)
 {
     ensure_tables();
@@ -5212,14 +5391,25 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
     }
     // the FLAT form for NMS margins of 5+ (the reference's 35 / 37; VO_ST_FLAT=1 turns it on); the
     // general form keeps the border masks (small margins, the response map)
-    static const int flat_env = getenv("VO_ST_FLAT") ? atoi(getenv("VO_ST_FLAT")) : ST_FLAT_DEFAULT;
-    const bool flat = flat_env && !write_response && d.brow >= 5 && d.bcol >= 5;
+    const bool flat = !write_response && stencil_flat(d);
     const int waves = nsx * ((nty + st - 1) / st);             // one (strip, segment) per wave
     dim3 g(xcd_grid((waves + 3) / 4, nb));
 #define ST_LAUNCH(S, F) hipLaunchKernelGGL((k_stencil<S, false, F>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb)
+#define ST_LAUNCH_NH(S) hipLaunchKernelGGL((k_stencil<S, false, false, true>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb)
+    // no histogram where k_select builds its own (ST_LHIST=0: the stencil's, as before round 6)
+    const bool nh = ST_LHIST && !write_response && !flat && select_single_wg(d, nb);
     if (write_response)
         hipLaunchKernelGGL((k_stencil<4, true, false>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response, nb);
-    else if (!flat) {
+    else if (nh) {
+        switch (st) {
+        case 2: ST_LAUNCH_NH(2); break;
+        case 4: ST_LAUNCH_NH(4); break;
+        case 5: ST_LAUNCH_NH(5); break;
+        case 6: ST_LAUNCH_NH(6); break;
+        case 1: ST_LAUNCH_NH(1); break;
+        default: ST_LAUNCH_NH(8); break;
+        }
+    } else if (!flat) {
         switch (st) {
         case 1: ST_LAUNCH(1, false); break;
         case 2: ST_LAUNCH(2, false); break;
@@ -5239,7 +5429,8 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
         }
     }
 #undef ST_LAUNCH
-    if (d.fault_inject && !write_response) hipLaunchKernelGGL(k_inject_hist, dim3(nb), dim3(64), 0, s, d, nb);
+#undef ST_LAUNCH_NH
+    if (d.fault_inject && !write_response && !nh) hipLaunchKernelGGL(k_inject_hist, dim3(nb), dim3(64), 0, s, d, nb);
 }
 void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_t s)
 {
@@ -5257,7 +5448,9 @@ void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_
         return;
     }
     if (d.sel1 && !(d.single && d.sel_emit_lds >= 0)) {
-        hipLaunchKernelGGL(k_select, dim3(nb), dim3(1024), (size_t)d.sel_lds, s, d, f0, slot_override);
+        // the stencil of this batch wrote no histogram (launch_stencil's nh, the same condition)
+        const int lhist = ST_LHIST && !stencil_flat(d) ? 1 : 0;
+        hipLaunchKernelGGL(k_select, dim3(nb), dim3(1024), (size_t)d.sel_lds, s, d, f0, slot_override, lhist);
         return;
     }
     const dim3 g(xcd_grid(VO_SEL_BANDS, nb));

@@ -39,8 +39,10 @@ extern "C" {
 #define VO_ERR_STATE         (-5)
 #define VO_ERR_IO            (-6)   /* image file missing or not decodable (cv::imread -> empty) */
 #define VO_ERR_INTERNAL      (-7)   /* a device consistency check failed (VO_STATUS_INCONSISTENT
-                                       frames; vo_device_error_count); results of the call are not
-                                       those of the reference.  Sticky until vo_reset. */
+                                       frames) or a bounded in-kernel wait timed out (the per-frame
+                                       call's fused select / fused RANSAC); vo_device_error_count
+                                       counts both.  Results of the call are not those of the
+                                       reference.  Sticky until vo_reset. */
 #define VO_ERR_DEGENERATE_E  (-10)  /* PoseUpdate.hpp:71-73 throws "Degenerate essential matrix" */
 
 /* per-frame status (VisualOdometry.cpp:68-189) */
@@ -239,8 +241,8 @@ int  vo_device_upload(vo_ctx* ctx, void* dptr, const void* src, size_t bytes);
 int  vo_reference_samples(uint32_t seed32, int m, int nhyp, int32_t* out);
 
 /* Device consistency failures since vo_create / the last vo_reset (frames marked
- * VO_STATUS_INCONSISTENT by the top-N select).  Waits for the context's queues.  The bench and the
- * GPU tests assert it is 0. */
+ * VO_STATUS_INCONSISTENT by the top-N select, and timed-out bounded waits of the fused per-frame
+ * kernels).  Waits for the context's queues.  The bench and the GPU tests assert it is 0. */
 int  vo_device_error_count(vo_ctx* ctx, uint32_t* count);
 
 /* Reset the trajectory state (frame counter, T_curr, model, prev descriptors). */

@@ -220,6 +220,12 @@ def test_select_consistency_failure_is_loud(sel1, scene, monkeypatch):
     assert ctx.device_errors() >= 4
     with pytest.raises(RuntimeError, match=r"consistency.*\(-7\)"):
         ctx.extract_frames_device(dfr)
+    # a batch past VO_SEL_SMALL frames: the one-workgroup k_select builds the histogram in LDS from
+    # its keys (the stencil writes none, ST_LHIST) and the injection lands there
+    d24 = ctx.device_frames(np.concatenate([frames] * 4))
+    with pytest.raises(RuntimeError, match=r"consistency.*\(-7\)"):
+        ctx.extract_frames_device(d24)
+    d24.free()
     ctx.reset()
     assert ctx.device_errors() == 0
     with pytest.raises(RuntimeError, match=r"consistency.*\(-7\)"):

@@ -361,18 +361,46 @@ def test_sequence_shards_two_processes(leak_case):
 
 
 # -- execution knobs: every measured-and-kept-off alternative still gives the oracle's rows ------
-@pytest.mark.parametrize("env", ["VO_SPLIT=1", "VO_SPLIT=2", "VO_PRIO=1", "VO_PRIO=-1", "VO_FUSE_FIN=1", "VO_PIPELINE=0", "VO_SEL1=0",
-                                 "VO_RANSAC_Q=0"])
+@pytest.mark.parametrize("env", ["VO_PIPELINE=0", "VO_SEL1=0", "VO_RANSAC_Q=0"])
 def test_queue_knobs_match_oracle(leak_case, monkeypatch, env):
-    """Per-context queue layouts (read by vo_create): select + describe on a second extract queue
-    (VO_SPLIT), pose or extract queues at high priority (VO_PRIO), the pass's finalize in the last
-    workgroup of k_triangulate (VO_FUSE_FIN), every pass on the pose queue without cross-pass
+    """Per-context queue layouts (read by vo_create): every pass on the pose queue without cross-pass
     pipelining (VO_PIPELINE=0), the banded select below its default frame size (VO_SEL1=0), the later
     RANSAC chunks on the fit queue and the trajectory chain on its own queue (VO_RANSAC_Q=0)."""
     seq, frames, ref = leak_case
     k, v = env.split("=")
     monkeypatch.setenv(k, v)
     _device_run(seq, frames, ref=ref, frame_batch=16)
+
+
+@pytest.mark.parametrize("rq", ["1", "0"])
+def test_non_pipelined_passes_follow_the_queues(leak_case, monkeypatch, rq):
+    """Round 5's r5final2 failure, isolated: a non-pipelined pass -- the host re-pass rounds after a
+    speculation miss (VO_SLACK=0: no slack pass hides them) and a missing frame's pass -- runs its
+    trajectory chain on the pose queue, and the commit-point read on the fit / trajectory queue must
+    follow it (vo_api.cpp run_chunk: the ev_fin wait).  Under the default layout (the later RANSAC
+    chunks on the trajectory queue, the chain on the fit queue) and VO_RANSAC_Q=0 (chunks on the fit
+    queue, the chain on its own queue): batched frames 0-29, a missing image at 30 (vo_process_frame
+    NULL), batched frames 31-79 -- rows, statuses and counts equal the oracle's run with frame 30
+    missing (VisualOdometry.cpp:77-82)."""
+    seq, frames, _ = leak_case
+    monkeypatch.setenv("VO_SLACK", "0")
+    monkeypatch.setenv("VO_RANSAC_Q", rq)
+    fr = list(frames)
+    fr[30] = None
+    ref = _oracle_rows(seq, fr)
+    ctx = Context(seq.W, seq.H, K=seq.K, frame_batch=16)
+    ctx.set_ground_truth(seq.gt())
+    a = ctx.device_frames(np.stack(frames[:30]))
+    pa, sa, ia = ctx.process_frames_device(a)
+    pm, sm, im = ctx.process_frame(None)
+    b = ctx.device_frames(np.stack(frames[31:]))
+    pb, sb, ib = ctx.process_frames_device(b)
+    a.free(); b.free(); ctx.close()
+    poses = np.concatenate([pa, pm[None], pb])
+    st = np.concatenate([sa, [sm], sb])
+    info = np.concatenate([ia, im[None], ib])
+    assert sm == 2                                            # MISSING
+    _check(ref, poses, st, info)
 
 
 _KNOB_SCRIPT = r"""
@@ -391,21 +419,17 @@ print("KNOB_OK" if ok else "KNOB_DIFF")
 
 
 @pytest.mark.parametrize("env,batch", [("VO_STSEG=4", 16), ("VO_STSEG=5", 64), ("VO_STSEG=8", 64), ("VO_HYP_CUT1=512", 16),
-                                       ("VO_TRI_BPF=0", 64), ("VO_RREPS=4", 16), ("VO_EXTQ=2", 8), ("VO_XCD=0", 64),
-                                       ("VO_EVENT_WAIT=0,VO_FORCE_WAIT_REFUSAL=1,VO_EXTQ=2", 8),
-                                       ("VO_EVENT_WAIT=0,VO_EV_SKIP=1", 16),
-                                       ("VO_EVENT_WAIT=0,VO_EV_SKIP=1,VO_FORCE_WAIT_REFUSAL=1,VO_EXTQ=2", 8),
+                                       ("VO_TRI_BPF=0", 64), ("VO_RREPS=4", 16), ("VO_XCD=0", 64),
+                                       ("VO_EVENT_WAIT=0", 16), ("VO_EVENT_WAIT=0,VO_FORCE_WAIT_REFUSAL=1", 8),
                                        ("VO_ST_FLAT=1", 64), ("VO_ST_FLAT=1,VO_STSEG=8", 64), ("VO_ST_FLAT=1", 8),
-                                       ("VO_ST_PAIR=1", 16), ("VO_ST_PAIR=1", 8),
                                        ("VO_SEL_LDS_KB=48", 64), ("VO_PIPE_FIRST=0", 16), ("VO_RANSAC_SPLIT=0", 16),
                                        ("VO_SEL_SMALL=0", 8), ("VO_STSEG_ADAPT=0", 8)])
 def test_process_knobs_match_oracle(leak_case, tmp_path, env, batch):
     """Knobs the library reads once per process (stencil segment height, RANSAC cut and loop,
-    triangulation grid, alternating extract queues, XCD placement, the branch-free FLAT stencil),
+    triangulation grid, XCD placement, the branch-free FLAT stencil, the wait-value packet),
     each in a child process on the
-    leak sequence: rows, statuses and counts equal the oracle's.  The last case makes the first
-    stream-wait-value packet count as refused with batches alternating over two extract queues: the
-    passes fall back to each batch's own event, recorded on the queue that batch ran on."""
+    leak sequence: rows, statuses and counts equal the oracle's.  One case makes the first
+    stream-wait-value packet count as refused: the passes fall back to each batch's own event."""
     import sys
     seq, frames, ref = leak_case
     npz = tmp_path / "case.npz"
