@@ -1237,8 +1237,11 @@ __host__ __device__ inline SelLayout sel_layout(int ntiles, int lds_bytes)
     L.bits = L.segw + segb;
     L.chunk = L.bits + SEL_LDS_BITS / 8;                      // u16 prefix per 4 segments
     L.keys = L.chunk + al(((nseg + 3) / 4) * 2);
-    L.hist = lds_bytes - VO_HIST_BINS * 4;                     // the LDS histogram (lhist launches)
-    L.key_cap = (L.hist - L.keys) / 8;
+    // the LDS histogram (lhist launches) at the end, if 1024 keys still fit before it (a small
+    // VO_SEL_LDS_KB request: no LDS histogram, the stencil's)
+    L.hist = lds_bytes - VO_HIST_BINS * 4;
+    if (L.hist - L.keys < 1024 * 8) L.hist = -1;
+    L.key_cap = ((L.hist >= 0 ? L.hist : lds_bytes) - L.keys) / 8;
     L.total = lds_bytes;
     return L;
 }
@@ -5360,6 +5363,13 @@ static bool stencil_flat(const VoDev& d)
     static const int flat_env = getenv("VO_ST_FLAT") ? atoi(getenv("VO_ST_FLAT")) : ST_FLAT_DEFAULT;
     return flat_env && d.brow >= 5 && d.bcol >= 5;
 }
+// k_select builds the batch's histogram in LDS (the stencil writes none): not with the FLAT stencil,
+// nor when the LDS request leaves no room for it
+static bool select_lhist(const VoDev& d)
+{
+    const int ntiles = ((d.W + ST_TW - 1) / ST_TW) * ((d.H + ST_TH - 1) / ST_TH);
+    return ST_LHIST && !stencil_flat(d) && sel_layout(ntiles, d.sel_lds).hist >= 0;
+}
 // the batch's select is the one-workgroup k_select (launch_select's choice, shared so the two agree)
 static bool select_single_wg(const VoDev& d, int nb)
 {
@@ -5397,7 +5407,7 @@ void launch_stencil(const VoDev& d, const uint8_t* img0, size_t frame_bytes, int
 #define ST_LAUNCH(S, F) hipLaunchKernelGGL((k_stencil<S, false, F>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb)
 #define ST_LAUNCH_NH(S) hipLaunchKernelGGL((k_stencil<S, false, false, true>), g, dim3(256), 0, s, d, img0, frame_bytes, 0, nb)
     // no histogram where k_select builds its own (ST_LHIST=0: the stencil's, as before round 6)
-    const bool nh = ST_LHIST && !write_response && !flat && select_single_wg(d, nb);
+    const bool nh = !write_response && select_lhist(d) && select_single_wg(d, nb);
     if (write_response)
         hipLaunchKernelGGL((k_stencil<4, true, false>), g, dim3(256), 0, s, d, img0, frame_bytes, write_response, nb);
     else if (nh) {
@@ -5449,7 +5459,7 @@ void launch_select(const VoDev& d, int f0, int nb, int slot_override, hipStream_
     }
     if (d.sel1 && !(d.single && d.sel_emit_lds >= 0)) {
         // the stencil of this batch wrote no histogram (launch_stencil's nh, the same condition)
-        const int lhist = ST_LHIST && !stencil_flat(d) ? 1 : 0;
+        const int lhist = select_lhist(d) ? 1 : 0;
         hipLaunchKernelGGL(k_select, dim3(nb), dim3(1024), (size_t)d.sel_lds, s, d, f0, slot_override, lhist);
         return;
     }
