@@ -63,7 +63,7 @@ ROCPROF_NAME = {"stencil": "k_stencil", "select": "k_select", "describe": "k_des
 # durations, PMC HBM bytes and VALU counters per launch
 # (tools/gpu_evidence.sh writes them on the GPU box before the bench runs, from the same build;
 # PROFILE_ROUND names the round whose files are read)
-PROFILE_ROUND = os.environ.get("VO_PROFILE_ROUND", "r5")
+PROFILE_ROUND = os.environ.get("VO_PROFILE_ROUND", "r6")
 PROFILES = {(1241, 376, 32): f"{PROFILE_ROUND}_kitti_kernels.json", (1920, 1080, 32): f"{PROFILE_ROUND}_1080_kernels.json",
             (1920, 1080, 512): f"{PROFILE_ROUND}_1080_512_kernels.json",
             (1241, 376, 32, 0.12): f"{PROFILE_ROUND}_kitti_012_kernels.json"}
