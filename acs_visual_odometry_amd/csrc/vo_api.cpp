@@ -596,6 +596,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     // extract batch j on its queue (+ its event in event-wait mode)
     std::vector<int> f0s(sched.size() + 1, 0);
     for (size_t j = 0; j < sched.size(); ++j) f0s[j + 1] = f0s[j] + sched[j];
+
     auto extract = [&](int j) -> int {
         const int f0 = f0s[j], cnt = sched[j];
         // describe publishes the extracted-frame count only for the wait-value packet
@@ -619,8 +620,10 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         }
         if (multi) {
             // recorded in both wait modes: if the runtime refuses a wait-value packet, the passes
-            // fall back to these events, and every batch enqueued so far -- on any extract queue --
-            // already has its own
+            // fall back to these events, and every batch enqueued so far already has its own.
+            // (The record costs the extract queue ~8 us between a describe and the next stencil,
+            // kernel trace r6e; a pose pass per two batches, recording every second event, measured
+            // 227-228k vs 298-300k KITTI frames/s: the pose queue then runs in 128-frame bursts, r6f)
             hipEvent_t e;
             int rc = batch_event(c, VO_EV_WAIT, (size_t)j, &e);
             if (rc) return rc;
@@ -629,6 +632,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         return VO_OK;
     };
     // pass k waits for batch k (the extract queue runs batches in order)
+    bool first_pass = true;                    // the chunk's first pass (its window from the state)
     auto pass = [&](int k) -> int {
         if (multi) {
             hipEvent_t e;
@@ -659,8 +663,9 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         // pipelined one's), so pass 1's match need not wait for them (VO_PIPE_FIRST=0: the whole
         // first pass on the pose queue)
         static const bool pipe_first = !(getenv("VO_PIPE_FIRST") && atoi(getenv("VO_PIPE_FIRST")) == 0);
-        enqueue_pass(c, out, out_base, ev, base + f0s[k + 1], multi && c->pipeline && (k > 0 || pipe_first), host_frame,
-                     k == 0);
+        enqueue_pass(c, out, out_base, ev, base + f0s[k + 1], multi && c->pipeline && (!first_pass || pipe_first),
+                     host_frame, first_pass);
+        first_pass = false;
         return VO_OK;
     };
     if (!img0 && !hs) {
