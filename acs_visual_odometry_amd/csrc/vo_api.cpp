@@ -10,7 +10,7 @@
 // `se` into a ring of VO_RING keypoint/descriptor slots; pose passes on stream `s` each take
 // the window of the next B uncommitted frames (match, RANSAC, refit, triangulate: one
 // launch each for the whole window; finalize commits in frame order, vo_internal.h).  The
-// pose queue waits for the extract counter with a stream-wait-value packet; a chunk of at
+// pose queue waits for each extract batch on its event (or a polling wait kernel); a chunk of at
 // most VO_CHUNK frames never rewrites a slot its passes still read, so the extract queue
 // runs ahead freely.  One host sync per chunk reads how far the passes committed.
 #include <hip/hip_runtime.h>
@@ -46,11 +46,8 @@ struct vo_ctx {
     int mt_err = 0;                   // VO_RNG_MT19937: a failed sample upload of a pass (returned by run_chunk)
     bool serial = false;              // VO_SERIAL=1: every kernel on one queue, no cross-queue
                                       // waits (for profilers that serialize dispatches: PMC passes)
-    bool event_wait = true;           // pose queue waits for extract batches on events (default)
-                                      // or on the stream-wait-value packet (VO_EVENT_WAIT=0; events
-                                      // again after the runtime refused a wait-value packet)
-    bool force_wait_refusal = false;  // VO_FORCE_WAIT_REFUSAL=1 (tests): treat the first wait-value packet as
-                                      // refused, so the event fallback path runs
+    bool event_wait = true;           // pose queue waits for extract batches on events, or (VO_EVENT_WAIT=0)
+                                      // in a one-wave kernel polling the counter describe publishes
     int slack = 0;                    // VO_SLACK: extra passes enqueued per chunk (misses re-run without a host round trip)
     hipStream_t st = nullptr;         // trajectory queue: k_traj of each pass (T_curr chain, pose rows)
     hipEvent_t ev_fin = nullptr;      // a pass's k_finalize done (the trajectory queue waits on it)
@@ -599,7 +596,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
 
     auto extract = [&](int j) -> int {
         const int f0 = f0s[j], cnt = sched[j];
-        // describe publishes the extracted-frame count only for the wait-value packet
+        // describe publishes the extracted-frame count only for the polling wait kernel
         const bool publish = multi && !c->event_wait;
         hipStream_t q = multi ? c->se[0] : s;
         if (hs) {
@@ -618,12 +615,11 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
                                      0, nullptr, host_frame);
             if (rc) return rc;
         }
-        if (multi) {
-            // recorded in both wait modes: if the runtime refuses a wait-value packet, the passes
-            // fall back to these events, and every batch enqueued so far already has its own.
-            // (The record costs the extract queue ~8 us between a describe and the next stencil,
-            // kernel trace r6e; a pose pass per two batches, recording every second event, measured
-            // 227-228k vs 298-300k KITTI frames/s: the pose queue then runs in 128-frame bursts, r6f)
+        if (multi && c->event_wait) {
+            // the event the pass of this batch waits on.  (The record costs the extract queue ~8 us
+            // between a describe and the next stencil, kernel trace r6e; a pose pass per two batches,
+            // recording every second event, measured 227-228k vs 298-300k KITTI frames/s: the pose
+            // queue then runs in 128-frame bursts, r6f)
             hipEvent_t e;
             int rc = batch_event(c, VO_EV_WAIT, (size_t)j, &e);
             if (rc) return rc;
@@ -635,23 +631,12 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
     bool first_pass = true;                    // the chunk's first pass (its window from the state)
     auto pass = [&](int k) -> int {
         if (multi) {
-            hipEvent_t e;
             if (!c->event_wait) {
-                const hipError_t we = hipStreamWaitValue32(s, c->d.ctr + VO_SYNC_EXT,
-                                                           (uint32_t)(base + f0s[k + 1]), hipStreamWaitValueGte,
-                                                           0xFFFFFFFFu);
-                if (we != hipSuccess || c->force_wait_refusal) {
-                    // the packet was refused: events from now on -- batch k's own event, recorded
-                    // on the queue its describe ran on when the batch was enqueued
-                    fprintf(stderr, "[vo_mi355x] hipStreamWaitValue32 failed (%s): event waits\n",
-                            we != hipSuccess ? hipGetErrorString(we) : "refusal forced by VO_FORCE_WAIT_REFUSAL");
-                    (void)hipGetLastError();
-                    c->event_wait = true;
-                    int rc = batch_event(c, VO_EV_WAIT, (size_t)k, &e);
-                    if (rc) return rc;
-                    HIPCHK(hipStreamWaitEvent(s, e, 0));
-                }
+                // one wave on the pose queue polls the frame count describe's last workgroup publishes
+                // (bounded: a timeout counts in the error counter, VO_ERR_INTERNAL)
+                vo::launch_wait_ext(c->d, (unsigned)(base + f0s[k + 1]), s);
             } else {
+                hipEvent_t e;
                 int rc = batch_event(c, VO_EV_WAIT, (size_t)k, &e);
                 if (rc) return rc;
                 HIPCHK(hipStreamWaitEvent(s, e, 0));
@@ -885,13 +870,12 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     auto bail = [&](int r) { vo_destroy(c); return r; };
     c->serial = getenv("VO_SERIAL") && atoi(getenv("VO_SERIAL")) != 0;
     // the pose queue waits for extract batches on events by default (barrier packets the queue
-    // processes itself); VO_EVENT_WAIT=0 selects the stream-wait-value packet on the describe
-    // counter, which ROCm runs as a polling blit kernel (measured equal or slightly slower)
+    // processes itself); VO_EVENT_WAIT=0: a one-wave kernel on the pose queue polls the counter
+    // describe publishes, so the extract queue records no event (k_wait_ext)
     c->event_wait = !(getenv("VO_EVENT_WAIT") && atoi(getenv("VO_EVENT_WAIT")) == 0);
     d.xcd_map = getenv("VO_XCD") ? atoi(getenv("VO_XCD")) : 1;
     c->pf_profile = getenv("VO_PF_PROFILE") && atoi(getenv("VO_PF_PROFILE")) != 0;
     c->pipeline = !c->serial && !(getenv("VO_PIPELINE") && atoi(getenv("VO_PIPELINE")) == 0);
-    c->force_wait_refusal = getenv("VO_FORCE_WAIT_REFUSAL") && atoi(getenv("VO_FORCE_WAIT_REFUSAL")) != 0;
     c->slack = getenv("VO_SLACK") ? std::max(0, std::min(64, atoi(getenv("VO_SLACK")))) : VO_SLACK_DEFAULT;
     d.fault_inject = getenv("VO_FAULT_INJECT") && atoi(getenv("VO_FAULT_INJECT")) != 0;   // tests only
     d.spin_limit = getenv("VO_SPIN_LIMIT") ? (unsigned)atoi(getenv("VO_SPIN_LIMIT")) : (1u << 22);   // tests only

@@ -345,6 +345,9 @@ int select_emit_lds_bytes(int W, int H);              // banded select: sets the
 int select_fused_lds_bytes(int W, int H);             // k_select_fused with staged keys: sets the attribute; <0: no fit
 void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned publish, hipStream_t s);
 void launch_ext_missing(const VoDev& d, int slot, hipStream_t s);   // extract side of a missing image
+// the pose queue's wait for an extract batch (VO_EVENT_WAIT=0): one wave polls ctr[VO_SYNC_EXT]
+// until describe has published `target` frames
+void launch_wait_ext(const VoDev& d, unsigned target, hipStream_t s);
 // pose pass over the window (stage = 0) or over work[0] prepared by a stage API (stage = 1)
 void launch_match(const VoDev& d, int stage, hipStream_t s);        // + ordered compaction per frame
 void launch_ransac(const VoDev& d, int stage, hipStream_t s, int part = 0);   // all hypotheses + replay per frame

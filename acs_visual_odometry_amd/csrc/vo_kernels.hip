@@ -5497,6 +5497,28 @@ int select_fused_lds_bytes(int W, int H)
         return -1;
     return fbytes;
 }
+// VO_EVENT_WAIT=0: the pose queue's wait for extract batch k without an event on the extract queue
+// (whose record costs that queue ~8 us between a describe and the next stencil): one wave polls the
+// frame count describe's last workgroup publishes (publish_seq: every workgroup's stores released
+// first), relaxed loads with a sleep between them, one acquire after; bounded like the fused
+// kernels' waits (a timeout is loud: VO_CTR_ERR)
+__global__ void __launch_bounds__(64) k_wait_ext(VoDev d, unsigned target)
+{
+    if (threadIdx.x != 0) return;
+    const unsigned* c = d.ctr + VO_SYNC_EXT;
+    unsigned it = 0u;
+    const unsigned lim = d.spin_limit << 6;          // ~64x the fused waits' bound: a whole batch may be ahead
+    while (__hip_atomic_load((gu32*)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && it < lim) {
+        __builtin_amdgcn_s_sleep(8);
+        ++it;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (it >= lim) atomicAdd(d.ctr + VO_CTR_ERR, 1u);
+}
+void launch_wait_ext(const VoDev& d, unsigned target, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_wait_ext, dim3(1), dim3(64), 0, s, d, target);
+}
 void launch_ext_missing(const VoDev& d, int slot, hipStream_t s)
 {
     hipLaunchKernelGGL(k_ext_missing, dim3(1), dim3(64), 0, s, d, slot);

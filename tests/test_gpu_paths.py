@@ -66,9 +66,9 @@ def test_finalize_leak_and_few_inliers_paths(leak_case, batch):
 
 @pytest.mark.parametrize("mode", ["0", "1"])
 def test_cross_queue_wait_modes(leak_case, monkeypatch, mode):
-    """The pose queue waits for extract batches on events (VO_EVENT_WAIT=1, the default, also
-    the fallback when the runtime refuses a wait-value packet) or on a stream-wait-value packet
-    on the describe counter (VO_EVENT_WAIT=0); results are the same."""
+    """The pose queue waits for extract batches on events (VO_EVENT_WAIT=1, the default) or in a
+    one-wave kernel polling the counter describe publishes (VO_EVENT_WAIT=0, no event on the extract
+    queue); results are the same."""
     seq, frames, ref = leak_case
     monkeypatch.setenv("VO_EVENT_WAIT", mode)
     _device_run(seq, frames, ref=ref, frame_batch=16)
@@ -420,16 +420,14 @@ print("KNOB_OK" if ok else "KNOB_DIFF")
 
 @pytest.mark.parametrize("env,batch", [("VO_STSEG=4", 16), ("VO_STSEG=5", 64), ("VO_STSEG=8", 64), ("VO_HYP_CUT1=512", 16),
                                        ("VO_TRI_BPF=0", 64), ("VO_RREPS=4", 16), ("VO_XCD=0", 64),
-                                       ("VO_EVENT_WAIT=0", 16), ("VO_EVENT_WAIT=0,VO_FORCE_WAIT_REFUSAL=1", 8),
+                                       ("VO_EVENT_WAIT=0", 16), ("VO_EVENT_WAIT=0", 8),
                                        ("VO_ST_FLAT=1", 64), ("VO_ST_FLAT=1,VO_STSEG=8", 64), ("VO_ST_FLAT=1", 8),
                                        ("VO_SEL_LDS_KB=48", 64), ("VO_PIPE_FIRST=0", 16), ("VO_RANSAC_SPLIT=0", 16),
                                        ("VO_SEL_SMALL=0", 8), ("VO_STSEG_ADAPT=0", 8)])
 def test_process_knobs_match_oracle(leak_case, tmp_path, env, batch):
     """Knobs the library reads once per process (stencil segment height, RANSAC cut and loop,
-    triangulation grid, XCD placement, the branch-free FLAT stencil, the wait-value packet),
-    each in a child process on the
-    leak sequence: rows, statuses and counts equal the oracle's.  One case makes the first
-    stream-wait-value packet count as refused: the passes fall back to each batch's own event."""
+    triangulation grid, XCD placement, the branch-free FLAT stencil, the polling wait kernel), each
+    in a child process on the leak sequence: rows, statuses and counts equal the oracle's."""
     import sys
     seq, frames, ref = leak_case
     npz = tmp_path / "case.npz"
@@ -440,8 +438,6 @@ def test_process_knobs_match_oracle(leak_case, tmp_path, env, batch):
     out = subprocess.run([sys.executable, "-c", _KNOB_SCRIPT, ROOT, str(npz), str(batch)], capture_output=True,
                          text=True, timeout=240, env={**os.environ, **kv})
     assert "KNOB_OK" in out.stdout, (out.stdout[-2000:], out.stderr[-2000:])
-    if "VO_FORCE_WAIT_REFUSAL" in kv:
-        assert "event waits" in out.stderr
 
 
 _PF_SCRIPT = r"""
