@@ -641,6 +641,9 @@ __device__ __forceinline__ void st_for(F&& f, std::integer_sequence<int, I...>)
 #define ST_DROP_SOFFSET 0
 #endif      // gfx9 buffer descriptor word 3 (raw bytes, no format)
 
+#ifndef SL_STAGE2
+#define SL_STAGE2 1                    // k_select: two threads per tile stage its keys (eight loads in flight)
+#endif
 #ifndef ST_LHIST
 #define ST_LHIST 1                     // k_select builds the histogram from its keys; the stencil writes none
 #endif
@@ -1362,7 +1365,28 @@ __global__ void __launch_bounds__(1024) k_select(VoDev d, int f0, int slot_overr
     const bool staged = C <= L.key_cap;
     uint64_t* keys = staged ? s_keys : d.ckeys + (size_t)z * d.cand_cap;
     // a thread per tile copies the tile's keys to their compact positions (the keys of a tile
-    // are contiguous in both; a binary search of the tile per key cost ten dependent LDS reads)
+    // are contiguous in both; a binary search of the tile per key cost ten dependent LDS reads).
+    // SL_STAGE2: two threads per tile (every other key), eight loads in flight per thread -- a
+    // KITTI tile's ~14 keys in one round trip, and all 1024 threads busy (528 tiles)
+#if SL_STAGE2 && !ST_DIAG
+    for (int t2 = tid; t2 < 2 * ntiles; t2 += 1024) {
+        const int t = t2 >> 1, h = t2 & 1;
+        const int b = s_tpre[t], n = s_tpre[t + 1] - b;
+        const uint64_t* src = cand + (size_t)t * TCAP;
+        for (int i = h; i < n; i += 16) {
+            uint64_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = i + 2 * u < n ? src[i + 2 * u] : 0ull;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (i + 2 * u < n) {
+                    keys[b + i + 2 * u] = v[u];
+                    if (lhist) atomicAdd(&s_lh[sel_bin(v[u], d.thr_bits)], 1u);
+                }
+        }
+    }
+    if (false)
+#endif
     for (int t = tid; t < ntiles; t += 1024) {
         const int b = s_tpre[t], n = s_tpre[t + 1] - b;
         const uint64_t* src = cand + (size_t)t * TCAP;
