@@ -120,7 +120,7 @@ inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_T
 #define VO_EV_POOLS 5
 #define VO_MAX_HYP 2000
 #define VO_HYP_CHUNK0 100     // RANSAC launch chunks (vo_kernels.hip launch_ransac); 100 = the clamp
-#define VO_HYP_CHUNK1 2000    // = max_hyp: two launches, [0, 100) and [100, 2000) (a third cut at 512 measured: KITTI 1.0 m/frame within noise, 0.12 m/frame 149k vs 151-162k)
+#define VO_HYP_CHUNK1 700     // the later chunks [100, 700) and [700, 2000) (VO_HYP_CUTS): most frames' adaptive loops stop before 700, and the second chunk's replay lets their [700, 2000) exit at once
 #define VO_HYP_REPS 1        // hypotheses per wave in the last chunk (VO_RREPS; 4 and 8 measured 1-6 % slower)
 
 struct VoFrameOut {

@@ -13,6 +13,8 @@
 #include <type_traits>
 #include <utility>
 #include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 #include "vo_internal.h"
 #include "vo_sampson32.h"
@@ -4151,7 +4153,25 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
             VO_STAMP(d, k, 1);
             double F[9];
             fit_F8_group(pts, s8, r, lane & ~7, F, &d, k);
+#if RS_PROBE == 1
+            {   // timing probe: the fit twice (the second result only kept alive)
+                double F2[9];
+                fit_F8_group(pts, s8, r, lane & ~7, F2);
+#pragma unroll
+                for (int j = 0; j < 9; ++j) asm volatile("" ::"v"(F2[j]));
+            }
+#endif
             VO_STAMP(d, k, 2);
+#if RS_PROBE == 2
+            {   // timing probe: rank 2 twice
+                double F2[9];
+#pragma unroll
+                for (int j = 0; j < 9; ++j) { F2[j] = F[j]; asm volatile("" : "+v"(F2[j])); }
+                rank2(F2);
+#pragma unroll
+                for (int j = 0; j < 9; ++j) asm volatile("" ::"v"(F2[j]));
+            }
+#endif
             rank2(F);
             VO_STAMP(d, k, 5);
             if (mine && (!W1 || h == 0)) {
@@ -4216,6 +4236,9 @@ __device__ __forceinline__ void ransac_chunk(const VoDev& d, int k0, int k1, int
     }
 }
 
+#ifndef RS_PROBE
+#define RS_PROBE 0                     // timing probes (variant builds only): 1 the fit twice, 2 rank 2 twice
+#endif
 #ifndef RS_WAVES_EU
 #define RS_WAVES_EU 0                  // 0: the compiler's register budget
 #endif
@@ -5642,16 +5665,32 @@ void launch_ransac(const VoDev& d, int stage, hipStream_t s, int part)
         else hipLaunchKernelGGL((k_ransac_fused<4, false>), dim3(b0 + n1, nb), dim3(256), 0, s, d, VO_HYP_CHUNK0, nhyp, stage, b0, reps1);
         return;
     }
-    // VO_HYP_CUT1: the second cut (VO_HYP_CHUNK1; >= max_hyp merges the last two chunks)
-    static const int cut1 = getenv("VO_HYP_CUT1") ? std::max(VO_HYP_CHUNK0, atoi(getenv("VO_HYP_CUT1"))) : VO_HYP_CHUNK1;
-    const int cut[3] = {std::min(nhyp, VO_HYP_CHUNK0), std::min(nhyp, cut1), nhyp};
+    // the cuts after [0, VO_HYP_CHUNK0): VO_HYP_CHUNK1 (VO_HYP_CUTS: a list, ascending, e.g. "400,700"; "0"
+    // or a cut >= max_hyp merges every later chunk into one)
+    static const std::vector<int> cuts_env = [] {
+        std::vector<int> v;
+        const char* e = getenv("VO_HYP_CUTS");
+        if (!e) { v.push_back(VO_HYP_CHUNK1); return v; }
+        for (const char* q = e; *q;) {
+            const int x = atoi(q);
+            if (x > VO_HYP_CHUNK0 && (v.empty() || x > v.back())) v.push_back(x);
+            while (*q >= '0' && *q <= '9') ++q;
+            if (*q) ++q;                          // any one separator (',' or ':')
+        }
+        return v;
+    }();
+    int cut[16], nc = 0;
+    cut[nc++] = std::min(nhyp, VO_HYP_CHUNK0);
+    for (int x : cuts_env)
+        if (x < nhyp && nc < 15) cut[nc++] = x;
+    cut[nc++] = nhyp;
     int k0 = 0;
-    for (int c = 0; c < 3; ++c) {
+    for (int c = 0; c < nc; ++c) {
         const int k1 = cut[c];
         if (k1 <= k0) continue;
         if ((part == 1 && c > 0) || (part == 2 && c == 0)) { k0 = k1; continue; }
         static const int r2 = getenv("VO_RREPS") ? std::max(1, atoi(getenv("VO_RREPS"))) : VO_HYP_REPS;
-        const int reps = c == 0 ? 1 : (c == 1 ? std::max(1, r2 / 2) : r2);
+        const int reps = c == 0 ? 1 : (c < nc - 1 ? std::max(1, r2 / 2) : r2);
         const int blocks = ((k1 - k0 + 31) / 32 + reps - 1) / reps;      // 32 hypotheses per workgroup
         hipLaunchKernelGGL((k_ransac_hyp<4>), dim3(blocks, nb), dim3(256), 0, s, d, k0, k1, nhyp, stage, reps);
         k0 = k1;

@@ -418,7 +418,7 @@ print("KNOB_OK" if ok else "KNOB_DIFF")
 """
 
 
-@pytest.mark.parametrize("env,batch", [("VO_STSEG=4", 16), ("VO_STSEG=5", 64), ("VO_STSEG=8", 64), ("VO_HYP_CUT1=512", 16),
+@pytest.mark.parametrize("env,batch", [("VO_STSEG=4", 16), ("VO_STSEG=5", 64), ("VO_STSEG=8", 64), ("VO_HYP_CUTS=300:512:1000", 16),
                                        ("VO_TRI_BPF=0", 64), ("VO_RREPS=4", 16), ("VO_XCD=0", 64),
                                        ("VO_EVENT_WAIT=0", 16), ("VO_EVENT_WAIT=0", 8),
                                        ("VO_ST_FLAT=1", 64), ("VO_ST_FLAT=1,VO_STSEG=8", 64), ("VO_ST_FLAT=1", 8),
