@@ -426,6 +426,9 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #ifndef ST_LTMASK_ASM
 #define ST_LTMASK_ASM 1                // the NMS maxima's lane masks straight from an asm v_cmp
 #endif
+#ifndef ST_GRAD_DPP
+#define ST_GRAD_DPP (!ST_SHIFT_BPERM)  // the gradients' neighbour columns as DPP operands (not the FLAT form's shifts)
+#endif
 #ifndef ST_DPP_ADD
 #define ST_DPP_ADD 1                   // box sums with v_add_f32_dpp (0: v_mov_b32_dpp + packed adds)
 #endif
@@ -713,8 +716,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
     // wave shifts: pinned against sinking into a masked arm, except in the FLAT form (no masked arm)
     auto shl = [](int v) { if constexpr (FLAT && !ST_SHIFT_BPERM) return __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true); else return from_right(v); };
     auto shr = [](int v) { if constexpr (FLAT && !ST_SHIFT_BPERM) return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true); else return from_left(v); };
-    auto shrf = [&](float v) { return st_i2f(shr(st_f2i(v))); };
-    auto shlf = [&](float v) { return st_i2f(shl(st_f2i(v))); };
+    [[maybe_unused]] auto shrf = [&](float v) { return st_i2f(shr(st_f2i(v))); };
+    [[maybe_unused]] auto shlf = [&](float v) { return st_i2f(shl(st_f2i(v))); };
 
     const int xs = sxi * ST_SW, ys = seg * SEG;
     const int c0 = xs - VO_STRIP_XL + 2 * lane;                // this lane's columns: c0, c0 + 1
@@ -866,11 +869,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
             //    the reference's f32 values are these integers (all below 2^11)
             const int yg = ys - 11 + k;
             const st_f2 DV = BA - BE, SV = st_fma(BM, st_f2{2.0f, 2.0f}, BA + BE);
+#if ST_GRAD_DPP
+            // the neighbour columns' dv / sv as DPP operands of the adds and subtracts that use them
+            // (the same operations on the same values as the shifted-copy form below: six VALU for
+            // its four v_mov_b32_dpp and six adds / subtracts).  s_nop 1: the two wait states a DPP
+            // read of a VGPR written by the previous VALU needs (DV and SV are computed just before)
+            float a1, a2, jy0, jy1, jxy0, jxy1;
+            asm("s_nop 1\n\t"
+                "v_add_f32_dpp %[a1], %[dy], %[dy] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                "v_add_f32_dpp %[a2], %[dx], %[dx] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                "v_sub_f32_dpp %[jxy0], %[dy], %[dy] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                "v_subrev_f32_dpp %[jxy1], %[dx], %[dx] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                "v_sub_f32_dpp %[jy0], %[sy], %[sy] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                "v_subrev_f32_dpp %[jy1], %[sx], %[sx] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+                : [a1] "=&v"(a1), [a2] "=&v"(a2), [jxy0] "=&v"(jxy0), [jxy1] "=&v"(jxy1), [jy0] "=&v"(jy0),
+                  [jy1] "=&v"(jy1)
+                : [dx] "v"(DV.x), [dy] "v"(DV.y), [sx] "v"(SV.x), [sy] "v"(SV.y));
+            st_f2 JX = st_fma(DV, st_f2{2.0f, 2.0f}, st_f2{a1, a2}); // (dL + 2 dv0 + dv1, dv0 + 2 dv1 + dR)
+            st_f2 JY = {jy0, jy1};                                    // (sL - sv1, sv0 - sR)
+            st_f2 JXY = {jxy0, jxy1};                                 // (dL - dv1, dv0 - dR)
+#else
             const st_f2 Y = {shrf(DV.y), shlf(DV.x)};                 // dv of columns c0 - 1, c0 + 2
             const st_f2 Z = {shrf(SV.y), shlf(SV.x)};
             st_f2 JX = st_fma(DV, st_f2{2.0f, 2.0f}, Y + DV.yx);      // (dL + 2 dv0 + dv1, dv0 + 2 dv1 + dR)
             st_f2 JY = st_xsub(Z, SV);                                // (sL - sv1, sv0 - sR)
             st_f2 JXY = st_xsub(Y, DV);                               // (dL - dv1, dv0 - dR)
+#endif
             // both conditions are wave-uniform and rare (the image's outer columns and rows): the
             // empty volatile asm keeps them branches (if-converted, they cost 12 selects a row)
             if constexpr (!FLAT) {
@@ -5591,6 +5615,8 @@ void launch_describe(const VoDev& d, int f0, int nb, int slot_override, unsigned
     // VO_DS_LDS_TABLE=1: the per-frame call's describe reads the pair table from LDS (measured: describe
     // 26 -> 30 us, the call 165 -> 168 us, so the scalar-cache path stays the default)
     static const int lt_env = getenv("VO_DS_LDS_TABLE") ? atoi(getenv("VO_DS_LDS_TABLE")) : 0;
+    // (the batched describe with the LDS table, measured round 6: KITTI 280.6-281.5k vs 297.7-302.5k,
+    // describe 0.96 -> 1.11 us/frame, r6t)
     const bool lt = lt_env != 0 && nb == 1 && d.single;
     // the per-frame call: eight waves per 64 keypoints (VO_DS_PF=0: one, k_describe)
     static const int pf_env = getenv("VO_DS_PF") ? atoi(getenv("VO_DS_PF")) : 1;
