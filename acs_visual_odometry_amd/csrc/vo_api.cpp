@@ -849,8 +849,8 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     d.ring = VO_RING_DEFAULT;
     if (getenv("VO_RING_SLOTS")) d.ring = std::max(2 * VO_MAX_BATCH, std::min(1 << 16, atoi(getenv("VO_RING_SLOTS"))));
     d.nms_k = k.nms_k; d.brow = k.border_row; d.bcol = k.border_col;
-    d.resp_thr = k.resp_thr;
-    std::memcpy(&d.thr_bits, &k.resp_thr, 4);
+    d.resp_thr = k.resp_thr * (float)VO_RESP_SCALE;   // the stencil's responses carry VO_RESP_SCALE
+    std::memcpy(&d.thr_bits, &d.resp_thr, 4);
     d.ratio = k.ratio; d.match_bits = k.match_bits;
     d.ransac_p = k.ransac_p; d.sampson_thr = k.sampson_thr; d.T = k.ransac_chunk_threads;
     d.seed = k.seed;

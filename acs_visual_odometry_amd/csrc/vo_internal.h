@@ -119,6 +119,15 @@ inline int vo_blur_rows(int H) { return ((H + VO_TILE_H - 1) / VO_TILE_H) * VO_T
 #define VO_EV_SPLIT_D 4        // split extract: describe of batch j done (its scratch copy is free again)
 #define VO_EV_POOLS 5
 #define VO_MAX_HYP 2000
+#ifndef VO_RESP_SCALE
+// The stencil computes twice the corner response, tr - sqrt(tr^2 - 4 det), without the reference's
+// final halving (kernel .c:108-114: (tr * 0.5) - (0.5 * s), which is exactly half of it): every
+// consumer only orders responses or compares them with the threshold, and doubling is exact and
+// order-preserving (the threshold is doubled with them, d.resp_thr; the select's histogram bins,
+// (bits - thr_bits) >> 15, are unchanged since both exponents grow by one).  The response map
+// (vo_response) is halved back.  Two VALU fewer per stencil row.
+#define VO_RESP_SCALE 2
+#endif
 #define VO_HYP_CHUNK0 100     // RANSAC launch chunks (vo_kernels.hip launch_ransac); 100 = the clamp
 #define VO_HYP_CHUNK1 700     // the later chunks [100, 700) and [700, 2000) (VO_HYP_CUTS): most frames' adaptive loops stop before 700, and the second chunk's replay lets their [700, 2000) exit at once
 #define VO_HYP_REPS 1        // hypotheses per wave in the last chunk (VO_RREPS; 4 and 8 measured 1-6 % slower)

@@ -626,7 +626,11 @@ __device__ __forceinline__ st_f2 st_response2(st_f2 jx2, st_f2 jy2, st_f2 sxy)
     r.x = rp.x > 0.0f ? sp.x : (rm.x <= 0.0f ? sm.x : s.x);
     r.y = rp.y > 0.0f ? sp.y : (rm.y <= 0.0f ? sm.y : s.y);
 #endif
+#if VO_RESP_SCALE == 2
+    return tr - r;                    // twice the response (exact): see VO_RESP_SCALE
+#else
     return 0.5f * (tr - r);
+#endif
 }
 // f(integral_constant<int, I>) for I = 0 .. N-1, unrolled at compile time
 template <typename F, int... I>
@@ -971,9 +975,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST_WAV
                 if (write_response && yr >= ys && yr < min(ys + SEG, H)) {
                     float* R = d.response + (size_t)yr * W;
                     const float w0 = write_response == 2 ? SX.x : write_response == 3 ? SY.x
-                                   : write_response == 4 ? SS.x : st_i2f(o0);
+                                   : write_response == 4 ? SS.x : st_i2f(o0) * (1.0f / VO_RESP_SCALE);
                     const float w1 = write_response == 2 ? SX.y : write_response == 3 ? SY.y
-                                   : write_response == 4 ? SS.y : st_i2f(o1);
+                                   : write_response == 4 ? SS.y : st_i2f(o1) * (1.0f / VO_RESP_SCALE);
                     if (outc(c0) && c0 >= 0 && c0 < W) R[c0] = w0;
                     if (outc(c0 + 1) && c0 + 1 < W) R[c0 + 1] = w1;
                 }
