@@ -42,6 +42,7 @@ struct vo_ctx {
     hipStream_t s = nullptr;          // pose passes, stage APIs, the single-frame path
     hipStream_t se[VO_EXT_QUEUES] = {};   // the extract queue of the device path (se[0])
     int B = VO_DEFAULT_BATCH;         // frames per extract batch / pose-pass window
+    int Bx = VO_DEFAULT_BATCH;        // extract batch capacity: B + B / 2 (a chunk's short tail joins its last batch)
     int fidx = 0;                     // frames enqueued since vo_reset
     int mt_err = 0;                   // VO_RNG_MT19937: a failed sample upload of a pass (returned by run_chunk)
     bool serial = false;              // VO_SERIAL=1: every kernel on one queue, no cross-queue
@@ -92,6 +93,13 @@ struct vo_ctx {
     int last_frames = 0;
     // VO_PF_PROFILE=1: host-side phases of vo_process_frame (us, summed; printed by vo_destroy)
     bool pf_profile = false;
+    // VO_HOST_PROFILE=1: host time of each run_frames call to its first extract launch, its last pass
+    // launch and its return (stderr)
+    bool host_profile = false;
+    // work may be in flight on the extract, fit or trajectory queues (set when a call enqueues there,
+    // cleared once that call has synchronised them all): upload_meta orders its copy after them only then
+    bool others_busy = true;
+    double hp_t[3] = {0.0, 0.0, 0.0};
     double pf_t[5] = {0, 0, 0, 0, 0};     // sync, copy, enqueue, wait, total
     long pf_n = 0;
     double pf_enq_end = 0, pf_wait_end = 0;
@@ -179,6 +187,7 @@ int sync_all(vo_ctx* c)
     if (c->s) HIPCHK(hipStreamSynchronize(c->s));
     if (c->sf) HIPCHK(hipStreamSynchronize(c->sf));
     if (c->st) HIPCHK(hipStreamSynchronize(c->st));
+    c->others_busy = false;
     return VO_OK;
 }
 #define SYNC_ALL(c)                        \
@@ -362,7 +371,7 @@ int enqueue_extract(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int f0, 
 {
     VoDev d = c->d;
     d.single = single ? 1 : 0;          // the single-frame call: latency-shaped extract launches
-    const size_t B = (size_t)c->B;
+    const size_t B = (size_t)c->Bx;     // the scratch copies' capacity
     const int scr = eq;                 // scratch copy
     const int st_nb = nb;
     d.eq = eq;
@@ -556,8 +565,13 @@ void enqueue_pass(vo_ctx* c, VoFrameOut* out, int out_base, EvRec* ev, int gmax,
 // Host streaming (first_default > 0): the first batch is short, so its H2D copy (the pipeline
 // fill: 64 KITTI frames are 30 MB, ~0.5 ms at PCIe's ~56 GB/s) does not hold back the first extract
 // (tools/host_stream_diag.py: first batch 8/16/32 measured +5 % over 64).
-std::vector<int> batch_schedule(int nf, int B, int first_default = 0)
+// cap > B (device frames): a remainder of at most B / 2 frames after a full batch joins that batch
+// (up to cap frames) -- a short last batch costs nearly a full batch's extract launches (the stencil,
+// the banded select and describe run latency-bound on few frames) and a pose pass of its own
+// (VO_TAIL=0: the short batch).  Host streaming keeps B: its device ring slots hold B frames.
+std::vector<int> batch_schedule(int nf, int B, int first_default = 0, int cap = 0)
 {
+    static const bool env_tail = !(getenv("VO_TAIL") && atoi(getenv("VO_TAIL")) == 0);
     // experiment knob: VO_FIRST = size of the first batch (pipeline fill), default B
     static const int env_first = getenv("VO_FIRST") ? atoi(getenv("VO_FIRST")) : -1;
     // experiment knob: VO_LAST = size of the batches the chunk's last B frames are split into (the
@@ -568,6 +582,7 @@ std::vector<int> batch_schedule(int nf, int B, int first_default = 0)
     for (int done = 0; done < nf;) {
         int want = (done == 0 && first > 0 && first < B) ? first : B;
         if (env_last > 0 && env_last < B && nf - done <= B) want = env_last;
+        else if (env_tail && want == B && nf - done > B && nf - done <= cap && nf - done - B <= B / 2) want = nf - done;
         v.push_back(std::min(want, nf - done));
         done += v.back();
     }
@@ -583,13 +598,14 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
 {
     const int base = c->fidx, end = base + nf, B = c->B;
     hipStream_t s = c->s;
+    c->others_busy = true;
     const bool multi = hs || !(c->serial || host_frame || !img0);   // extract on its own queues
     if (multi && c->reset_pending) {
         for (hipStream_t q : c->se)
             if (q) HIPCHK(hipStreamWaitEvent(q, c->ev_reset, 0));
         c->reset_pending = false;
     }
-    const std::vector<int> sched = batch_schedule(nf, B, hs ? VO_HOST_FIRST_BATCH : 0);
+    const std::vector<int> sched = batch_schedule(nf, B, hs ? VO_HOST_FIRST_BATCH : 0, hs ? 0 : c->Bx);
     // extract batch j on its queue (+ its event in event-wait mode)
     std::vector<int> f0s(sched.size() + 1, 0);
     for (size_t j = 0; j < sched.size(); ++j) f0s[j + 1] = f0s[j] + sched[j];
@@ -664,6 +680,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         // the host time of every extract launch of the chunk)
         int rc = extract(0);
         if (rc) return rc;
+        if (c->host_profile) c->hp_t[1] = now_us();
         c->fidx = end;
         for (size_t k = 0; k < sched.size(); ++k) {
             if (k + 1 < sched.size() && (rc = extract((int)k + 1)) != VO_OK) return rc;
@@ -674,6 +691,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         if (sched.size() >= 4)
             for (int k = 0; k < c->slack; ++k) enqueue_pass(c, out, out_base, ev, end, multi && c->pipeline);
     }
+    if (c->host_profile) c->hp_t[2] = now_us();
     // every pass commits at least its first frame, so nf re-pass rounds bound the loop
     for (int round = 0, prev_lo = base;; ++round) {
         HIPCHK(hipGetLastError());
@@ -705,7 +723,12 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
             return VO_ERR_STATE;
         }
         const int lo = host_frame && nf == 1 ? end : *c->lo_host;
-        if (lo >= end) break;
+        if (lo >= end) {
+            // every queue is idle: each extract batch's event was waited on by a pass, and the pose, fit
+            // and trajectory queues were synchronised above
+            c->others_busy = false;
+            break;
+        }
         if (lo < base || lo > end || round > nf || (round > 0 && lo <= prev_lo)) {
             fprintf(stderr, "[vo_mi355x] pose passes made no progress (committed %d of [%d, %d), round %d)\n", lo,
                     base, end, round);
@@ -839,7 +862,11 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     const int W = k.width, H = k.height, N = k.max_kpts;
     const int B = k.frame_batch ? k.frame_batch : VO_DEFAULT_BATCH;
     c->B = B;
-    d.B = B;
+    // extract buffers hold up to Bx frames: a chunk whose remainder after a full batch is at most B / 2
+    // frames extracts it with that batch (batch_schedule) instead of as a short batch of its own
+    const int Bx = std::min(VO_MAX_BATCH, B + B / 2);
+    c->Bx = Bx;
+    d.B = Bx;
     d.WB = std::min(VO_MAX_WIN, 2 * B);
     if (getenv("VO_WIN")) d.WB = std::max(1, std::min(VO_MAX_WIN, atoi(getenv("VO_WIN"))));
     d.gridw = d.WB;
@@ -875,6 +902,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     c->event_wait = !(getenv("VO_EVENT_WAIT") && atoi(getenv("VO_EVENT_WAIT")) == 0);
     d.xcd_map = getenv("VO_XCD") ? atoi(getenv("VO_XCD")) : 1;
     c->pf_profile = getenv("VO_PF_PROFILE") && atoi(getenv("VO_PF_PROFILE")) != 0;
+    c->host_profile = getenv("VO_HOST_PROFILE") && atoi(getenv("VO_HOST_PROFILE")) != 0;
     c->pipeline = !c->serial && !(getenv("VO_PIPELINE") && atoi(getenv("VO_PIPELINE")) == 0);
     c->slack = getenv("VO_SLACK") ? std::max(0, std::min(64, atoi(getenv("VO_SLACK")))) : VO_SLACK_DEFAULT;
     d.fault_inject = getenv("VO_FAULT_INJECT") && atoi(getenv("VO_FAULT_INJECT")) != 0;   // tests only
@@ -922,14 +950,14 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc_rec(c, "frame_in", &d.frame_in, np);
     d.bstride = vo_blur_stride(W);
     d.bplane = (size_t)d.bstride * vo_blur_rows(H);
-    rc |= dalloc_rec(c, "blurred", &d.blurred, d.bplane * B * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "blurred", &d.blurred, d.bplane * Bx * VO_EXT_QUEUES);
     rc |= dalloc_rec(c, "response", &d.response, np);
-    rc |= dalloc_rec(c, "cand", &d.cand, (size_t)d.cand_cap * B * VO_EXT_QUEUES);
-    rc |= dalloc_rec(c, "tilerows", &d.tilerows, (size_t)ntiles * 16 * B * VO_EXT_QUEUES);
-    rc |= dalloc_rec(c, "ckeys", &d.ckeys, (size_t)d.cand_cap * B * VO_EXT_QUEUES);
-    rc |= dalloc_rec(c, "selbits", &d.selbits, ((size_t)d.cand_cap / 64 + 1) * B * VO_EXT_QUEUES);
-    rc |= dalloc_rec(c, "hist", &d.hist, (size_t)VO_HIST_BINS * B * VO_EXT_QUEUES);
-    rc |= dalloc_rec(c, "selctl", &d.selctl, (size_t)B * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "cand", &d.cand, (size_t)d.cand_cap * Bx * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "tilerows", &d.tilerows, (size_t)ntiles * 16 * Bx * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "ckeys", &d.ckeys, (size_t)d.cand_cap * Bx * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "selbits", &d.selbits, ((size_t)d.cand_cap / 64 + 1) * Bx * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "hist", &d.hist, (size_t)VO_HIST_BINS * Bx * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "selctl", &d.selctl, (size_t)Bx * VO_EXT_QUEUES);
     rc |= dalloc_rec(c, "kps", &d.kps, (size_t)N * VO_SLOTS);
     rc |= dalloc_rec(c, "desc", &d.desc, (size_t)N * 8 * VO_SLOTS);
     rc |= dalloc_rec(c, "pre", &d.pre, (size_t)N * VO_SLOTS);
@@ -963,7 +991,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     rc |= dalloc_rec(c, "dbg", &d.dbg, (size_t)d.max_hyp * 16);   // stamps / diagnostic counters (words 6000..6003)
 #endif
 #if ST_DIAG
-    rc |= dalloc_rec(c, "tile_ck", &d.tile_ck, (size_t)ntiles * B * VO_EXT_QUEUES);
+    rc |= dalloc_rec(c, "tile_ck", &d.tile_ck, (size_t)ntiles * Bx * VO_EXT_QUEUES);
     rc |= dalloc_rec(c, "diag_tile", &d.diag_tile, (size_t)ntiles * VO_DIAG_FRAMES);
     rc |= dalloc_rec(c, "diag_src", &d.diag_src, (size_t)ntiles * VO_DIAG_FRAMES);
     rc |= dalloc_rec(c, "diag_resp", &d.diag_resp, (size_t)ntiles * VO_DIAG_FRAMES);
@@ -983,7 +1011,7 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     (void)hipMemset(d.kps, 0, sizeof(int2) * N * VO_SLOTS);
     (void)hipMemset(d.desc, 0, sizeof(uint64_t) * 8 * N * VO_SLOTS);
     (void)hipMemset(d.pre, 0, sizeof(uint32_t) * N * VO_SLOTS);
-    (void)hipMemset(d.selctl, 0, sizeof(VoSelCtl) * B * VO_EXT_QUEUES);   // arrival / boundary counters
+    (void)hipMemset(d.selctl, 0, sizeof(VoSelCtl) * Bx * VO_EXT_QUEUES);   // arrival / boundary counters
     if (d.dbg) (void)hipMemset(d.dbg, 0, sizeof(unsigned long long) * (size_t)d.max_hyp * 16);
     d.n_seq_starts = 0;
     d.origin = 0;
@@ -1087,7 +1115,7 @@ int upload_meta(vo_ctx* c, int which, void* dst, const void* src, size_t bytes)
     for (hipStream_t q : c->se) others[no++] = q;
     others[no++] = c->sf;
     others[no++] = c->st;
-    for (int i = 0; i < no; ++i) {
+    for (int i = 0; i < no && c->others_busy; ++i) {
         if (!others[i]) continue;
         if (!c->ev_meta_q[i]) HIPCHK(hipEventCreateWithFlags(&c->ev_meta_q[i], hipEventDisableTiming));
         HIPCHK(hipEventRecord(c->ev_meta_q[i], others[i]));
@@ -1476,6 +1504,7 @@ void copy_results(vo_ctx* c, int nframes, double* poses_out, int* status_out, in
 int run_frames(vo_ctx* c, const uint8_t* dev, const uint8_t* host, bool pinned, size_t frame_bytes, int nframes,
                double* poses_out, int* status_out, int32_t* info_out)
 {
+    if (c->host_profile) c->hp_t[0] = now_us();
     int rc = ensure_out(c, std::max(nframes, 1));
     if (rc) return rc;
     c->klaunch.assign(vo::kernel_count(), 0);
@@ -1483,6 +1512,7 @@ int run_frames(vo_ctx* c, const uint8_t* dev, const uint8_t* host, bool pinned, 
     EvRec* evp = c->timing ? &rec : nullptr;
     const int base = c->fidx;
     const int chunk = c->d.ring - 1;
+    const int pass0 = c->npass;
     for (int f0 = 0; f0 < nframes; f0 += chunk) {
         const int nf = std::min(chunk, nframes - f0);
         if (host) {
@@ -1495,8 +1525,20 @@ int run_frames(vo_ctx* c, const uint8_t* dev, const uint8_t* host, bool pinned, 
     }
     rc = finish_timing(c, evp);
     if (rc) return rc;
+    // diagnostic (VO_PLAN_DUMP=1): each pose pass of the call as (first frame, frames committed)
+    static const bool plan_dump = getenv("VO_PLAN_DUMP") && atoi(getenv("VO_PLAN_DUMP")) != 0;
+    if (plan_dump && c->npass > pass0 && c->npass - pass0 <= VO_PLOG) {
+        std::vector<int2> lg(VO_PLOG);
+        HIPCHK(hipMemcpy(lg.data(), c->d.plog, sizeof(int2) * VO_PLOG, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[vo_mi355x] passes of the call (lo:committed):");
+        for (int p = pass0; p < c->npass; ++p) fprintf(stderr, " %d:%d", lg[p % VO_PLOG].x, lg[p % VO_PLOG].y);
+        fprintf(stderr, "\n");
+    }
     c->last_frames = nframes;
     copy_results(c, nframes, poses_out, status_out, info_out);
+    if (c->host_profile)
+        fprintf(stderr, "[vo_mi355x] host: first extract enqueued +%.1f us, all passes +%.1f us, done +%.1f us\n",
+                c->hp_t[1] - c->hp_t[0], c->hp_t[2] - c->hp_t[0], now_us() - c->hp_t[0]);
     return VO_OK;
 }
 
@@ -1579,7 +1621,7 @@ int vo_extract_frames_device(vo_ctx* c, const uint8_t* d_frames, size_t frame_by
     for (int f0 = 0; f0 < nframes; f0 += c->d.ring) {
         const int nf = std::min(c->d.ring, nframes - f0);
         int off = 0;
-        for (int cnt : batch_schedule(nf, c->B)) {
+        for (int cnt : batch_schedule(nf, c->B, 0, c->Bx)) {
             rc = enqueue_extract(c, d_frames + (size_t)(f0 + off) * frame_bytes, frame_bytes, off, cnt, false, c->s,
                                  evp, 0);
             if (rc) return rc;

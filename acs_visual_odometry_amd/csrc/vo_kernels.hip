@@ -2443,6 +2443,9 @@ __global__ void k_ext_missing(VoDev d, int slot)
 #ifndef DS_PKSUB
 #define DS_PKSUB 0             // 1: the orientation sums' sample differences two per v_pk_add_f32 (12 % fewer orientation VALU, but KITTI 288-290k vs 293-298k, r4s)
 #endif
+#ifndef DS_PROBE
+#define DS_PROBE 0             // diagnostic builds only: 1 hot table, 2 no orientation sums (wrong descriptors)
+#endif
 #ifndef DS_UNROLL
 #define DS_UNROLL 0            // 1: the orientation sums fully unrolled from sample registers (describe
                                // 0.92 -> 0.85 us/frame but KITTI 278-285k vs 283-289k: 110 VGPRs, 30 KB code)
@@ -2576,7 +2579,11 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
     //    the zero rows past the samples.  Software-pipelined: the samples and table entries of
     //    group g + 1 are requested before group g is summed.
     {
+#if DS_PROBE == 2
+        constexpr int NG = 1;                           // probe: no orientation sums
+#else
         constexpr int NG = DS_ONPAD / DS_OG;
+#endif
         const float* col = &s_I0[0][lane];
         int p = 0, qs = 1;                              // group g: row p, samples qs .. qs + 7
         float ip = col[0], iq[DS_OG];
@@ -2602,7 +2609,13 @@ __device__ __forceinline__ void describe_wave(const VoDev& d, const uint8_t* __r
             float iqn[DS_OG];
             float4 tbn[DS_OG];
 #pragma unroll
-            for (int u = 0; u < DS_OG; ++u) { iqn[u] = col[(qn + u) * DS_KPW]; tbn[u] = LT ? s_tab[gn * DS_OG + u] : c_orient[gn * DS_OG + u]; }
+            for (int u = 0; u < DS_OG; ++u) {
+#if DS_PROBE == 1
+                iqn[u] = col[(qn + u) * DS_KPW]; tbn[u] = c_orient[(gn & 3) * DS_OG + u];   // probe: a hot 512-byte table
+#else
+                iqn[u] = col[(qn + u) * DS_KPW]; tbn[u] = LT ? s_tab[gn * DS_OG + u] : c_orient[gn * DS_OG + u];
+#endif
+            }
             __builtin_amdgcn_sched_barrier(0);          // the requests stay ahead of the sums
 #pragma unroll
 #if DS_PKSUB
