@@ -99,6 +99,7 @@ struct vo_ctx {
     // work may be in flight on the extract, fit or trajectory queues (set when a call enqueues there,
     // cleared once that call has synchronised them all): upload_meta orders its copy after them only then
     bool others_busy = true;
+    std::vector<float> kcont_ms;      // per kernel: the continuation spans' share of ktime_ms (other queues)
     double hp_t[3] = {0.0, 0.0, 0.0};
     double pf_t[5] = {0, 0, 0, 0, 0};     // sync, copy, enqueue, wait, total
     long pf_n = 0;
@@ -781,6 +782,7 @@ int finish_timing(vo_ctx* c, EvRec* ev)
 {
     const int nk = vo::kernel_count();
     c->ktime_ms.assign(nk, 0.f);
+    c->kcont_ms.assign(nk, 0.f);
     c->kcount.assign(nk, 0);
     if (!ev) return VO_OK;
     SYNC_ALL(c);
@@ -790,6 +792,7 @@ int finish_timing(vo_ctx* c, EvRec* ev)
         (void)hipEventElapsedTime(&ms, c->ev_pool[sp.second], c->ev_pool[sp.second + 1]);
         const bool cont = sp.first >= kContSpan;
         c->ktime_ms[cont ? sp.first - kContSpan : sp.first] += ms;
+        if (cont) c->kcont_ms[sp.first - kContSpan] += ms;
         if (!cont) c->kcount[sp.first] += 1;
     }
     return VO_OK;
@@ -1713,6 +1716,17 @@ int vo_last_kernel_stats(vo_ctx* c, const char** names, float* ms_per_launch, fl
         if (ms_per_launch) ms_per_launch[k] = c->kcount[k] ? c->ktime_ms[k] / (float)c->kcount[k] : -1.f;
         if (frames_per_launch)
             frames_per_launch[k] = c->klaunch[k] ? (float)c->last_frames / (float)c->klaunch[k] : 0.f;
+    }
+    // one more entry: "ransac_pose", the part of a pass's RANSAC on the pose queue (its first chunk; the
+    // later chunks run on the trajectory or fit queue as continuation spans of the same timed launch)
+    constexpr int kR = 4;                             // "ransac"
+    if (nk == vo::kernel_count() && cap > nk && (int)c->kcont_ms.size() > kR) {
+        if (names) names[nk] = "ransac_pose";
+        if (ms_per_launch)
+            ms_per_launch[nk] = c->kcount[kR] ? (c->ktime_ms[kR] - c->kcont_ms[kR]) / (float)c->kcount[kR] : -1.f;
+        if (frames_per_launch)
+            frames_per_launch[nk] = c->klaunch[kR] ? (float)c->last_frames / (float)c->klaunch[kR] : 0.f;
+        ++nk;
     }
     return nk;
 }

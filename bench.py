@@ -137,7 +137,9 @@ def dominant_kernel(per_frame: dict) -> str:
     the step's critical path (tools/step_timeline.py on a kernel trace: the extract queue ~87 %
     busy, the pose queue ~72 %), not merely the largest kernel of any queue."""
     ext = sum(per_frame.get(k, 0.0) for k in EXTRACT_QUEUE)
-    pose = sum(per_frame.get(k, 0.0) for k in POSE_ONLY)
+    # the pose queue runs the matcher and a pass's first RANSAC chunk ("ransac_pose"); "ransac" also
+    # times the later chunks, which run on the trajectory queue
+    pose = per_frame.get("match", 0.0) + per_frame.get("ransac_pose", per_frame.get("ransac", 0.0))
     queue = EXTRACT_QUEUE if ext >= pose else POSE_ONLY
     return max(queue, key=lambda k: per_frame.get(k, 0.0))
 
@@ -730,9 +732,9 @@ def main():
     bd = []
     step(timing=1, stats=bd)
     ks = {k: (float(np.mean([b[k][0] for b in bd if k in b])), float(np.mean([b[k][1] for b in bd if k in b])))
-          for k in KERNELS if any(k in b for b in bd)}
+          for k in KERNELS + ["ransac_pose"] if any(k in b for b in bd)}
     info_all = np.concatenate([last[s][2] for s in my_seqs])
-    per_frame = {k: ks[k][0] / ks[k][1] if k in ks and ks[k][1] > 0 else 0.0 for k in KERNELS}
+    per_frame = {k: ks[k][0] / ks[k][1] if k in ks and ks[k][1] > 0 else 0.0 for k in KERNELS + ["ransac_pose"]}
     dominant = dominant_kernel(per_frame)
     kidx = KERNELS.index(dominant)
 
@@ -792,8 +794,9 @@ def main():
         bd5 = []
         step5(timing=1, stats=bd5)
         ks5 = {k: (float(np.mean([b[k][0] for b in bd5 if k in b])), float(np.mean([b[k][1] for b in bd5 if k in b])))
-               for k in KERNELS if any(k in b for b in bd5)}
-        dom5 = dominant_kernel({k: ks5[k][0] / ks5[k][1] if k in ks5 and ks5[k][1] > 0 else 0.0 for k in KERNELS})
+               for k in KERNELS + ["ransac_pose"] if any(k in b for b in bd5)}
+        dom5 = dominant_kernel({k: ks5[k][0] / ks5[k][1] if k in ks5 and ks5[k][1] > 0 else 0.0
+                                for k in KERNELS + ["ransac_pose"]})
         live5 = []
         barrier()
         t5 = time.perf_counter()
@@ -834,6 +837,9 @@ def main():
                        "queue": "pose" if k in POSE_QUEUE else ("trajectory" if k == "trajectory" else "extract"),
                        "pmc_hbm_bytes_per_launch": r["hbm_bytes"] if r else None,
                        "valu_issue_frac": r["valu_issue_frac"] if r else None}
+        if "ransac_pose" in ks and ks["ransac_pose"][1] > 0:
+            kern["ransac_pose"] = {"us_per_frame": round(per_frame["ransac_pose"] * 1e3, 4), "queue": "pose",
+                                   "note": "the first RANSAC chunk of each pass (the pose queue's share of 'ransac')"}
         st_all = np.concatenate([last[s][1] for s in my_seqs])
         line = {
             "metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,

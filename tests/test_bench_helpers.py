@@ -65,3 +65,9 @@ def test_dominant_kernel_is_on_the_critical_queue():
     assert bench.dominant_kernel(kitti) == "stencil"
     low_inlier = dict(kitti, ransac=4.2)
     assert bench.dominant_kernel(low_inlier) == "ransac"
+    # "ransac" also times a pass's later chunks on the trajectory queue: the pose queue counts only
+    # its first chunk ("ransac_pose") when the breakdown has it (round 6's evidence breakdown)
+    r6 = {"stencil": 1.478, "select": 0.498, "describe": 0.937, "match": 1.593, "ransac": 1.370,
+          "refit": 0.588, "triangulate": 0.524, "finalize": 0.349, "trajectory": 0.457}
+    assert bench.dominant_kernel(r6) == "match"
+    assert bench.dominant_kernel(dict(r6, ransac_pose=0.35)) == "stencil"
