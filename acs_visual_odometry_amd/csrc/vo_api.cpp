@@ -99,6 +99,7 @@ struct vo_ctx {
     // work may be in flight on the extract, fit or trajectory queues (set when a call enqueues there,
     // cleared once that call has synchronised them all): upload_meta orders its copy after them only then
     bool others_busy = true;
+    bool out_zc = true;               // VO_OUT_ZC: batched calls write their rows and commit point to pinned host memory
     std::vector<float> kcont_ms;      // per kernel: the continuation spans' share of ktime_ms (other queues)
     double hp_t[3] = {0.0, 0.0, 0.0};
     double pf_t[5] = {0, 0, 0, 0, 0};     // sync, copy, enqueue, wait, total
@@ -711,7 +712,7 @@ int run_chunk(vo_ctx* c, const uint8_t* img0, size_t frame_bytes, int nf, VoFram
         // the commit point after the last finalize (the fit queue's, which the trajectory queue waited
         // for).  A single frame's pass (window of one, no speculation) commits it: its row is read
         // alone and checked to be that frame's
-        if (!host_frame)
+        if (!host_frame && !(c->d.lo_host_dev && out == c->out_host_dev))
             HIPCHK(hipMemcpyAsync(c->lo_host, &c->d.st->lo, sizeof(int32_t), hipMemcpyDeviceToHost, tq));
         if (c->pf_profile && host_frame) c->pf_enq_end = now_us();
         HIPCHK(hipStreamSynchronize(s));
@@ -1010,6 +1011,14 @@ int vo_create(const vo_config* cfg, vo_ctx** out)
     if (hip_ok(hipHostMalloc((void**)&c->stage_host, np, hipHostMallocDefault)) != VO_OK) return bail(VO_ERR_HIP);
     if (hip_ok(hipHostMalloc((void**)&c->lo_host, sizeof(int32_t), hipHostMallocDefault)) != VO_OK)
         return bail(VO_ERR_HIP);
+    // batched calls: the pose rows and the commit point straight into pinned host memory (VO_OUT_ZC=0:
+    // device rows and two D2H copies after the last pass, ~25 us at the end of every call, traces tr012c, trkitti)
+    d.lo_host_dev = nullptr;
+    c->out_zc = !(getenv("VO_OUT_ZC") && atoi(getenv("VO_OUT_ZC")) == 0);
+    if (c->out_zc && hipHostGetDevicePointer((void**)&d.lo_host_dev, c->lo_host, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        d.lo_host_dev = nullptr;
+    }
     // deterministic contents before first use
     (void)hipMemset(d.kps, 0, sizeof(int2) * N * VO_SLOTS);
     (void)hipMemset(d.desc, 0, sizeof(uint64_t) * 8 * N * VO_SLOTS);
@@ -1518,11 +1527,12 @@ int run_frames(vo_ctx* c, const uint8_t* dev, const uint8_t* host, bool pinned, 
     const int pass0 = c->npass;
     for (int f0 = 0; f0 < nframes; f0 += chunk) {
         const int nf = std::min(chunk, nframes - f0);
+        VoFrameOut* out = c->out_zc && c->out_host_dev && c->d.lo_host_dev ? c->out_host_dev : c->out_dev;
         if (host) {
             const HostSrc hs{host + (size_t)f0 * frame_bytes, frame_bytes, pinned};
-            rc = run_chunk(c, nullptr, frame_bytes, nf, c->out_dev, base, evp, false, &hs);
+            rc = run_chunk(c, nullptr, frame_bytes, nf, out, base, evp, false, &hs);
         } else {
-            rc = run_chunk(c, dev + (size_t)f0 * frame_bytes, frame_bytes, nf, c->out_dev, base, evp, false);
+            rc = run_chunk(c, dev + (size_t)f0 * frame_bytes, frame_bytes, nf, out, base, evp, false);
         }
         if (rc) return rc;
     }

@@ -312,6 +312,7 @@ struct VoDev {
     unsigned* ctr;
     VoTrajRec* trec;      // x ring: committed frames' trajectory inputs (k_finalize -> k_traj)
     int2* plog;           // x VO_PLOG: (lo, committed) per pose pass
+    int32_t* lo_host_dev; // pinned host word (device address): each k_traj stores VoState::lo there (the commit point)
     int pass;             // pose pass number (its plog entry)
     int nospec;           // every earlier pass is finalized: the window comes from the state itself
     VoPlan* plan;         // x VO_PASS_RING

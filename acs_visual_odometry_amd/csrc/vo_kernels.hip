@@ -5309,6 +5309,9 @@ __device__ void traj_chain(const VoDev& d, VoFrameOut* out, int out_base, int lo
 
 __global__ void __launch_bounds__(256) k_traj(VoDev d, VoFrameOut* out, int out_base)
 {
+    // the commit point for the host (every pass's k_traj runs after its k_finalize, in pass order on
+    // one queue, so the chunk's last one leaves the final value): no D2H copy after the last pass
+    if (threadIdx.x == 0 && d.lo_host_dev) __hip_atomic_store(d.lo_host_dev, d.st->lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const int2 lg = d.plog[d.pass % VO_PLOG];
     if (lg.y <= 0) return;
     traj_chain(d, out, out_base, lg.x, lg.y);

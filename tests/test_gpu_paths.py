@@ -423,7 +423,8 @@ print("KNOB_OK" if ok else "KNOB_DIFF")
                                        ("VO_EVENT_WAIT=0", 16), ("VO_EVENT_WAIT=0", 8),
                                        ("VO_ST_FLAT=1", 64), ("VO_ST_FLAT=1,VO_STSEG=8", 64), ("VO_ST_FLAT=1", 8),
                                        ("VO_SEL_LDS_KB=48", 64), ("VO_PIPE_FIRST=0", 16), ("VO_RANSAC_SPLIT=0", 16),
-                                       ("VO_SEL_SMALL=0", 8), ("VO_STSEG_ADAPT=0", 8), ("VO_TAIL=0", 64)])
+                                       ("VO_SEL_SMALL=0", 8), ("VO_STSEG_ADAPT=0", 8), ("VO_TAIL=0", 64),
+                                       ("VO_OUT_ZC=0", 16)])
 def test_process_knobs_match_oracle(leak_case, tmp_path, env, batch):
     """Knobs the library reads once per process (stencil segment height, RANSAC cut and loop,
     triangulation grid, XCD placement, the branch-free FLAT stencil, the polling wait kernel, the
